@@ -1,0 +1,298 @@
+"""Seeded synthetic SIGNALduino corpora.
+
+Everything here is vectorised numpy so that a 1M-message corpus is built in a
+few seconds outside the timed region of ``bench.py``.  The same generators
+feed the golden-vector script (``tests/golden/make_golden.py``), the parity
+tests and the benchmark, so the benchmark measures exactly the distribution
+the parity tests check.
+
+Batch layout (the device SoA layout, see DESIGN.md "Data layout in HBM"):
+
+``PulseBatch``  (MU / MS)
+    data     uint8 [total]      pulse-id characters of every message, concatenated
+    offsets  int64 [n+1]        message i owns data[offsets[i]:offsets[i+1]]
+    npat     uint8 [n]          number of P# patterns (<= 10)
+    pat_id   uint8 [n, 10]      pattern id characters ('0'..'9') in line order
+    pat_val  float64 [n, 10]    pattern values (float(P#)) in line order
+    cp_slot  int8 [n]           MS only: slot of the CP pattern, -1 when CP is
+                                missing from the patterns
+    rssi     int32 [n]          R= value (-1 = absent)
+    ms_ok    uint8 [n]          MS only: CP/SP/R string gates passed
+
+``McBatch``
+    hexdata  uint8 [total], offsets int64 [n+1], clock int32 [n],
+    mcbitnum int32 [n], mtype uint8 [n] (0 = 'MC', 1 = 'Mc'), v32 uint8 [n]
+    (version string starts with 'V 3.2.').
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+MAXPAT = 10
+
+
+@dataclass
+class PulseBatch:
+    kind: str
+    data: np.ndarray
+    offsets: np.ndarray
+    npat: np.ndarray
+    pat_id: np.ndarray
+    pat_val: np.ndarray
+    cp_slot: np.ndarray
+    sp_slot: np.ndarray
+    rssi: np.ndarray
+    ms_ok: np.ndarray
+    src_proto: np.ndarray = field(default=None)  # generating protocol index (-1 noise)
+
+    @property
+    def n(self) -> int:
+        return int(self.npat.shape[0])
+
+    def message(self, i: int) -> str:
+        return bytes(self.data[self.offsets[i]:self.offsets[i + 1]]).decode("latin-1")
+
+    def to_msg_dict(self, i: int) -> Dict[str, str]:
+        """msg_data exactly as MUParser/MSParser would build it (parser/mu.py:82-94)."""
+        d: Dict[str, str] = {self.kind: ""}
+        for k in range(int(self.npat[i])):
+            v = self.pat_val[i, k]
+            d["P" + chr(self.pat_id[i, k])] = str(int(v)) if float(v).is_integer() else repr(float(v))
+        d["D"] = self.message(i)
+        if self.kind == "MS":
+            d["CP"] = chr(self.pat_id[i, self.cp_slot[i]]) if self.cp_slot[i] >= 0 else "9"
+            d["SP"] = chr(self.pat_id[i, self.sp_slot[i]]) if self.sp_slot[i] >= 0 else "9"
+        else:
+            d["CP"] = chr(self.pat_id[i, 0])
+        if self.rssi[i] >= 0:
+            d["R"] = str(int(self.rssi[i]))
+        d["data"] = d["D"]
+        return d
+
+    def subset(self, idx) -> "PulseBatch":
+        idx = np.asarray(idx, dtype=np.int64)
+        lens = self.offsets[idx + 1] - self.offsets[idx]
+        offs = np.zeros(len(idx) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        data = np.concatenate([self.data[self.offsets[i]:self.offsets[i + 1]] for i in idx]) if len(idx) else np.zeros(0, np.uint8)
+        return PulseBatch(self.kind, data, offs, self.npat[idx].copy(), self.pat_id[idx].copy(),
+                          self.pat_val[idx].copy(), self.cp_slot[idx].copy(), self.sp_slot[idx].copy(),
+                          self.rssi[idx].copy(), self.ms_ok[idx].copy(),
+                          None if self.src_proto is None else self.src_proto[idx].copy())
+
+
+@dataclass
+class McBatch:
+    hexdata: np.ndarray
+    offsets: np.ndarray
+    clock: np.ndarray
+    mcbitnum: np.ndarray
+    mtype: np.ndarray
+    v32: np.ndarray
+    src_proto: np.ndarray = field(default=None)
+
+    @property
+    def n(self) -> int:
+        return int(self.clock.shape[0])
+
+    def hex(self, i: int) -> str:
+        return bytes(self.hexdata[self.offsets[i]:self.offsets[i + 1]]).decode("latin-1")
+
+    def to_msg_dict(self, i: int) -> Dict[str, str]:
+        """msg_data as MCParser builds it (parser/mc.py:59-62)."""
+        d = {"MC" if self.mtype[i] == 0 else "Mc": "", "D": self.hex(i), "C": str(int(self.clock[i])),
+             "L": str(int(self.mcbitnum[i]))}
+        d["raw_hex"] = d["D"]
+        d["clock"] = d["C"]
+        d["mcbitnum"] = d["L"]
+        d["messagetype"] = "MC" if self.mtype[i] == 0 else "Mc"
+        return d
+
+    def subset(self, idx) -> "McBatch":
+        idx = np.asarray(idx, dtype=np.int64)
+        lens = self.offsets[idx + 1] - self.offsets[idx]
+        offs = np.zeros(len(idx) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        data = np.concatenate([self.hexdata[self.offsets[i]:self.offsets[i + 1]] for i in idx]) if len(idx) else np.zeros(0, np.uint8)
+        return McBatch(data, offs, self.clock[idx].copy(), self.mcbitnum[idx].copy(), self.mtype[idx].copy(),
+                       self.v32[idx].copy(), None if self.src_proto is None else self.src_proto[idx].copy())
+
+
+def _numeric(seq) -> Optional[List[float]]:
+    if not isinstance(seq, list) or not seq:
+        return None
+    try:
+        return [float(x) for x in seq]
+    except (TypeError, ValueError):
+        return None
+
+
+def _templates(protocols: Dict[str, dict], key_start: str):
+    """Per eligible protocol: distinct values, start/one/zero as value-slot lists."""
+    out = []
+    for idx, (pid, p) in enumerate(protocols.items()):
+        if key_start == "sync" and "sync" not in p:
+            continue
+        if key_start == "start" and "clockabs" not in p:
+            continue
+        one, zero = _numeric(p.get("one")), _numeric(p.get("zero"))
+        if one is None or zero is None or len(one) != len(zero):
+            continue
+        head = _numeric(p.get(key_start)) if key_start in p else []
+        if head is None:
+            continue
+        vals: List[float] = []
+        for v in head + one + zero:
+            if v not in vals:
+                vals.append(v)
+        if len(vals) > 8:
+            continue
+        ca = float(p.get("clockabs", 0) or 0)
+        lmin = int(p.get("length_min", 8) or 8)
+        lmax = int(p.get("length_max", lmin + 8) or (lmin + 8))
+        lmax = max(lmin, min(lmax, 200))
+        out.append(dict(idx=idx, pid=pid, vals=vals, head=[vals.index(v) for v in head],
+                        one=[vals.index(v) for v in one], zero=[vals.index(v) for v in zero],
+                        clock=ca, lmin=lmin, lmax=lmax))
+    return out
+
+
+def _assemble(rng, n, tpls, npulse_fn, repeat: bool, clock_sweep, noise_frac: float, kind: str,
+              fixed_len: Optional[int]):
+    """Shared vectorised MU/MS message assembly (padded [n, Tmax] then packed ragged)."""
+    ntpl = len(tpls)
+    Tmax = fixed_len if fixed_len else 256
+    choice = rng.integers(0, ntpl, size=n)
+    is_noise = rng.random(n) < noise_frac
+    npat = np.zeros(n, np.uint8)
+    pat_id = np.zeros((n, MAXPAT), np.uint8)
+    pat_val = np.zeros((n, MAXPAT), np.float64)
+    cp_slot = np.full(n, -1, np.int8)
+    sp_slot = np.full(n, -1, np.int8)
+    rssi = rng.integers(0, 256, size=n).astype(np.int32)
+    rssi[rng.random(n) < 0.1] = -1
+    lengths = np.zeros(n, np.int64)
+    msgs = np.zeros((n, Tmax), np.uint8)
+    src = np.where(is_noise, -1, np.array([t["idx"] for t in tpls])[choice]).astype(np.int32)
+    # id permutation per message: slot k gets id perm[k]; ids are emitted in ascending
+    # id order like the firmware prints P0..P7, so the dict order differs from slot order.
+    perms = np.argsort(rng.random((n, MAXPAT)), axis=1).astype(np.int64)
+    for t_i, t in enumerate(tpls):
+        sel = np.nonzero((choice == t_i) & ~is_noise)[0]
+        if len(sel) == 0:
+            continue
+        m = len(sel)
+        nv = len(t["vals"])
+        base = t["clock"] if t["clock"] > 0 else 0.0
+        clk = np.full(m, base) if base > 0 else rng.uniform(250, 500, size=m)
+        clk = clk * clock_sweep(rng, m)
+        jit = rng.uniform(0.95, 1.05, size=(m, nv))
+        vals = np.clip(np.rint(np.array(t["vals"])[None, :] * clk[:, None] * jit), -99999, 99999)
+        nb = rng.integers(t["lmin"], t["lmax"] + 1, size=m)
+        bits = rng.integers(0, 2, size=(m, max(t["lmax"], 1))).astype(np.int64)
+        head = np.array(t["head"], np.int64)
+        L = len(t["one"])
+        units = np.array([t["zero"], t["one"]], np.int64)  # [2, L]
+        frame_len = len(head) + nb * L
+        total = np.full(m, fixed_len, np.int64) if fixed_len else np.minimum(npulse_fn(rng, m, frame_len), Tmax)
+        pos = np.arange(Tmax)[None, :]
+        j = pos % frame_len[:, None] if repeat else np.minimum(pos, frame_len[:, None] - 1)
+        in_head = j < len(head)
+        hj = np.minimum(j, max(len(head) - 1, 0))
+        bj = np.maximum(j - len(head), 0)
+        bit_idx = np.minimum(bj // L, bits.shape[1] - 1)
+        u = bj % L
+        bitv = np.take_along_axis(bits, bit_idx, axis=1)
+        slot = np.where(in_head, head[hj] if len(head) else 0, units[bitv, u])
+        P = perms[sel, :nv]                       # slot -> id
+        order = np.argsort(P, axis=1)             # q -> slot, ascending id
+        npat[sel] = nv
+        pat_id[sel, :nv] = (np.take_along_axis(P, order, axis=1) + ord("0")).astype(np.uint8)
+        pat_val[sel, :nv] = np.take_along_axis(vals, order, axis=1)
+        if kind == "MS":
+            av = np.abs(np.array(t["vals"]))
+            cps = int(np.argmin(np.abs(av - 1.0)))
+            sync_slots = t["head"] if t["head"] else [0]
+            sps = max(sync_slots, key=lambda s: abs(t["vals"][s]))
+            cp_slot[sel] = np.argmax(order == cps, axis=1)
+            sp_slot[sel] = np.argmax(order == sps, axis=1)
+        msgs[sel] = (np.take_along_axis(P, slot, axis=1) + ord("0")).astype(np.uint8)
+        lengths[sel] = total
+    noise = np.nonzero(is_noise)[0]
+    if len(noise):
+        m = len(noise)
+        nvs = rng.integers(2, 9, size=m)
+        P = perms[noise]                          # first nv entries are the ids in use
+        mag = rng.uniform(100, 20000, size=(m, MAXPAT))
+        sgn = np.where(rng.random((m, MAXPAT)) < 0.5, -1.0, 1.0)
+        valid = np.arange(MAXPAT)[None, :] < nvs[:, None]
+        ids_sorted = np.sort(np.where(valid, P, 99), axis=1)
+        npat[noise] = nvs
+        pat_id[noise] = np.where(ids_sorted < 99, ids_sorted + ord("0"), 0).astype(np.uint8)
+        pat_val[noise] = np.where(ids_sorted < 99, np.rint(mag * sgn), 0.0)
+        pick = (rng.random((m, Tmax)) * nvs[:, None]).astype(np.int64)
+        msgs[noise] = (np.take_along_axis(ids_sorted, pick, axis=1) + ord("0")).astype(np.uint8)
+        lengths[noise] = fixed_len if fixed_len else rng.integers(16, 200, size=m)
+        if kind == "MS":
+            absv = np.where(valid, np.abs(pat_val[noise]), np.inf)
+            cp_slot[noise] = np.argmin(absv, axis=1)
+            sp_slot[noise] = np.argmax(np.where(valid, np.abs(pat_val[noise]), -1.0), axis=1)
+    offsets = np.zeros(n + 1, np.int64)
+    np.cumsum(lengths, out=offsets[1:])
+    data = msgs[np.arange(Tmax)[None, :] < lengths[:, None]]
+    ms_ok = np.ones(n, np.uint8)
+    return PulseBatch(kind, np.ascontiguousarray(data), offsets, npat, pat_id, pat_val, cp_slot, sp_slot,
+                      rssi, ms_ok, src)
+
+
+def mu_corpus(protocols: Dict[str, dict], n: int, seed: int = 42, npulse: int = 256,
+              noise_frac: float = 0.15) -> PulseBatch:
+    """Config 2: MU messages of exactly ``npulse`` pulses, frames repeated."""
+    rng = np.random.default_rng(seed)
+    tpls = _templates(protocols, "start")
+    return _assemble(rng, n, tpls, None, True, lambda r, m: np.ones(m), noise_frac, "MU", npulse)
+
+
+def ms_corpus(protocols: Dict[str, dict], n: int, seed: int = 43, noise_frac: float = 0.1) -> PulseBatch:
+    """Config 3: one sync+bits frame per message, clock swept x U(0.6,1.4) over the ±30 % gate."""
+    rng = np.random.default_rng(seed)
+    tpls = _templates(protocols, "sync")
+
+    def npulse_fn(r, m, frame_len):
+        # one frame, sometimes followed by a partial repeat (firmware buffer tail)
+        extra = np.where(r.random(m) < 0.3, r.integers(1, 9, size=m), 0)
+        return np.minimum(frame_len + extra, 256)
+
+    return _assemble(rng, n, tpls, npulse_fn, True, lambda r, m: r.uniform(0.6, 1.4, size=m),
+                     noise_frac, "MS", None)
+
+
+def mc_protocols(protocols: Dict[str, dict]) -> List[int]:
+    return [i for i, p in enumerate(protocols.values()) if "clockrange" in p]
+
+
+def mc_corpus(protocols: Dict[str, dict], n: int, seed: int = 44) -> McBatch:
+    """Config 4: random-hex Manchester frames for the 12 clockrange protocols."""
+    rng = np.random.default_rng(seed)
+    plist = list(protocols.values())
+    mc = mc_protocols(protocols)
+    choice = np.array(mc)[rng.integers(0, len(mc), size=n)]
+    lmin = np.array([int(plist[i].get("length_min", 8)) for i in choice])
+    lmax = np.array([int(plist[i].get("length_max", 64)) for i in choice])
+    L = (lmin + (rng.random(n) * (lmax - lmin + 1)).astype(np.int64)).astype(np.int32)
+    # a few out-of-range lengths to exercise the gates
+    L = np.where(rng.random(n) < 0.05, np.maximum(L + rng.integers(-6, 7, size=n), 1), L).astype(np.int32)
+    lo = np.array([plist[i]["clockrange"][0] for i in choice], np.float64)
+    hi = np.array([plist[i]["clockrange"][1] for i in choice], np.float64)
+    clock = np.rint(rng.uniform(0.9 * lo, 1.1 * hi)).astype(np.int32)
+    hexlen = (L + 3) // 4
+    offsets = np.zeros(n + 1, np.int64)
+    np.cumsum(hexlen, out=offsets[1:])
+    digits = np.frombuffer(b"0123456789ABCDEF", np.uint8)
+    hexdata = digits[rng.integers(0, 16, size=int(offsets[-1]))]
+    mtype = (rng.random(n) < 0.5).astype(np.uint8)
+    v32 = (rng.random(n) < 0.1).astype(np.uint8)
+    return McBatch(hexdata.copy(), offsets, clock, L, mtype, v32, choice.astype(np.int32))
