@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Benchmark: RF messages/s demodulated (MU+MS+MC, full protocol bank) on 1..8 MI355X.
+
+One "step" = one pass of the hot path over one batch resident in HBM: every MU message
+(256 pulses) x the full MU bank, every MS message x the MS bank, every MC frame x the 12
+clockrange protocols, results written in reference order -- and, for N > 1, the RCCL
+all-gather of the decoded dmsg buffers (BASELINE config 5).  Weak scaling: each rank owns
+``--msgs`` messages (1/3 of each type).
+
+Prints ONE JSON line on rank 0 (contract in the task statement); see DESIGN.md §Measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--msgs", type=int, default=1_000_000, help="messages per rank (1/3 MU, 1/3 MS, 1/3 MC)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(P, budget_s: float):
+    """The CPU oracle (pure-Python restatement of the reference path, kind 'port') on a bounded
+    sample of the same workload, 1 core; MU:MS:MC in the same 1:1:1 mix."""
+    from oracle import sd_oracle as O
+    from pysignalduino_amd import synth
+    ob = O.OracleBank()
+    mu = synth.mu_corpus(P, 400, seed=9001)
+    ms = synth.ms_corpus(P, 400, seed=9002)
+    mc = synth.mc_corpus(P, 400, seed=9003)
+    t0 = time.perf_counter()
+    done = 0
+    i = 0
+    while time.perf_counter() - t0 < budget_s and i < 400:
+        for kind, b in (("MU", mu), ("MS", ms)):
+            try:
+                O.demod(ob, b.to_msg_dict(i), kind)
+            except Exception:
+                pass
+        try:
+            O.demod_mc_fixed(ob, mc.hex(i), int(mc.clock[i]), int(mc.mcbitnum[i]),
+                             "Mc" if mc.mtype[i] else "MC", "V 3.2.0" if mc.v32[i] else None)
+        except Exception:
+            pass
+        done += 3
+        i += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "msgs/s", "cores": 1, "kind": "port",
+            "sample": f"{done} messages (1:1:1 MU/MS/MC, seeds 9001-9003) through oracle/sd_oracle.py, "
+                      f"{dt:.1f} s, 1 thread, {platform.processor() or platform.machine()}"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from pysignalduino_amd import bank as bankmod, runtime, synth
+    bk = bankmod.Bank()
+    P = bk.protocols
+    eng = runtime.Engine(bk, local)
+    n3 = args.msgs // 3
+    mu = synth.mu_corpus(P, n3, seed=42 + 1000 * rank)
+    ms = synth.ms_corpus(P, n3, seed=43 + 1000 * rank)
+    mc = synth.mc_corpus(P, args.msgs - 2 * n3, seed=44 + 1000 * rank)
+    bmu, bms, bmc = eng.to_device_pulses(mu), eng.to_device_pulses(ms), eng.to_device_mc(mc)
+    outs = {
+        "MU": eng.alloc_out(mu.n, 8 * mu.n + 4096, 200 * mu.n + 65536),
+        "MS": eng.alloc_out(ms.n, 4 * ms.n + 4096, 64 * ms.n + 65536),
+        "MC": eng.alloc_out(mc.n, 4 * mc.n + 4096, 96 * mc.n + 65536),
+    }
+    stream = torch.cuda.current_stream(dev)
+    ev = {k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in outs}
+    ktimes = {k: [] for k in outs}
+
+    def step(record=False):
+        for k in outs:
+            outs[k]["cursor"].zero_()
+        for k, bd in (("MU", bmu), ("MS", bms), ("MC", bmc)):
+            if record:
+                ev[k][0].record(stream)
+            if k == "MC":
+                eng.launch_mc(bd, outs[k])
+            else:
+                eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, outs[k])
+            if record:
+                ev[k][1].record(stream)
+        if world > 1:  # RCCL all-gather of the decoded dmsg buffers (config 5)
+            for k in outs:
+                o = outs[k]
+                used = o["cursor"][:2].clone()
+                mx = used.clone()
+                dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+                hb = int(mx[1].item())
+                hb = max(hb, 1)
+                gh = torch.empty(world * hb, dtype=torch.uint8, device=dev)
+                dist.all_gather_into_tensor(gh, o["heap"][:hb].contiguous())
+                rb = max(int(mx[0].item()), 1) * runtime.RES_DT.itemsize
+                gr = torch.empty(world * rb, dtype=torch.uint8, device=dev)
+                dist.all_gather_into_tensor(gr, o["rec"][:rb].contiguous())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # overflow check (capacities sized so that the timed steps never re-run)
+    for k, o in outs.items():
+        cur = o["cursor"].cpu().numpy()
+        if cur[2] != 0:
+            raise SystemExit(f"{k}: result capacity overflow in bench configuration ({cur})")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+        torch.cuda.synchronize()
+        for k in outs:
+            ktimes[k].append(ev[k][0].elapsed_time(ev[k][1]) * 1e-3)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    total_msgs = args.msgs * world * args.steps
+    value = total_msgs / dt
+
+    # roofline of the dominant kernel (MU): algorithmic bytes / measured kernel time
+    kt = {k: float(np.mean(v)) for k, v in ktimes.items()}
+    dom = max(kt, key=kt.get)
+    bd = {"MU": bmu, "MS": bms, "MC": bmc}[dom]
+    o = outs[dom]
+    cur = o["cursor"].cpu().numpy().astype(np.int64)
+    n = bd["n"]
+    if dom == "MC":
+        in_bytes = int(bd["lengths"].sum()) + n * (8 + 4 + 4 + 1)
+    else:
+        in_bytes = int(bd["lengths"].sum()) + n * (8 + 1 + 10 + 80 + (2 if dom == "MS" else 0))
+    out_bytes = n * runtime.DESC_DT.itemsize + int(cur[0]) * runtime.RES_DT.itemsize + int(cur[1])
+    alg = in_bytes + out_bytes + len(bk.blob)
+    achieved = alg / kt[dom]
+    res = {
+        "metric": "RF messages/sec demodulated (MU+MS+MC, full protocol bank)",
+        "value": value, "unit": "msgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8+f64", "data": "synthetic (seeded generators, pysignalduino_amd/synth.py)",
+        "config": {"workload": "mixed MU/MS/MC stream, 1/3 each per rank: MU 256-pulse messages x 129-id MU bank, "
+                               "MS sync+bits x 66-id MS bank (clock x U(0.6,1.4)), MC frames x 12 clockrange ids "
+                               "('fixed' chain); N>1 adds the RCCL all-gather of dmsg buffers (config 5)",
+                   "msgs_per_gpu": args.msgs, "parallelism": f"dp{world}"},
+        "per_kernel_ms": {k: 1e3 * v for k, v in kt.items()},
+        "per_type_msgs_per_s": {"MU": mu.n / kt["MU"], "MS": ms.n / kt["MS"], "MC": mc.n / kt["MC"]},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": None, "kernel": f"k_pulses<{dom}>" if dom != "MC" else "k_mc",
+                     "alg_bytes_per_launch": alg},
+    }
+    if rank == 0 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(P, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

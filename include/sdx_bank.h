@@ -1,0 +1,102 @@
+/*
+ * sdx_bank.h -- binary layout of a compiled SIGNALduino protocol bank.
+ *
+ * The bank is compiled on the host from protocols.json (the reference's
+ * sd_protocols/protocols.json, loaded by sd_protocols/sd_protocols.py:30-41)
+ * by pysignalduino_amd/bank.py into ONE contiguous blob that is uploaded to
+ * HBM once per device and read (through L2/LDS) by every kernel.  All records
+ * are naturally aligned C structs; the Python side mirrors them with numpy
+ * dtypes (align=True) and checks sizeof() through sdx_layout_size().
+ *
+ * Record order inside each class table = JSON insertion order of the bank,
+ * which is the reference's iteration order (get_keys, sd_protocols.py:49-52)
+ * and therefore the result order.
+ */
+#ifndef SDX_BANK_H
+#define SDX_BANK_H
+#include <stdint.h>
+
+#define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
+#define SDX_BANK_VERSION 2u
+#define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
+#define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
+#define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
+
+/* one search list (start/sync/one/zero/float) = pattern_exists() argument,
+ * pattern_utils.py:34-136, with its unique values (first-appearance order)
+ * and their tolerances (calculate_tolerance, pattern_utils.py:15-26) */
+typedef struct {
+  double uval[SDX_MAXUNIQ];
+  double utol[SDX_MAXUNIQ];
+  uint8_t len;   /* search length; 0 = key absent/falsy */
+  uint8_t nuniq; /* number of distinct values */
+  uint8_t pad[6];
+  uint8_t uidx[SDX_MAXSEARCH]; /* search position -> unique index */
+} sdx_patspec;                 /* 152 bytes */
+
+enum sdx_postdemo {
+  SDX_PD_NONE = 0, SDX_PD_EM, SDX_PD_REVOLT, SDX_PD_FS20, SDX_PD_FHT80, SDX_PD_FHT80TF,
+  SDX_PD_WS2000, SDX_PD_WS7035, SDX_PD_WS7053, SDX_PD_LENPREFIX
+};
+
+/* MU protocol = every id with 'clockabs' (message_unsynced.py:45) */
+typedef struct {
+  double clock;                         /* float(clockabs)  (:59) */
+  sdx_patspec start, one, zero, flt;    /* (:67-141) */
+  int32_t proto_index;                  /* index into the full bank (host: pid string) */
+  int32_t length_min;                   /* regex {min,}  (:178) */
+  int32_t length_max;                   /* chunk-count limit, INT32_MAX = none (:217) */
+  int32_t width;                        /* len(one)  (:201-206) */
+  int32_t pad_bits;                     /* paddingbits (:257) */
+  int32_t postdemo;                     /* enum sdx_postdemo (:231-250) */
+  int32_t mm_dfa;                       /* modulematch DFA index, -1 = none (:277) */
+  int32_t mm_pre_state;                 /* DFA state after consuming the (constant) preamble */
+  int32_t pre_off, pre_len, post_off, post_len; /* string heap (:271-274) */
+  uint8_t has_start, recon, dispatch_bin, remove_zero, active, never, res0, res1;
+  int32_t res2;
+} sdx_mu_proto;
+
+/* MS protocol = every id with 'sync' (message_synced.py:79) */
+typedef struct {
+  double pclock;                        /* float(clockabs or 0)  (:83) */
+  sdx_patspec key[4];                   /* sync, one, zero, float (:109) */
+  int32_t proto_index;
+  int32_t width;                        /* len(one) (:106-107) */
+  int32_t lmin_sync;                    /* int(length_min or -1) (:152) */
+  int32_t lir_min;                      /* length_in_range min, -1 none (helpers.py:144-154) */
+  int32_t lir_max;                      /* length_in_range max, INT32_MAX none (helpers.py:157-164) */
+  int32_t pad_bits, postdemo, pre_off, pre_len, post_off, post_len;
+  uint8_t recon, never, res[2];
+} sdx_ms_proto;
+
+enum sdx_mc_method {
+  SDX_MC_FUNKBUS = 1, SDX_MC_SAINLOGIC, SDX_MC_AS, SDX_MC_PLAIN, SDX_MC_RAW, SDX_MC_HMCRAW, SDX_MC_TFA,
+  SDX_MC_GROTHE, SDX_MC_SOMFY
+};
+
+/* MC protocol = every id with 'clockrange' (manchester.py:49-144) */
+typedef struct {
+  double cr_lo, cr_hi;                  /* clockrange[0], clockrange[1] */
+  int32_t proto_index;
+  int32_t method;                       /* enum sdx_mc_method */
+  int32_t lmin, lmax;                   /* parsed length_min / length_max */
+  int32_t pre_off, pre_len;
+  int32_t pid_num;                      /* int(pid) when integral (Funkbus id test) else -1 */
+  uint8_t has_lmin, has_lmax, lmax_is_str, invert, has_cr, res[3];
+} sdx_mc_proto;
+
+/* modulematch DFA (search semantics of re.search over the payload).
+ * flags: bit0 = a match has been found (absorbing), bit1 = match if the payload
+ * ends here ('$'), bit2 = dead (no match possible any more). */
+typedef struct {
+  int32_t nstates, start, trans_off, flags_off; /* into the DFA heap (u16 trans, u8 flags) */
+} sdx_dfa;
+
+typedef struct {
+  uint32_t magic, version;
+  uint32_t n_proto, n_mu, n_ms, n_mc, n_dfa, n_class;
+  uint32_t off_mu, off_ms, off_mc, off_dfa, off_cls, off_trans, off_flags, off_str;
+  uint32_t total_bytes, res[3];
+} sdx_bank_hdr;
+
+#endif

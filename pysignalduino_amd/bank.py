@@ -1,0 +1,345 @@
+"""Protocol-bank compiler: protocols.json -> one device-ready blob (include/sdx_bank.h).
+
+Mirrors how the reference consumes the bank (sd_protocols/sd_protocols.py:25-58,
+157-160; message_unsynced.py; message_synced.py; manchester.py) and resolves,
+ONCE per bank, every property lookup and string/number conversion those files
+repeat per message: float(clockabs), the search lists with their unique values
+and tolerances, int(length_min/max), paddingbits, postDemodulation method
+resolution (``hasattr`` on the reference class -- a missing method is skipped,
+message_unsynced.py:233-234), preamble/postamble f-string formatting and the
+modulematch regexes (compiled to DFAs by regex_dfa.py).
+
+Anything in a (user-modified) bank whose reference behaviour is not modelled
+on the device raises ``NotImplementedError`` here, at bank-compile time.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import os
+import struct
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from . import regex_dfa
+
+DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
+
+MAXSEARCH, MAXUNIQ = 16, 4
+MAGIC, VERSION = 0x4B4E4253, 2
+INT_NONE = 2147483647  # "no length_max" sentinel
+
+PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
+                    ("pad", "u1", (6,)), ("uidx", "u1", (MAXSEARCH,))], align=True)
+MU_REC = np.dtype([("clock", "<f8"), ("start", PATSPEC), ("one", PATSPEC), ("zero", PATSPEC), ("flt", PATSPEC),
+                   ("proto_index", "<i4"), ("length_min", "<i4"), ("length_max", "<i4"), ("width", "<i4"),
+                   ("pad_bits", "<i4"), ("postdemo", "<i4"), ("mm_dfa", "<i4"), ("mm_pre_state", "<i4"), ("pre_off", "<i4"),
+                   ("pre_len", "<i4"), ("post_off", "<i4"), ("post_len", "<i4"), ("has_start", "u1"),
+                   ("recon", "u1"), ("dispatch_bin", "u1"), ("remove_zero", "u1"), ("active", "u1"),
+                   ("never", "u1"), ("res0", "u1"), ("res1", "u1"), ("res2", "<i4")], align=True)
+MS_REC = np.dtype([("pclock", "<f8"), ("key", PATSPEC, (4,)), ("proto_index", "<i4"), ("width", "<i4"),
+                   ("lmin_sync", "<i4"), ("lir_min", "<i4"), ("lir_max", "<i4"), ("pad_bits", "<i4"),
+                   ("postdemo", "<i4"), ("pre_off", "<i4"), ("pre_len", "<i4"), ("post_off", "<i4"),
+                   ("post_len", "<i4"), ("recon", "u1"), ("never", "u1"), ("res", "u1", (2,))], align=True)
+MC_REC = np.dtype([("cr_lo", "<f8"), ("cr_hi", "<f8"), ("proto_index", "<i4"), ("method", "<i4"), ("lmin", "<i4"),
+                   ("lmax", "<i4"), ("pre_off", "<i4"), ("pre_len", "<i4"), ("pid_num", "<i4"),
+                   ("has_lmin", "u1"), ("has_lmax", "u1"), ("lmax_is_str", "u1"), ("invert", "u1"),
+                   ("has_cr", "u1"), ("res", "u1", (3,))], align=True)
+DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4")])
+HDR_FMT = "<" + "I" * 20  # sdx_bank_hdr: 20 uint32
+
+POSTDEMO = {"postDemo_EM": 1, "postDemo_Revolt": 2, "postDemo_FS20": 3, "postDemo_FHT80": 4,
+            "postDemo_FHT80TF": 5, "postDemo_WS2000": 6, "postDemo_WS7035": 7, "postDemo_WS7053": 8,
+            "postDemo_lengtnPrefix": 9}
+# every method name the reference SDProtocols class defines that a bank may reference for MC
+MC_METHODS = {"mcBit2Funkbus": 1, "mcBit2Sainlogic": 2, "mcBit2AS": 3, "mcBit2Hideki": 4, "mcBit2Maverick": 4,
+              "mcBit2OSV1": 4, "mcBit2OSV2o3": 4, "mcBit2OSPIR": 4, "mcRaw": 5, "mcraw": 6, "mcBit2TFA": 7,
+              "mcBit2Grothe": 8, "mcBit2SomfyRTS": 9}
+
+
+def load_protocols(path: Optional[str] = None) -> Dict[str, dict]:
+    """sd_protocols.py:30-41 (``data.get('protocols', {})``)."""
+    with open(path or DEFAULT_BANK, "r", encoding="utf-8") as f:
+        data = json.load(f)
+    return data.get("protocols", {})
+
+
+def set_defaults(protocols: Dict[str, dict]) -> None:
+    """sd_protocols.py:157-160."""
+    for pid, proto in protocols.items():
+        proto.setdefault("active", True)
+        proto.setdefault("name", f"Protocol_{pid}")
+
+
+def _tolerance(v: float) -> float:
+    """pattern_utils.py:15-26 (evaluated once per bank value, same fp64 ops)."""
+    a = abs(v)
+    if a > 3:
+        if a > 16:
+            return a * 0.18
+        return a * 0.3
+    return 1.0
+
+
+def _int_exact(v, what) -> int:
+    """int(v) for the bank's numeric strings / ints; refuse anything else (not modelled)."""
+    if isinstance(v, bool) or not isinstance(v, (int, str)):
+        raise NotImplementedError(f"{what}: unsupported value {v!r}")
+    if isinstance(v, str) and not v.strip().lstrip("+-").isdigit():
+        raise NotImplementedError(f"{what}: non-integer string {v!r}")
+    return int(v)
+
+
+class Bank:
+    """A compiled bank: the device blob plus host-side metadata for result building."""
+
+    def __init__(self, protocols: Optional[Dict[str, dict]] = None, path: Optional[str] = None):
+        raw = protocols if protocols is not None else load_protocols(path)
+        self.protocols: Dict[str, dict] = copy.deepcopy(raw)
+        set_defaults(self.protocols)
+        self.pids: List[str] = list(self.protocols.keys())
+        self.compile()
+
+    # -- helpers -------------------------------------------------------------------------------
+    def _str(self, s: str):
+        b = s.encode("latin-1")
+        off = len(self._heap)
+        self._heap += b
+        return off, len(b)
+
+    def _patspec(self, rec, search: List[float], what: str):
+        if len(search) > MAXSEARCH:
+            raise NotImplementedError(f"{what}: search list longer than {MAXSEARCH}")
+        uniq: List[float] = []
+        for v in search:
+            if v not in uniq:
+                uniq.append(v)
+        if len(uniq) > MAXUNIQ:
+            raise NotImplementedError(f"{what}: more than {MAXUNIQ} distinct values")
+        rec["len"] = len(search)
+        rec["nuniq"] = len(uniq)
+        for i, v in enumerate(uniq):
+            rec["uval"][i] = v
+            t = _tolerance(v)
+            if not t >= 0.001:
+                raise NotImplementedError(f"{what}: tolerance below 0.001")
+            rec["utol"][i] = t
+        for i, v in enumerate(search):
+            rec["uidx"][i] = uniq.index(v)
+
+    @staticmethod
+    def _float_list(spec):
+        """[float(x) for x in spec] -- None when the reference's conversion raises."""
+        try:
+            return [float(x) for x in spec]
+        except (ValueError, TypeError):
+            return None
+
+    def _postdemo(self, props) -> int:
+        name = props.get("postDemodulation", None)
+        if not name:
+            return 0
+        if not isinstance(name, str):
+            raise NotImplementedError("postDemodulation: non-string")
+        return POSTDEMO.get(name.split(".")[-1], 0)  # missing method -> silently skipped
+
+    # -- compile -------------------------------------------------------------------------------
+    def compile(self) -> None:
+        P = self.protocols
+        self._heap = bytearray()
+        self.mu_pids = [pid for pid, p in P.items() if "clockabs" in p]
+        self.ms_pids = [pid for pid, p in P.items() if "sync" in p]
+        self.mc_pids = [pid for pid, p in P.items() if "clockrange" in p]
+        mm_patterns: List[str] = []
+
+        mu = np.zeros(len(self.mu_pids), MU_REC)
+        self.mu_clock: List[float] = []
+        for r, pid in enumerate(self.mu_pids):
+            p = P[pid]
+            rec = mu[r]
+            rec["proto_index"] = self.pids.index(pid)
+            ca = p.get("clockabs", 1)
+            try:
+                clock = float(ca)
+            except (ValueError, TypeError):
+                raise NotImplementedError(f"MU {pid}: clockabs {ca!r} not numeric")
+            if clock == 0:
+                raise NotImplementedError(f"MU {pid}: clockabs 0 (ZeroDivisionError path not modelled)")
+            rec["clock"] = clock
+            self.mu_clock.append(clock)
+            rec["active"] = 1 if p.get("active", True) else 0
+            sp = p.get("start")
+            if sp and isinstance(sp, list):
+                fl = self._float_list(sp)
+                if fl is None:
+                    raise NotImplementedError(f"MU {pid}: non-numeric start raises ValueError (not modelled)")
+                rec["has_start"] = 1
+                self._patspec(rec["start"], fl, f"MU {pid} start")
+            never = False
+            nkeys = 0
+            for key, field in (("one", "one"), ("zero", "zero"), ("float", "flt")):
+                spec = p.get(key)
+                if not spec:
+                    continue
+                fl = self._float_list(spec)
+                if fl is None:
+                    never = True   # match_failed -> protocol skipped (message_unsynced.py:105-109)
+                    break
+                if not fl:
+                    never = True
+                    break
+                self._patspec(rec[field], fl, f"MU {pid} {key}")
+                nkeys += 1
+            lens = {int(rec[f]["len"]) for f in ("one", "zero", "flt") if rec[f]["len"]}
+            if len(lens) > 1:
+                raise NotImplementedError(f"MU {pid}: one/zero/float of different lengths")
+            rec["never"] = 1 if (never or nkeys == 0 or not p.get("one")) else 0
+            rec["length_min"] = _int_exact(p.get("length_min", 0), f"MU {pid} length_min")
+            lm = p.get("length_max", None)
+            rec["length_max"] = _int_exact(lm, f"MU {pid} length_max") if lm else INT_NONE
+            one = p.get("one")
+            rec["width"] = len(one) if one else 0
+            if one and lens and rec["width"] != next(iter(lens)):
+                raise NotImplementedError(f"MU {pid}: len(one) differs from unit length")
+            rec["recon"] = 1 if p.get("reconstructBit") else 0
+            rec["dispatch_bin"] = 1 if _int_exact(p.get("dispatchBin", 0), "dispatchBin") == 1 else 0
+            pad = _int_exact(p.get("paddingbits", 4), f"MU {pid} paddingbits")
+            if pad < 1:
+                raise NotImplementedError(f"MU {pid}: paddingbits < 1")
+            rec["pad_bits"] = pad
+            rec["remove_zero"] = 1 if p.get("remove_zero", 0) else 0
+            rec["postdemo"] = self._postdemo(p)
+            rec["pre_off"], rec["pre_len"] = self._str(f"{p.get('preamble', '')}")
+            rec["post_off"], rec["post_len"] = self._str(f"{p.get('postamble', '')}")
+            mm = p.get("modulematch")
+            if mm:
+                if mm not in mm_patterns:
+                    mm_patterns.append(mm)
+                rec["mm_dfa"] = mm_patterns.index(mm)
+            else:
+                rec["mm_dfa"] = -1
+
+        ms = np.zeros(len(self.ms_pids), MS_REC)
+        for r, pid in enumerate(self.ms_pids):
+            p = P[pid]
+            rec = ms[r]
+            rec["proto_index"] = self.pids.index(pid)
+            try:
+                rec["pclock"] = float(p.get("clockabs", 0))
+            except (ValueError, TypeError):
+                raise NotImplementedError(f"MS {pid}: clockabs not numeric (raises in reference)")
+            one = p.get("one")
+            width = len(one) if one else 0
+            rec["width"] = width
+            never = False
+            for k, key in enumerate(("sync", "one", "zero", "float")):
+                spec = p.get(key)
+                if not spec:
+                    continue
+                fl = self._float_list(spec)
+                if fl is None or not fl:
+                    never = True  # match_failed (message_synced.py:114-118)
+                    break
+                self._patspec(rec["key"][k], fl, f"MS {pid} {key}")
+            lmin_raw = p.get("length_min", -1)
+            if not never:
+                rec["lmin_sync"] = _int_exact(lmin_raw, f"MS {pid} length_min")
+                if width == 0 and rec["key"][0]["len"]:
+                    # bit_length is 0 -> the gate fails for any length_min > 0
+                    if rec["lmin_sync"] > 0:
+                        never = True
+                    else:
+                        raise NotImplementedError(f"MS {pid}: zero signal width reaches range(..., 0)")
+                if not rec["key"][0]["len"]:
+                    raise NotImplementedError(f"MS {pid}: falsy sync not modelled")
+            rec["never"] = 1 if never else 0
+            rec["lir_min"] = _int_exact(lmin_raw, f"MS {pid} length_min") if not never else -1
+            lm = p.get("length_max")
+            rec["lir_max"] = _int_exact(lm, f"MS {pid} length_max") if (lm is not None and not never) else INT_NONE
+            rec["recon"] = 1 if p.get("reconstructBit") else 0
+            pad = _int_exact(p.get("paddingbits", 4), f"MS {pid} paddingbits")
+            if pad < 1:
+                raise NotImplementedError(f"MS {pid}: paddingbits < 1")
+            rec["pad_bits"] = pad
+            rec["postdemo"] = self._postdemo(p)
+            rec["pre_off"], rec["pre_len"] = self._str(f"{p.get('preamble', '')}")
+            rec["post_off"], rec["post_len"] = self._str(f"{p.get('postamble', '')}")
+
+        mc = np.zeros(len(self.mc_pids), MC_REC)
+        self.mc_preamble: List[str] = []
+        for r, pid in enumerate(self.mc_pids):
+            p = P[pid]
+            rec = mc[r]
+            rec["proto_index"] = self.pids.index(pid)
+            cr = p["clockrange"]
+            if not (isinstance(cr, list) and len(cr) >= 2):
+                raise NotImplementedError(f"MC {pid}: clockrange {cr!r}")
+            rec["has_cr"] = 1
+            rec["cr_lo"], rec["cr_hi"] = float(cr[0]), float(cr[1])
+            meth = str(p.get("method", "")).split(".")[-1]
+            if meth not in MC_METHODS:
+                raise NotImplementedError(f"MC {pid}: method {meth!r} not on the device")
+            rec["method"] = MC_METHODS[meth]
+            if "length_min" in p:
+                rec["has_lmin"] = 1
+                rec["lmin"] = _int_exact(p["length_min"], f"MC {pid} length_min")
+            if "length_max" in p and p["length_max"] is not None:
+                rec["has_lmax"] = 1
+                rec["lmax"] = _int_exact(p["length_max"], f"MC {pid} length_max")
+                rec["lmax_is_str"] = 1 if isinstance(p["length_max"], str) else 0
+            rec["invert"] = 1 if p.get("polarity", "") == "invert" else 0
+            try:
+                rec["pid_num"] = int(pid)
+            except ValueError:
+                rec["pid_num"] = -1
+            pre = f"{p.get('preamble', '')}"
+            self.mc_preamble.append(pre)
+            rec["pre_off"], rec["pre_len"] = self._str(pre)
+
+        if b"\n" in bytes(self._heap):
+            raise NotImplementedError("newline inside a preamble/postamble ($ semantics)")
+        cls_of, n_class, dfas = regex_dfa.compile_bank_dfas(mm_patterns)
+        for r, pid in enumerate(self.mu_pids):
+            d = int(mu[r]["mm_dfa"])
+            if d >= 0:
+                pre = f"{P[pid].get('preamble', '')}".encode("latin-1")
+                mu[r]["mm_pre_state"] = regex_dfa.dfa_walk(dfas[d], cls_of, dfas[d][1], pre)
+        self.mm_patterns = mm_patterns
+        self.dfa_host = (cls_of, dfas)
+        drec = np.zeros(len(dfas), DFA_REC)
+        trans_parts, flag_parts = [], []
+        toff = foff = 0
+        for i, (nst, start, trans, flags) in enumerate(dfas):
+            drec[i] = (nst, start, toff, foff)
+            t = np.asarray(trans, dtype=np.uint16).reshape(-1)
+            trans_parts.append(t)
+            flag_parts.append(np.asarray(flags, dtype=np.uint8))
+            toff += t.size
+            foff += len(flags)
+        trans_all = np.concatenate(trans_parts) if trans_parts else np.zeros(0, np.uint16)
+        flags_all = np.concatenate(flag_parts) if flag_parts else np.zeros(0, np.uint8)
+        cls_arr = np.asarray(cls_of, dtype=np.uint8)
+
+        # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings   (16-B aligned sections)
+        hdr_size = struct.calcsize(HDR_FMT)
+        sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
+                    trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap)]
+        offs = []
+        cur = (hdr_size + 15) // 16 * 16
+        for s in sections:
+            offs.append(cur)
+            cur = (cur + len(s) + 15) // 16 * 16
+        total = cur
+        blob = bytearray(total)
+        hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
+                          len(self.mc_pids), len(dfas), n_class, *offs, total, 0, 0, 0)
+        blob[:hdr_size] = hdr
+        for o, s in zip(offs, sections):
+            blob[o:o + len(s)] = s
+        self.blob = bytes(blob)
+        self.mu_table, self.ms_table, self.mc_table = mu, ms, mc
+
+    # -- host-side metadata used when turning device records into reference dicts -------------
+    def class_pid(self, kind: str, rec_index: int) -> str:
+        return {"MU": self.mu_pids, "MS": self.ms_pids, "MC": self.mc_pids}[kind][rec_index]

@@ -1,0 +1,32 @@
+"""Build libsdx.so (hand-written HIP for gfx950) in-tree:  python -m pysignalduino_amd.build"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "sdx_kernels.hip")
+OUT = os.path.join(HERE, "_lib", "libsdx.so")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    deps = [SRC, os.path.join(HERE, "csrc", "sdx_device.h"),
+            os.path.join(os.path.dirname(HERE), "include", "sdx.h"),
+            os.path.join(os.path.dirname(HERE), "include", "sdx_bank.h")]
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+        return OUT
+    cmd = [HIPCC, *FLAGS, SRC, "-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

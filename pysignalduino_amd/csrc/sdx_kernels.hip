@@ -1,0 +1,1304 @@
+// sdx_kernels.hip -- MI355X (gfx950) kernels of the batched SIGNALduino demodulator.
+//
+// MU / MS engine (k_pulses): one 256-thread workgroup per tile of TM messages.
+//   stage    : the tile's pulse strings are read coalesced from HBM once and turned into
+//              per-id position bitmaps in LDS (10 ballots per 64 characters).
+//   filter   : lane = message, the 4 waves split the class table (bank order) into
+//              contiguous quarters; every protocol is wave-uniform, so the bank record is
+//              read with scalar loads and the loop structure is uniform.  A lane runs
+//              the reference's candidate gates (clock gate, pattern_exists for
+//              start/sync/one/zero/float) for its message.
+//   decode   : each surviving (message x protocol) pair is decoded by the WHOLE wave
+//              (one wavefront per candidate pair): unit bitmaps, stride streams built with
+//              ballots, an exact re.finditer emulation, lane-parallel chunk->bit mapping,
+//              postDemodulation, padding, hex, modulematch DFA, staged in LDS.
+//   flush    : results are written in reference order (message, bank order, match order)
+//              with one global atomic per tile for the record/heap space.
+// MC engine (k_mc): lane = frame, the 12 clockrange protocols are a uniform loop.
+#include "sdx_device.h"
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+namespace sdx {
+
+constexpr int REC_CAP = 160;   // staged results per wave per tile
+constexpr int HEAP_CAP = 4096; // staged payload bytes per wave per tile
+
+struct StageRec {
+  uint32_t off;
+  uint16_t len, proto;
+  uint32_t bitlen;
+  uint16_t msg, rank;
+};
+
+template <int NW, int TM>
+struct TileLds {
+  static constexpr int WS = NW;              // words per id bitmap
+  static constexpr int MSTRIDE = 10 * NW + 1;  // odd stride: fewer LDS bank conflicts across lanes
+  static constexpr int NBITS = 64 * NW + 64;
+  struct Wave {
+    uint64_t umask[3][NW];
+    uint64_t uany[NW];
+    uint64_t smask[NW];
+    uint64_t stream[NW + 18];
+    uint8_t bits[NBITS];
+    uint8_t bits2[NBITS];
+    StageRec rec[REC_CAP];
+    uint8_t heap[HEAP_CAP];
+    int nrec, nheap, ovf;
+  };
+  uint64_t bm[TM * MSTRIDE];
+  int32_t nlen[TM];
+  uint32_t raise_key[TM];
+  uint32_t digit_ok[TM];
+  uint16_t cnt[4][TM];
+  uint32_t rec_base, heap_base, tile_bad;
+  uint32_t wheap_pre[4];
+  uint32_t mbase[TM];
+  Wave w[4];
+};
+
+SDX_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+SDX_DEV int lanes_below(uint64_t mask) {
+  const int l = lane_id();
+  return popc64(l ? (mask & ((1ull << l) - 1)) : 0ull);
+}
+
+// ---------------------------------------------------------------------------------------------
+// staged-result helpers (wave-uniform callers)
+// ---------------------------------------------------------------------------------------------
+template <class W>
+SDX_DEV bool stage_reserve(W& wv, int total) {
+  if (wv.nrec >= REC_CAP || wv.nheap + total > HEAP_CAP) {
+    wv.ovf = 1;
+    return false;
+  }
+  return true;
+}
+
+template <class T>
+SDX_DEV void stage_commit(T& L, typename T::Wave& wv, int wave, int msg_local, int proto, int total, int bitlen) {
+  if (lane_id() == 0) {
+    StageRec r;
+    r.off = (uint32_t)wv.nheap;
+    r.len = (uint16_t)total;
+    r.proto = (uint16_t)proto;
+    r.bitlen = (uint32_t)bitlen;
+    r.msg = (uint16_t)msg_local;
+    r.rank = L.cnt[wave][msg_local];
+    wv.rec[wv.nrec] = r;
+    L.cnt[wave][msg_local] = (uint16_t)(r.rank + 1);
+    wv.nrec = wv.nrec + 1;
+    wv.nheap = wv.nheap + total;
+  }
+  wave_sync();
+}
+
+// copy a bank string to LDS (lanes in parallel)
+SDX_DEV void copy_str(uint8_t* dst, const uint8_t* src, int n) {
+  for (int i = lane_id(); i < n; i += WAVE) dst[i] = src[i];
+}
+
+// bits[0..nb) (values 0/1/2='F') -> dmsg bytes at dst; returns length, or -1 for the 'None'
+// (bin_str_2_hex_str -> None, helpers.py:44-45) case.  Wave-cooperative.
+SDX_DEV int any_float(const uint8_t* bits, int nb) {
+  bool f = false;
+  for (int i = lane_id(); i < nb; i += WAVE) f |= bits[i] == 2;
+  return ballot(f) != 0;
+}
+
+// helpers.py:28-64: nibbles from the right, leading partial nibble kept, uppercase
+SDX_DEV int hex_digits(const uint8_t* bits, int nb, uint8_t* dst, int strip_zero) {
+  const int nd = (nb + 3) >> 2;
+  // digit d (from the left) covers bits [e-4, e) with e = nb - 4*(nd-1-d), clipped at 0
+  int skip = 0;
+  if (strip_zero) {  // str.lstrip('0')
+    skip = nd;
+    for (int d0 = 0; d0 < nd; d0 += WAVE) {
+      const int d = d0 + lane_id();
+      int v = 0;
+      if (d < nd) {
+        const int e = nb - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+        for (int i = a; i < e; ++i) v = (v << 1) | bits[i];
+      }
+      const uint64_t nz = ballot(d < nd && v != 0);
+      if (nz) {
+        skip = d0 + ffs64(nz);
+        break;
+      }
+    }
+  }
+  for (int d = skip + lane_id(); d < nd; d += WAVE) {
+    const int e = nb - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+    int v = 0;
+    for (int i = a; i < e; ++i) v = (v << 1) | bits[i];
+    dst[d - skip] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+  }
+  return nd - skip;
+}
+
+template <class T>
+SDX_DEV void raise_msg(T& L, int msg_local, int proto, int kind) {
+  if (lane_id() == 0) atomicMin(&L.raise_key[msg_local], ((uint32_t)proto << 8) | (uint32_t)kind);
+  wave_sync();
+}
+
+// ---------------------------------------------------------------------------------------------
+// MU: finish one match (message_unsynced.py:230-290)
+// ---------------------------------------------------------------------------------------------
+template <int NW, int TM>
+SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
+                       int nb) {
+  auto& W = L.w[wave];
+  uint8_t* buf = W.bits;
+  // postDemodulation (:231-250): 'F' -> int() ValueError caught -> bits unchanged
+  if (rec->postdemo != SDX_PD_NONE && !any_float(buf, nb)) {
+    int rc = 0, no = 0;
+    if (lane_id() == 0) rc = run_postdemo(rec->postdemo, buf, nb, W.bits2, &no);
+    rc = bcast_i(rc, 0);
+    no = bcast_i(no, 0);
+    wave_sync();
+    if (rc == 0) return;  // rcode < 1 -> match dropped
+    if (rc == 1) {
+      buf = W.bits2;
+      nb = no;
+    }  // rc == -1: ValueError inside the method, caught -> bits unchanged
+  }
+  // padding (:257-259), after postDemod
+  const int pad = rec->pad_bits;
+  int nbp = nb;
+  while (nbp % pad) ++nbp;
+  for (int i = nb + lane_id(); i < nbp; i += WAVE) buf[i] = 0;
+  wave_sync();
+  const bool isf = any_float(buf, nbp);
+  int dlen;
+  if (rec->dispatch_bin) dlen = nbp;
+  else if (isf) {
+    if (rec->remove_zero) {  // None.lstrip('0') -> AttributeError (:269)
+      raise_msg(L, s, p, SDX_RAISE_ATTRIBUTE);
+      return;
+    }
+    dlen = 4;  // f"{None}"
+  } else {
+    dlen = -2;  // computed below
+  }
+  // stage payload = preamble + dmsg + postamble
+  if (!stage_reserve(W, rec->pre_len + (dlen >= 0 ? dlen : (nbp + 3) / 4) + rec->post_len)) return;
+  uint8_t* dst = W.heap + W.nheap;
+  copy_str(dst, bv.str + rec->pre_off, rec->pre_len);
+  uint8_t* dm = dst + rec->pre_len;
+  if (rec->dispatch_bin) {
+    for (int i = lane_id(); i < nbp; i += WAVE) dm[i] = buf[i] == 2 ? 'F' : (uint8_t)('0' + buf[i]);
+  } else if (isf) {
+    if (lane_id() == 0) { dm[0] = 'N'; dm[1] = 'o'; dm[2] = 'n'; dm[3] = 'e'; }
+  } else {
+    dlen = hex_digits(buf, nbp, dm, rec->remove_zero);
+  }
+  wave_sync();
+  copy_str(dm + dlen, bv.str + rec->post_off, rec->post_len);
+  wave_sync();
+  const int total = rec->pre_len + dlen + rec->post_len;
+  if (rec->mm_dfa >= 0) {  // re.search(modulematch, payload) (:277-280)
+    int ok = 0;
+    if (lane_id() == 0) ok = dfa_accepts(bv, rec->mm_dfa, rec->mm_pre_state, dm, dlen + rec->post_len);
+    ok = bcast_i(ok, 0);
+    if (!ok) return;
+  }
+  stage_commit(L, W, wave, s, p, total, nbp);
+}
+
+// ---------------------------------------------------------------------------------------------
+// MU: decode one surviving (message, protocol) pair with the whole wave
+// (message_unsynced.py:146-290; re.finditer emulated exactly)
+// ---------------------------------------------------------------------------------------------
+template <int NW, int TM>
+SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
+                       int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1, uint64_t ut2, int fmask) {
+  using T = TileLds<NW, TM>;
+  auto& W = L.w[wave];
+  const int lane = lane_id();
+  const uint64_t* bm = &L.bm[s * T::MSTRIDE];
+  const int n = L.nlen[s], nw = (n + 63) >> 6;
+  const int Lw = rec->width;
+  const int lenS = rec->has_start ? (int)rec->start.len : 0;
+  const uint64_t ut[3] = {ut0, ut1, ut2};
+  const uint8_t SYM[3] = {1, 0, 2};
+  // pattern_lookup: distinct unit strings, value = last writer (:122)
+  uint64_t uni[3] = {0, 0, 0};
+  uint8_t usym[3] = {0, 0, 0};
+  int nu = 0;
+  for (int k = 0; k < 3; ++k) {
+    if (!((fmask >> k) & 1)) continue;
+    int j = 0;
+    for (; j < nu; ++j)
+      if (uni[j] == ut[k]) break;
+    if (j == nu) uni[nu++] = ut[k];
+    usym[j] = SYM[k];
+  }
+  // end_pattern_lookup: pstr[:-1], first writer wins (:124-127); regex tail only with reconstructBit
+  uint64_t ek[3] = {0, 0, 0};
+  uint8_t esym[3] = {0, 0, 0};
+  int ne = 0;
+  if (rec->recon && Lw > 1) {
+    const uint64_t msk = (Lw - 1 >= 16) ? ~0ull : ((1ull << (4 * (Lw - 1))) - 1);
+    for (int k = 0; k < 3; ++k) {
+      if (!((fmask >> k) & 1)) continue;
+      const uint64_t key = ut[k] & msk;
+      int j = 0;
+      for (; j < ne; ++j)
+        if (ek[j] == key) break;
+      if (j == ne) {
+        ek[ne] = key;
+        esym[ne] = SYM[k];
+        ++ne;
+      }
+    }
+  }
+  // unit / start position bitmaps
+  if (lane < nw) {
+    uint64_t any = 0;
+    for (int j = 0; j < nu; ++j) {
+      uint64_t m = ~0ull;
+      for (int i = 0; i < Lw; ++i) {
+        const int id = (int)((uni[j] >> (4 * i)) & 15), wo = lane + (i >> 6);
+        m &= (wo < nw) ? bm_window(bm + id * T::WS, wo, i & 63, nw) : 0ull;
+      }
+      W.umask[j][lane] = m;
+      any |= m;
+    }
+    W.uany[lane] = any;
+    uint64_t sm = ~0ull;
+    for (int i = 0; i < lenS; ++i) {
+      const int id = (int)((st_tgt >> (4 * i)) & 15), wo = lane + (i >> 6);
+      sm &= (wo < nw) ? bm_window(bm + id * T::WS, wo, i & 63, nw) : 0ull;
+    }
+    W.smask[lane] = sm;
+  }
+  wave_sync();
+  // stride streams: stream r, bit i = a unit starts at position r + i*Lw
+  const int nunits = (n + Lw - 1) / Lw;
+  const int sw = (nunits + 63) >> 6;
+  for (int r = 0; r < Lw; ++r) {
+    for (int c = 0; c < sw; ++c) {
+      const int x = r + (c * 64 + lane) * Lw;
+      const bool b = x < n && ((W.uany[x >> 6] >> (x & 63)) & 1ull);
+      const uint64_t bb = ballot(b);
+      if (lane == 0) W.stream[r * sw + c] = bb;
+    }
+  }
+  wave_sync();
+  auto runlen = [&](int q) -> int {
+    const int r = q % Lw, i = q / Lw;
+    const uint64_t* S = W.stream + r * sw;
+    int k = 0;
+    for (int w = i >> 6, b = i & 63; w < sw; ++w, b = 0) {
+      const uint64_t x = S[w] >> b;
+      const uint64_t inv = ~x;
+      const int t = inv ? ffs64(inv) : 64;
+      k += t;
+      if (t < 64 - b) break;
+    }
+    return k;
+  };
+  const int lmin = rec->length_min;
+  int pos = idx;
+  while (true) {
+    // first s >= pos where START occurs and >= length_min units follow
+    int sfound = -1, kfound = 0;
+    const int last = n - lenS;
+    for (int c = pos >> 6; c <= (last >> 6); ++c) {
+      const int sx = c * 64 + lane;
+      bool cand = sx >= pos && sx <= last;
+      if (cand && lenS > 0) cand = (W.smask[sx >> 6] >> (sx & 63)) & 1ull;
+      const int k = cand ? runlen(sx + lenS) : 0;
+      const uint64_t bb = ballot(cand && k >= lmin);
+      if (bb) {
+        const int l = ffs64(bb);
+        sfound = c * 64 + l;
+        kfound = bcast_i(k, l);
+        break;
+      }
+    }
+    if (sfound < 0) break;
+    const int q = sfound + lenS, e0 = q + kfound * Lw;
+    int em = -1;
+    for (int j = 0; j < ne; ++j)
+      if (match_at(bm, T::WS, n, ek[j], Lw - 1, e0)) {
+        em = j;
+        break;
+      }
+    const int G = kfound * Lw + (em >= 0 ? Lw - 1 : 0);
+    if (G == 0) {  // chunks == [] -> chunks[-1] IndexError (:212): the whole message raises
+      raise_msg(L, s, p, SDX_RAISE_INDEX);
+      return;
+    }
+    pos = q + G;
+    const int nchunks = kfound + (em >= 0 ? 1 : 0);
+    if (nchunks > rec->length_max) continue;  // (:217-218)
+    for (int i = lane; i < kfound; i += WAVE) {
+      const int x = q + i * Lw;
+      uint8_t sy = 0;
+      for (int j = 0; j < nu; ++j)
+        if ((W.umask[j][x >> 6] >> (x & 63)) & 1ull) sy = usym[j];
+      W.bits[i] = sy;
+    }
+    if (em >= 0 && lane == 0) W.bits[kfound] = esym[em];
+    wave_sync();
+    finish_mu(L, wave, bv, rec, p, s, nchunks);
+    if ((L.raise_key[s] >> 8) <= (uint32_t)p) return;  // this protocol made the message raise
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MS: finish (message_synced.py:191-241)
+// ---------------------------------------------------------------------------------------------
+template <int NW, int TM>
+SDX_DEV void finish_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
+                       int nb) {
+  auto& W = L.w[wave];
+  uint8_t* buf = W.bits;
+  if (nb == 0) return;                                      // (:191-192)
+  if (rec->lir_min != -1 && nb < rec->lir_min) return;      // length_in_range (:194-196)
+  if (nb > rec->lir_max) return;
+  int nbp = nb;                                             // padding BEFORE postDemod (:198-200)
+  while (nbp % rec->pad_bits) ++nbp;
+  for (int i = nb + lane_id(); i < nbp; i += WAVE) buf[i] = 0;
+  wave_sync();
+  nb = nbp;
+  if (rec->postdemo != SDX_PD_NONE) {                       // no try: 'F' -> ValueError (:209)
+    if (any_float(buf, nb)) {
+      raise_msg(L, s, p, SDX_RAISE_VALUE);
+      return;
+    }
+    int rc = 0, no = 0;
+    if (lane_id() == 0) rc = run_postdemo(rec->postdemo, buf, nb, W.bits2, &no);
+    rc = bcast_i(rc, 0);
+    no = bcast_i(no, 0);
+    wave_sync();
+    if (rc == -1) {
+      raise_msg(L, s, p, SDX_RAISE_VALUE);
+      return;
+    }
+    if (rc == 0) return;
+    if (no > 0) {
+      buf = W.bits2;
+      nb = no;
+    }
+  }
+  if (any_float(buf, nb)) return;  // bin_str_2_hex_str -> None -> skipped (:224-226)
+  const int dl = (nb + 3) / 4;
+  if (!stage_reserve(W, rec->pre_len + dl + rec->post_len)) return;
+  uint8_t* dst = W.heap + W.nheap;
+  copy_str(dst, bv.str + rec->pre_off, rec->pre_len);
+  hex_digits(buf, nb, dst + rec->pre_len, 0);
+  copy_str(dst + rec->pre_len + dl, bv.str + rec->post_off, rec->post_len);
+  wave_sync();
+  stage_commit(L, W, wave, s, p, rec->pre_len + dl + rec->post_len, nb);
+}
+
+// MS decode loop (:172-189) for one surviving pair, wave-cooperative over chunks
+template <int NW, int TM>
+SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
+                       int start, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3, int fmask) {
+  using T = TileLds<NW, TM>;
+  auto& W = L.w[wave];
+  const int lane = lane_id();
+  const uint64_t* bm = &L.bm[s * T::MSTRIDE];
+  const int n = L.nlen[s];
+  const int Wd = rec->width;
+  const uint64_t kt[4] = {k0, k1, k2, k3};
+  const int klen[4] = {rec->key[0].len, rec->key[1].len, rec->key[2].len, rec->key[3].len};
+  const uint8_t KSYM[4] = {3, 1, 0, 2};  // 3 = '' (sync: no bit)
+  // pattern_lookup with dict semantics: distinct (string) keys, value = last writer
+  uint64_t kk[4];
+  int kl[4];
+  uint8_t ks[4];
+  int nk = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (!((fmask >> k) & 1)) continue;
+    int j = 0;
+    for (; j < nk; ++j)
+      if (kk[j] == kt[k] && kl[j] == klen[k]) break;
+    if (j == nk) {
+      kk[nk] = kt[k];
+      kl[nk] = klen[k];
+      ++nk;
+    }
+    ks[j] = KSYM[k];
+  }
+  // end_pattern_lookup: reset after sync, then one/zero/float pstr[:-1], first wins
+  uint64_t ek[3];
+  uint8_t es[3];
+  int ne = 0;
+  const int el = Wd - 1;
+  const uint64_t emsk = (el >= 16) ? ~0ull : ((1ull << (4 * el)) - 1);
+  for (int k = 1; k < 4; ++k) {
+    if (!((fmask >> k) & 1) || klen[k] < 1) continue;
+    const uint64_t key = kt[k] & emsk;
+    const int kel = klen[k] - 1;
+    if (kel != el) continue;  // unit lengths equal the width in every modelled bank
+    int j = 0;
+    for (; j < ne; ++j)
+      if (ek[j] == key) break;
+    if (j == ne) {
+      ek[ne] = key;
+      es[ne] = KSYM[k];
+      ++ne;
+    }
+  }
+  const bool recon = rec->recon != 0;
+  const int nch = (start < n) ? (n - start + Wd - 1) / Wd : 0;
+  int nb = 0;
+  for (int c0 = 0; c0 < nch; c0 += WAVE) {
+    const int i = c0 + lane;
+    const bool valid = i < nch;
+    int cls = -1;  // -1 break, 0..2 bit, 3 skip
+    if (valid) {
+      const int x = start + i * Wd;
+      const int cl = (n - x < Wd) ? n - x : Wd;
+      for (int j = 0; j < nk && cls < 0; ++j)
+        if (kl[j] == cl && match_at(bm, T::WS, n, kk[j], cl, x)) cls = ks[j];
+      if (cls < 0 && recon) {
+        const int tl = (cl == Wd) ? cl - 1 : cl;  // chunk[:-1] if full else chunk
+        if (tl == el)
+          for (int j = 0; j < ne && cls < 0; ++j)
+            if (match_at(bm, T::WS, n, ek[j], el, x)) cls = es[j];
+      }
+    }
+    const uint64_t brk = ballot(valid && cls < 0);
+    const int lim = brk ? ffs64(brk) : WAVE;
+    const bool emit = valid && lane < lim && cls >= 0 && cls != 3;
+    const uint64_t em = ballot(emit);
+    if (emit) W.bits[nb + lanes_below(em)] = (uint8_t)cls;
+    nb += popc64(em);
+    if (brk) break;
+  }
+  wave_sync();
+  finish_ms(L, wave, bv, rec, p, s, nb);
+}
+
+// ---------------------------------------------------------------------------------------------
+// tile flush: records in (message, protocol, match) order, one atomic per tile
+// ---------------------------------------------------------------------------------------------
+template <int NW, int TM>
+SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid == 0) {
+    int bad = 0;
+    for (int w = 0; w < 4; ++w) bad |= L.w[w].ovf;
+    L.tile_bad = bad;
+    uint32_t nrec = 0, nheap = 0;
+    for (int m = 0; m < nvalid; ++m) {
+      L.mbase[m] = nrec;
+      if (L.raise_key[m] == 0xFFFFFFFFu && !bad)
+        for (int w = 0; w < 4; ++w) nrec += L.cnt[w][m];
+    }
+    for (int w = 0; w < 4; ++w) {
+      L.wheap_pre[w] = nheap;
+      nheap += L.w[w].nheap;
+    }
+    uint32_t rb = 0, hb = 0;
+    if (!bad) {
+      rb = atomicAdd(&out.cursor_dev[0], nrec);
+      hb = atomicAdd(&out.cursor_dev[1], nheap);
+      if (rb + nrec > out.rec_cap || hb + nheap > out.heap_cap) {
+        bad = 2;
+        atomicOr(&out.cursor_dev[2], 1u);
+      }
+    } else {
+      atomicOr(&out.cursor_dev[2], 2u);
+    }
+    L.tile_bad = bad;
+    L.rec_base = rb;
+    L.heap_base = hb;
+  }
+  __syncthreads();
+  const int bad = L.tile_bad;
+  if (!bad) {
+    auto& W = L.w[wave];
+    for (int r = lane; r < W.nrec; r += WAVE) {
+      const StageRec sr = W.rec[r];
+      if (L.raise_key[sr.msg] != 0xFFFFFFFFu) continue;
+      uint32_t before = 0;
+      for (int w = 0; w < wave; ++w) before += L.cnt[w][sr.msg];
+      const uint32_t dst = L.rec_base + L.mbase[sr.msg] + before + sr.rank;
+      sdx_result o;
+      o.payload_off = L.heap_base + L.wheap_pre[wave] + sr.off;
+      o.payload_len = sr.len;
+      o.proto = sr.proto;
+      o.bit_length = sr.bitlen;
+      o.msg = (uint32_t)msg_of[sr.msg];
+      out.rec_dev[dst] = o;
+    }
+    uint8_t* hd = out.heap_dev + L.heap_base + L.wheap_pre[wave];
+    for (int i = lane; i < W.nheap; i += WAVE) hd[i] = W.heap[i];
+  }
+  for (int m = tid; m < nvalid; m += blockDim.x) {
+    sdx_desc d;
+    d.rec_begin = L.rec_base + L.mbase[m];
+    uint32_t nr = 0;
+    for (int w = 0; w < 4; ++w) nr += L.cnt[w][m];
+    const uint32_t rk = L.raise_key[m];
+    if (rk != 0xFFFFFFFFu) {
+      d.status = SDX_ST_RAISED;
+      d.raise_kind = (uint8_t)(rk & 0xFF);
+      d.n_rec = 0;
+    } else if (bad) {
+      d.status = bad == 2 ? SDX_ST_OVF_OUT : SDX_ST_OVF_TILE;
+      d.raise_kind = 0;
+      d.n_rec = 0;
+    } else {
+      d.status = SDX_ST_OK;
+      d.raise_kind = 0;
+      d.n_rec = (uint16_t)nr;
+    }
+    out.desc_dev[msg_of[m]] = d;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MU / MS tile kernel
+// ---------------------------------------------------------------------------------------------
+template <int KIND, int NW, int TM>
+__global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
+  using T = TileLds<NW, TM>;
+  __shared__ T L;
+  const BankView bv = bank_view(bank);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int tile0 = blockIdx.x * TM;
+  const int nvalid = (ntot - tile0 < TM) ? ntot - tile0 : TM;
+  __shared__ int msg_of[TM];
+  if (tid < TM) {
+    msg_of[tid] = (tid < nvalid) ? (b.sel_dev ? b.sel_dev[tile0 + tid] : tile0 + tid) : 0;
+    L.raise_key[tid] = 0xFFFFFFFFu;
+    for (int w = 0; w < 4; ++w) L.cnt[w][tid] = 0;
+  }
+  if (lane == 0) {
+    L.w[wave].nrec = 0;
+    L.w[wave].nheap = 0;
+    L.w[wave].ovf = 0;
+  }
+  __syncthreads();
+  // ---- stage: per-id position bitmaps (coalesced 64-character rows, 10 ballots each)
+  for (int mi = wave; mi < nvalid; mi += 4) {
+    const int msg = msg_of[mi];
+    const int64_t off = b.offsets_dev[msg];
+    int n = (int)(b.offsets_dev[msg + 1] - off);
+    if (n > 64 * NW) n = 64 * NW;  // host routes longer messages to the long variant
+    bool nondigit = false;
+    for (int w = 0; w < NW; ++w) {
+      const int pos = w * 64 + lane;
+      const uint8_t c = pos < n ? b.data_dev[off + pos] : (uint8_t)0xFF;
+      nondigit |= pos < n && !((c >= '0' && c <= '9') || c == 0xFE);
+      uint64_t mine = 0;
+#pragma unroll
+      for (int id = 0; id < 10; ++id) {
+        const uint64_t bb = ballot(c == (uint8_t)('0' + id));
+        if (lane == id) mine = bb;
+      }
+      if (lane < 10) L.bm[mi * T::MSTRIDE + lane * T::WS + w] = mine;
+    }
+    const uint64_t nd = ballot(nondigit);
+    if (lane == 0) {
+      L.nlen[mi] = n;
+      L.digit_ok[mi] = (nd == 0 && n > 0) ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  // ---- per-lane message state (lane = message of the tile)
+  const int mi = lane;
+  const bool mvalid = mi < nvalid;
+  int npat = 0, n = 0;
+  uint64_t ids = 0;
+  double val[SDX_MAXPAT], norm[SDX_MAXPAT];
+#pragma unroll
+  for (int k = 0; k < SDX_MAXPAT; ++k) val[k] = norm[k] = 0.0;
+  bool lane_ok = false;
+  if (mvalid) {
+    const int msg = msg_of[mi];
+    npat = b.npat_dev[msg];
+    if (npat > SDX_MAXPAT) npat = SDX_MAXPAT;
+#pragma unroll
+    for (int k = 0; k < SDX_MAXPAT; ++k) {
+      if (k < npat) {
+        ids |= (uint64_t)((b.pat_id_dev[msg * SDX_MAXPAT + k] - '0') & 15) << (4 * k);
+        val[k] = b.pat_val_dev[msg * SDX_MAXPAT + k];
+      }
+    }
+    n = L.nlen[mi];
+    lane_ok = n > 0;  // empty D -> [] (message_unsynced.py:22-25 / message_synced.py:23-25)
+  }
+  const uint64_t* bmine = &L.bm[(mvalid ? mi : 0) * T::MSTRIDE];
+  const int nw = (n + 63) >> 6;
+  double clock = 0.0;
+  if (KIND == SDX_KIND_MS && mvalid) {
+    // gates (message_synced.py:21-66): data.isdigit(), CP/SP/R string checks, CP in patterns, clock != 0
+    const int msg = msg_of[mi];
+    const int cp = b.cp_slot_dev[msg];
+    lane_ok = lane_ok && L.digit_ok[mi] && b.ms_ok_dev[msg] && cp >= 0 && cp < npat;
+#pragma unroll
+    for (int k = 0; k < SDX_MAXPAT; ++k)
+      if (k == cp) clock = fabs(val[k]);
+    lane_ok = lane_ok && clock != 0.0;
+    if (lane_ok) {
+#pragma unroll
+      for (int k = 0; k < SDX_MAXPAT; ++k)
+        if (k < npat) norm[k] = py_round1(val[k] / clock);
+    }
+  }
+  // ---- protocol loop: this wave's contiguous quarter of the class table
+  const int nproto = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu : (int)bv.hdr->n_ms;
+  const int qn = (nproto + 3) / 4;
+  const int p0 = wave * qn, p1 = (p0 + qn < nproto) ? p0 + qn : nproto;
+  for (int p = p0; p < p1; ++p) {
+    if (KIND == SDX_KIND_MU) {
+      const sdx_mu_proto* rec = bv.mu + p;
+      if (rec->never || !rec->active) continue;
+      bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
+      int idx = 0;
+      uint64_t st_tgt = 0, ut0 = 0, ut1 = 0, ut2 = 0;
+      int fmask = 0;
+      if (alive) {
+        const double ck = rec->clock;
+#pragma unroll
+        for (int k = 0; k < SDX_MAXPAT; ++k)
+          if (k < npat) norm[k] = py_round1(val[k] / ck);
+        if (rec->has_start) {
+          const PexRes r = pattern_exists(&rec->start, norm, ids, npat, bmine, T::WS, nw, 0);
+          alive = r.found;
+          idx = r.pos;
+          st_tgt = r.tgt;
+        }
+      }
+      if (alive && rec->one.len) {
+        const PexRes r = pattern_exists(&rec->one, norm, ids, npat, bmine, T::WS, nw, idx);
+        if (r.found) { ut0 = r.tgt; fmask |= 1; } else alive = false;
+      }
+      if (alive && rec->zero.len) {
+        const PexRes r = pattern_exists(&rec->zero, norm, ids, npat, bmine, T::WS, nw, idx);
+        if (r.found) { ut1 = r.tgt; fmask |= 2; } else alive = false;
+      }
+      if (alive && rec->flt.len) {
+        const PexRes r = pattern_exists(&rec->flt, norm, ids, npat, bmine, T::WS, nw, idx);
+        if (r.found) { ut2 = r.tgt; fmask |= 4; }
+      }
+      alive = alive && fmask != 0;
+      uint64_t surv = ballot(alive);
+      while (surv) {
+        const int sl = ffs64(surv);
+        surv &= surv - 1;
+        decode_mu(L, wave, bv, rec, p, sl, bcast_i(idx, sl), bcast_u64(st_tgt, sl), bcast_u64(ut0, sl),
+                  bcast_u64(ut1, sl), bcast_u64(ut2, sl), bcast_i(fmask, sl));
+      }
+    } else {
+      const sdx_ms_proto* rec = bv.ms + p;
+      if (rec->never) continue;
+      bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
+      if (alive && rec->pclock > 0.0)  // clock tolerance gate (:83-88)
+        alive = !(fabs(rec->pclock - clock) > clock * 0.3);
+      int start = 0;
+      uint64_t kt0 = 0, kt1 = 0, kt2 = 0, kt3 = 0;
+      int fmask = 0;
+      if (alive && rec->key[0].len) {  // sync (:140-158)
+        const PexRes r = pattern_exists(&rec->key[0], norm, ids, npat, bmine, T::WS, nw, 0);
+        if (r.found) {
+          kt0 = r.tgt;
+          fmask |= 1;
+          start = r.pos + rec->key[0].len;
+          const double avail = rec->width > 0 ? (double)(n - start) / (double)rec->width : 0.0;
+          if ((double)rec->lmin_sync > avail) alive = false;
+        } else alive = false;
+      }
+      if (alive && rec->key[1].len) {
+        const PexRes r = pattern_exists(&rec->key[1], norm, ids, npat, bmine, T::WS, nw, 0);
+        if (r.found) { kt1 = r.tgt; fmask |= 2; } else alive = false;
+      }
+      if (alive && rec->key[2].len) {
+        const PexRes r = pattern_exists(&rec->key[2], norm, ids, npat, bmine, T::WS, nw, 0);
+        if (r.found) { kt2 = r.tgt; fmask |= 4; } else alive = false;
+      }
+      if (alive && rec->key[3].len) {
+        const PexRes r = pattern_exists(&rec->key[3], norm, ids, npat, bmine, T::WS, nw, 0);
+        if (r.found) { kt3 = r.tgt; fmask |= 8; }
+      }
+      alive = alive && fmask != 0;
+      uint64_t surv = ballot(alive);
+      while (surv) {
+        const int sl = ffs64(surv);
+        surv &= surv - 1;
+        decode_ms(L, wave, bv, rec, p, sl, bcast_i(start, sl), bcast_u64(kt0, sl), bcast_u64(kt1, sl),
+                  bcast_u64(kt2, sl), bcast_u64(kt3, sl), bcast_i(fmask, sl));
+      }
+    }
+  }
+  __syncthreads();
+  flush_tile(L, msg_of, nvalid, out);
+}
+
+// =============================================================================================
+// MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
+// =============================================================================================
+constexpr int MC_MAXW = 8;  // <= 512 bits = 128 hex characters per frame (device contract)
+
+struct LaneBits {
+  uint64_t* base;  // word w at base[w * 256]
+  SDX_DEV uint64_t word(int w) const { return w < MC_MAXW ? base[w * 256] : 0ull; }
+  SDX_DEV int get(int i) const { return (int)((word(i >> 6) >> (63 - (i & 63))) & 1ull); }
+  // P <= 32 bits starting at i (MSB-first), zero beyond the array
+  SDX_DEV uint32_t win(int i, int P) const {
+    const int w = i >> 6, o = i & 63;
+    uint64_t hi = word(w) << o;
+    if (o) hi |= word(w + 1) >> (64 - o);
+    return (uint32_t)(hi >> (64 - P));
+  }
+  SDX_DEV int find(uint32_t pat, int P, int from, int n) const {
+    for (int i = from < 0 ? 0 : from; i + P <= n; ++i)
+      if (win(i, P) == pat) return i;
+    return -1;
+  }
+};
+
+struct McLds {
+  uint64_t bn[MC_MAXW * 256];   // bits, polarity as given
+  uint64_t bi[MC_MAXW * 256];   // bits, polarity inverted
+  uint64_t dm[MC_MAXW * 256];   // Funkbus differential-manchester scratch
+  StageRec rec[4][REC_CAP];
+  uint8_t heap[4][HEAP_CAP];
+  int nrec[4], nheap[4], ovf[4];
+};
+
+// bin_str_2_hex_str of bits [a, e) of LaneBits -> dst; returns the length
+SDX_DEV int lane_hex(const LaneBits& B, int a, int e, uint8_t* dst) {
+  const int nb = e - a;
+  if (nb <= 0) return 0;
+  const int nd = (nb + 3) >> 2;
+  for (int d = 0; d < nd; ++d) {
+    const int de = e - 4 * (nd - 1 - d), da = (de - 4 > a) ? de - 4 : a;
+    int v = 0;
+    for (int i = da; i < de; ++i) v = (v << 1) | B.get(i);
+    if (dst) dst[d] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+  }
+  return nd;
+}
+
+SDX_DEV bool hex_equal(const LaneBits& B, int a1, int e1, int a2, int e2) {
+  if (((e1 - a1 + 3) >> 2) != ((e2 - a2 + 3) >> 2)) return false;
+  const int m = (e1 - a1 > e2 - a2) ? e1 - a1 : e2 - a2;
+  for (int t = 0; t < m; ++t) {
+    const int x = (e1 - 1 - t >= a1) ? B.get(e1 - 1 - t) : 0;
+    const int y = (e2 - 1 - t >= a2) ? B.get(e2 - 1 - t) : 0;
+    if (x != y) return false;
+  }
+  return true;
+}
+
+// length_in_range (helpers.py:124-166) for a clockrange protocol
+SDX_DEV bool mc_lir(const sdx_mc_proto* r, int n) {
+  const int lo = r->has_lmin ? r->lmin : -1;
+  if (lo != -1 && n < lo) return false;
+  if (r->has_lmax && n > r->lmax) return false;
+  return true;
+}
+
+// TFA message iterator (manchester.py:615-719): yields windows [pos, end)
+struct TfaIter {
+  int pos, end, n, loops;
+  bool first_done;
+  SDX_DEV bool next(const LaneBits& B, int* a, int* e) {
+    if (!(end < n)) return false;
+    int me = B.find(0x1FFDu /*1111111111101*/, 13, pos, n);
+    if (me < pos) me = n;
+    *a = pos;
+    *e = me;
+    end = me;
+    const int nx = B.find(0xDu /*1101*/, 4, me, n);
+    if (nx != -1) pos = nx + 4;
+    else end = n;
+    ++loops;
+    return true;
+  }
+};
+
+// result of one (frame, protocol): rc and how to print it
+struct McOut {
+  int rc;        // 1 ok, 0 no result, -1 raise TypeError, -2 raise ValueError
+  int kind;      // 0 hex window, 1 funkbus bytes, 2 tfa list
+  int a, e;      // hex window
+  uint64_t fb;   // funkbus 6 bytes (big-endian)
+  int len;       // payload length without the preamble
+};
+
+SDX_DEV McOut mc_method(const sdx_mc_proto* r, const LaneBits& B, int n, const LaneBits& D) {
+  McOut o{0, 0, 0, 0, 0, 0};
+  switch (r->method) {
+    case SDX_MC_FUNKBUS: {  // manchester.py:207-300
+      const int lmin = r->has_lmin ? r->lmin : -1;
+      if (n < lmin) return o;
+      if (r->has_lmax && n > r->lmax) return o;
+      const int dn = n > 0 ? n - 1 : 0;  // mc2dmc of the lh/hl expansion
+      int base, slen;
+      if (r->pid_num == 119) {
+        const int pos = D.find(0xCu /*01100*/, 5, 0, dn);
+        if (!(pos >= 0 && pos < 5)) return o;
+        base = pos;
+        slen = 3 + dn - pos;
+        if (slen < 48) return o;
+      } else {
+        base = 0;
+        slen = 1 + dn;
+      }
+      const uint32_t pre = (r->pid_num == 119) ? 1u /*001*/ : 0u;
+      const int plen = (r->pid_num == 119) ? 3 : 1;
+      auto sbit = [&](int t) -> int { return t < plen ? (int)((pre >> (plen - 1 - t)) & 1) : D.get(base + t - plen); };
+      uint64_t bytes = 0;
+      int xr = 0, chk = 0, par = 0;
+      for (int i = 0; i < 6; ++i) {
+        const int a = 8 * i, e = (8 * i + 8 < slen) ? 8 * i + 8 : slen;
+        if (e <= a) { o.rc = -2; return o; }  // int('', 2)
+        int d = 0;
+        for (int t = a; t < e; ++t) d = (d << 1) | sbit(t);
+        bytes = (bytes << 8) | (uint64_t)d;
+        if (i < 5) xr ^= d;
+        else {
+          chk = d & 0x0F;
+          xr ^= d & 0xE0;
+          d &= 0xF0;
+        }
+        par ^= __popc(d) & 1;
+      }
+      if (par == 1) return o;
+      const int nib = ((xr & 0xF0) >> 4) ^ (xr & 0x0F);
+      int res = 0;
+      if (nib & 8) res ^= 0xC;
+      if (nib & 4) res ^= 0x2;
+      if (nib & 2) res ^= 0x8;
+      if (nib & 1) res ^= 0x3;
+      if (res != chk) return o;
+      o.rc = 1; o.kind = 1; o.fb = bytes; o.len = 12;
+      return o;
+    }
+    case SDX_MC_SAINLOGIC: {  // manchester.py:302-354
+      const int lmax = r->has_lmax ? r->lmax : 0;
+      if (n > lmax) return o;
+      int pad = 0, m = n;
+      if (n < 128) {
+        const int st = B.find(0x14u /*010100*/, 6, 0, n);
+        if (st < 0 || st > 10) return o;
+        pad = st < 10 ? 10 - st : 0;
+        m = (n + pad < 128) ? n + pad : 128;
+      }
+      const int lmin = r->has_lmin ? r->lmin : 0;
+      if (m < lmin) return o;
+      // bits = '1'*pad + B[0 : m-pad]; encode as window with a virtual prefix
+      o.rc = 1; o.kind = 3; o.a = pad; o.e = m; o.len = (m + 3) >> 2;
+      return o;
+    }
+    case SDX_MC_AS: {  // manchester.py:356-416
+      const int lmin = r->has_lmin ? r->lmin : -1, lmax = r->has_lmax ? r->lmax : 9999;
+      const int st = B.find(0xCu /*1100*/, 4, 16, n);
+      if (st >= 0) {
+        int en = B.find(0xCu, 4, st + 16, n);
+        if (en == -1) en = n;
+        const int ml = en - st;
+        if (ml < lmin || ml > lmax) return o;
+        o.rc = 1; o.a = st; o.e = n; o.len = (n - st + 3) >> 2;
+        return o;
+      }
+      if (n < lmin || n > lmax) return o;
+      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
+      return o;
+    }
+    case SDX_MC_PLAIN: {  // manchester.py:418-586
+      const int lmin = r->has_lmin ? r->lmin : -1, lmax = r->has_lmax ? r->lmax : 9999;
+      if (n < lmin || n > lmax) return o;
+      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
+      return o;
+    }
+    case SDX_MC_RAW: {  // manchester.py:588-613
+      const int lmax = r->has_lmax ? r->lmax : 0;
+      if (n > lmax) return o;
+      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
+      return o;
+    }
+    case SDX_MC_HMCRAW: {  // helpers.py:90-122: un-converted str length_max -> int > str TypeError
+      if (r->has_lmax) {
+        if (r->lmax_is_str) { o.rc = -1; return o; }
+        if (n > r->lmax) return o;
+      }
+      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
+      return o;
+    }
+    case SDX_MC_TFA: {  // manchester.py:615-719
+      const int p0 = B.find(0xFFDu /*111111111101*/, 12, 0, n);
+      if (p0 == -1) return o;
+      TfaIter it{p0 + 12, -1, n, 1, false};
+      int a, e, ndup = 0, len = 2;
+      // messages = accepted windows; a duplicate is emitted when exactly one equal one precedes it
+      TfaIter outer = it;
+      int j = 0;
+      while (outer.next(B, &a, &e)) {
+        if (mc_lir(r, e - a)) {
+          int eq = 0;
+          TfaIter inner = it;
+          int a2, e2, k = 0;
+          while (k < j && inner.next(B, &a2, &e2)) {
+            if (mc_lir(r, e2 - a2) && hex_equal(B, a, e, a2, e2)) ++eq;
+            ++k;
+          }
+          if (eq == 1) {
+            len += (ndup ? 2 : 0) + 2 + ((e - a + 3) >> 2);
+            ++ndup;
+          }
+        }
+        ++j;
+      }
+      if (outer.loops == 10) return o;  // 'loop error'
+      if (ndup == 0) return o;
+      o.rc = 1; o.kind = 2; o.len = len; o.a = p0 + 12;
+      return o;
+    }
+    case SDX_MC_GROTHE: {  // manchester.py:721-754
+      if (n != 32) return o;
+      o.rc = 1; o.a = 0; o.e = n; o.len = 8;
+      return o;
+    }
+    case SDX_MC_SOMFY: {  // manchester.py:756-795
+      int a = 0, e = n;
+      if (n == 57) { a = 1; e = 57; }
+      if (e - a != 56) return o;
+      o.rc = 1; o.a = a; o.e = e; o.len = 14;
+      return o;
+    }
+  }
+  return o;
+}
+
+SDX_DEV void mc_write(const sdx_mc_proto* r, const McOut& o, const LaneBits& B, int n, uint8_t* dst) {
+  if (o.kind == 0) {
+    lane_hex(B, o.a, o.e, dst);
+  } else if (o.kind == 1) {
+    for (int i = 0; i < 12; ++i) {
+      const int v = (int)((o.fb >> (4 * (11 - i))) & 15);
+      dst[i] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+    }
+  } else if (o.kind == 3) {  // Sainlogic: '1'*pad + bits, truncated to e (<=128) characters
+    const int pad = o.a, m = o.e, nd = (m + 3) >> 2;
+    for (int d = 0; d < nd; ++d) {
+      const int de = m - 4 * (nd - 1 - d), da = (de - 4 > 0) ? de - 4 : 0;
+      int v = 0;
+      for (int i = da; i < de; ++i) v = (v << 1) | (i < pad ? 1 : B.get(i - pad));
+      dst[d] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+    }
+  } else {  // TFA: Python list repr "['A', 'B']"
+    TfaIter it{o.a, -1, n, 1, false}, outer = it;
+    int a, e, j = 0, q = 0, nd = 0;
+    dst[q++] = '[';
+    while (outer.next(B, &a, &e)) {
+      if (mc_lir(r, e - a)) {
+        int eq = 0, a2, e2, k = 0;
+        TfaIter inner = it;
+        while (k < j && inner.next(B, &a2, &e2)) {
+          if (mc_lir(r, e2 - a2) && hex_equal(B, a, e, a2, e2)) ++eq;
+          ++k;
+        }
+        if (eq == 1) {
+          if (nd) { dst[q++] = ','; dst[q++] = ' '; }
+          dst[q++] = '\'';
+          q += lane_hex(B, a, e, dst + q);
+          dst[q++] = '\'';
+          ++nd;
+        }
+      }
+      ++j;
+    }
+    dst[q++] = ']';
+  }
+}
+
+SDX_DEV int hexval(uint8_t c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  return -1;
+}
+
+__global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
+  __shared__ McLds L;
+  const BankView bv = bank_view(bank);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int gi = blockIdx.x * 256 + tid;
+  const bool valid = gi < ntot;
+  const int msg = valid ? (b.sel_dev ? b.sel_dev[gi] : gi) : 0;
+  if (lane == 0) { L.nrec[wave] = 0; L.nheap[wave] = 0; L.ovf[wave] = 0; }
+  LaneBits BN{&L.bn[tid]}, BI{&L.bi[tid]}, DM{&L.dm[tid]};
+  // hex -> bits for both polarities (helpers.py:168-188: leading zero nibbles are dropped)
+  int nN = 0, nI = 0;
+  bool hex_ok = false;
+  int clock = 0, mcbit = 0, flags = 0;
+  if (valid) {
+    const int64_t off = b.offsets_dev[msg];
+    const int hl = (int)(b.offsets_dev[msg + 1] - off);
+    clock = b.clock_dev[msg];
+    mcbit = b.mcbitnum_dev[msg];
+    flags = b.flags_dev[msg];
+    hex_ok = hl > 0 && hl <= MC_MAXW * 16;
+    bool startedN = false, startedI = false;
+    for (int w = 0; w < MC_MAXW; ++w) { L.bn[w * 256 + tid] = 0; L.bi[w * 256 + tid] = 0; }
+    for (int i = 0; i < hl && hex_ok; ++i) {
+      const uint8_t c = b.hex_dev[off + i];
+      const int v = hexval(c);
+      if (v < 0) { hex_ok = false; break; }
+      const bool upper = (c >= '0' && c <= '9') || (c >= 'A' && c <= 'F');  // str.translate table
+      const int vi = upper ? 15 - v : v;
+      if (v || startedN || i == hl - 1) {
+        startedN = true;
+        const int w = nN >> 6, o = nN & 63;
+        L.bn[w * 256 + tid] |= (uint64_t)v << (60 - o);
+        nN += 4;
+      }
+      if (vi || startedI || i == hl - 1) {
+        startedI = true;
+        const int w = nI >> 6, o = nI & 63;
+        L.bi[w * 256 + tid] |= (uint64_t)vi << (60 - o);
+        nI += 4;
+      }
+    }
+  }
+  const int nmc = (int)bv.hdr->n_mc;
+  int raise = 0;
+  for (int p = 0; p < nmc; ++p) {
+    const sdx_mc_proto* r = bv.mc + p;
+    bool go = valid && !raise;
+    // gates of _demodulate_mc_data (manchester.py:70-89; clockrange fixed to [0] / [1])
+    if (go && mcbit < (r->has_lmin ? r->lmin : -1)) go = false;
+    if (go && mcbit > (r->has_lmax ? r->lmax : 9999)) go = false;
+    if (go && r->has_cr && !((double)clock > r->cr_lo && (double)clock < r->cr_hi)) go = false;
+    McOut o{0, 0, 0, 0, 0, 0};
+    const bool inv = (r->invert != 0) ^ ((flags & 3) != 0);  // (:91-96)
+    const LaneBits& B = inv ? BI : BN;
+    const int nb = inv ? nI : nN;
+    if (go && !hex_ok) { raise = SDX_RAISE_TYPE; go = false; }  // len(None) -> TypeError
+    if (go) {
+      if (r->method == SDX_MC_FUNKBUS) {
+        for (int w = 0; w < MC_MAXW; ++w) {  // mc2dmc(lh/hl): bit k = (b[k] == b[k+1])
+          const uint64_t x = B.word(w), nx = B.word(w + 1);
+          L.dm[w * 256 + tid] = ~(x ^ ((x << 1) | (nx >> 63)));
+        }
+      }
+      o = mc_method(r, B, nb, DM);
+      if (o.rc == -1) { raise = SDX_RAISE_TYPE; o.rc = 0; }
+      if (o.rc == -2) { raise = SDX_RAISE_VALUE; o.rc = 0; }
+    }
+    // stage results of the wave in lane (= frame) order for this protocol
+    const bool has = o.rc == 1;
+    const int plen = has ? r->pre_len + o.len : 0;
+    int incl = plen;  // inclusive scan over lanes
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const int t = __shfl_up(incl, d);
+      if (lane >= d) incl += t;
+    }
+    const int wtot = __shfl(incl, WAVE - 1);
+    const uint64_t hm = ballot(has);
+    const int nnew = popc64(hm);
+    const int hb = L.nheap[wave], rb = L.nrec[wave];
+    const bool fits = hb + wtot <= HEAP_CAP && rb + nnew <= REC_CAP;
+    if (has && fits) {
+      uint8_t* dst = &L.heap[wave][hb + incl - plen];
+      for (int i = 0; i < r->pre_len; ++i) dst[i] = bv.str[r->pre_off + i];
+      mc_write(r, o, B, nb, dst + r->pre_len);
+      StageRec sr;
+      sr.off = (uint32_t)(hb + incl - plen);
+      sr.len = (uint16_t)plen;
+      sr.proto = (uint16_t)p;
+      sr.bitlen = 0;
+      sr.msg = (uint16_t)lane;
+      sr.rank = 0;
+      L.rec[wave][rb + lanes_below(hm)] = sr;
+    }
+    wave_sync();
+    if (lane == 0) {
+      if (fits) { L.nheap[wave] = hb + wtot; L.nrec[wave] = rb + nnew; }
+      else if (nnew) L.ovf[wave] = 1;
+    }
+    wave_sync();
+  }
+  // flush this wave's frames (records are in protocol-major order: count per lane)
+  const int nr = L.nrec[wave], nh = L.nheap[wave];
+  const bool bad = L.ovf[wave] != 0;
+  int mycnt = 0;
+  for (int i = 0; i < nr; ++i) mycnt += (L.rec[wave][i].msg == lane) ? 1 : 0;
+  if (raise) mycnt = 0;
+  int incl = mycnt;
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const int t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  const int wrec = __shfl(incl, WAVE - 1);
+  uint32_t rbase = 0, hbase = 0;
+  int st = bad ? 2 : 0;
+  if (lane == 0 && !bad) {
+    rbase = atomicAdd(&out.cursor_dev[0], (uint32_t)wrec);
+    hbase = atomicAdd(&out.cursor_dev[1], (uint32_t)nh);
+    if (rbase + wrec > out.rec_cap || hbase + nh > out.heap_cap) { st = 3; atomicOr(&out.cursor_dev[2], 1u); }
+  }
+  if (lane == 0 && bad) atomicOr(&out.cursor_dev[2], 2u);
+  rbase = (uint32_t)__shfl((int)rbase, 0);
+  hbase = (uint32_t)__shfl((int)hbase, 0);
+  st = __shfl(st, 0);
+  if (st == 0) {
+    // each lane writes its own records in protocol order
+    int q = incl - mycnt;
+    if (mycnt)
+      for (int i = 0; i < nr; ++i) {
+        const StageRec sr = L.rec[wave][i];
+        if (sr.msg != lane) continue;
+        sdx_result o;
+        o.payload_off = hbase + sr.off;
+        o.payload_len = sr.len;
+        o.proto = sr.proto;
+        o.bit_length = 0;
+        o.msg = (uint32_t)msg;
+        out.rec_dev[rbase + q] = o;
+        ++q;
+      }
+    for (int i = lane; i < nh; i += WAVE) out.heap_dev[hbase + i] = L.heap[wave][i];
+  }
+  if (valid) {
+    sdx_desc d;
+    d.rec_begin = rbase + (uint32_t)(incl - mycnt);
+    if (raise) { d.status = SDX_ST_RAISED; d.raise_kind = (uint8_t)raise; d.n_rec = 0; }
+    else if (st) { d.status = st == 2 ? SDX_ST_OVF_TILE : SDX_ST_OVF_OUT; d.raise_kind = 0; d.n_rec = 0; }
+    else { d.status = SDX_ST_OK; d.raise_kind = 0; d.n_rec = (uint16_t)mycnt; }
+    out.desc_dev[msg] = d;
+  }
+}
+
+}  // namespace sdx
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+struct sdx_bank {
+  int device;
+  void* dev;
+  size_t nbytes;
+  sdx_bank_hdr hdr;
+};
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) return fail(SDX_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" {
+
+int sdx_abi_version(void) { return SDX_ABI_VERSION; }
+const char* sdx_last_error(void) { return g_err.c_str(); }
+
+int sdx_layout_size(int which) {
+  switch (which) {
+    case 0: return (int)sizeof(sdx_bank_hdr);
+    case 1: return (int)sizeof(sdx_patspec);
+    case 2: return (int)sizeof(sdx_mu_proto);
+    case 3: return (int)sizeof(sdx_ms_proto);
+    case 4: return (int)sizeof(sdx_mc_proto);
+    case 5: return (int)sizeof(sdx_result);
+    case 6: return (int)sizeof(sdx_desc);
+  }
+  return -1;
+}
+
+int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out) {
+  if (!blob || !out || nbytes < sizeof(sdx_bank_hdr)) return fail(SDX_EINVAL, "bad bank arguments");
+  sdx_bank_hdr h;
+  std::memcpy(&h, blob, sizeof h);
+  if (h.magic != SDX_BANK_MAGIC || h.version != SDX_BANK_VERSION || h.total_bytes != nbytes)
+    return fail(SDX_EBANK, "bank blob magic/version/size mismatch (rebuild the bank and the library)");
+  HIPCHK(hipSetDevice(device));
+  void* d = nullptr;
+  HIPCHK(hipMalloc(&d, nbytes));
+  hipError_t e = hipMemcpy(d, blob, nbytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return fail(SDX_EHIP, std::string("bank upload: ") + hipGetErrorString(e));
+  }
+  sdx_bank* b = new sdx_bank{device, d, nbytes, h};
+  *out = b;
+  return SDX_OK;
+}
+
+int sdx_bank_destroy(sdx_bank* bank) {
+  if (!bank) return SDX_OK;
+  if (bank->dev) (void)hipFree(bank->dev);
+  delete bank;
+  return SDX_OK;
+}
+
+const void* sdx_bank_device_ptr(const sdx_bank* bank) { return bank ? bank->dev : nullptr; }
+
+int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
+                     void* hip_stream) {
+  if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
+  if (kind != SDX_KIND_MU && kind != SDX_KIND_MS) return fail(SDX_EINVAL, "kind must be MU or MS");
+  if (kind == SDX_KIND_MS && (!batch->cp_slot_dev || !batch->ms_ok_dev)) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+  const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
+  if (ntot <= 0) return SDX_OK;
+  hipStream_t st = (hipStream_t)hip_stream;
+  // variant: short (<= 256 pulses, 64 messages per tile) -- the caller routes longer messages
+  // (<= 4096) through sel_dev to the long variant by passing kind | 0x100.
+  constexpr int TM = 64;
+  const int grid = (ntot + TM - 1) / TM;
+  if (kind == SDX_KIND_MU)
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  else
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  HIPCHK(hipGetLastError());
+  return SDX_OK;
+}
+
+int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
+                          void* hip_stream) {
+  if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
+  const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
+  if (ntot <= 0) return SDX_OK;
+  hipStream_t st = (hipStream_t)hip_stream;
+  constexpr int TM = 4;
+  const int grid = (ntot + TM - 1) / TM;
+  if (kind == SDX_KIND_MU)
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 64, 4>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  else if (kind == SDX_KIND_MS)
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 64, 4>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  else
+    return fail(SDX_EINVAL, "kind must be MU or MS");
+  HIPCHK(hipGetLastError());
+  return SDX_OK;
+}
+
+int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream) {
+  if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
+  const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
+  if (ntot <= 0) return SDX_OK;
+  hipStream_t st = (hipStream_t)hip_stream;
+  const int grid = (ntot + 255) / 256;
+  hipLaunchKernelGGL(sdx::k_mc, dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  HIPCHK(hipGetLastError());
+  return SDX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,273 @@
+"""ctypes binding of libsdx.so (include/sdx.h) + device-buffer plumbing.
+
+PyTorch is used only for device memory and streams (``torch.cuda``); every
+byte of demodulation work runs in the hand-written HIP kernels of
+``csrc/sdx_kernels.hip``.  There is NO CPU fallback: when the library or a
+GPU is missing, :func:`load_library` / :class:`Engine` raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_int, c_int32, c_size_t, c_uint32, c_void_p
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from . import bank as bankmod
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libsdx.so")
+
+KIND_MU, KIND_MS, KIND_MC = 0, 1, 2
+ST_OK, ST_RAISED, ST_OVF_TILE, ST_OVF_OUT = 0, 1, 2, 3
+RAISE_NAMES = {1: IndexError, 2: AttributeError, 3: ValueError, 4: TypeError, 5: ZeroDivisionError}
+SHORT_MAX = 256    # k_pulses<.., 4 words, 64 messages/tile>
+LONG_MAX = 4096    # k_pulses<.., 64 words, 4 messages/tile>
+MC_HEX_MAX = 128   # MC_MAXW * 16 hex characters
+
+DESC_DT = np.dtype([("rec_begin", "<u4"), ("n_rec", "<u2"), ("status", "u1"), ("raise_kind", "u1")])
+RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u2"), ("bit_length", "<u4"),
+                   ("msg", "<u4")])
+
+EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
+            "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc"]
+
+
+class SdxPulseBatch(Structure):
+    _fields_ = [("data_dev", c_void_p), ("offsets_dev", c_void_p), ("npat_dev", c_void_p),
+                ("pat_id_dev", c_void_p), ("pat_val_dev", c_void_p), ("cp_slot_dev", c_void_p),
+                ("ms_ok_dev", c_void_p), ("sel_dev", c_void_p), ("n", c_int32), ("n_sel", c_int32)]
+
+
+class SdxMcBatch(Structure):
+    _fields_ = [("hex_dev", c_void_p), ("offsets_dev", c_void_p), ("clock_dev", c_void_p),
+                ("mcbitnum_dev", c_void_p), ("flags_dev", c_void_p), ("sel_dev", c_void_p),
+                ("n", c_int32), ("n_sel", c_int32)]
+
+
+class SdxOut(Structure):
+    _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("cursor_dev", c_void_p),
+                ("rec_cap", c_uint32), ("heap_cap", c_uint32)]
+
+
+_LIB = None
+
+
+def load_library(path: Optional[str] = None):
+    """Load libsdx.so (fails loudly -- the product path has no fallback)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    # torch bundles its own libamdhip64.so.7: load it FIRST so that libsdx's NEEDED
+    # libamdhip64.so.7 resolves to the same runtime (one HIP runtime per process).
+    import torch  # noqa: F401
+    if not os.path.exists(p):
+        raise RuntimeError(f"libsdx.so not built ({p}); run __graft_entry__.build() "
+                           "or python -m pysignalduino_amd.build")
+    lib = ctypes.CDLL(p)
+    lib.sdx_abi_version.restype = c_int
+    lib.sdx_last_error.restype = c_char_p
+    lib.sdx_layout_size.argtypes = [c_int]
+    lib.sdx_layout_size.restype = c_int
+    lib.sdx_bank_create.argtypes = [c_void_p, c_size_t, c_int, POINTER(c_void_p)]
+    lib.sdx_bank_create.restype = c_int
+    lib.sdx_bank_destroy.argtypes = [c_void_p]
+    lib.sdx_bank_destroy.restype = c_int
+    lib.sdx_bank_device_ptr.argtypes = [c_void_p]
+    lib.sdx_bank_device_ptr.restype = c_void_p
+    for fn in ("sdx_demod_pulses", "sdx_demod_pulses_long"):
+        f = getattr(lib, fn)
+        f.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), POINTER(SdxOut), c_void_p]
+        f.restype = c_int
+    lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
+    lib.sdx_demod_mc.restype = c_int
+    if lib.sdx_abi_version() != 1:
+        raise RuntimeError("libsdx ABI version mismatch")
+    check_layout(lib)
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def check_layout(lib) -> None:
+    """The numpy mirrors of the C structs must match sizeof() on the C side."""
+    want = {0: 80, 1: bankmod.PATSPEC.itemsize, 2: bankmod.MU_REC.itemsize, 3: bankmod.MS_REC.itemsize,
+            4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize}
+    for k, v in want.items():
+        got = lib.sdx_layout_size(k)
+        if got != v:
+            raise RuntimeError(f"struct layout mismatch (item {k}): C {got} vs Python {v}")
+
+
+def _check(lib, rc):
+    if rc != 0:
+        raise RuntimeError(f"libsdx error {rc}: {lib.sdx_last_error().decode(errors='replace')}")
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else int(t.data_ptr())
+
+
+class Engine:
+    """One device + one uploaded bank.  All launches go to the caller's (torch) stream."""
+
+    def __init__(self, bank: "bankmod.Bank", device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("pysignalduino_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
+        self.torch = torch
+        self.lib = load_library()
+        self.bank = bank
+        self.device = device
+        self.dev = torch.device("cuda", device)
+        h = c_void_p()
+        blob = ctypes.create_string_buffer(bank.blob, len(bank.blob))
+        with torch.cuda.device(device):
+            _check(self.lib, self.lib.sdx_bank_create(ctypes.cast(blob, c_void_p), len(bank.blob), device,
+                                                      ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self.lib.sdx_bank_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- buffers --------------------------------------------------------------------------------
+    def to_device_pulses(self, pb) -> Dict[str, "object"]:
+        t = self.torch
+        d = self.dev
+        out = {
+            "data": t.from_numpy(np.ascontiguousarray(pb.data) if len(pb.data) else np.zeros(1, np.uint8)).to(d),
+            "offsets": t.from_numpy(np.ascontiguousarray(pb.offsets, dtype=np.int64)).to(d),
+            "npat": t.from_numpy(np.ascontiguousarray(pb.npat, dtype=np.uint8)).to(d),
+            "pat_id": t.from_numpy(np.ascontiguousarray(pb.pat_id, dtype=np.uint8)).to(d),
+            "pat_val": t.from_numpy(np.ascontiguousarray(pb.pat_val, dtype=np.float64)).to(d),
+            "cp_slot": t.from_numpy(np.ascontiguousarray(pb.cp_slot, dtype=np.int8)).to(d),
+            "ms_ok": t.from_numpy(np.ascontiguousarray(pb.ms_ok, dtype=np.uint8)).to(d),
+            "n": int(pb.n),
+            "lengths": np.diff(pb.offsets),
+        }
+        return out
+
+    def to_device_mc(self, mb) -> Dict[str, "object"]:
+        t = self.torch
+        d = self.dev
+        flags = (mb.mtype.astype(np.uint8) & 1) | ((mb.v32.astype(np.uint8) & 1) << 1)
+        return {
+            "hex": t.from_numpy(np.ascontiguousarray(mb.hexdata) if len(mb.hexdata) else np.zeros(1, np.uint8)).to(d),
+            "offsets": t.from_numpy(np.ascontiguousarray(mb.offsets, dtype=np.int64)).to(d),
+            "clock": t.from_numpy(np.ascontiguousarray(mb.clock, dtype=np.int32)).to(d),
+            "mcbitnum": t.from_numpy(np.ascontiguousarray(mb.mcbitnum, dtype=np.int32)).to(d),
+            "flags": t.from_numpy(np.ascontiguousarray(flags, dtype=np.uint8)).to(d),
+            "n": int(mb.n),
+            "lengths": np.diff(mb.offsets),
+        }
+
+    def alloc_out(self, n: int, rec_cap: int, heap_cap: int):
+        t = self.torch
+        d = self.dev
+        return {
+            "desc": t.zeros(max(n, 1) * DESC_DT.itemsize, dtype=t.uint8, device=d),
+            "rec": t.empty(max(rec_cap, 1) * RES_DT.itemsize, dtype=t.uint8, device=d),
+            "heap": t.empty(max(heap_cap, 1), dtype=t.uint8, device=d),
+            "cursor": t.zeros(4, dtype=t.int32, device=d),
+            "rec_cap": rec_cap, "heap_cap": heap_cap, "n": n,
+        }
+
+    @staticmethod
+    def _out_struct(o) -> SdxOut:
+        return SdxOut(_ptr(o["desc"]), _ptr(o["rec"]), _ptr(o["heap"]), _ptr(o["cursor"]), o["rec_cap"],
+                      o["heap_cap"])
+
+    def stream_ptr(self):
+        return c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    # -- launches -------------------------------------------------------------------------------
+    def launch_pulses(self, kind: int, bd, out, sel=None, long_variant: bool = False) -> None:
+        b = SdxPulseBatch(_ptr(bd["data"]), _ptr(bd["offsets"]), _ptr(bd["npat"]), _ptr(bd["pat_id"]),
+                          _ptr(bd["pat_val"]), _ptr(bd["cp_slot"]), _ptr(bd["ms_ok"]), _ptr(sel), bd["n"],
+                          0 if sel is None else int(sel.numel()))
+        o = self._out_struct(out)
+        fn = self.lib.sdx_demod_pulses_long if long_variant else self.lib.sdx_demod_pulses
+        _check(self.lib, fn(self.handle, kind, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
+
+    def launch_mc(self, bd, out, sel=None) -> None:
+        b = SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
+                       _ptr(bd["flags"]), _ptr(sel), bd["n"], 0 if sel is None else int(sel.numel()))
+        o = self._out_struct(out)
+        _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
+
+    # -- full run with contract routing and overflow re-runs (all on the GPU) --------------------
+    def run(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None):
+        """Demodulate a device batch; returns host numpy (desc, rec, heap)."""
+        t = self.torch
+        n = bd["n"]
+        lengths = bd["lengths"]
+        if kind == KIND_MC:
+            if n and int(lengths.max(initial=0)) > MC_HEX_MAX:
+                raise NotImplementedError(f"MC frames longer than {MC_HEX_MAX} hex characters are outside "
+                                          "the device contract")
+        elif n and int(lengths.max(initial=0)) > LONG_MAX:
+            raise NotImplementedError(f"messages longer than {LONG_MAX} pulses are outside the device contract")
+        rec_cap = rec_cap or (8 * n + 1024)
+        heap_cap = heap_cap or (200 * n + 65536)
+        out = self.alloc_out(n, rec_cap, heap_cap)
+        if kind == KIND_MC:
+            self.launch_mc(bd, out)
+        else:
+            short = lengths <= SHORT_MAX
+            if short.all():
+                self.launch_pulses(kind, bd, out)
+            else:
+                if short.any():
+                    self.launch_pulses(kind, bd, out, sel=t.from_numpy(np.nonzero(short)[0].astype(np.int32)).to(self.dev))
+                self.launch_pulses(kind, bd, out, sel=t.from_numpy(np.nonzero(~short)[0].astype(np.int32)).to(self.dev),
+                                   long_variant=True)
+        desc, rec, heap = self.fetch(out)
+        # re-runs on the GPU: grown output buffers / the long variant's larger per-message staging
+        for attempt in range(4):
+            st = desc["status"]
+            redo_out = np.nonzero(st == ST_OVF_OUT)[0]
+            redo_tile = np.nonzero(st == ST_OVF_TILE)[0]
+            if not len(redo_out) and not len(redo_tile):
+                break
+            if attempt == 3:
+                raise RuntimeError("result staging overflow persists (pathological message)")
+            redo = np.concatenate([redo_out, redo_tile]).astype(np.int32)
+            out2 = self.alloc_out(n, 2 * rec_cap + 64 * len(redo), 2 * heap_cap + 8192 * len(redo))
+            sel = t.from_numpy(redo).to(self.dev)
+            if kind == KIND_MC:
+                self.launch_mc(bd, out2, sel=sel)
+            else:
+                self.launch_pulses(kind, bd, out2, sel=sel, long_variant=True)
+            d2, r2, h2 = self.fetch(out2)
+            # merge: re-based records appended after the first pass
+            base_r, base_h = len(rec), len(heap)
+            r2 = r2.copy()
+            r2["payload_off"] += base_h
+            rec = np.concatenate([rec, r2])
+            heap = np.concatenate([heap, h2])
+            for i in redo:
+                d = d2[i].copy()
+                d["rec_begin"] += base_r
+                desc[i] = d
+        return desc, rec, heap
+
+    def fetch(self, out):
+        self.torch.cuda.current_stream(self.dev).synchronize()
+        cur = out["cursor"].cpu().numpy().astype(np.uint32)
+        n = out["n"]
+        desc = out["desc"][: n * DESC_DT.itemsize].cpu().numpy().view(DESC_DT).copy()
+        nrec = min(int(cur[0]), out["rec_cap"])
+        nheap = min(int(cur[1]), out["heap_cap"])
+        rec = out["rec"][: nrec * RES_DT.itemsize].cpu().numpy().view(RES_DT).copy()
+        heap = out["heap"][:nheap].cpu().numpy().copy()
+        return desc, rec, heap

@@ -1,0 +1,329 @@
+"""Drop-in ``SDProtocols`` whose MU/MS/MC demodulation runs on the MI355X.
+
+Mirrors the reference class RFD-FHEM/PySignalduino ``sd_protocols.SDProtocols``
+(sd_protocols/sd_protocols.py:13-170) for the hot path:
+
+  * property API: protocol_exists / get_protocol_list / get_keys / check_property /
+    get_property / set_defaults / register_log_callback / length_in_range
+    (sd_protocols.py:43-58,157-170; helpers.py:124-166) -- host dictionary logic;
+  * demodulate / demodulate_mu / demodulate_ms / demodulate_mc (sd_protocols.py:60-111,
+    message_unsynced.py:11, message_synced.py:10) -- packed and run by the HIP
+    kernels in csrc/sdx_kernels.hip through the C-ABI include/sdx.h;
+  * demodulate_batch(list_of_msg_data, msg_type) -- the batched entry point.
+
+It is injected where the reference injects its engine:
+``SignalParser(protocols=SDProtocols())`` (signalduino/parser/__init__.py:21-27).
+
+Results are the reference's list of ``{"protocol_id", "payload", "meta"}`` dicts,
+bit-exact; a message on which the reference raises re-raises the same exception
+class here (the parsers catch ``Exception`` and yield nothing, parser/mu.py:64-68).
+There is no CPU fallback: without the HIP library / a GPU every demodulate call raises.
+"""
+from __future__ import annotations
+
+import json
+from typing import Any, Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from . import bank as bankmod
+from . import packing
+from . import runtime
+
+_SENTINEL = object()
+
+
+class _Observed(dict):
+    """dict that bumps a shared version counter on mutation (nested protocol dicts too),
+    so a test or user editing ``_protocols[pid][key]`` gets the bank recompiled."""
+
+    def __init__(self, data, owner):
+        super().__init__()
+        self._owner = owner
+        for k, v in data.items():
+            dict.__setitem__(self, k, _Observed(v, owner) if isinstance(v, dict) and not isinstance(v, _Observed) else v)
+
+    def _bump(self):
+        self._owner._version += 1
+
+    def __setitem__(self, k, v):
+        if isinstance(v, dict) and not isinstance(v, _Observed):
+            v = _Observed(v, self._owner)
+        dict.__setitem__(self, k, v)
+        self._bump()
+
+    def __delitem__(self, k):
+        dict.__delitem__(self, k)
+        self._bump()
+
+    def setdefault(self, k, default=None):
+        if k not in self:
+            self[k] = default
+        return dict.__getitem__(self, k)
+
+    def update(self, *a, **kw):
+        for k, v in dict(*a, **kw).items():
+            self[k] = v
+
+    def pop(self, *a):
+        r = dict.pop(self, *a)
+        self._bump()
+        return r
+
+    def clear(self):
+        dict.clear(self)
+        self._bump()
+
+
+class SDProtocols:
+    """GPU-backed drop-in for ``sd_protocols.SDProtocols`` (demodulation path)."""
+
+    def __init__(self, protocols_path: Optional[str] = None, device: int = 0, mc_mode: str = "strict"):
+        if mc_mode not in ("strict", "fixed"):
+            raise ValueError("mc_mode must be 'strict' (reference-observable) or 'fixed'")
+        self._version = 0
+        self._protocols = _Observed(bankmod.load_protocols(protocols_path), self)
+        self._log_callback = None
+        self.device = device
+        self.mc_mode = mc_mode
+        self.set_defaults()
+        self._bank = None
+        self._bank_version = -1
+        self._engine = None
+
+    # ---------------------------------------------------------------- property API (host) ------
+    def protocol_exists(self, pid: str) -> bool:
+        return pid in self._protocols
+
+    def get_protocol_list(self) -> dict:
+        return self._protocols
+
+    def get_keys(self, filter_key: str = None) -> list:
+        if filter_key:
+            return [pid for pid, props in self._protocols.items() if filter_key in props]
+        return list(self._protocols.keys())
+
+    def check_property(self, pid: str, value_name: str, default=None):
+        return self._protocols.get(pid, {}).get(value_name, default)
+
+    def get_property(self, pid: str, value_name: str):
+        return self._protocols.get(pid, {}).get(value_name)
+
+    def set_defaults(self):
+        for pid, proto in self._protocols.items():
+            proto.setdefault("active", True)
+            proto.setdefault("name", f"Protocol_{pid}")
+
+    def register_log_callback(self, callback):
+        if callable(callback):
+            self._log_callback = callback
+
+    def _logging(self, message: str, level: int = 3):
+        if self._log_callback:
+            self._log_callback(message, level)
+
+    def length_in_range(self, protocol_id, message_length):
+        """helpers.py:124-166."""
+        if not self.protocol_exists(str(protocol_id)):
+            return (0, "protocol does not exists")
+        min_len = self.check_property(protocol_id, "length_min", -1)
+        if min_len is not None:
+            try:
+                min_len = int(min_len)
+            except (ValueError, TypeError):
+                pass
+        if min_len != -1 and message_length < min_len:
+            return (0, "message is too short")
+        max_len = self.get_property(protocol_id, "length_max")
+        if max_len is not None:
+            try:
+                max_len = int(max_len)
+                if message_length > max_len:
+                    return (0, "message is too long")
+            except (ValueError, TypeError):
+                pass
+        return (1, "")
+
+    # ---------------------------------------------------------------- device plumbing ----------
+    def _ensure(self):
+        if self._bank is None or self._bank_version != self._version:
+            raw = json.loads(json.dumps(self._protocols))
+            self._bank = bankmod.Bank(raw)
+            self._bank_version = self._version
+            if self._engine is not None:
+                self._engine.close()
+                self._engine = None
+        if self._engine is None:
+            self._engine = runtime.Engine(self._bank, self.device)
+        return self._engine
+
+    # ---------------------------------------------------------------- demodulation -------------
+    def demodulate(self, msg_data: Dict[str, Any], msg_type: str) -> list:
+        """sd_protocols.py:60-74."""
+        if msg_type == "MS":
+            return self.demodulate_ms(msg_data, msg_type)
+        if msg_type == "MC":
+            return self.demodulate_mc(msg_data, msg_type)
+        if msg_type == "MN":
+            return self.demodulate_mn(msg_data, msg_type)
+        if msg_type == "MU":
+            return self.demodulate_mu(msg_data, msg_type)
+        self._logging(f"Unknown message type {msg_type}", 3)
+        return []
+
+    def demodulate_mu(self, msg_data: Dict[str, Any], msg_type: str = "MU") -> list:
+        return self._single(msg_data, "MU")
+
+    def demodulate_ms(self, msg_data: Dict[str, Any], msg_type: str = "MS") -> list:
+        return self._single(msg_data, "MS")
+
+    def demodulate_mn(self, msg_data: Dict[str, Any], msg_type: str = "MN") -> list:
+        raise NotImplementedError("the MN (FSK) path is outside this build's scope (SURVEY.md §8(f) item 2)")
+
+    def _single(self, msg_data, kind):
+        out = self.demodulate_batch([msg_data], kind, raise_errors=True)
+        return out[0]
+
+    def demodulate_batch(self, messages: Sequence[Dict[str, Any]], msg_type: str, raise_errors: bool = False):
+        """Demodulate many messages in one GPU pass.
+
+        Returns one result list per message.  A message on which the reference raises
+        yields the exception instance (or re-raises it when ``raise_errors``).
+        """
+        if msg_type == "MC":
+            return [self._catch(self.demodulate_mc, m, "MC", raise_errors=raise_errors) for m in messages] \
+                if self.mc_mode == "strict" else self.demodulate_mc_batch(messages, raise_errors=raise_errors)
+        if msg_type not in ("MU", "MS"):
+            return [self.demodulate(m, msg_type) for m in messages]
+        packer = packing.PulsePacker(msg_type)
+        pack_err: Dict[int, BaseException] = {}
+        for i, m in enumerate(messages):
+            try:
+                packer.add(m)
+            except packing.ContractError:
+                raise
+            except Exception as e:  # the reference raises on this message (same class)
+                if raise_errors:
+                    raise
+                pack_err[i] = e
+                packer.add({"data": ""})
+        pb = packer.batch()
+        eng = self._ensure()
+        kind = runtime.KIND_MU if msg_type == "MU" else runtime.KIND_MS
+        desc, rec, heap = eng.run(kind, eng.to_device_pulses(pb))
+        return self._decode_pulses(msg_type, desc, rec, heap, packer, pack_err, raise_errors)
+
+    @staticmethod
+    def _catch(fn, m, t, raise_errors):
+        try:
+            return fn(m, t)
+        except Exception as e:
+            if raise_errors:
+                raise
+            return e
+
+    def _decode_pulses(self, kind, desc, rec, heap, packer, pack_err, raise_errors):
+        bk = self._bank
+        pids = bk.mu_pids if kind == "MU" else bk.ms_pids
+        hb = heap.tobytes()
+        out: List[Any] = []
+        for i in range(len(desc)):
+            if i in pack_err:
+                out.append(pack_err[i])
+                continue
+            d = desc[i]
+            if d["status"] == runtime.ST_RAISED:
+                exc = runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)(
+                    f"reference raises {runtime.RAISE_NAMES.get(int(d['raise_kind']), RuntimeError).__name__} "
+                    f"on this {kind} message")
+                if raise_errors:
+                    raise exc
+                out.append(exc)
+                continue
+            if d["status"] != runtime.ST_OK:
+                raise RuntimeError(f"device status {int(d['status'])} for message {i}")
+            rs = rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]
+            res = []
+            rssi = packer.rssi[i]
+            for r in rs:
+                p = int(r["proto"])
+                off = int(r["payload_off"])
+                payload = hb[off: off + int(r["payload_len"])].decode("latin-1")
+                clock = bk.mu_clock[p] if kind == "MU" else packer.clock_abs[i]
+                res.append({"protocol_id": pids[p], "payload": payload,
+                            "meta": {"bit_length": int(r["bit_length"]), "rssi": rssi, "clock": clock}})
+            out.append(res)
+        return out
+
+    # ---------------------------------------------------------------- MC -----------------------
+    def demodulate_mc(self, msg_data: Dict[str, Any], msg_type: str, version: Optional[str] = None) -> list:
+        """sd_protocols.py:76-111.
+
+        mc_mode='strict' (default): exactly the reference's observable behaviour.  Without a
+        ``protocol_id`` (how MCParser calls it, parser/mc.py:78) the result is [].  With one, the
+        reference's gates run (manchester.py:70-89) and every MC protocol then raises TypeError
+        (``int > list`` at :83-84) -- nothing is ever decoded, so no device work is involved.
+        mc_mode='fixed': the intended chain (clockrange[0] < C < clockrange[1], method called
+        without the extra ``self``) on the GPU for every clockrange protocol (or the given id).
+        """
+        if self.mc_mode == "fixed":
+            return self.demodulate_mc_batch([msg_data], msg_type=msg_type, version=version, raise_errors=True)[0]
+        protocol_id = msg_data.get("protocol_id")
+        if not protocol_id or not self.protocol_exists(protocol_id):
+            self._logging(f"MC Demodulation failed: Protocol ID {protocol_id} not found or missing.", 3)
+            return []
+        clock = msg_data.get("clock", 0)
+        mcbitnum = msg_data.get("bit_length", 0)
+        # manchester.py:70-89, evaluated with the same Python operations (same exceptions)
+        length_min = int(self.check_property(protocol_id, "length_min", -1))
+        if mcbitnum < length_min:
+            return []
+        length_max = int(self.check_property(protocol_id, "length_max", 9999))
+        if mcbitnum > length_max:
+            return []
+        clockrange = self.get_property(protocol_id, "clockrange")
+        if clockrange and len(clockrange) >= 2:
+            clock_min, clock_max = clockrange, clockrange
+            if not (clock > clock_min and clock < clock_max):
+                return []
+        raise NotImplementedError("strict-mode MC for a protocol without clockrange (reference reaches its "
+                                  "method-call bug); use mc_mode='fixed'")
+
+    def demodulate_mc_batch(self, messages: Sequence[Dict[str, Any]], msg_type: str = "MC",
+                            version: Optional[str] = None, raise_errors: bool = False):
+        """'fixed' MC chain on the GPU; accepts MCParser dicts (raw_hex/clock/mcbitnum/messagetype)
+        or demodulate_mc dicts (data/clock/bit_length)."""
+        frames = []
+        for m in messages:
+            hx = m.get("raw_hex", m.get("data", m.get("D", "")))
+            clk = m.get("clock", m.get("C", 0))
+            L = m.get("mcbitnum", m.get("bit_length", m.get("L", 0)))
+            mt = m.get("messagetype", msg_type if msg_type in ("MC", "Mc") else "MC")
+            frames.append((hx, int(clk), int(L), mt, m.get("version", version)))
+        mb = packing.mc_batch_from_frames(frames)
+        eng = self._ensure()
+        desc, rec, heap = eng.run(runtime.KIND_MC, eng.to_device_mc(mb))
+        only = [m.get("protocol_id") for m in messages]
+        bk = self._bank
+        hb = heap.tobytes()
+        out: List[Any] = []
+        for i in range(len(desc)):
+            d = desc[i]
+            if d["status"] == runtime.ST_RAISED:
+                exc = runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)("reference raises on this MC frame")
+                if raise_errors:
+                    raise exc
+                out.append(exc)
+                continue
+            if d["status"] != runtime.ST_OK:
+                raise RuntimeError(f"device status {int(d['status'])} for frame {i}")
+            res = []
+            for r in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
+                pid = bk.mc_pids[int(r["proto"])]
+                if only[i] and pid != only[i]:
+                    continue
+                off = int(r["payload_off"])
+                res.append({"protocol_id": str(pid), "payload": hb[off: off + int(r["payload_len"])].decode("latin-1"),
+                            "meta": {"protocol_id": pid, "rssi": None, "freq_afc": None}})
+            out.append(res)
+        return out

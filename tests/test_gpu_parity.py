@@ -1,0 +1,142 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the reference goldens and the CPU oracle.
+
+Bit-exact for everything (integer/byte/string work; the fp64 normalisation must reproduce
+Python's round(x, 1) exactly, which the results below depend on)."""
+import numpy as np
+import pytest
+
+from oracle import sd_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def proto():
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    return SDProtocols()
+
+
+@pytest.fixture(scope="module")
+def obank():
+    return O.OracleBank()
+
+
+def _flat(res):
+    if isinstance(res, BaseException):
+        return {"raise": type(res).__name__}
+    return {"results": [[r["protocol_id"], r["payload"], r["meta"]["bit_length"], r["meta"]["rssi"],
+                         r["meta"]["clock"]] for r in res]}
+
+
+def _oracle(ob, msg, kind):
+    try:
+        return _flat(O.demod(ob, dict(msg), kind))
+    except Exception as e:
+        return {"raise": type(e).__name__}
+
+
+@pytest.mark.parametrize("kind,fname", [("MU", "mu_golden.json.gz"), ("MS", "ms_golden.json.gz")])
+def test_golden_vectors(proto, golden, kind, fname):
+    cases = golden(fname)
+    got = proto.demodulate_batch([c["msg"] for c in cases], kind)
+    bad = [(i, c["src"], c["exp"], _flat(g)) for i, (c, g) in enumerate(zip(cases, got)) if _flat(g) != c["exp"]]
+    assert not bad, f"{len(bad)}/{len(cases)} mismatches; first: {bad[:3]}"
+
+
+def test_golden_mc_fixed(golden):
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    p = SDProtocols(mc_mode="fixed")
+    frames = golden("mc_golden.json.gz")
+    msgs = [{"raw_hex": f["hex"], "clock": f["clock"], "mcbitnum": f["L"], "messagetype": f["mtype"],
+             "version": f["version"]} for f in frames]
+    got = p.demodulate_mc_batch(msgs)
+    bad = []
+    for f, g in zip(frames, got):
+        gg = {"raise": type(g).__name__} if isinstance(g, BaseException) else \
+            {"results": [[r["protocol_id"], r["payload"]] for r in g]}
+        if gg != f["fixed"]:
+            bad.append((f, gg))
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:2]}"
+
+
+def test_mc_strict_reference_behaviour(proto, golden):
+    frames = golden("mc_golden.json.gz")[:300]
+    mc_ids = proto.get_keys("clockrange")
+    for f in frames:
+        for pid, (kind, val) in zip(mc_ids, f["strict"]):
+            msg = {"protocol_id": pid, "data": f["hex"], "clock": f["clock"], "bit_length": f["L"]}
+            try:
+                r = proto.demodulate_mc(msg, f["mtype"], version=f["version"])
+                got = ["ok", [[x["protocol_id"], x["payload"]] for x in r]]
+            except Exception as e:
+                got = ["raise", type(e).__name__]
+            assert got == [kind, val]
+    assert proto.demodulate_mc({"raw_hex": "AA", "clock": "450", "mcbitnum": "8"}, "MC") == []
+
+
+@pytest.mark.parametrize("kind,seed,n", [("MU", 1234, 2000), ("MS", 4321, 4000)])
+def test_synthetic_vs_oracle(proto, obank, kind, seed, n):
+    from pysignalduino_amd import synth
+    gen = synth.mu_corpus if kind == "MU" else synth.ms_corpus
+    pb = gen(proto.get_protocol_list(), n, seed=seed)
+    msgs = [pb.to_msg_dict(i) for i in range(pb.n)]
+    got = proto.demodulate_batch(msgs, kind)
+    bad = []
+    for i, (m, g) in enumerate(zip(msgs, got)):
+        exp = _oracle(obank, m, kind)
+        if _flat(g) != exp:
+            bad.append((i, m, exp, _flat(g)))
+    assert not bad, f"{len(bad)}/{n} mismatches; first: {bad[:2]}"
+
+
+def test_long_messages_vs_oracle(proto, obank):
+    """Messages beyond 256 pulses run through the long-message kernel variant."""
+    from pysignalduino_amd import synth
+    P = proto.get_protocol_list()
+    msgs = []
+    for npulse in (257, 300, 512, 1000):
+        pb = synth.mu_corpus(P, 40, seed=npulse, npulse=npulse)
+        msgs += [pb.to_msg_dict(i) for i in range(pb.n)]
+    got = proto.demodulate_batch(msgs, "MU")
+    bad = [(m, _oracle(obank, m, "MU"), _flat(g)) for m, g in zip(msgs, got) if _flat(g) != _oracle(obank, m, "MU")]
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:1]}"
+
+
+def test_edge_cases(proto, obank):
+    edges = [
+        ({"data": "", "P0": "1"}, "MU"),
+        ({"P0": "500", "P1": "-1000", "data": "0101010101", "CP": "0"}, "MU"),
+        ({"P0": "1e3", "P1": " -500 ", "P2": "nan", "P3": "inf", "data": "0101010123", "CP": "0"}, "MU"),
+        ({"P0": "500", "P1": "-5000", "data": "01٣1", "CP": "0", "SP": "1"}, "MS"),
+        ({"P0": "500", "P1": "-5000", "data": "0101", "CP": "٠", "SP": "1"}, "MS"),
+        ({"P0": "-0", "P1": "-5000", "data": "0101", "CP": "0", "SP": "1"}, "MS"),
+    ]
+    for msg, kind in edges:
+        got = proto.demodulate_batch([msg], kind)[0]
+        assert _flat(got) == _oracle(obank, msg, kind), msg
+
+
+def test_size_independent_properties(proto):
+    """At larger sizes: results are independent of batch composition (sharding invariance)
+    and deterministic across runs."""
+    from pysignalduino_amd import runtime, synth
+    pb = synth.mu_corpus(proto.get_protocol_list(), 20000, seed=99)
+    eng = proto._ensure()
+    bd = eng.to_device_pulses(pb)
+    d1, r1, h1 = eng.run(runtime.KIND_MU, bd)
+    d2, r2, h2 = eng.run(runtime.KIND_MU, bd)
+
+    def per_msg(desc, rec, heap):
+        hb = heap.tobytes()
+        out = []
+        for d in desc:
+            rs = rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]
+            out.append((int(d["status"]), tuple((int(r["proto"]), int(r["bit_length"]),
+                                                 hb[int(r["payload_off"]): int(r["payload_off"]) + int(r["payload_len"])])
+                                                for r in rs)))
+        return out
+    a = per_msg(d1, r1, h1)
+    assert a == per_msg(d2, r2, h2)
+    half = pb.subset(np.arange(10000, 20000))
+    d3, r3, h3 = eng.run(runtime.KIND_MU, eng.to_device_pulses(half))
+    assert per_msg(d3, r3, h3) == a[10000:]
