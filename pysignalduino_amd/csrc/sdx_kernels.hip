@@ -25,14 +25,17 @@
 
 namespace sdx {
 
-constexpr int REC_CAP = 160;   // staged results per wave per tile
-constexpr int HEAP_CAP = 4096; // staged payload bytes per wave per tile
+constexpr int REC_CAP = 160;     // MC: staged results per wave
+constexpr int HEAP_CAP = 4096;   // MC: staged payload bytes per wave
+constexpr int POOL_REC = 640;    // MU/MS: staged results per tile (shared by the 4 waves)
+constexpr int POOL_HEAP = 16384; // MU/MS: staged payload bytes per tile
 
 struct StageRec {
   uint32_t off;
   uint16_t len, proto;
   uint32_t bitlen;
-  uint16_t msg, rank;
+  uint8_t msg, wave;
+  uint16_t rank;
 };
 
 template <int NW, int TM>
@@ -47,9 +50,6 @@ struct TileLds {
     uint64_t stream[NW + 18];
     uint8_t bits[NBITS];
     uint8_t bits2[NBITS];
-    StageRec rec[REC_CAP];
-    uint8_t heap[HEAP_CAP];
-    int nrec, nheap, ovf;
   };
   uint64_t bm[TM * MSTRIDE];
   int32_t nlen[TM];
@@ -60,6 +60,9 @@ struct TileLds {
   uint32_t wheap_pre[4];
   uint32_t mbase[TM];
   Wave w[4];
+  StageRec rec[POOL_REC];
+  uint8_t heap[POOL_HEAP];
+  int pool_nrec, pool_nheap, ovf;
 };
 
 SDX_DEV void wave_sync() {
@@ -75,29 +78,37 @@ SDX_DEV int lanes_below(uint64_t mask) {
 // ---------------------------------------------------------------------------------------------
 // staged-result helpers (wave-uniform callers)
 // ---------------------------------------------------------------------------------------------
-template <class W>
-SDX_DEV bool stage_reserve(W& wv, int total) {
-  if (wv.nrec >= REC_CAP || wv.nheap + total > HEAP_CAP) {
-    wv.ovf = 1;
-    return false;
+// allocate `total` payload bytes + one record in the tile pool (lane 0 does the LDS atomics);
+// returns the heap offset (broadcast to the wave) or -1 when the pool is full
+template <class T>
+SDX_DEV int pool_alloc(T& L, int total, int* rec_slot) {
+  int h = -1, r = -1;
+  if (lane_id() == 0) {
+    r = atomicAdd(&L.pool_nrec, 1);
+    h = atomicAdd(&L.pool_nheap, total);
+    if (r >= POOL_REC || h + total > POOL_HEAP) {
+      L.ovf = 1;
+      h = -1;
+    }
   }
-  return true;
+  h = bcast_i(h, 0);
+  *rec_slot = bcast_i(r, 0);
+  return h;
 }
 
 template <class T>
-SDX_DEV void stage_commit(T& L, typename T::Wave& wv, int wave, int msg_local, int proto, int total, int bitlen) {
+SDX_DEV void pool_commit(T& L, int slot, int wave, int msg_local, int proto, int off, int total, int bitlen) {
   if (lane_id() == 0) {
     StageRec r;
-    r.off = (uint32_t)wv.nheap;
+    r.off = (uint32_t)off;
     r.len = (uint16_t)total;
     r.proto = (uint16_t)proto;
     r.bitlen = (uint32_t)bitlen;
-    r.msg = (uint16_t)msg_local;
+    r.msg = (uint8_t)msg_local;
+    r.wave = (uint8_t)wave;
     r.rank = L.cnt[wave][msg_local];
-    wv.rec[wv.nrec] = r;
     L.cnt[wave][msg_local] = (uint16_t)(r.rank + 1);
-    wv.nrec = wv.nrec + 1;
-    wv.nheap = wv.nheap + total;
+    L.rec[slot] = r;
   }
   wave_sync();
 }
@@ -190,29 +201,66 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   } else {
     dlen = -2;  // computed below
   }
-  // stage payload = preamble + dmsg + postamble
-  if (!stage_reserve(W, rec->pre_len + (dlen >= 0 ? dlen : (nbp + 3) / 4) + rec->post_len)) return;
-  uint8_t* dst = W.heap + W.nheap;
-  copy_str(dst, bv.str + rec->pre_off, rec->pre_len);
-  uint8_t* dm = dst + rec->pre_len;
-  if (rec->dispatch_bin) {
-    for (int i = lane_id(); i < nbp; i += WAVE) dm[i] = buf[i] == 2 ? 'F' : (uint8_t)('0' + buf[i]);
-  } else if (isf) {
-    if (lane_id() == 0) { dm[0] = 'N'; dm[1] = 'o'; dm[2] = 'n'; dm[3] = 'e'; }
-  } else {
-    dlen = hex_digits(buf, nbp, dm, rec->remove_zero);
+  // hex digit geometry (helpers.py:28-64) and str.lstrip('0') for remove_zero
+  const int nd = (nbp + 3) >> 2;
+  int skip = 0;
+  if (dlen == -2) {
+    if (rec->remove_zero) {
+      skip = nd;
+      for (int d0 = 0; d0 < nd; d0 += WAVE) {
+        const int d = d0 + lane_id();
+        int v = 0;
+        if (d < nd) {
+          const int e = nbp - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+          for (int i = a; i < e; ++i) v = (v << 1) | buf[i];
+        }
+        const uint64_t nz = ballot(d < nd && v != 0);
+        if (nz) {
+          skip = d0 + ffs64(nz);
+          break;
+        }
+      }
+    }
+    dlen = nd - skip;
   }
-  wave_sync();
-  copy_str(dm + dlen, bv.str + rec->post_off, rec->post_len);
-  wave_sync();
-  const int total = rec->pre_len + dlen + rec->post_len;
-  if (rec->mm_dfa >= 0) {  // re.search(modulematch, payload) (:277-280)
+  auto dchar = [&](int d) -> uint8_t {  // character d of dmsg, computed from the bits
+    if (rec->dispatch_bin) return buf[d] == 2 ? 'F' : (uint8_t)('0' + buf[d]);
+    if (isf) return (uint8_t)"None"[d];
+    const int dd = d + skip, e = nbp - 4 * (nd - 1 - dd), a = (e - 4 > 0) ? e - 4 : 0;
+    int v = 0;
+    for (int i = a; i < e; ++i) v = (v << 1) | buf[i];
+    return (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+  };
+  if (rec->mm_dfa >= 0) {  // re.search(modulematch, payload) (:277-280) before staging anything
     int ok = 0;
-    if (lane_id() == 0) ok = dfa_accepts(bv, rec->mm_dfa, rec->mm_pre_state, dm, dlen + rec->post_len);
-    ok = bcast_i(ok, 0);
-    if (!ok) return;
+    if (lane_id() == 0) {
+      const sdx_dfa D = bv.dfa[rec->mm_dfa];
+      const uint16_t* tr = bv.trans + D.trans_off;
+      const uint8_t* fl = bv.dflags + D.flags_off;
+      const int ncls = (int)bv.hdr->n_class;
+      int st = rec->mm_pre_state;
+      const int tot = dlen + rec->post_len;
+      int i = 0;
+      for (; i < tot; ++i) {
+        const uint8_t f = fl[st];
+        if (f & 5) break;  // accepted or dead
+        const uint8_t c = i < dlen ? dchar(i) : bv.str[rec->post_off + i - dlen];
+        st = tr[st * ncls + bv.cls[c]];
+      }
+      const uint8_t f = fl[st];
+      ok = (f & 1) ? 1 : ((f & 4) ? 0 : ((i == tot && (f & 2)) ? 1 : 0));
+    }
+    if (!bcast_i(ok, 0)) return;
   }
-  stage_commit(L, W, wave, s, p, total, nbp);
+  const int total = rec->pre_len + dlen + rec->post_len;
+  int slot;
+  const int off = pool_alloc(L, total, &slot);
+  if (off < 0) return;
+  uint8_t* dst = L.heap + off;
+  copy_str(dst, bv.str + rec->pre_off, rec->pre_len);
+  for (int d = lane_id(); d < dlen; d += WAVE) dst[rec->pre_len + d] = dchar(d);
+  copy_str(dst + rec->pre_len + dlen, bv.str + rec->post_off, rec->post_len);
+  pool_commit(L, slot, wave, s, p, off, total, nbp);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -395,13 +443,16 @@ SDX_DEV void finish_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   }
   if (any_float(buf, nb)) return;  // bin_str_2_hex_str -> None -> skipped (:224-226)
   const int dl = (nb + 3) / 4;
-  if (!stage_reserve(W, rec->pre_len + dl + rec->post_len)) return;
-  uint8_t* dst = W.heap + W.nheap;
+  const int total = rec->pre_len + dl + rec->post_len;
+  int slot;
+  const int off = pool_alloc(L, total, &slot);
+  if (off < 0) return;
+  uint8_t* dst = L.heap + off;
   copy_str(dst, bv.str + rec->pre_off, rec->pre_len);
   hex_digits(buf, nb, dst + rec->pre_len, 0);
   copy_str(dst + rec->pre_len + dl, bv.str + rec->post_off, rec->post_len);
   wave_sync();
-  stage_commit(L, W, wave, s, p, rec->pre_len + dl + rec->post_len, nb);
+  pool_commit(L, slot, wave, s, p, off, total, nb);
 }
 
 // MS decode loop (:172-189) for one surviving pair, wave-cooperative over chunks
@@ -490,21 +541,16 @@ SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
 // ---------------------------------------------------------------------------------------------
 template <int NW, int TM>
 SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x;
   if (tid == 0) {
-    int bad = 0;
-    for (int w = 0; w < 4; ++w) bad |= L.w[w].ovf;
-    L.tile_bad = bad;
-    uint32_t nrec = 0, nheap = 0;
+    int bad = L.ovf ? 1 : 0;
+    uint32_t nrec = 0;
     for (int m = 0; m < nvalid; ++m) {
       L.mbase[m] = nrec;
       if (L.raise_key[m] == 0xFFFFFFFFu && !bad)
         for (int w = 0; w < 4; ++w) nrec += L.cnt[w][m];
     }
-    for (int w = 0; w < 4; ++w) {
-      L.wheap_pre[w] = nheap;
-      nheap += L.w[w].nheap;
-    }
+    const uint32_t nheap = bad ? 0u : (uint32_t)L.pool_nheap;
     uint32_t rb = 0, hb = 0;
     if (!bad) {
       rb = atomicAdd(&out.cursor_dev[0], nrec);
@@ -523,23 +569,24 @@ SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const
   __syncthreads();
   const int bad = L.tile_bad;
   if (!bad) {
-    auto& W = L.w[wave];
-    for (int r = lane; r < W.nrec; r += WAVE) {
-      const StageRec sr = W.rec[r];
+    const int nr = L.pool_nrec;
+    for (int r = tid; r < nr; r += blockDim.x) {
+      const StageRec sr = L.rec[r];
       if (L.raise_key[sr.msg] != 0xFFFFFFFFu) continue;
       uint32_t before = 0;
-      for (int w = 0; w < wave; ++w) before += L.cnt[w][sr.msg];
+      for (int w = 0; w < (int)sr.wave; ++w) before += L.cnt[w][sr.msg];
       const uint32_t dst = L.rec_base + L.mbase[sr.msg] + before + sr.rank;
       sdx_result o;
-      o.payload_off = L.heap_base + L.wheap_pre[wave] + sr.off;
+      o.payload_off = L.heap_base + sr.off;
       o.payload_len = sr.len;
       o.proto = sr.proto;
       o.bit_length = sr.bitlen;
       o.msg = (uint32_t)msg_of[sr.msg];
       out.rec_dev[dst] = o;
     }
-    uint8_t* hd = out.heap_dev + L.heap_base + L.wheap_pre[wave];
-    for (int i = lane; i < W.nheap; i += WAVE) hd[i] = W.heap[i];
+    uint8_t* hd = out.heap_dev + L.heap_base;
+    const int nh = L.pool_nheap;
+    for (int i = tid; i < nh; i += blockDim.x) hd[i] = L.heap[i];
   }
   for (int m = tid; m < nvalid; m += blockDim.x) {
     sdx_desc d;
@@ -582,10 +629,10 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     L.raise_key[tid] = 0xFFFFFFFFu;
     for (int w = 0; w < 4; ++w) L.cnt[w][tid] = 0;
   }
-  if (lane == 0) {
-    L.w[wave].nrec = 0;
-    L.w[wave].nheap = 0;
-    L.w[wave].ovf = 0;
+  if (tid == 0) {
+    L.pool_nrec = 0;
+    L.pool_nheap = 0;
+    L.ovf = 0;
   }
   __syncthreads();
   // ---- stage: per-id position bitmaps (coalesced 64-character rows, 10 ballots each)
