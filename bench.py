@@ -43,13 +43,14 @@ def cpu_baseline(P, budget_s: float):
     from oracle import sd_oracle as O
     from pysignalduino_amd import synth
     ob = O.OracleBank()
-    mu = synth.mu_corpus(P, 400, seed=9001)
-    ms = synth.ms_corpus(P, 400, seed=9002)
-    mc = synth.mc_corpus(P, 400, seed=9003)
+    NS = 6000
+    mu = synth.mu_corpus(P, NS, seed=9001)
+    ms = synth.ms_corpus(P, NS, seed=9002)
+    mc = synth.mc_corpus(P, NS, seed=9003)
     t0 = time.perf_counter()
     done = 0
     i = 0
-    while time.perf_counter() - t0 < budget_s and i < 400:
+    while time.perf_counter() - t0 < budget_s and i < NS:
         for kind, b in (("MU", mu), ("MS", ms)):
             try:
                 O.demod(ob, b.to_msg_dict(i), kind)
@@ -81,6 +82,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from pysignalduino_amd import bank as bankmod, runtime, synth
+    from pysignalduino_amd import dist as sdist
     bk = bankmod.Bank()
     P = bk.protocols
     eng = runtime.Engine(bk, local)
@@ -110,19 +112,11 @@ def main():
                 eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, outs[k])
             if record:
                 ev[k][1].record(stream)
-        if world > 1:  # RCCL all-gather of the decoded dmsg buffers (config 5)
-            for k in outs:
+        if world > 1:  # RCCL all-gather of the decoded dmsg buffers (config 5), pysignalduino_amd/dist.py
+            for k, bd in (("MU", bmu), ("MS", bms), ("MC", bmc)):
                 o = outs[k]
-                used = o["cursor"][:2].clone()
-                mx = used.clone()
-                dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-                hb = int(mx[1].item())
-                hb = max(hb, 1)
-                gh = torch.empty(world * hb, dtype=torch.uint8, device=dev)
-                dist.all_gather_into_tensor(gh, o["heap"][:hb].contiguous())
-                rb = max(int(mx[0].item()), 1) * runtime.RES_DT.itemsize
-                gr = torch.empty(world * rb, dtype=torch.uint8, device=dev)
-                dist.all_gather_into_tensor(gr, o["rec"][:rb].contiguous())
+                cur = o["cursor"].cpu()
+                sdist.allgather_results(o["desc"], o["rec"], o["heap"], bd["n"], int(cur[0]), int(cur[1]))
 
     for _ in range(args.warmup):
         step()

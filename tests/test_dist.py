@@ -1,0 +1,111 @@
+"""N>1 path on CPU: world_size-2 gloo run of the shard + all-gather step (pysignalduino_amd/dist.py).
+
+Each rank encodes the oracle's results for its contiguous shard into the device result-buffer
+format (sdx_desc / sdx_result / heap), all-gathers, and must reconstruct exactly the results of
+the un-sharded stream."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import sd_oracle as O
+from pysignalduino_amd import dist as sdist
+from pysignalduino_amd import runtime, synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def encode(results, pids):
+    desc = np.zeros(len(results), runtime.DESC_DT)
+    recs, heap = [], bytearray()
+    for i, res in enumerate(results):
+        desc[i]["rec_begin"] = len(recs)
+        if isinstance(res, Exception):
+            desc[i]["status"] = runtime.ST_RAISED
+            desc[i]["raise_kind"] = 1
+            continue
+        desc[i]["n_rec"] = len(res)
+        for r in res:
+            b = r["payload"].encode("latin-1")
+            recs.append((len(heap), len(b), pids.index(r["protocol_id"]), r["meta"]["bit_length"], i))
+            heap += b
+    rec = np.array(recs, dtype=runtime.RES_DT) if recs else np.zeros(0, runtime.RES_DT)
+    return desc, rec, np.frombuffer(bytes(heap), np.uint8)
+
+
+def decode(desc, rec, heap, pids):
+    out = []
+    hb = heap.tobytes()
+    for d in desc:
+        if d["status"] == runtime.ST_RAISED:
+            out.append("raise")
+            continue
+        rs = rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]
+        out.append([(pids[int(r["proto"])], hb[int(r["payload_off"]): int(r["payload_off"]) + int(r["payload_len"])],
+                     int(r["bit_length"])) for r in rs])
+    return out
+
+
+def _oracle_results(msgs):
+    ob = O.OracleBank()
+    res = []
+    for m in msgs:
+        try:
+            res.append(O.demod(ob, dict(m), "MU"))
+        except Exception as e:
+            res.append(e)
+    return res
+
+
+def _worker(rank, world, port, msgs, pids, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = sdist.shard_bounds(len(msgs), rank, world)
+    d, r, h = encode(_oracle_results(msgs[lo:hi]), pids)
+    td = torch.from_numpy(d.view(np.uint8).copy())
+    tr = torch.from_numpy(r.view(np.uint8).copy()) if len(r) else torch.zeros(1, dtype=torch.uint8)
+    th = torch.from_numpy(h.copy()) if len(h) else torch.zeros(1, dtype=torch.uint8)
+    gd, gr, gh = sdist.allgather_results(td, tr, th, hi - lo, len(r), len(h))
+    got = decode(gd.numpy().view(runtime.DESC_DT), gr.numpy().view(runtime.RES_DT), gh.numpy(), pids)
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+def test_shard_bounds():
+    for n in (0, 1, 7, 100, 1001):
+        for w in (1, 2, 3, 8):
+            spans = [sdist.shard_bounds(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_gloo_world2_allgather_matches_unsharded():
+    from pysignalduino_amd import bank
+    P = bank.load_protocols()
+    pb = synth.mu_corpus(P, 120, seed=5)
+    msgs = [pb.to_msg_dict(i) for i in range(pb.n)]
+    pids = bank.Bank().mu_pids
+    full = decode(*encode(_oracle_results(msgs), pids), pids)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, msgs, pids, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, got in outs:
+        assert got == full, f"rank {rank} gathered stream differs"
