@@ -202,6 +202,10 @@ class Bank:
             rec["width"] = len(one) if one else 0
             if one and lens and rec["width"] != next(iter(lens)):
                 raise NotImplementedError(f"MU {pid}: len(one) differs from unit length")
+            if not rec["has_start"] and rec["length_min"] == 0 and not rec["never"]:
+                raise NotImplementedError(f"MU {pid}: no start and length_min 0 (empty matches) not modelled")
+            if rec["width"] not in (0, 1, 2, 4):
+                raise NotImplementedError(f"MU {pid}: unit width {int(rec['width'])} not in (1, 2, 4)")
             rec["recon"] = 1 if p.get("reconstructBit") else 0
             rec["dispatch_bin"] = 1 if _int_exact(p.get("dispatchBin", 0), "dispatchBin") == 1 else 0
             pad = _int_exact(p.get("paddingbits", 4), f"MU {pid} paddingbits")

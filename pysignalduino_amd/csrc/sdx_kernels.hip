@@ -16,12 +16,30 @@
 //              with one global atomic per tile for the record/heap space.
 // MC engine (k_mc): lane = frame, the 12 clockrange protocols are a uniform loop.
 #include "sdx_device.h"
+#include "sdx_lane.h"
 
 #include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+
+#ifdef SDX_PROF
+__device__ unsigned long long g_prof[32];
+#define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(slot, v)                                                                   \
+  do {                                                                                      \
+    if (__lane_id() == 0) L.prof[wave][slot] += __builtin_amdgcn_s_memtime() - (v);        \
+  } while (0)
+#define PROF_CNT(slot, x)                                                                   \
+  do {                                                                                      \
+    if (__lane_id() == 0) L.prof[wave][slot] += (unsigned long long)(x);                   \
+  } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(slot, v)
+#define PROF_CNT(slot, x)
+#endif
 
 namespace sdx {
 
@@ -63,6 +81,9 @@ struct TileLds {
   StageRec rec[POOL_REC];
   uint8_t heap[POOL_HEAP];
   int pool_nrec, pool_nheap, ovf;
+#ifdef SDX_PROF
+  unsigned long long prof[4][32];
+#endif
 };
 
 SDX_DEV void wave_sync() {
@@ -170,6 +191,7 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
                        int nb) {
   auto& W = L.w[wave];
   uint8_t* buf = W.bits;
+  PROF_T(t_pd);
   // postDemodulation (:231-250): 'F' -> int() ValueError caught -> bits unchanged
   if (rec->postdemo != SDX_PD_NONE && !any_float(buf, nb)) {
     int rc = 0, no = 0;
@@ -183,6 +205,8 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
       nb = no;
     }  // rc == -1: ValueError inside the method, caught -> bits unchanged
   }
+  PROF_ADD(7, t_pd);
+  PROF_T(t_fmt);
   // padding (:257-259), after postDemod
   const int pad = rec->pad_bits;
   int nbp = nb;
@@ -250,8 +274,10 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
       const uint8_t f = fl[st];
       ok = (f & 1) ? 1 : ((f & 4) ? 0 : ((i == tot && (f & 2)) ? 1 : 0));
     }
+    PROF_ADD(9, t_fmt);
     if (!bcast_i(ok, 0)) return;
   }
+  PROF_T(t_wr);
   const int total = rec->pre_len + dlen + rec->post_len;
   int slot;
   const int off = pool_alloc(L, total, &slot);
@@ -261,6 +287,8 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   for (int d = lane_id(); d < dlen; d += WAVE) dst[rec->pre_len + d] = dchar(d);
   copy_str(dst + rec->pre_len + dlen, bv.str + rec->post_off, rec->post_len);
   pool_commit(L, slot, wave, s, p, off, total, nbp);
+  PROF_ADD(8, t_wr);
+  PROF_CNT(20, 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -279,6 +307,8 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   const int lenS = rec->has_start ? (int)rec->start.len : 0;
   const uint64_t ut[3] = {ut0, ut1, ut2};
   const uint8_t SYM[3] = {1, 0, 2};
+  PROF_T(t_setup);
+  PROF_CNT(21, 1);
   // pattern_lookup: distinct unit strings, value = last writer (:122)
   uint64_t uni[3] = {0, 0, 0};
   uint8_t usym[3] = {0, 0, 0};
@@ -358,7 +388,9 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   };
   const int lmin = rec->length_min;
   int pos = idx;
+  PROF_ADD(4, t_setup);
   while (true) {
+    PROF_T(t_scan);
     // first s >= pos where START occurs and >= length_min units follow
     int sfound = -1, kfound = 0;
     const int last = n - lenS;
@@ -375,7 +407,9 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
         break;
       }
     }
+    PROF_ADD(5, t_scan);
     if (sfound < 0) break;
+    PROF_CNT(22, 1);
     const int q = sfound + lenS, e0 = q + kfound * Lw;
     int em = -1;
     for (int j = 0; j < ne; ++j)
@@ -391,6 +425,7 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
     pos = q + G;
     const int nchunks = kfound + (em >= 0 ? 1 : 0);
     if (nchunks > rec->length_max) continue;  // (:217-218)
+    PROF_T(t_bits);
     for (int i = lane; i < kfound; i += WAVE) {
       const int x = q + i * Lw;
       uint8_t sy = 0;
@@ -400,8 +435,205 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
     }
     if (em >= 0 && lane == 0) W.bits[kfound] = esym[em];
     wave_sync();
+    PROF_ADD(6, t_bits);
     finish_mu(L, wave, bv, rec, p, s, nchunks);
     if ((L.raise_key[s] >> 8) <= (uint32_t)p) return;  // this protocol made the message raise
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MU, lane = message (short variant): finish one match (message_unsynced.py:230-290).
+// The chunk symbols are not materialised unless a postDemod method needs them: symbol b is
+// read from the unit masks at position q + b*Lw (V1: units mapping to '1', VF: to 'F').
+// ---------------------------------------------------------------------------------------------
+template <int NW>
+SDX_DEV M<NW> m_range(int a, int b) {  // positions [a, b)
+  M<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int lo = a - 64 * i, hi = b - 64 * i;
+    uint64_t w = 0;
+    if (hi > 0 && lo < 64) {
+      w = ~0ull;
+      if (lo > 0) w &= ~0ull << lo;
+      if (hi < 64) w &= (hi > 0) ? ((1ull << hi) - 1) : 0ull;
+    }
+    r.w[i] = w;
+  }
+  return r;
+}
+
+template <int NW, int TM>
+SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int mi,
+                            int q, int k, int Lw, bool emf, uint8_t esym, const M<NW>& V1, const M<NW>& VF) {
+  constexpr int NB = 64 * NW + 64;
+  int nb = k + ((emf && Lw > 1) ? 1 : 0);
+  // the chunk symbols as two packed bitstrings: P1 = symbol '1', PF = symbol 'F'
+  M<NW> P1 = m_stride_extract(V1, q, Lw, k), PF = m_stride_extract(VF, q, Lw, k);
+  if (nb > k) {
+    if (esym == 1) m_set(P1, k);
+    if (esym == 2) m_set(PF, k);
+  }
+  bool anyf = m_any(PF);
+  uint8_t pout[NB];
+  bool usearr = false;
+  if (rec->postdemo != SDX_PD_NONE && !anyf) {  // 'F' -> int() ValueError caught -> unchanged
+    uint8_t pin[NB];
+    for (int b = 0; b < nb; ++b) pin[b] = m_test(P1, b) ? 1 : 0;
+    int no = 0;
+    const int rc = run_postdemo(rec->postdemo, pin, nb, pout, &no);
+    if (rc == 0) return;  // rcode < 1: match dropped
+    if (rc == 1) {
+      usearr = true;
+      nb = no;
+    }
+  }
+  const int pad = rec->pad_bits;
+  int nbp = nb;
+  while (nbp % pad) ++nbp;
+  const int nd = (nbp + 3) >> 2;
+  auto digit = [&](int d) -> int {  // hex digit d of bin_str_2_hex_str (helpers.py:28-64)
+    const int e = nbp - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+    if (!usearr) return m_nibble(P1, a, e - a);  // bits >= nb are the '0' padding
+    int v = 0;
+    for (int i = a; i < e; ++i) v = (v << 1) | (i < nb ? pout[i] : 0);
+    return v;
+  };
+  int dlen, skip = 0;
+  if (rec->dispatch_bin) {
+    dlen = nbp;
+  } else if (anyf) {
+    if (rec->remove_zero) {  // None.lstrip('0') -> AttributeError (:269)
+      atomicMin(&L.raise_key[mi], ((uint32_t)p << 8) | SDX_RAISE_ATTRIBUTE);
+      return;
+    }
+    dlen = 4;
+  } else {
+    if (rec->remove_zero)
+      while (skip < nd && digit(skip) == 0) ++skip;
+    dlen = nd - skip;
+  }
+  auto dchar = [&](int i) -> uint8_t {
+    if (rec->dispatch_bin) {
+      if (usearr) return (uint8_t)('0' + (i < nb ? pout[i] : 0));
+      return m_test(PF, i) ? 'F' : (uint8_t)('0' + (m_test(P1, i) ? 1 : 0));
+    }
+    if (anyf) return (uint8_t)"None"[i];
+    const int v = digit(i + skip);
+    return (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+  };
+  if (rec->mm_dfa >= 0) {  // re.search(modulematch, payload) (:277-280)
+    const sdx_dfa D = bv.dfa[rec->mm_dfa];
+    const uint16_t* tr = bv.trans + D.trans_off;
+    const uint8_t* fl = bv.dflags + D.flags_off;
+    const int ncls = (int)bv.hdr->n_class;
+    int st = rec->mm_pre_state;
+    const int tot = dlen + rec->post_len;
+    int i = 0;
+    for (; i < tot; ++i) {
+      if (fl[st] & 5) break;
+      const uint8_t c = i < dlen ? dchar(i) : bv.str[rec->post_off + i - dlen];
+      st = tr[st * ncls + bv.cls[c]];
+    }
+    const uint8_t f = fl[st];
+    if (!((f & 1) || (!(f & 4) && i == tot && (f & 2)))) return;
+  }
+  const int total = rec->pre_len + dlen + rec->post_len;
+  const int slot = atomicAdd(&L.pool_nrec, 1);
+  const int off = atomicAdd(&L.pool_nheap, total);
+  if (slot >= POOL_REC || off + total > POOL_HEAP) {
+    L.ovf = 1;
+    return;
+  }
+  uint8_t* dst = L.heap + off;
+  for (int i = 0; i < rec->pre_len; ++i) dst[i] = bv.str[rec->pre_off + i];
+  for (int i = 0; i < dlen; ++i) dst[rec->pre_len + i] = dchar(i);
+  for (int i = 0; i < rec->post_len; ++i) dst[rec->pre_len + dlen + i] = bv.str[rec->post_off + i];
+  StageRec r;
+  r.off = (uint32_t)off;
+  r.len = (uint16_t)total;
+  r.proto = (uint16_t)p;
+  r.bitlen = (uint32_t)nbp;
+  r.msg = (uint8_t)mi;
+  r.wave = (uint8_t)wave;
+  r.rank = L.cnt[wave][mi];
+  L.cnt[wave][mi] = (uint16_t)(r.rank + 1);
+  L.rec[slot] = r;
+}
+
+// MU, lane = message: exact re.finditer emulation on register bitmasks (message_unsynced.py:146-290)
+template <int NW, int TM>
+SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p,
+                            int mi, const uint64_t* bm, int n, int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1,
+                            uint64_t ut2, int fmask) {
+  const int Lw = rec->width;
+  const int lenS = rec->has_start ? (int)rec->start.len : 0;
+  const uint64_t ut[3] = {ut0, ut1, ut2};
+  const uint8_t SYM[3] = {1, 0, 2};
+  M<NW> U = m_zero<NW>(), V1 = m_zero<NW>(), VF = m_zero<NW>();
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    if (!((fmask >> kk) & 1)) continue;
+    uint8_t fs = SYM[kk];  // dict: the LAST writer of an identical string decides the symbol (:122)
+#pragma unroll
+    for (int j = kk + 1; j < 3; ++j)
+      if (((fmask >> j) & 1) && ut[j] == ut[kk]) fs = SYM[j];
+    const M<NW> occ = m_occ<NW>(bm, ut[kk], Lw);
+    U = m_or(U, occ);
+    if (fs == 1) V1 = m_or(V1, occ);
+    if (fs == 2) VF = m_or(VF, occ);
+  }
+  // end_pattern_lookup: pstr[:-1], first writer wins (:124-127); regex tail only with reconstructBit
+  uint64_t ek[3] = {0, 0, 0};
+  uint8_t es[3] = {0, 0, 0};
+  int ne = 0;
+  if (rec->recon && Lw > 1) {
+    const uint64_t msk = (Lw - 1 >= 16) ? ~0ull : ((1ull << (4 * (Lw - 1))) - 1);
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      if (!((fmask >> kk) & 1)) continue;
+      const uint64_t key = ut[kk] & msk;
+      bool seen = false;
+      for (int j = 0; j < ne; ++j) seen |= ek[j] == key;
+      if (!seen) {
+        ek[ne] = key;
+        es[ne] = SYM[kk];
+        ++ne;
+      }
+    }
+  }
+  const M<NW> S = lenS ? m_occ<NW>(bm, st_tgt, lenS) : m_all<NW>();
+  const int lmin = rec->length_min;
+  // s: START at s and >= length_min units at s+lenS (with length_min 0 every START qualifies,
+  // including one that ends exactly at the end of the data: empty group -> IndexError)
+  const M<NW> V = lmin > 0 ? m_and(S, m_shr(m_runs(U, lmin, Lw), lenS)) : S;
+  const M<NW> NU = m_not(U);
+  int pos = idx;
+  while (true) {
+    const int s = m_first(V, pos);
+    if (s < 0 || s > n) break;
+    const int q = s + lenS;
+    M<NW> Z = NU;
+    const uint64_t rw = residue_word(Lw, q % Lw);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) Z.w[i] &= rw;
+    int z = m_first(Z, q);
+    if (z < 0) z = q + Lw * ((64 * NW - q + Lw - 1) / Lw);
+    const int k = (z - q) / Lw;
+    const int e0 = q + k * Lw;
+    int em = -1;
+    for (int j = 0; j < ne && em < 0; ++j)
+      if (match_at(bm, NW, n, ek[j], Lw - 1, e0)) em = j;
+    const int G = k * Lw + (em >= 0 ? Lw - 1 : 0);
+    if (G == 0) {  // chunks == [] -> chunks[-1] IndexError (:212)
+      atomicMin(&L.raise_key[mi], ((uint32_t)p << 8) | SDX_RAISE_INDEX);
+      return;
+    }
+    pos = q + G;
+    const int nch = k + (em >= 0 ? 1 : 0);
+    if (nch > rec->length_max) continue;  // (:217-218)
+    finish_mu_lane(L, wave, bv, rec, p, mi, q, k, Lw, em >= 0, em >= 0 ? es[em] : (uint8_t)0, V1, VF);
+    if ((L.raise_key[mi] >> 8) <= (uint32_t)p) return;
   }
 }
 
@@ -465,6 +697,8 @@ SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   const uint64_t* bm = &L.bm[s * T::MSTRIDE];
   const int n = L.nlen[s];
   const int Wd = rec->width;
+  PROF_T(t_msd);
+  PROF_CNT(23, 1);
   const uint64_t kt[4] = {k0, k1, k2, k3};
   const int klen[4] = {rec->key[0].len, rec->key[1].len, rec->key[2].len, rec->key[3].len};
   const uint8_t KSYM[4] = {3, 1, 0, 2};  // 3 = '' (sync: no bit)
@@ -533,7 +767,10 @@ SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
     if (brk) break;
   }
   wave_sync();
+  PROF_ADD(10, t_msd);
+  PROF_T(t_msf);
   finish_ms(L, wave, bv, rec, p, s, nb);
+  PROF_ADD(11, t_msf);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -634,7 +871,12 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     L.pool_nheap = 0;
     L.ovf = 0;
   }
+#ifdef SDX_PROF
+  if (lane < 32) L.prof[wave][lane] = 0;
+#endif
   __syncthreads();
+  PROF_T(t_kernel);
+  PROF_T(t_stage);
   // ---- stage: per-id position bitmaps (coalesced 64-character rows, 10 ballots each)
   for (int mi = wave; mi < nvalid; mi += 4) {
     const int msg = msg_of[mi];
@@ -661,6 +903,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     }
   }
   __syncthreads();
+  PROF_ADD(0, t_stage);
   // ---- per-lane message state (lane = message of the tile)
   const int mi = lane;
   const bool mvalid = mi < nvalid;
@@ -702,6 +945,10 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
         if (k < npat) norm[k] = py_round1(val[k] / clock);
     }
   }
+  auto PEX = [&](const sdx_patspec* sp, int minpos) -> PexRes {
+    if constexpr (NW <= 4) return pexists_lane<NW>(sp, norm, ids, npat, bmine, minpos);
+    else return pattern_exists(sp, norm, ids, npat, bmine, T::WS, nw, minpos);
+  };
   // ---- protocol loop: this wave's contiguous quarter of the class table
   const int nproto = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu : (int)bv.hdr->n_ms;
   const int qn = (nproto + 3) / 4;
@@ -714,38 +961,52 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       int idx = 0;
       uint64_t st_tgt = 0, ut0 = 0, ut1 = 0, ut2 = 0;
       int fmask = 0;
+      PROF_T(t_norm);
       if (alive) {
         const double ck = rec->clock;
 #pragma unroll
         for (int k = 0; k < SDX_MAXPAT; ++k)
           if (k < npat) norm[k] = py_round1(val[k] / ck);
+      }
+      PROF_ADD(1, t_norm);
+      PROF_T(t_st);
+      if (alive) {
         if (rec->has_start) {
-          const PexRes r = pattern_exists(&rec->start, norm, ids, npat, bmine, T::WS, nw, 0);
+          const PexRes r = PEX(&rec->start, 0);
           alive = r.found;
           idx = r.pos;
           st_tgt = r.tgt;
         }
       }
+      PROF_ADD(2, t_st);
+      PROF_T(t_ozf);
       if (alive && rec->one.len) {
-        const PexRes r = pattern_exists(&rec->one, norm, ids, npat, bmine, T::WS, nw, idx);
+        const PexRes r = PEX(&rec->one, idx);
         if (r.found) { ut0 = r.tgt; fmask |= 1; } else alive = false;
       }
       if (alive && rec->zero.len) {
-        const PexRes r = pattern_exists(&rec->zero, norm, ids, npat, bmine, T::WS, nw, idx);
+        const PexRes r = PEX(&rec->zero, idx);
         if (r.found) { ut1 = r.tgt; fmask |= 2; } else alive = false;
       }
       if (alive && rec->flt.len) {
-        const PexRes r = pattern_exists(&rec->flt, norm, ids, npat, bmine, T::WS, nw, idx);
+        const PexRes r = PEX(&rec->flt, idx);
         if (r.found) { ut2 = r.tgt; fmask |= 4; }
       }
       alive = alive && fmask != 0;
-      uint64_t surv = ballot(alive);
-      while (surv) {
-        const int sl = ffs64(surv);
-        surv &= surv - 1;
-        decode_mu(L, wave, bv, rec, p, sl, bcast_i(idx, sl), bcast_u64(st_tgt, sl), bcast_u64(ut0, sl),
-                  bcast_u64(ut1, sl), bcast_u64(ut2, sl), bcast_i(fmask, sl));
+      PROF_ADD(3, t_ozf);
+      PROF_T(t_dec);
+      if constexpr (NW <= 4) {
+        if (alive) decode_mu_lane(L, wave, bv, rec, p, mi, bmine, n, idx, st_tgt, ut0, ut1, ut2, fmask);
+      } else {
+        uint64_t surv = ballot(alive);
+        while (surv) {
+          const int sl = ffs64(surv);
+          surv &= surv - 1;
+          decode_mu(L, wave, bv, rec, p, sl, bcast_i(idx, sl), bcast_u64(st_tgt, sl), bcast_u64(ut0, sl),
+                    bcast_u64(ut1, sl), bcast_u64(ut2, sl), bcast_i(fmask, sl));
+        }
       }
+      PROF_ADD(12, t_dec);
     } else {
       const sdx_ms_proto* rec = bv.ms + p;
       if (rec->never) continue;
@@ -756,7 +1017,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       uint64_t kt0 = 0, kt1 = 0, kt2 = 0, kt3 = 0;
       int fmask = 0;
       if (alive && rec->key[0].len) {  // sync (:140-158)
-        const PexRes r = pattern_exists(&rec->key[0], norm, ids, npat, bmine, T::WS, nw, 0);
+        const PexRes r = PEX(&rec->key[0], 0);
         if (r.found) {
           kt0 = r.tgt;
           fmask |= 1;
@@ -766,15 +1027,15 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
         } else alive = false;
       }
       if (alive && rec->key[1].len) {
-        const PexRes r = pattern_exists(&rec->key[1], norm, ids, npat, bmine, T::WS, nw, 0);
+        const PexRes r = PEX(&rec->key[1], 0);
         if (r.found) { kt1 = r.tgt; fmask |= 2; } else alive = false;
       }
       if (alive && rec->key[2].len) {
-        const PexRes r = pattern_exists(&rec->key[2], norm, ids, npat, bmine, T::WS, nw, 0);
+        const PexRes r = PEX(&rec->key[2], 0);
         if (r.found) { kt2 = r.tgt; fmask |= 4; } else alive = false;
       }
       if (alive && rec->key[3].len) {
-        const PexRes r = pattern_exists(&rec->key[3], norm, ids, npat, bmine, T::WS, nw, 0);
+        const PexRes r = PEX(&rec->key[3], 0);
         if (r.found) { kt3 = r.tgt; fmask |= 8; }
       }
       alive = alive && fmask != 0;
@@ -787,8 +1048,16 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       }
     }
   }
+  PROF_T(t_bar);
   __syncthreads();
+  PROF_ADD(14, t_bar);
+  PROF_T(t_fl);
   flush_tile(L, msg_of, nvalid, out);
+  PROF_ADD(13, t_fl);
+  PROF_ADD(15, t_kernel);
+#ifdef SDX_PROF
+  if (lane < 32) atomicAdd(&g_prof[lane], L.prof[wave][lane]);
+#endif
 }
 
 // =============================================================================================
@@ -1256,6 +1525,17 @@ static int fail(int code, const std::string& msg) {
 extern "C" {
 
 int sdx_abi_version(void) { return SDX_ABI_VERSION; }
+
+#ifdef SDX_PROF
+int sdx_prof_read(unsigned long long* out32, int reset) {
+  HIPCHK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 32));
+  if (reset) {
+    unsigned long long z[32] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
+  }
+  return SDX_OK;
+}
+#endif
 const char* sdx_last_error(void) { return g_err.c_str(); }
 
 int sdx_layout_size(int which) {

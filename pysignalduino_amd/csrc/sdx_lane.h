@@ -1,0 +1,307 @@
+// sdx_lane.h -- lane-per-message primitives for messages of <= 64*NW pulses (NW <= 4).
+//
+// A message's position bitmaps live in LDS (one u64 word per 64 pulses per pattern id); here
+// every mask that one (message x protocol) pair needs -- a target's occurrences, the unit
+// positions, "a run of >= m units starts here" -- is an NW-word register array, so a wave runs
+// 64 independent messages through pattern_exists AND through the exact re.finditer emulation
+// without any cross-lane traffic.  Bit p of the mask = position p of the message.
+#pragma once
+#include "sdx_device.h"
+
+namespace sdx {
+
+template <int NW>
+struct M {
+  uint64_t w[NW];
+};
+
+template <int NW>
+SDX_DEV M<NW> m_all() {
+  M<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = ~0ull;
+  return r;
+}
+template <int NW>
+SDX_DEV M<NW> m_zero() {
+  M<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = 0ull;
+  return r;
+}
+template <int NW>
+SDX_DEV M<NW> m_and(const M<NW>& a, const M<NW>& b) {
+  M<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] & b.w[i];
+  return r;
+}
+template <int NW>
+SDX_DEV M<NW> m_or(const M<NW>& a, const M<NW>& b) {
+  M<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] | b.w[i];
+  return r;
+}
+template <int NW>
+SDX_DEV M<NW> m_not(const M<NW>& a) {
+  M<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = ~a.w[i];
+  return r;
+}
+// word i of a, selected without dynamic register indexing (i may be out of range -> 0)
+template <int NW>
+SDX_DEV uint64_t m_word(const M<NW>& a, int i) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v = (i == k) ? a.w[k] : v;
+  return v;
+}
+// out bit p = a bit (p + s): positions move DOWN by s (0 <= s < 64*NW)
+template <int NW>
+SDX_DEV M<NW> m_shr(const M<NW>& a, int s) {
+  const int q = s >> 6, r = s & 63;
+  M<NW> o;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint64_t lo = m_word(a, i + q), hi = m_word(a, i + q + 1);
+    o.w[i] = r ? ((lo >> r) | (hi << (64 - r))) : lo;
+  }
+  return o;
+}
+// first set bit at position >= from, or -1
+template <int NW>
+SDX_DEV int m_first(const M<NW>& a, int from) {
+  int res = -1;
+#pragma unroll
+  for (int i = NW - 1; i >= 0; --i) {
+    uint64_t x = a.w[i];
+    const int lo = from - 64 * i;
+    if (lo >= 64) x = 0;
+    else if (lo > 0) x &= ~0ull << lo;
+    if (x) res = 64 * i + (__ffsll((unsigned long long)x) - 1);
+  }
+  return res;
+}
+template <int NW>
+SDX_DEV bool m_test(const M<NW>& a, int p) {
+  return (m_word(a, p >> 6) >> (p & 63)) & 1ull;
+}
+template <int NW>
+SDX_DEV bool m_any(const M<NW>& a) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) x |= a.w[i];
+  return x != 0;
+}
+
+// positions where the packed-id string `tgt` (tlen chars) occurs: AND of shifted id bitmaps
+template <int NW>
+SDX_DEV M<NW> m_occ(const uint64_t* bm, uint64_t tgt, int tlen) {
+  M<NW> acc = m_all<NW>();
+  for (int i = 0; i < tlen; ++i) {
+    const int id = (int)((tgt >> (4 * i)) & 15);
+    M<NW> b;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) b.w[k] = bm[id * NW + k];
+    acc = m_and(acc, m_shr(b, i));
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// pattern_exists (pattern_utils.py:34-136) for one lane; fast path = one candidate per value
+// ---------------------------------------------------------------------------------------------
+template <int NW>
+SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const double* norm, uint64_t ids, int npat, const uint64_t* bm,
+                            int minpos) {
+  PexRes res{false, -1, 0};
+  const int nu = sp->nuniq, slen = sp->len;
+  uint64_t cand[SDX_MAXUNIQ];
+  int cnt[SDX_MAXUNIQ];
+  long long total = 1;
+#pragma unroll
+  for (int u = 0; u < SDX_MAXUNIQ; ++u) {
+    cand[u] = 0;
+    cnt[u] = 1;
+    if (u < nu) {
+      const double v = sp->uval[u], tol = sp->utol[u];
+      uint32_t okm = 0;
+#pragma unroll
+      for (int j = 0; j < SDX_MAXPAT; ++j) {
+        const double g = fabs(norm[j] - v);
+        if (j < npat && (g <= 0.001 || g <= tol)) okm |= 1u << j;
+      }
+      const int c = __popc(okm);
+      if (c == 0) return res;  // pattern_utils.py:78-80
+      if (c == 1) {
+        cand[u] = (uint64_t)(__ffs(okm) - 1);
+      } else {  // stable sort by gap, ties in dict order (list.sort is stable)
+        uint64_t packed = 0;
+        for (uint32_t mj = okm; mj; mj &= mj - 1) {
+          const int j = __ffs(mj) - 1;
+          double gj = 0.0;
+#pragma unroll
+          for (int k = 0; k < SDX_MAXPAT; ++k) gj = (k == j) ? fabs(norm[k] - v) : gj;
+          int rank = 0;
+#pragma unroll
+          for (int k = 0; k < SDX_MAXPAT; ++k) {
+            const double gk = fabs(norm[k] - v);
+            rank += (((okm >> k) & 1u) && (gk < gj || (gk == gj && k < j))) ? 1 : 0;
+          }
+          packed |= (uint64_t)j << (4 * rank);
+        }
+        cand[u] = packed;
+      }
+      cnt[u] = c;
+      total *= c;
+      if (total > 10000) total = 10001;
+    }
+  }
+  if (nu == 0 || total > 10000) return res;
+  int digit[SDX_MAXUNIQ];
+#pragma unroll
+  for (int u = 0; u < SDX_MAXUNIQ; ++u) digit[u] = 0;
+  for (long long it = 0; it < total; ++it) {
+    uint32_t used = 0, uid = 0;
+    bool dup = false;
+#pragma unroll
+    for (int u = 0; u < SDX_MAXUNIQ; ++u) {
+      if (u < nu) {
+        const int slot = (int)((cand[u] >> (4 * digit[u])) & 15);
+        if (used & (1u << slot)) dup = true;
+        used |= 1u << slot;
+        uid |= (uint32_t)((ids >> (4 * slot)) & 15) << (4 * u);
+      }
+    }
+    if (!dup) {
+      uint64_t tgt = 0;
+      for (int i = 0; i < slen; ++i) tgt |= (uint64_t)((uid >> (4 * sp->uidx[i])) & 15) << (4 * i);
+      const int p = m_first(m_occ<NW>(bm, tgt, slen), minpos);
+      if (p >= 0) {
+        res.found = true;
+        res.pos = p;
+        res.tgt = tgt;
+        return res;
+      }
+    }
+#pragma unroll
+    for (int u = SDX_MAXUNIQ - 1; u >= 0; --u) {
+      if (u < nu) {
+        if (digit[u] + 1 < cnt[u]) {
+          digit[u]++;
+          break;
+        }
+        digit[u] = 0;
+      }
+    }
+  }
+  return res;
+}
+
+// bits [0, k)
+template <int NW>
+SDX_DEV M<NW> m_range_lo(int k) {
+  M<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int hi = k - 64 * i;
+    r.w[i] = hi >= 64 ? ~0ull : (hi <= 0 ? 0ull : ((1ull << hi) - 1));
+  }
+  return r;
+}
+// set/test bit b of a packed bitstring
+template <int NW>
+SDX_DEV void m_set(M<NW>& a, int b) {
+#pragma unroll
+  for (int i = 0; i < NW; ++i)
+    if ((b >> 6) == i) a.w[i] |= 1ull << (b & 63);
+}
+// len (<= 4) bits starting at b, first bit = most significant (int(''.join(bits[b:b+len]), 2))
+template <int NW>
+SDX_DEV int m_nibble(const M<NW>& a, int b, int len) {
+  const uint64_t lo = m_word(a, b >> 6), hi = m_word(a, (b >> 6) + 1);
+  const int sh = b & 63;
+  const uint32_t x = (uint32_t)((sh ? ((lo >> sh) | (hi << (64 - sh))) : lo) & 15u);
+  const uint32_t r4 = ((x & 1u) << 3) | ((x & 2u) << 1) | ((x & 4u) >> 1) | ((x & 8u) >> 3);
+  return (int)(r4 >> (4 - len));
+}
+
+// positions congruent to r modulo L (L in {1,2,4,8,16}: 64 % L == 0)
+SDX_DEV uint64_t residue_word(int L, int r) {
+  uint64_t m = 0;
+  switch (L) {
+    case 1: m = ~0ull; break;
+    case 2: m = 0x5555555555555555ull; break;
+    case 4: m = 0x1111111111111111ull; break;
+    case 8: m = 0x0101010101010101ull; break;
+    default: m = 0x0001000100010001ull; break;
+  }
+  return m << r;
+}
+
+// "a run of >= m units (stride L) starts here": AND_{j<m} (U >> jL), by doubling
+template <int NW>
+SDX_DEV M<NW> m_runs(const M<NW>& U, int m, int L) {
+  M<NW> res = m_all<NW>();
+  int res_len = 0, cur_len = 1;
+  M<NW> cur = U;
+  while (m) {
+    if (m & 1) {
+      res = m_and(res, m_shr(cur, res_len * L));
+      res_len += cur_len;
+    }
+    m >>= 1;
+    if (m) {
+      cur = m_and(cur, m_shr(cur, cur_len * L));
+      cur_len *= 2;
+    }
+  }
+  return res;
+}
+
+// compact every L-th bit (L in {1,2,4}) of a 64-bit word into its low 64/L bits
+SDX_DEV uint64_t compact_stride(uint64_t x, int L) {
+  if (L == 2) {
+    x &= 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+  } else if (L == 4) {
+    x &= 0x1111111111111111ull;
+    x = (x | (x >> 3)) & 0x0303030303030303ull;
+    x = (x | (x >> 6)) & 0x000F000F000F000Full;
+    x = (x | (x >> 12)) & 0x000000FF000000FFull;
+    x = (x | (x >> 24)) & 0x000000000000FFFFull;
+  }
+  return x;
+}
+
+// packed bit i = A bit (q + i*L), i < k (L in {1,2,4})
+template <int NW>
+SDX_DEV M<NW> m_stride_extract(const M<NW>& A, int q, int L, int k) {
+  const M<NW> B = m_shr(A, q);
+  M<NW> P = m_zero<NW>();
+  if (L == 1) {
+    P = B;
+  } else {
+    const int per = 64 / L;  // packed bits contributed by one source word
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint64_t c = compact_stride(B.w[w], L);
+      const int bitpos = w * per;
+#pragma unroll
+      for (int o = 0; o < NW; ++o) {
+        const int lo = bitpos - 64 * o;
+        if (lo >= 0 && lo < 64) P.w[o] |= c << lo;
+        else if (lo < 0 && lo > -64) P.w[o] |= c >> (-lo);
+      }
+    }
+  }
+  return m_and(P, m_range_lo<NW>(k));
+}
+
+}  // namespace sdx

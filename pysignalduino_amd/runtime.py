@@ -59,7 +59,7 @@ def load_library(path: Optional[str] = None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or LIB_PATH
+    p = path or os.environ.get("SDX_LIB") or LIB_PATH
     # torch bundles its own libamdhip64.so.7: load it FIRST so that libsdx's NEEDED
     # libamdhip64.so.7 resolves to the same runtime (one HIP runtime per process).
     import torch  # noqa: F401

@@ -1,0 +1,56 @@
+"""Phase breakdown of k_pulses from the SDX_PROF build (s_memtime cycle counters per wave).
+usage: SDX_LIB=pysignalduino_amd/_lib/libsdx_prof.so python tools/prof_phases.py [n]"""
+import ctypes
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from pysignalduino_amd import bank as bankmod, runtime, synth
+
+NAMES = {0: "stage bitmaps", 1: "MU normalise", 2: "MU pexists(start)", 3: "MU pexists(one/zero/float)",
+         4: "MU decode setup", 5: "MU finditer scan", 6: "MU chunk->bits", 7: "MU postDemod",
+         8: "MU payload write", 9: "MU format+DFA", 10: "MS decode", 11: "MS finish", 12: "MU decode total",
+         13: "flush", 14: "end barrier wait", 15: "kernel total", 20: "#results(MU)", 21: "#survivors(MU)",
+         22: "#matches(MU)", 23: "#survivors(MS)"}
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 333333
+    lib = runtime.load_library()
+    lib.sdx_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    bk = bankmod.Bank()
+    eng = runtime.Engine(bk, 0)
+    buf = (ctypes.c_ulonglong * 32)()
+    for kind, gen in (("MU", synth.mu_corpus), ("MS", synth.ms_corpus)):
+        pb = gen(bk.protocols, n, seed=42)
+        bd = eng.to_device_pulses(pb)
+        out = eng.alloc_out(pb.n, 8 * pb.n + 4096, 200 * pb.n + 65536)
+        k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
+        eng.launch_pulses(k, bd, out)
+        torch.cuda.synchronize()
+        lib.sdx_prof_read(buf, 1)
+        out["cursor"].zero_()
+        t = time.perf_counter()
+        eng.launch_pulses(k, bd, out)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        lib.sdx_prof_read(buf, 1)
+        v = np.array(list(buf), dtype=np.float64)
+        tot = v[15]
+        print(f"== {kind}: {pb.n} msgs, {dt*1e3:.2f} ms wall; wave-cycles total {tot:.3e} "
+              f"({tot/pb.n:.0f} per message)")
+        for i in sorted(NAMES):
+            if v[i] == 0:
+                continue
+            if i >= 20:
+                print(f"  {NAMES[i]:28s} {v[i]:.0f}  ({v[i]/pb.n:.2f} per message)")
+            else:
+                print(f"  {NAMES[i]:28s} {v[i]/tot*100:6.2f} %   {v[i]/pb.n:9.0f} wave-cycles/msg")
+
+
+if __name__ == "__main__":
+    main()
