@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 2u
+#define SDX_BANK_VERSION 3u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -89,14 +89,15 @@ typedef struct {
  * flags: bit0 = a match has been found (absorbing), bit1 = match if the payload
  * ends here ('$'), bit2 = dead (no match possible any more). */
 typedef struct {
-  int32_t nstates, start, trans_off, flags_off; /* into the DFA heap (u16 trans, u8 flags) */
+  int32_t nstates, start, trans_off, flags_off; /* into the DFA heaps (u16 class trans, u8 flags) */
+  int32_t t256_off, res[3];                     /* u8 [nstates][256] byte-indexed transitions */
 } sdx_dfa;
 
 typedef struct {
   uint32_t magic, version;
   uint32_t n_proto, n_mu, n_ms, n_mc, n_dfa, n_class;
   uint32_t off_mu, off_ms, off_mc, off_dfa, off_cls, off_trans, off_flags, off_str;
-  uint32_t total_bytes, res[3];
+  uint32_t total_bytes, off_t256, res[2];
 } sdx_bank_hdr;
 
 #endif

@@ -27,7 +27,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 2
+MAGIC, VERSION = 0x4B4E4253, 3
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
@@ -46,7 +46,8 @@ MC_REC = np.dtype([("cr_lo", "<f8"), ("cr_hi", "<f8"), ("proto_index", "<i4"), (
                    ("lmax", "<i4"), ("pre_off", "<i4"), ("pre_len", "<i4"), ("pid_num", "<i4"),
                    ("has_lmin", "u1"), ("has_lmax", "u1"), ("lmax_is_str", "u1"), ("invert", "u1"),
                    ("has_cr", "u1"), ("res", "u1", (3,))], align=True)
-DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4")])
+DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4"),
+                    ("t256_off", "<i4"), ("res", "<i4", (3,))])
 HDR_FMT = "<" + "I" * 20  # sdx_bank_hdr: 20 uint32
 
 POSTDEMO = {"postDemo_EM": 1, "postDemo_Revolt": 2, "postDemo_FS20": 3, "postDemo_FHT80": 4,
@@ -312,23 +313,30 @@ class Bank:
         self.mm_patterns = mm_patterns
         self.dfa_host = (cls_of, dfas)
         drec = np.zeros(len(dfas), DFA_REC)
-        trans_parts, flag_parts = [], []
-        toff = foff = 0
+        trans_parts, flag_parts, t256_parts = [], [], []
+        toff = foff = t2off = 0
+        cls_np = np.asarray(cls_of, dtype=np.int64)
         for i, (nst, start, trans, flags) in enumerate(dfas):
-            drec[i] = (nst, start, toff, foff)
-            t = np.asarray(trans, dtype=np.uint16).reshape(-1)
-            trans_parts.append(t)
+            if nst > 256:
+                raise NotImplementedError("modulematch DFA with more than 256 states")
+            drec[i]["nstates"], drec[i]["start"] = nst, start
+            drec[i]["trans_off"], drec[i]["flags_off"], drec[i]["t256_off"] = toff, foff, t2off
+            t = np.asarray(trans, dtype=np.uint16)
+            trans_parts.append(t.reshape(-1))
+            t256_parts.append(t[:, cls_np].astype(np.uint8).reshape(-1))  # [state][byte]
             flag_parts.append(np.asarray(flags, dtype=np.uint8))
             toff += t.size
             foff += len(flags)
+            t2off += nst * 256
         trans_all = np.concatenate(trans_parts) if trans_parts else np.zeros(0, np.uint16)
+        t256_all = np.concatenate(t256_parts) if t256_parts else np.zeros(0, np.uint8)
         flags_all = np.concatenate(flag_parts) if flag_parts else np.zeros(0, np.uint8)
         cls_arr = np.asarray(cls_of, dtype=np.uint8)
 
         # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings   (16-B aligned sections)
         hdr_size = struct.calcsize(HDR_FMT)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
-                    trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap)]
+                    trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
         for s in sections:
@@ -337,7 +345,7 @@ class Bank:
         total = cur
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
-                          len(self.mc_pids), len(dfas), n_class, *offs, total, 0, 0, 0)
+                          len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], 0, 0)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s

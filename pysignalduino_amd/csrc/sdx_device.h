@@ -446,8 +446,22 @@ SDX_DEV int run_postdemo(int which, const uint8_t* b, int n, uint8_t* o, int* no
 }
 
 // ------------------------------------------------------------------------------------------------
-// bank accessors
+// bank accessors.  Every bank pointer is made provably wave-uniform (readfirstlane), so the
+// compiler reads protocol records with scalar loads into SGPRs instead of per-lane vector loads.
 // ------------------------------------------------------------------------------------------------
+// load through the constant address space: with a uniform address this is an s_load into SGPRs
+template <class T>
+SDX_DEV T cld(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+
+template <class T>
+SDX_DEV const T* uniform_ptr(const T* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const T*)(((uint64_t)hi << 32) | lo);
+}
 struct BankView {
   const uint8_t* base;
   const sdx_bank_hdr* hdr;
@@ -457,13 +471,14 @@ struct BankView {
   const sdx_dfa* dfa;
   const uint8_t* cls;
   const uint16_t* trans;
+  const uint8_t* t256;
   const uint8_t* dflags;
   const uint8_t* str;
 };
 
 SDX_DEV BankView bank_view(const void* blob) {
   BankView v;
-  v.base = (const uint8_t*)blob;
+  v.base = uniform_ptr((const uint8_t*)blob);
   v.hdr = (const sdx_bank_hdr*)blob;
   v.mu = (const sdx_mu_proto*)(v.base + v.hdr->off_mu);
   v.ms = (const sdx_ms_proto*)(v.base + v.hdr->off_ms);
@@ -471,22 +486,32 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.dfa = (const sdx_dfa*)(v.base + v.hdr->off_dfa);
   v.cls = v.base + v.hdr->off_cls;
   v.trans = (const uint16_t*)(v.base + v.hdr->off_trans);
+  v.t256 = v.base + v.hdr->off_t256;
   v.dflags = v.base + v.hdr->off_flags;
   v.str = v.base + v.hdr->off_str;
+  v.hdr = uniform_ptr(v.hdr);
+  v.mu = uniform_ptr(v.mu);
+  v.ms = uniform_ptr(v.ms);
+  v.mc = uniform_ptr(v.mc);
+  v.dfa = uniform_ptr(v.dfa);
+  v.cls = uniform_ptr(v.cls);
+  v.trans = uniform_ptr(v.trans);
+  v.t256 = uniform_ptr(v.t256);
+  v.dflags = uniform_ptr(v.dflags);
+  v.str = uniform_ptr(v.str);
   return v;
 }
 
 // re.search(modulematch, payload): continue the DFA from the preamble state over the rest
 SDX_DEV bool dfa_accepts(const BankView& bv, int d, int state, const uint8_t* s, int n) {
   const sdx_dfa D = bv.dfa[d];
-  const uint16_t* tr = bv.trans + D.trans_off;
+  const uint8_t* t256 = bv.t256 + D.t256_off;
   const uint8_t* fl = bv.dflags + D.flags_off;
-  const int ncls = (int)bv.hdr->n_class;
   for (int i = 0; i < n; ++i) {
     const uint8_t f = fl[state];
     if (f & 1) return true;
     if (f & 4) return false;
-    state = tr[state * ncls + bv.cls[s[i]]];
+    state = t256[state * 256 + s[i]];
   }
   const uint8_t f = fl[state];
   return (f & 3) != 0;

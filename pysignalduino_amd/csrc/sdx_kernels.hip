@@ -193,9 +193,9 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   uint8_t* buf = W.bits;
   PROF_T(t_pd);
   // postDemodulation (:231-250): 'F' -> int() ValueError caught -> bits unchanged
-  if (rec->postdemo != SDX_PD_NONE && !any_float(buf, nb)) {
+  if (cld(&rec->postdemo) != SDX_PD_NONE && !any_float(buf, nb)) {
     int rc = 0, no = 0;
-    if (lane_id() == 0) rc = run_postdemo(rec->postdemo, buf, nb, W.bits2, &no);
+    if (lane_id() == 0) rc = run_postdemo(cld(&rec->postdemo), buf, nb, W.bits2, &no);
     rc = bcast_i(rc, 0);
     no = bcast_i(no, 0);
     wave_sync();
@@ -208,16 +208,16 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   PROF_ADD(7, t_pd);
   PROF_T(t_fmt);
   // padding (:257-259), after postDemod
-  const int pad = rec->pad_bits;
+  const int pad = cld(&rec->pad_bits);
   int nbp = nb;
   while (nbp % pad) ++nbp;
   for (int i = nb + lane_id(); i < nbp; i += WAVE) buf[i] = 0;
   wave_sync();
   const bool isf = any_float(buf, nbp);
   int dlen;
-  if (rec->dispatch_bin) dlen = nbp;
+  if (cld(&rec->dispatch_bin)) dlen = nbp;
   else if (isf) {
-    if (rec->remove_zero) {  // None.lstrip('0') -> AttributeError (:269)
+    if (cld(&rec->remove_zero)) {  // None.lstrip('0') -> AttributeError (:269)
       raise_msg(L, s, p, SDX_RAISE_ATTRIBUTE);
       return;
     }
@@ -229,7 +229,7 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   const int nd = (nbp + 3) >> 2;
   int skip = 0;
   if (dlen == -2) {
-    if (rec->remove_zero) {
+    if (cld(&rec->remove_zero)) {
       skip = nd;
       for (int d0 = 0; d0 < nd; d0 += WAVE) {
         const int d = d0 + lane_id();
@@ -248,28 +248,27 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
     dlen = nd - skip;
   }
   auto dchar = [&](int d) -> uint8_t {  // character d of dmsg, computed from the bits
-    if (rec->dispatch_bin) return buf[d] == 2 ? 'F' : (uint8_t)('0' + buf[d]);
+    if (cld(&rec->dispatch_bin)) return buf[d] == 2 ? 'F' : (uint8_t)('0' + buf[d]);
     if (isf) return (uint8_t)"None"[d];
     const int dd = d + skip, e = nbp - 4 * (nd - 1 - dd), a = (e - 4 > 0) ? e - 4 : 0;
     int v = 0;
     for (int i = a; i < e; ++i) v = (v << 1) | buf[i];
     return (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
   };
-  if (rec->mm_dfa >= 0) {  // re.search(modulematch, payload) (:277-280) before staging anything
+  if (cld(&rec->mm_dfa) >= 0) {  // re.search(modulematch, payload) (:277-280) before staging anything
     int ok = 0;
     if (lane_id() == 0) {
-      const sdx_dfa D = bv.dfa[rec->mm_dfa];
-      const uint16_t* tr = bv.trans + D.trans_off;
+      const sdx_dfa D = bv.dfa[cld(&rec->mm_dfa)];
+      const uint8_t* t256 = bv.t256 + D.t256_off;
       const uint8_t* fl = bv.dflags + D.flags_off;
-      const int ncls = (int)bv.hdr->n_class;
-      int st = rec->mm_pre_state;
-      const int tot = dlen + rec->post_len;
+      int st = cld(&rec->mm_pre_state);
+      const int tot = dlen + cld(&rec->post_len);
       int i = 0;
       for (; i < tot; ++i) {
         const uint8_t f = fl[st];
         if (f & 5) break;  // accepted or dead
-        const uint8_t c = i < dlen ? dchar(i) : bv.str[rec->post_off + i - dlen];
-        st = tr[st * ncls + bv.cls[c]];
+        const uint8_t c = i < dlen ? dchar(i) : bv.str[cld(&rec->post_off) + i - dlen];
+        st = t256[st * 256 + c];
       }
       const uint8_t f = fl[st];
       ok = (f & 1) ? 1 : ((f & 4) ? 0 : ((i == tot && (f & 2)) ? 1 : 0));
@@ -278,14 +277,14 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
     if (!bcast_i(ok, 0)) return;
   }
   PROF_T(t_wr);
-  const int total = rec->pre_len + dlen + rec->post_len;
+  const int total = cld(&rec->pre_len) + dlen + cld(&rec->post_len);
   int slot;
   const int off = pool_alloc(L, total, &slot);
   if (off < 0) return;
   uint8_t* dst = L.heap + off;
-  copy_str(dst, bv.str + rec->pre_off, rec->pre_len);
-  for (int d = lane_id(); d < dlen; d += WAVE) dst[rec->pre_len + d] = dchar(d);
-  copy_str(dst + rec->pre_len + dlen, bv.str + rec->post_off, rec->post_len);
+  copy_str(dst, bv.str + cld(&rec->pre_off), cld(&rec->pre_len));
+  for (int d = lane_id(); d < dlen; d += WAVE) dst[cld(&rec->pre_len) + d] = dchar(d);
+  copy_str(dst + cld(&rec->pre_len) + dlen, bv.str + cld(&rec->post_off), cld(&rec->post_len));
   pool_commit(L, slot, wave, s, p, off, total, nbp);
   PROF_ADD(8, t_wr);
   PROF_CNT(20, 1);
@@ -303,8 +302,8 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   const int lane = lane_id();
   const uint64_t* bm = &L.bm[s * T::MSTRIDE];
   const int n = L.nlen[s], nw = (n + 63) >> 6;
-  const int Lw = rec->width;
-  const int lenS = rec->has_start ? (int)rec->start.len : 0;
+  const int Lw = cld(&rec->width);
+  const int lenS = cld(&rec->has_start) ? (int)cld(&rec->start.len) : 0;
   const uint64_t ut[3] = {ut0, ut1, ut2};
   const uint8_t SYM[3] = {1, 0, 2};
   PROF_T(t_setup);
@@ -325,7 +324,7 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   uint64_t ek[3] = {0, 0, 0};
   uint8_t esym[3] = {0, 0, 0};
   int ne = 0;
-  if (rec->recon && Lw > 1) {
+  if (cld(&rec->recon) && Lw > 1) {
     const uint64_t msk = (Lw - 1 >= 16) ? ~0ull : ((1ull << (4 * (Lw - 1))) - 1);
     for (int k = 0; k < 3; ++k) {
       if (!((fmask >> k) & 1)) continue;
@@ -386,7 +385,7 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
     }
     return k;
   };
-  const int lmin = rec->length_min;
+  const int lmin = cld(&rec->length_min);
   int pos = idx;
   PROF_ADD(4, t_setup);
   while (true) {
@@ -424,7 +423,7 @@ SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
     }
     pos = q + G;
     const int nchunks = kfound + (em >= 0 ? 1 : 0);
-    if (nchunks > rec->length_max) continue;  // (:217-218)
+    if (nchunks > cld(&rec->length_max)) continue;  // (:217-218)
     PROF_T(t_bits);
     for (int i = lane; i < kfound; i += WAVE) {
       const int x = q + i * Lw;
@@ -477,68 +476,79 @@ SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
   bool anyf = m_any(PF);
   uint8_t pout[NB];
   bool usearr = false;
-  if (rec->postdemo != SDX_PD_NONE && !anyf) {  // 'F' -> int() ValueError caught -> unchanged
+  if (cld(&rec->postdemo) != SDX_PD_NONE && !anyf) {  // 'F' -> int() ValueError caught -> unchanged
     uint8_t pin[NB];
     for (int b = 0; b < nb; ++b) pin[b] = m_test(P1, b) ? 1 : 0;
     int no = 0;
-    const int rc = run_postdemo(rec->postdemo, pin, nb, pout, &no);
+    const int rc = run_postdemo(cld(&rec->postdemo), pin, nb, pout, &no);
     if (rc == 0) return;  // rcode < 1: match dropped
     if (rc == 1) {
       usearr = true;
       nb = no;
     }
   }
-  const int pad = rec->pad_bits;
+  const int pad = cld(&rec->pad_bits);
   int nbp = nb;
   while (nbp % pad) ++nbp;
   const int nd = (nbp + 3) >> 2;
-  auto digit = [&](int d) -> int {  // hex digit d of bin_str_2_hex_str (helpers.py:28-64)
+  if (!usearr && 4 * nd > 64 * NW) {  // does not fit the packed words: use the byte array
+    for (int b = 0; b < nb; ++b) pout[b] = m_test(PF, b) ? 2 : (m_test(P1, b) ? 1 : 0);
+    usearr = true;
+  }
+  // hex digits (helpers.py:28-64): right-align the bitstring to a nibble boundary and reverse the
+  // bits inside each nibble -> nibble d of H is hex digit d
+  M<NW> H = m_zero<NW>();
+  if (!usearr) {
+    H = m_shl_small(P1, 4 * nd - nbp);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) H.w[i] = nibrev(H.w[i]);
+  }
+  auto digit = [&](int d) -> int {
+    if (!usearr) return (int)((m_word(H, d >> 4) >> (4 * (d & 15))) & 15ull);
     const int e = nbp - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
-    if (!usearr) return m_nibble(P1, a, e - a);  // bits >= nb are the '0' padding
     int v = 0;
     for (int i = a; i < e; ++i) v = (v << 1) | (i < nb ? pout[i] : 0);
     return v;
   };
   int dlen, skip = 0;
-  if (rec->dispatch_bin) {
+  if (cld(&rec->dispatch_bin)) {
     dlen = nbp;
   } else if (anyf) {
-    if (rec->remove_zero) {  // None.lstrip('0') -> AttributeError (:269)
+    if (cld(&rec->remove_zero)) {  // None.lstrip('0') -> AttributeError (:269)
       atomicMin(&L.raise_key[mi], ((uint32_t)p << 8) | SDX_RAISE_ATTRIBUTE);
       return;
     }
     dlen = 4;
   } else {
-    if (rec->remove_zero)
+    if (cld(&rec->remove_zero))
       while (skip < nd && digit(skip) == 0) ++skip;
     dlen = nd - skip;
   }
   auto dchar = [&](int i) -> uint8_t {
-    if (rec->dispatch_bin) {
-      if (usearr) return (uint8_t)('0' + (i < nb ? pout[i] : 0));
+    if (cld(&rec->dispatch_bin)) {
+      if (usearr) return (uint8_t)(i < nb ? (pout[i] == 2 ? 'F' : '0' + pout[i]) : '0');
       return m_test(PF, i) ? 'F' : (uint8_t)('0' + (m_test(P1, i) ? 1 : 0));
     }
     if (anyf) return (uint8_t)"None"[i];
     const int v = digit(i + skip);
     return (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
   };
-  if (rec->mm_dfa >= 0) {  // re.search(modulematch, payload) (:277-280)
-    const sdx_dfa D = bv.dfa[rec->mm_dfa];
-    const uint16_t* tr = bv.trans + D.trans_off;
+  if (cld(&rec->mm_dfa) >= 0) {  // re.search(modulematch, payload) (:277-280)
+    const sdx_dfa D = bv.dfa[cld(&rec->mm_dfa)];
+    const uint8_t* t256 = bv.t256 + D.t256_off;
     const uint8_t* fl = bv.dflags + D.flags_off;
-    const int ncls = (int)bv.hdr->n_class;
-    int st = rec->mm_pre_state;
-    const int tot = dlen + rec->post_len;
+    int st = cld(&rec->mm_pre_state);
+    const int tot = dlen + cld(&rec->post_len);
     int i = 0;
     for (; i < tot; ++i) {
       if (fl[st] & 5) break;
-      const uint8_t c = i < dlen ? dchar(i) : bv.str[rec->post_off + i - dlen];
-      st = tr[st * ncls + bv.cls[c]];
+      const uint8_t c = i < dlen ? dchar(i) : bv.str[cld(&rec->post_off) + i - dlen];
+      st = t256[st * 256 + c];
     }
     const uint8_t f = fl[st];
     if (!((f & 1) || (!(f & 4) && i == tot && (f & 2)))) return;
   }
-  const int total = rec->pre_len + dlen + rec->post_len;
+  const int total = cld(&rec->pre_len) + dlen + cld(&rec->post_len);
   const int slot = atomicAdd(&L.pool_nrec, 1);
   const int off = atomicAdd(&L.pool_nheap, total);
   if (slot >= POOL_REC || off + total > POOL_HEAP) {
@@ -546,9 +556,9 @@ SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
     return;
   }
   uint8_t* dst = L.heap + off;
-  for (int i = 0; i < rec->pre_len; ++i) dst[i] = bv.str[rec->pre_off + i];
-  for (int i = 0; i < dlen; ++i) dst[rec->pre_len + i] = dchar(i);
-  for (int i = 0; i < rec->post_len; ++i) dst[rec->pre_len + dlen + i] = bv.str[rec->post_off + i];
+  for (int i = 0; i < cld(&rec->pre_len); ++i) dst[i] = bv.str[cld(&rec->pre_off) + i];
+  for (int i = 0; i < dlen; ++i) dst[cld(&rec->pre_len) + i] = dchar(i);
+  for (int i = 0; i < cld(&rec->post_len); ++i) dst[cld(&rec->pre_len) + dlen + i] = bv.str[cld(&rec->post_off) + i];
   StageRec r;
   r.off = (uint32_t)off;
   r.len = (uint16_t)total;
@@ -566,8 +576,8 @@ template <int NW, int TM>
 SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p,
                             int mi, const uint64_t* bm, int n, int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1,
                             uint64_t ut2, int fmask) {
-  const int Lw = rec->width;
-  const int lenS = rec->has_start ? (int)rec->start.len : 0;
+  const int Lw = cld(&rec->width);
+  const int lenS = cld(&rec->has_start) ? (int)cld(&rec->start.len) : 0;
   const uint64_t ut[3] = {ut0, ut1, ut2};
   const uint8_t SYM[3] = {1, 0, 2};
   M<NW> U = m_zero<NW>(), V1 = m_zero<NW>(), VF = m_zero<NW>();
@@ -584,26 +594,23 @@ SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
     if (fs == 2) VF = m_or(VF, occ);
   }
   // end_pattern_lookup: pstr[:-1], first writer wins (:124-127); regex tail only with reconstructBit
-  uint64_t ek[3] = {0, 0, 0};
-  uint8_t es[3] = {0, 0, 0};
-  int ne = 0;
-  if (rec->recon && Lw > 1) {
+  // (kept per source key kk: key kk is live iff found and no earlier found key has the same
+  //  prefix -- first writer wins -- which is the insertion-ordered dict without dynamic indexing)
+  bool elive[3] = {false, false, false};
+  uint64_t ekey[3] = {0, 0, 0};
+  if (cld(&rec->recon) && Lw > 1) {
     const uint64_t msk = (Lw - 1 >= 16) ? ~0ull : ((1ull << (4 * (Lw - 1))) - 1);
 #pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
-      if (!((fmask >> kk) & 1)) continue;
-      const uint64_t key = ut[kk] & msk;
+      ekey[kk] = ut[kk] & msk;
       bool seen = false;
-      for (int j = 0; j < ne; ++j) seen |= ek[j] == key;
-      if (!seen) {
-        ek[ne] = key;
-        es[ne] = SYM[kk];
-        ++ne;
-      }
+#pragma unroll
+      for (int j = 0; j < kk; ++j) seen |= elive[j] && ekey[j] == ekey[kk];
+      elive[kk] = ((fmask >> kk) & 1) && !seen;
     }
   }
   const M<NW> S = lenS ? m_occ<NW>(bm, st_tgt, lenS) : m_all<NW>();
-  const int lmin = rec->length_min;
+  const int lmin = cld(&rec->length_min);
   // s: START at s and >= length_min units at s+lenS (with length_min 0 every START qualifies,
   // including one that ends exactly at the end of the data: empty group -> IndexError)
   const M<NW> V = lmin > 0 ? m_and(S, m_shr(m_runs(U, lmin, Lw), lenS)) : S;
@@ -621,18 +628,25 @@ SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
     if (z < 0) z = q + Lw * ((64 * NW - q + Lw - 1) / Lw);
     const int k = (z - q) / Lw;
     const int e0 = q + k * Lw;
-    int em = -1;
-    for (int j = 0; j < ne && em < 0; ++j)
-      if (match_at(bm, NW, n, ek[j], Lw - 1, e0)) em = j;
-    const int G = k * Lw + (em >= 0 ? Lw - 1 : 0);
+    // the regex tail (?:E1|E2|..)? : first end key (insertion order) that matches at e0
+    bool emf = false;
+    uint8_t esym = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (!emf && elive[j] && match_at(bm, NW, n, ekey[j], Lw - 1, e0)) {
+        emf = true;
+        esym = SYM[j];
+      }
+    }
+    const int G = k * Lw + (emf ? Lw - 1 : 0);
     if (G == 0) {  // chunks == [] -> chunks[-1] IndexError (:212)
       atomicMin(&L.raise_key[mi], ((uint32_t)p << 8) | SDX_RAISE_INDEX);
       return;
     }
     pos = q + G;
-    const int nch = k + (em >= 0 ? 1 : 0);
-    if (nch > rec->length_max) continue;  // (:217-218)
-    finish_mu_lane(L, wave, bv, rec, p, mi, q, k, Lw, em >= 0, em >= 0 ? es[em] : (uint8_t)0, V1, VF);
+    const int nch = k + (emf ? 1 : 0);
+    if (nch > cld(&rec->length_max)) continue;  // (:217-218)
+    finish_mu_lane(L, wave, bv, rec, p, mi, q, k, Lw, emf, esym, V1, VF);
     if ((L.raise_key[mi] >> 8) <= (uint32_t)p) return;
   }
 }
@@ -646,20 +660,20 @@ SDX_DEV void finish_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   auto& W = L.w[wave];
   uint8_t* buf = W.bits;
   if (nb == 0) return;                                      // (:191-192)
-  if (rec->lir_min != -1 && nb < rec->lir_min) return;      // length_in_range (:194-196)
-  if (nb > rec->lir_max) return;
+  if (cld(&rec->lir_min) != -1 && nb < cld(&rec->lir_min)) return;      // length_in_range (:194-196)
+  if (nb > cld(&rec->lir_max)) return;
   int nbp = nb;                                             // padding BEFORE postDemod (:198-200)
-  while (nbp % rec->pad_bits) ++nbp;
+  while (nbp % cld(&rec->pad_bits)) ++nbp;
   for (int i = nb + lane_id(); i < nbp; i += WAVE) buf[i] = 0;
   wave_sync();
   nb = nbp;
-  if (rec->postdemo != SDX_PD_NONE) {                       // no try: 'F' -> ValueError (:209)
+  if (cld(&rec->postdemo) != SDX_PD_NONE) {                       // no try: 'F' -> ValueError (:209)
     if (any_float(buf, nb)) {
       raise_msg(L, s, p, SDX_RAISE_VALUE);
       return;
     }
     int rc = 0, no = 0;
-    if (lane_id() == 0) rc = run_postdemo(rec->postdemo, buf, nb, W.bits2, &no);
+    if (lane_id() == 0) rc = run_postdemo(cld(&rec->postdemo), buf, nb, W.bits2, &no);
     rc = bcast_i(rc, 0);
     no = bcast_i(no, 0);
     wave_sync();
@@ -675,14 +689,14 @@ SDX_DEV void finish_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   }
   if (any_float(buf, nb)) return;  // bin_str_2_hex_str -> None -> skipped (:224-226)
   const int dl = (nb + 3) / 4;
-  const int total = rec->pre_len + dl + rec->post_len;
+  const int total = cld(&rec->pre_len) + dl + cld(&rec->post_len);
   int slot;
   const int off = pool_alloc(L, total, &slot);
   if (off < 0) return;
   uint8_t* dst = L.heap + off;
-  copy_str(dst, bv.str + rec->pre_off, rec->pre_len);
-  hex_digits(buf, nb, dst + rec->pre_len, 0);
-  copy_str(dst + rec->pre_len + dl, bv.str + rec->post_off, rec->post_len);
+  copy_str(dst, bv.str + cld(&rec->pre_off), cld(&rec->pre_len));
+  hex_digits(buf, nb, dst + cld(&rec->pre_len), 0);
+  copy_str(dst + cld(&rec->pre_len) + dl, bv.str + cld(&rec->post_off), cld(&rec->post_len));
   wave_sync();
   pool_commit(L, slot, wave, s, p, off, total, nb);
 }
@@ -696,11 +710,11 @@ SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
   const int lane = lane_id();
   const uint64_t* bm = &L.bm[s * T::MSTRIDE];
   const int n = L.nlen[s];
-  const int Wd = rec->width;
+  const int Wd = cld(&rec->width);
   PROF_T(t_msd);
   PROF_CNT(23, 1);
   const uint64_t kt[4] = {k0, k1, k2, k3};
-  const int klen[4] = {rec->key[0].len, rec->key[1].len, rec->key[2].len, rec->key[3].len};
+  const int klen[4] = {cld(&rec->key[0].len), cld(&rec->key[1].len), cld(&rec->key[2].len), cld(&rec->key[3].len)};
   const uint8_t KSYM[4] = {3, 1, 0, 2};  // 3 = '' (sync: no bit)
   // pattern_lookup with dict semantics: distinct (string) keys, value = last writer
   uint64_t kk[4];
@@ -739,7 +753,7 @@ SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
       ++ne;
     }
   }
-  const bool recon = rec->recon != 0;
+  const bool recon = cld(&rec->recon) != 0;
   const int nch = (start < n) ? (n - start + Wd - 1) / Wd : 0;
   int nb = 0;
   for (int c0 = 0; c0 < nch; c0 += WAVE) {
@@ -953,17 +967,19 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   const int nproto = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu : (int)bv.hdr->n_ms;
   const int qn = (nproto + 3) / 4;
   const int p0 = wave * qn, p1 = (p0 + qn < nproto) ? p0 + qn : nproto;
+  double last_clock = __builtin_nan("");  // NaN != anything: the first protocol normalises
   for (int p = p0; p < p1; ++p) {
     if (KIND == SDX_KIND_MU) {
-      const sdx_mu_proto* rec = bv.mu + p;
-      if (rec->never || !rec->active) continue;
+      const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
+      if (cld(&rec->never) || !cld(&rec->active)) continue;
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
       int idx = 0;
       uint64_t st_tgt = 0, ut0 = 0, ut1 = 0, ut2 = 0;
       int fmask = 0;
       PROF_T(t_norm);
-      if (alive) {
-        const double ck = rec->clock;
+      if (cld(&rec->clock) != last_clock) {  // wave-uniform: consecutive protocols often share a clock
+        last_clock = cld(&rec->clock);
+        const double ck = cld(&rec->clock);
 #pragma unroll
         for (int k = 0; k < SDX_MAXPAT; ++k)
           if (k < npat) norm[k] = py_round1(val[k] / ck);
@@ -971,7 +987,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       PROF_ADD(1, t_norm);
       PROF_T(t_st);
       if (alive) {
-        if (rec->has_start) {
+        if (cld(&rec->has_start)) {
           const PexRes r = PEX(&rec->start, 0);
           alive = r.found;
           idx = r.pos;
@@ -980,15 +996,15 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       }
       PROF_ADD(2, t_st);
       PROF_T(t_ozf);
-      if (alive && rec->one.len) {
+      if (alive && cld(&rec->one.len)) {
         const PexRes r = PEX(&rec->one, idx);
         if (r.found) { ut0 = r.tgt; fmask |= 1; } else alive = false;
       }
-      if (alive && rec->zero.len) {
+      if (alive && cld(&rec->zero.len)) {
         const PexRes r = PEX(&rec->zero, idx);
         if (r.found) { ut1 = r.tgt; fmask |= 2; } else alive = false;
       }
-      if (alive && rec->flt.len) {
+      if (alive && cld(&rec->flt.len)) {
         const PexRes r = PEX(&rec->flt, idx);
         if (r.found) { ut2 = r.tgt; fmask |= 4; }
       }
@@ -1008,33 +1024,33 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       }
       PROF_ADD(12, t_dec);
     } else {
-      const sdx_ms_proto* rec = bv.ms + p;
-      if (rec->never) continue;
+      const sdx_ms_proto* rec = uniform_ptr(bv.ms + p);
+      if (cld(&rec->never)) continue;
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
-      if (alive && rec->pclock > 0.0)  // clock tolerance gate (:83-88)
-        alive = !(fabs(rec->pclock - clock) > clock * 0.3);
+      if (alive && cld(&rec->pclock) > 0.0)  // clock tolerance gate (:83-88)
+        alive = !(fabs(cld(&rec->pclock) - clock) > clock * 0.3);
       int start = 0;
       uint64_t kt0 = 0, kt1 = 0, kt2 = 0, kt3 = 0;
       int fmask = 0;
-      if (alive && rec->key[0].len) {  // sync (:140-158)
+      if (alive && cld(&rec->key[0].len)) {  // sync (:140-158)
         const PexRes r = PEX(&rec->key[0], 0);
         if (r.found) {
           kt0 = r.tgt;
           fmask |= 1;
-          start = r.pos + rec->key[0].len;
-          const double avail = rec->width > 0 ? (double)(n - start) / (double)rec->width : 0.0;
-          if ((double)rec->lmin_sync > avail) alive = false;
+          start = r.pos + cld(&rec->key[0].len);
+          const double avail = cld(&rec->width) > 0 ? (double)(n - start) / (double)cld(&rec->width) : 0.0;
+          if ((double)cld(&rec->lmin_sync) > avail) alive = false;
         } else alive = false;
       }
-      if (alive && rec->key[1].len) {
+      if (alive && cld(&rec->key[1].len)) {
         const PexRes r = PEX(&rec->key[1], 0);
         if (r.found) { kt1 = r.tgt; fmask |= 2; } else alive = false;
       }
-      if (alive && rec->key[2].len) {
+      if (alive && cld(&rec->key[2].len)) {
         const PexRes r = PEX(&rec->key[2], 0);
         if (r.found) { kt2 = r.tgt; fmask |= 4; } else alive = false;
       }
-      if (alive && rec->key[3].len) {
+      if (alive && cld(&rec->key[3].len)) {
         const PexRes r = PEX(&rec->key[3], 0);
         if (r.found) { kt3 = r.tgt; fmask |= 8; }
       }
@@ -1119,9 +1135,9 @@ SDX_DEV bool hex_equal(const LaneBits& B, int a1, int e1, int a2, int e2) {
 
 // length_in_range (helpers.py:124-166) for a clockrange protocol
 SDX_DEV bool mc_lir(const sdx_mc_proto* r, int n) {
-  const int lo = r->has_lmin ? r->lmin : -1;
+  const int lo = cld(&r->has_lmin) ? cld(&r->lmin) : -1;
   if (lo != -1 && n < lo) return false;
-  if (r->has_lmax && n > r->lmax) return false;
+  if (cld(&r->has_lmax) && n > cld(&r->lmax)) return false;
   return true;
 }
 
@@ -1155,14 +1171,14 @@ struct McOut {
 
 SDX_DEV McOut mc_method(const sdx_mc_proto* r, const LaneBits& B, int n, const LaneBits& D) {
   McOut o{0, 0, 0, 0, 0, 0};
-  switch (r->method) {
+  switch (cld(&r->method)) {
     case SDX_MC_FUNKBUS: {  // manchester.py:207-300
-      const int lmin = r->has_lmin ? r->lmin : -1;
+      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : -1;
       if (n < lmin) return o;
-      if (r->has_lmax && n > r->lmax) return o;
+      if (cld(&r->has_lmax) && n > cld(&r->lmax)) return o;
       const int dn = n > 0 ? n - 1 : 0;  // mc2dmc of the lh/hl expansion
       int base, slen;
-      if (r->pid_num == 119) {
+      if (cld(&r->pid_num) == 119) {
         const int pos = D.find(0xCu /*01100*/, 5, 0, dn);
         if (!(pos >= 0 && pos < 5)) return o;
         base = pos;
@@ -1172,8 +1188,8 @@ SDX_DEV McOut mc_method(const sdx_mc_proto* r, const LaneBits& B, int n, const L
         base = 0;
         slen = 1 + dn;
       }
-      const uint32_t pre = (r->pid_num == 119) ? 1u /*001*/ : 0u;
-      const int plen = (r->pid_num == 119) ? 3 : 1;
+      const uint32_t pre = (cld(&r->pid_num) == 119) ? 1u /*001*/ : 0u;
+      const int plen = (cld(&r->pid_num) == 119) ? 3 : 1;
       auto sbit = [&](int t) -> int { return t < plen ? (int)((pre >> (plen - 1 - t)) & 1) : D.get(base + t - plen); };
       uint64_t bytes = 0;
       int xr = 0, chk = 0, par = 0;
@@ -1203,7 +1219,7 @@ SDX_DEV McOut mc_method(const sdx_mc_proto* r, const LaneBits& B, int n, const L
       return o;
     }
     case SDX_MC_SAINLOGIC: {  // manchester.py:302-354
-      const int lmax = r->has_lmax ? r->lmax : 0;
+      const int lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 0;
       if (n > lmax) return o;
       int pad = 0, m = n;
       if (n < 128) {
@@ -1212,14 +1228,14 @@ SDX_DEV McOut mc_method(const sdx_mc_proto* r, const LaneBits& B, int n, const L
         pad = st < 10 ? 10 - st : 0;
         m = (n + pad < 128) ? n + pad : 128;
       }
-      const int lmin = r->has_lmin ? r->lmin : 0;
+      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : 0;
       if (m < lmin) return o;
       // bits = '1'*pad + B[0 : m-pad]; encode as window with a virtual prefix
       o.rc = 1; o.kind = 3; o.a = pad; o.e = m; o.len = (m + 3) >> 2;
       return o;
     }
     case SDX_MC_AS: {  // manchester.py:356-416
-      const int lmin = r->has_lmin ? r->lmin : -1, lmax = r->has_lmax ? r->lmax : 9999;
+      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : -1, lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 9999;
       const int st = B.find(0xCu /*1100*/, 4, 16, n);
       if (st >= 0) {
         int en = B.find(0xCu, 4, st + 16, n);
@@ -1234,21 +1250,21 @@ SDX_DEV McOut mc_method(const sdx_mc_proto* r, const LaneBits& B, int n, const L
       return o;
     }
     case SDX_MC_PLAIN: {  // manchester.py:418-586
-      const int lmin = r->has_lmin ? r->lmin : -1, lmax = r->has_lmax ? r->lmax : 9999;
+      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : -1, lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 9999;
       if (n < lmin || n > lmax) return o;
       o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
       return o;
     }
     case SDX_MC_RAW: {  // manchester.py:588-613
-      const int lmax = r->has_lmax ? r->lmax : 0;
+      const int lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 0;
       if (n > lmax) return o;
       o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
       return o;
     }
     case SDX_MC_HMCRAW: {  // helpers.py:90-122: un-converted str length_max -> int > str TypeError
-      if (r->has_lmax) {
-        if (r->lmax_is_str) { o.rc = -1; return o; }
-        if (n > r->lmax) return o;
+      if (cld(&r->has_lmax)) {
+        if (cld(&r->lmax_is_str)) { o.rc = -1; return o; }
+        if (n > cld(&r->lmax)) return o;
       }
       o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
       return o;
@@ -1393,19 +1409,19 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   const int nmc = (int)bv.hdr->n_mc;
   int raise = 0;
   for (int p = 0; p < nmc; ++p) {
-    const sdx_mc_proto* r = bv.mc + p;
+    const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
     bool go = valid && !raise;
     // gates of _demodulate_mc_data (manchester.py:70-89; clockrange fixed to [0] / [1])
-    if (go && mcbit < (r->has_lmin ? r->lmin : -1)) go = false;
-    if (go && mcbit > (r->has_lmax ? r->lmax : 9999)) go = false;
-    if (go && r->has_cr && !((double)clock > r->cr_lo && (double)clock < r->cr_hi)) go = false;
+    if (go && mcbit < (cld(&r->has_lmin) ? cld(&r->lmin) : -1)) go = false;
+    if (go && mcbit > (cld(&r->has_lmax) ? cld(&r->lmax) : 9999)) go = false;
+    if (go && cld(&r->has_cr) && !((double)clock > cld(&r->cr_lo) && (double)clock < cld(&r->cr_hi))) go = false;
     McOut o{0, 0, 0, 0, 0, 0};
-    const bool inv = (r->invert != 0) ^ ((flags & 3) != 0);  // (:91-96)
+    const bool inv = (cld(&r->invert) != 0) ^ ((flags & 3) != 0);  // (:91-96)
     const LaneBits& B = inv ? BI : BN;
     const int nb = inv ? nI : nN;
     if (go && !hex_ok) { raise = SDX_RAISE_TYPE; go = false; }  // len(None) -> TypeError
     if (go) {
-      if (r->method == SDX_MC_FUNKBUS) {
+      if (cld(&r->method) == SDX_MC_FUNKBUS) {
         for (int w = 0; w < MC_MAXW; ++w) {  // mc2dmc(lh/hl): bit k = (b[k] == b[k+1])
           const uint64_t x = B.word(w), nx = B.word(w + 1);
           L.dm[w * 256 + tid] = ~(x ^ ((x << 1) | (nx >> 63)));
@@ -1417,7 +1433,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     }
     // stage results of the wave in lane (= frame) order for this protocol
     const bool has = o.rc == 1;
-    const int plen = has ? r->pre_len + o.len : 0;
+    const int plen = has ? cld(&r->pre_len) + o.len : 0;
     int incl = plen;  // inclusive scan over lanes
     for (int d = 1; d < WAVE; d <<= 1) {
       const int t = __shfl_up(incl, d);
@@ -1430,8 +1446,8 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     const bool fits = hb + wtot <= HEAP_CAP && rb + nnew <= REC_CAP;
     if (has && fits) {
       uint8_t* dst = &L.heap[wave][hb + incl - plen];
-      for (int i = 0; i < r->pre_len; ++i) dst[i] = bv.str[r->pre_off + i];
-      mc_write(r, o, B, nb, dst + r->pre_len);
+      for (int i = 0; i < cld(&r->pre_len); ++i) dst[i] = bv.str[cld(&r->pre_off) + i];
+      mc_write(r, o, B, nb, dst + cld(&r->pre_len));
       StageRec sr;
       sr.off = (uint32_t)(hb + incl - plen);
       sr.len = (uint16_t)plen;

@@ -50,25 +50,51 @@ SDX_DEV M<NW> m_not(const M<NW>& a) {
   for (int i = 0; i < NW; ++i) r.w[i] = ~a.w[i];
   return r;
 }
-// word i of a, selected without dynamic register indexing (i may be out of range -> 0)
+// word i of a, selected with bit masks (no dynamic register indexing -> no scratch)
 template <int NW>
 SDX_DEV uint64_t m_word(const M<NW>& a, int i) {
   uint64_t v = 0;
 #pragma unroll
-  for (int k = 0; k < NW; ++k) v = (i == k) ? a.w[k] : v;
+  for (int k = 0; k < NW; ++k) v |= a.w[k] & (0ull - (uint64_t)(i == k));
   return v;
 }
-// out bit p = a bit (p + s): positions move DOWN by s (0 <= s < 64*NW)
+// out bit p = a bit (p + r), 0 <= r < 64 (no dynamic word indexing)
 template <int NW>
-SDX_DEV M<NW> m_shr(const M<NW>& a, int s) {
-  const int q = s >> 6, r = s & 63;
+SDX_DEV M<NW> m_shr_small(const M<NW>& a, int r) {
   M<NW> o;
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
-    const uint64_t lo = m_word(a, i + q), hi = m_word(a, i + q + 1);
-    o.w[i] = r ? ((lo >> r) | (hi << (64 - r))) : lo;
+    const uint64_t hi = (i + 1 < NW) ? a.w[i + 1] : 0ull;
+    o.w[i] = r ? ((a.w[i] >> r) | (hi << (64 - r))) : a.w[i];
   }
   return o;
+}
+// out bit p = a bit (p - r), 0 <= r < 64
+template <int NW>
+SDX_DEV M<NW> m_shl_small(const M<NW>& a, int r) {
+  M<NW> o;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint64_t lo = (i > 0) ? a.w[i - 1] : 0ull;
+    o.w[i] = r ? ((a.w[i] << r) | (lo >> (64 - r))) : a.w[i];
+  }
+  return o;
+}
+// out bit p = a bit (p + s): positions move DOWN by s (s >= 0)
+template <int NW>
+SDX_DEV M<NW> m_shr(const M<NW>& a, int s) {
+  const int q = s >> 6;
+  if (q == 0) return m_shr_small(a, s);
+  M<NW> b;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) b.w[i] = m_word(a, i + q);
+  return m_shr_small(b, s & 63);
+}
+// reverse the 4 bits inside every nibble (packed-LSB-first bits -> hex digit values)
+SDX_DEV uint64_t nibrev(uint64_t x) {
+  x = ((x & 0x5555555555555555ull) << 1) | ((x >> 1) & 0x5555555555555555ull);
+  x = ((x & 0x3333333333333333ull) << 2) | ((x >> 2) & 0x3333333333333333ull);
+  return x;
 }
 // first set bit at position >= from, or -1
 template <int NW>
@@ -105,7 +131,7 @@ SDX_DEV M<NW> m_occ(const uint64_t* bm, uint64_t tgt, int tlen) {
     M<NW> b;
 #pragma unroll
     for (int k = 0; k < NW; ++k) b.w[k] = bm[id * NW + k];
-    acc = m_and(acc, m_shr(b, i));
+    acc = m_and(acc, m_shr(b, i));  // i < 64: the word-aligned branch is never taken
   }
   return acc;
 }
@@ -117,7 +143,7 @@ template <int NW>
 SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const double* norm, uint64_t ids, int npat, const uint64_t* bm,
                             int minpos) {
   PexRes res{false, -1, 0};
-  const int nu = sp->nuniq, slen = sp->len;
+  const int nu = cld(&sp->nuniq), slen = cld(&sp->len);
   uint64_t cand[SDX_MAXUNIQ];
   int cnt[SDX_MAXUNIQ];
   long long total = 1;
@@ -126,7 +152,7 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const double* norm, uint64_t 
     cand[u] = 0;
     cnt[u] = 1;
     if (u < nu) {
-      const double v = sp->uval[u], tol = sp->utol[u];
+      const double v = cld(&sp->uval[u]), tol = cld(&sp->utol[u]);
       uint32_t okm = 0;
 #pragma unroll
       for (int j = 0; j < SDX_MAXPAT; ++j) {
@@ -177,7 +203,7 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const double* norm, uint64_t 
     }
     if (!dup) {
       uint64_t tgt = 0;
-      for (int i = 0; i < slen; ++i) tgt |= (uint64_t)((uid >> (4 * sp->uidx[i])) & 15) << (4 * i);
+      for (int i = 0; i < slen; ++i) tgt |= (uint64_t)((uid >> (4 * cld(&sp->uidx[i]))) & 15) << (4 * i);
       const int p = m_first(m_occ<NW>(bm, tgt, slen), minpos);
       if (p >= 0) {
         res.found = true;
@@ -211,12 +237,13 @@ SDX_DEV M<NW> m_range_lo(int k) {
   }
   return r;
 }
-// set/test bit b of a packed bitstring
+// set bit b of a packed bitstring (branch-free per word)
 template <int NW>
 SDX_DEV void m_set(M<NW>& a, int b) {
+  const uint64_t bitv = 1ull << (b & 63);
+  const int wi = b >> 6;
 #pragma unroll
-  for (int i = 0; i < NW; ++i)
-    if ((b >> 6) == i) a.w[i] |= 1ull << (b & 63);
+  for (int i = 0; i < NW; ++i) a.w[i] |= bitv & (0ull - (uint64_t)(wi == i));
 }
 // len (<= 4) bits starting at b, first bit = most significant (int(''.join(bits[b:b+len]), 2))
 template <int NW>
