@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 3u
+#define SDX_BANK_VERSION 4u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -28,11 +28,14 @@
 typedef struct {
   double uval[SDX_MAXUNIQ];
   double utol[SDX_MAXUNIQ];
+  /* the same test on the integer k of a normalised value k/10 (round(x/clock, 1)):
+   * candidate  <=>  klo[u] <= k <= khi[u]  (exact; computed by bank.py _k_interval) */
+  int32_t klo[SDX_MAXUNIQ], khi[SDX_MAXUNIQ];
   uint8_t len;   /* search length; 0 = key absent/falsy */
   uint8_t nuniq; /* number of distinct values */
   uint8_t pad[6];
   uint8_t uidx[SDX_MAXSEARCH]; /* search position -> unique index */
-} sdx_patspec;                 /* 152 bytes */
+} sdx_patspec;                 /* 120 bytes */
 
 enum sdx_postdemo {
   SDX_PD_NONE = 0, SDX_PD_EM, SDX_PD_REVOLT, SDX_PD_FS20, SDX_PD_FHT80, SDX_PD_FHT80TF,
@@ -97,7 +100,9 @@ typedef struct {
   uint32_t magic, version;
   uint32_t n_proto, n_mu, n_ms, n_mc, n_dfa, n_class;
   uint32_t off_mu, off_ms, off_mc, off_dfa, off_cls, off_trans, off_flags, off_str;
-  uint32_t total_bytes, off_t256, res[2];
+  uint32_t total_bytes, off_t256;
+  uint32_t off_order; /* u16 processing order: n_mu MU record indices, then n_ms MS indices */
+  uint32_t res;
 } sdx_bank_hdr;
 
 #endif

@@ -17,6 +17,7 @@ from __future__ import annotations
 import copy
 import json
 import os
+import math
 import struct
 from typing import Any, Dict, List, Optional
 
@@ -27,10 +28,11 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 3
+MAGIC, VERSION = 0x4B4E4253, 4
 INT_NONE = 2147483647  # "no length_max" sentinel
 
-PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
+PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("klo", "<i4", (MAXUNIQ,)),
+                    ("khi", "<i4", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
                     ("pad", "u1", (6,)), ("uidx", "u1", (MAXSEARCH,))], align=True)
 MU_REC = np.dtype([("clock", "<f8"), ("start", PATSPEC), ("one", PATSPEC), ("zero", PATSPEC), ("flt", PATSPEC),
                    ("proto_index", "<i4"), ("length_min", "<i4"), ("length_max", "<i4"), ("width", "<i4"),
@@ -92,6 +94,31 @@ def _int_exact(v, what) -> int:
     return int(v)
 
 
+K_LIMIT = 1 << 28  # |k| bound of every interval (the device's k sentinel lies beyond it)
+
+
+def _k_interval(v: float, tol: float):
+    """The exact integer set {k : g <= 0.001 or g <= tol, g = abs(k/10 - v)} as [klo, khi].
+
+    A message pattern normalises to ``round(x / clock, 1) == k / 10`` (round's result is the
+    correctly rounded quotient k/10.0), so pattern_utils.py:53-61's candidate test is a predicate
+    on the integer k.  k/10, the subtraction and abs are monotone in fp64, hence the accepted
+    set is an interval; it is found here with the same fp64 operations and checked to be
+    contiguous.
+    """
+    def ok(k: int) -> bool:
+        g = abs(k / 10 - v)
+        return g <= 0.001 or g <= tol
+    lo = math.floor(10 * (v - tol)) - 4
+    hi = math.ceil(10 * (v + tol)) + 4
+    acc = [k for k in range(lo, hi + 1) if ok(k)]
+    if not acc or ok(lo) or ok(hi) or acc != list(range(acc[0], acc[-1] + 1)):
+        raise NotImplementedError(f"pattern value {v!r}: candidate set is not a bounded interval")
+    if max(abs(acc[0]), abs(acc[-1])) >= K_LIMIT:
+        raise NotImplementedError(f"pattern value {v!r}: too large")
+    return acc[0], acc[-1]
+
+
 class Bank:
     """A compiled bank: the device blob plus host-side metadata for result building."""
 
@@ -126,6 +153,7 @@ class Bank:
             if not t >= 0.001:
                 raise NotImplementedError(f"{what}: tolerance below 0.001")
             rec["utol"][i] = t
+            rec["klo"][i], rec["khi"][i] = _k_interval(v, t)
         for i, v in enumerate(search):
             rec["uidx"][i] = uniq.index(v)
 
@@ -333,10 +361,16 @@ class Bank:
         flags_all = np.concatenate(flag_parts) if flag_parts else np.zeros(0, np.uint8)
         cls_arr = np.asarray(cls_of, dtype=np.uint8)
 
-        # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings   (16-B aligned sections)
+        # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings | t256 | order  (16-B aligned)
         hdr_size = struct.calcsize(HDR_FMT)
+        # processing orders (results are placed by protocol index, so any order is exact):
+        # MU sorted by clock so consecutive protocols reuse the normalised patterns
+        self.mu_order = sorted(range(len(self.mu_pids)), key=lambda r: float(mu[r]["clock"]))
+        self.ms_order = list(range(len(self.ms_pids)))
+        order = np.asarray(self.mu_order + self.ms_order, dtype=np.uint16)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
-                    trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes()]
+                    trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
+                    order.tobytes()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
         for s in sections:
@@ -345,7 +379,7 @@ class Bank:
         total = cur
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
-                          len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], 0, 0)
+                          len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], 0)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s

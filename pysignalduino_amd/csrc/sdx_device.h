@@ -41,6 +41,25 @@ SDX_DEV double py_round1(double q) {
   return res;
 }
 
+// the integer k of py_round1(q) == k / 10.0, or SDX_K_NONE when |q| >= 2^26 / NaN / inf: such a
+// value lies outside every bank interval [klo, khi] (bank.py bounds them by 2^28), exactly as its
+// fp64 gap exceeds every tolerance
+constexpr int SDX_K_NONE = INT32_MIN;
+SDX_DEV int py_round1_k(double q) {
+  if (!(fabs(q) < 67108864.0)) return SDX_K_NONE;
+  double f = floor(q * 10.0);
+  if (fma(10.0, q, -f) < 0.0) f -= 1.0;
+  else if (fma(10.0, q, -(f + 1.0)) >= 0.0) f += 1.0;
+  const double r = fma(10.0, q, -(f + 0.5));
+  double k;
+  if (r > 0.0) k = f + 1.0;
+  else if (r < 0.0) k = f;
+  else k = (fmod(f, 2.0) == 0.0) ? f : f + 1.0;
+  return (int)k;
+}
+// klo <= k <= khi (SDX_K_NONE never passes: the unsigned difference exceeds any interval width)
+SDX_DEV bool k_in(int k, int klo, int khi) { return (uint32_t)k - (uint32_t)klo <= (uint32_t)khi - (uint32_t)klo; }
+
 // ------------------------------------------------------------------------------------------------
 // wave helpers
 // ------------------------------------------------------------------------------------------------
@@ -64,7 +83,8 @@ SDX_DEV uint64_t bm_window(const uint64_t* bm, int w, int sh, int nw) {
 
 // ------------------------------------------------------------------------------------------------
 // pattern_exists (pattern_utils.py:34-136), one lane = one message.
-//   norm[] / ids: the message's normalised pattern values and their id digits in dict order
+//   kq[] / ids:   the message's normalised pattern values (as k of k/10) and their id digits
+//                 in dict order
 //   bm:           the message's per-id position bitmaps, bm[id*ws + w]
 // Returns the first id assignment (itertools.product order over gap-sorted candidate lists,
 // no id reused) whose concatenation occurs at a position >= minpos; tgt = its id digits packed
@@ -96,7 +116,7 @@ SDX_DEV bool substr_first(const uint64_t* bm, int ws, int nw, uint64_t tgt, int 
   return false;
 }
 
-__device__ __noinline__ PexRes pattern_exists(const sdx_patspec* sp, const double* norm, uint64_t ids, int npat,
+__device__ __noinline__ PexRes pattern_exists(const sdx_patspec* sp, const int* kq, uint64_t ids, int npat,
                                               const uint64_t* bm, int ws, int nw, int minpos) {
   PexRes res{false, -1, 0};
   const int nu = sp->nuniq, slen = sp->len;
@@ -108,13 +128,14 @@ __device__ __noinline__ PexRes pattern_exists(const sdx_patspec* sp, const doubl
     cand[u] = 0;
     cnt[u] = 1;
     if (u < nu) {
-      const double v = sp->uval[u], tol = sp->utol[u];
+      const double v = sp->uval[u];
+      const int klo = sp->klo[u], khi = sp->khi[u];
       double gap[SDX_MAXPAT];
       bool ok[SDX_MAXPAT];
 #pragma unroll
       for (int j = 0; j < SDX_MAXPAT; ++j) {
-        gap[j] = fabs(norm[j] - v);
-        ok[j] = (j < npat) && (gap[j] <= 0.001 || gap[j] <= tol);
+        ok[j] = (j < npat) && k_in(kq[j], klo, khi);  // == (gap <= 0.001 or gap <= tol)
+        gap[j] = fabs((double)kq[j] / 10.0 - v);        // the fp64 gap of norm == k/10 (ranking only)
       }
       int c = 0;
       uint64_t packed = 0;
@@ -474,6 +495,7 @@ struct BankView {
   const uint8_t* t256;
   const uint8_t* dflags;
   const uint8_t* str;
+  const uint16_t* order;  // processing order: MU indices, then MS indices
 };
 
 SDX_DEV BankView bank_view(const void* blob) {
@@ -489,6 +511,7 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.t256 = v.base + v.hdr->off_t256;
   v.dflags = v.base + v.hdr->off_flags;
   v.str = v.base + v.hdr->off_str;
+  v.order = (const uint16_t*)(v.base + v.hdr->off_order);
   v.hdr = uniform_ptr(v.hdr);
   v.mu = uniform_ptr(v.mu);
   v.ms = uniform_ptr(v.ms);
@@ -499,6 +522,7 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.t256 = uniform_ptr(v.t256);
   v.dflags = uniform_ptr(v.dflags);
   v.str = uniform_ptr(v.str);
+  v.order = uniform_ptr(v.order);
   return v;
 }
 

@@ -56,6 +56,16 @@ struct StageRec {
   uint16_t rank;
 };
 
+// MU (NW <= 4): a (message, protocol) pair that passed the pattern filters, queued for the
+// compacted decode (lane = pair)
+struct MuItem {
+  uint64_t st, u0, u1, u2;  // start / one / zero / float target strings (nibbles)
+  uint16_t idx, p;          // search start position, protocol index
+  uint8_t mi, fmask;        // tile message, found-key mask
+  uint16_t pad;
+};
+constexpr int QCAP = 128;  // per-wave ring: < 64 pending before a push of <= 64
+
 template <int NW, int TM>
 struct TileLds {
   static constexpr int WS = NW;              // words per id bitmap
@@ -73,14 +83,14 @@ struct TileLds {
   int32_t nlen[TM];
   uint32_t raise_key[TM];
   uint32_t digit_ok[TM];
-  uint16_t cnt[4][TM];
-  uint32_t rec_base, heap_base, tile_bad;
+  uint32_t cnt[TM];    // staged results per message (atomic; the old value is the record's rank)
+  uint32_t rec_base, heap_base, tile_bad, tot_rec;
   uint32_t wheap_pre[4];
   uint32_t mbase[TM];
   Wave w[4];
   StageRec rec[POOL_REC];
   uint8_t heap[POOL_HEAP];
-  int pool_nrec, pool_nheap, ovf;
+  int pool_nrec, pool_nheap, ovf, next_p;
 #ifdef SDX_PROF
   unsigned long long prof[4][32];
 #endif
@@ -127,8 +137,7 @@ SDX_DEV void pool_commit(T& L, int slot, int wave, int msg_local, int proto, int
     r.bitlen = (uint32_t)bitlen;
     r.msg = (uint8_t)msg_local;
     r.wave = (uint8_t)wave;
-    r.rank = L.cnt[wave][msg_local];
-    L.cnt[wave][msg_local] = (uint16_t)(r.rank + 1);
+    r.rank = (uint16_t)atomicAdd(&L.cnt[msg_local], 1u);
     L.rec[slot] = r;
   }
   wave_sync();
@@ -566,8 +575,7 @@ SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
   r.bitlen = (uint32_t)nbp;
   r.msg = (uint8_t)mi;
   r.wave = (uint8_t)wave;
-  r.rank = L.cnt[wave][mi];
-  L.cnt[wave][mi] = (uint16_t)(r.rank + 1);
+  r.rank = (uint16_t)atomicAdd(&L.cnt[mi], 1u);
   L.rec[slot] = r;
 }
 
@@ -788,18 +796,26 @@ SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
 }
 
 // ---------------------------------------------------------------------------------------------
-// tile flush: records in (message, protocol, match) order, one atomic per tile
+// tile flush: records in (message, protocol, match) order, one atomic per tile.
+// Records reach the pool in any order (waves and drained (message, protocol) items run
+// concurrently); a record's place inside its message is the number of records of the same
+// message with a smaller (protocol, rank) key -- rank is the per-message atomic counter, which
+// increases monotonically along one (message, protocol) pair's finditer loop.
 // ---------------------------------------------------------------------------------------------
 template <int NW, int TM>
 SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
   const int tid = threadIdx.x;
+  // flush scratch aliases the id bitmaps (dead once every wave has left the protocol loop)
+  static_assert(sizeof(L.bm) >= TM * 4 + POOL_REC * 2, "flush scratch does not fit the bitmaps");
+  uint32_t* fill = reinterpret_cast<uint32_t*>(L.bm);          // bucket fill per message
+  uint16_t* bidx = reinterpret_cast<uint16_t*>(fill + TM);     // pool records bucketed by message
+  if (tid < TM) fill[tid] = 0;
   if (tid == 0) {
     int bad = L.ovf ? 1 : 0;
     uint32_t nrec = 0;
     for (int m = 0; m < nvalid; ++m) {
       L.mbase[m] = nrec;
-      if (L.raise_key[m] == 0xFFFFFFFFu && !bad)
-        for (int w = 0; w < 4; ++w) nrec += L.cnt[w][m];
+      if (L.raise_key[m] == 0xFFFFFFFFu && !bad) nrec += L.cnt[m];
     }
     const uint32_t nheap = bad ? 0u : (uint32_t)L.pool_nheap;
     uint32_t rb = 0, hb = 0;
@@ -816,24 +832,36 @@ SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const
     L.tile_bad = bad;
     L.rec_base = rb;
     L.heap_base = hb;
+    L.tot_rec = nrec;
   }
   __syncthreads();
-  const int bad = L.tile_bad;
+  const int bad = L.tile_bad;  // block-uniform
   if (!bad) {
     const int nr = L.pool_nrec;
     for (int r = tid; r < nr; r += blockDim.x) {
-      const StageRec sr = L.rec[r];
-      if (L.raise_key[sr.msg] != 0xFFFFFFFFu) continue;
-      uint32_t before = 0;
-      for (int w = 0; w < (int)sr.wave; ++w) before += L.cnt[w][sr.msg];
-      const uint32_t dst = L.rec_base + L.mbase[sr.msg] + before + sr.rank;
+      const int m = L.rec[r].msg;
+      if (L.raise_key[m] != 0xFFFFFFFFu) continue;
+      const uint32_t b = atomicAdd(&fill[m], 1u);
+      bidx[L.mbase[m] + b] = (uint16_t)r;
+    }
+    __syncthreads();
+    const int nt = (int)L.tot_rec;
+    for (int j = tid; j < nt; j += blockDim.x) {
+      const StageRec sr = L.rec[bidx[j]];
+      const uint32_t key = ((uint32_t)sr.proto << 16) | sr.rank;
+      const uint32_t b0 = L.mbase[sr.msg], b1 = b0 + L.cnt[sr.msg];
+      uint32_t rk = 0;
+      for (uint32_t i = b0; i < b1; ++i) {
+        const StageRec& o = L.rec[bidx[i]];
+        rk += (((uint32_t)o.proto << 16) | o.rank) < key ? 1u : 0u;
+      }
       sdx_result o;
       o.payload_off = L.heap_base + sr.off;
       o.payload_len = sr.len;
       o.proto = sr.proto;
       o.bit_length = sr.bitlen;
       o.msg = (uint32_t)msg_of[sr.msg];
-      out.rec_dev[dst] = o;
+      out.rec_dev[L.rec_base + b0 + rk] = o;
     }
     uint8_t* hd = out.heap_dev + L.heap_base;
     const int nh = L.pool_nheap;
@@ -842,8 +870,6 @@ SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const
   for (int m = tid; m < nvalid; m += blockDim.x) {
     sdx_desc d;
     d.rec_begin = L.rec_base + L.mbase[m];
-    uint32_t nr = 0;
-    for (int w = 0; w < 4; ++w) nr += L.cnt[w][m];
     const uint32_t rk = L.raise_key[m];
     if (rk != 0xFFFFFFFFu) {
       d.status = SDX_ST_RAISED;
@@ -856,7 +882,7 @@ SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const
     } else {
       d.status = SDX_ST_OK;
       d.raise_kind = 0;
-      d.n_rec = (uint16_t)nr;
+      d.n_rec = (uint16_t)L.cnt[m];
     }
     out.desc_dev[msg_of[m]] = d;
   }
@@ -878,9 +904,10 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   if (tid < TM) {
     msg_of[tid] = (tid < nvalid) ? (b.sel_dev ? b.sel_dev[tile0 + tid] : tile0 + tid) : 0;
     L.raise_key[tid] = 0xFFFFFFFFu;
-    for (int w = 0; w < 4; ++w) L.cnt[w][tid] = 0;
+    L.cnt[tid] = 0;
   }
   if (tid == 0) {
+    L.next_p = 0;
     L.pool_nrec = 0;
     L.pool_nheap = 0;
     L.ovf = 0;
@@ -923,9 +950,13 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   const bool mvalid = mi < nvalid;
   int npat = 0, n = 0;
   uint64_t ids = 0;
-  double val[SDX_MAXPAT], norm[SDX_MAXPAT];
+  double val[SDX_MAXPAT];
+  int kq[SDX_MAXPAT];  // normalised pattern values round(x / clock, 1) == kq / 10 (SDX_K_NONE: absent)
 #pragma unroll
-  for (int k = 0; k < SDX_MAXPAT; ++k) val[k] = norm[k] = 0.0;
+  for (int k = 0; k < SDX_MAXPAT; ++k) {
+    val[k] = 0.0;
+    kq[k] = SDX_K_NONE;
+  }
   bool lane_ok = false;
   if (mvalid) {
     const int msg = msg_of[mi];
@@ -956,19 +987,45 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     if (lane_ok) {
 #pragma unroll
       for (int k = 0; k < SDX_MAXPAT; ++k)
-        if (k < npat) norm[k] = py_round1(val[k] / clock);
+        if (k < npat) kq[k] = py_round1_k(val[k] / clock);
     }
   }
   auto PEX = [&](const sdx_patspec* sp, int minpos) -> PexRes {
-    if constexpr (NW <= 4) return pexists_lane<NW>(sp, norm, ids, npat, bmine, minpos);
-    else return pattern_exists(sp, norm, ids, npat, bmine, T::WS, nw, minpos);
+    if constexpr (NW <= 4) return pexists_lane<NW>(sp, kq, ids, npat, bmine, minpos);
+    else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
   };
-  // ---- protocol loop: this wave's contiguous quarter of the class table
+  // ---- protocol loop: waves take protocols one at a time, in the bank's processing order
+  // (MU: sorted by clock), from a tile counter -- results are ordered at the flush, so the
+  // processing order is free and dynamic assignment balances the waves
   const int nproto = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu : (int)bv.hdr->n_ms;
-  const int qn = (nproto + 3) / 4;
-  const int p0 = wave * qn, p1 = (p0 + qn < nproto) ? p0 + qn : nproto;
+  const uint16_t* order = bv.order + (KIND == SDX_KIND_MU ? 0 : (int)bv.hdr->n_mu);
   double last_clock = __builtin_nan("");  // NaN != anything: the first protocol normalises
-  for (int p = p0; p < p1; ++p) {
+  MuItem* Q = nullptr;
+  int q_head = 0, q_tail = 0;
+  if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
+    __shared__ MuItem Qs[4][QCAP];
+    Q = Qs[wave];
+  }
+  auto drain = [&](int head, int cnt) {
+    wave_sync();
+    if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
+      if (lane < cnt) {
+        const MuItem it = Q[(head + lane) & (QCAP - 1)];
+        const int qm = it.mi, qp = it.p;
+        const uint32_t rk = L.raise_key[qm];
+        if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp)
+          decode_mu_lane(L, wave, bv, bv.mu + qp, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx, it.st,
+                         it.u0, it.u1, it.u2, it.fmask);
+      }
+    }
+    wave_sync();
+  };
+  while (true) {
+    int g = 0;
+    if (lane == 0) g = atomicAdd(&L.next_p, 1);
+    g = __builtin_amdgcn_readfirstlane(g);
+    if (g >= nproto) break;
+    const int p = cld(&order[g]);
     if (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
       if (cld(&rec->never) || !cld(&rec->active)) continue;
@@ -982,7 +1039,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
         const double ck = cld(&rec->clock);
 #pragma unroll
         for (int k = 0; k < SDX_MAXPAT; ++k)
-          if (k < npat) norm[k] = py_round1(val[k] / ck);
+          if (k < npat) kq[k] = py_round1_k(val[k] / ck);
       }
       PROF_ADD(1, t_norm);
       PROF_T(t_st);
@@ -1012,7 +1069,27 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       PROF_ADD(3, t_ozf);
       PROF_T(t_dec);
       if constexpr (NW <= 4) {
-        if (alive) decode_mu_lane(L, wave, bv, rec, p, mi, bmine, n, idx, st_tgt, ut0, ut1, ut2, fmask);
+        // queue the survivors; drain 64 at a time with lane = (message, protocol) pair
+        const uint64_t pass = ballot(alive);
+        if (pass) {
+          if (alive) {
+            MuItem it;
+            it.st = st_tgt;
+            it.u0 = ut0;
+            it.u1 = ut1;
+            it.u2 = ut2;
+            it.idx = (uint16_t)idx;
+            it.p = (uint16_t)p;
+            it.mi = (uint8_t)mi;
+            it.fmask = (uint8_t)fmask;
+            Q[(q_tail + lanes_below(pass)) & (QCAP - 1)] = it;
+          }
+          q_tail += popc64(pass);
+          if (q_tail - q_head >= WAVE) {
+            drain(q_head, WAVE);
+            q_head += WAVE;
+          }
+        }
       } else {
         uint64_t surv = ballot(alive);
         while (surv) {
@@ -1063,6 +1140,15 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
                   bcast_u64(kt2, sl), bcast_u64(kt3, sl), bcast_i(fmask, sl));
       }
     }
+  }
+  if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
+    PROF_T(t_dec);
+    while (q_head < q_tail) {
+      const int c = (q_tail - q_head < WAVE) ? q_tail - q_head : WAVE;
+      drain(q_head, c);
+      q_head += c;
+    }
+    PROF_ADD(12, t_dec);
   }
   PROF_T(t_bar);
   __syncthreads();
@@ -1573,6 +1659,8 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
   std::memcpy(&h, blob, sizeof h);
   if (h.magic != SDX_BANK_MAGIC || h.version != SDX_BANK_VERSION || h.total_bytes != nbytes)
     return fail(SDX_EBANK, "bank blob magic/version/size mismatch (rebuild the bank and the library)");
+  if ((size_t)h.off_order + 2u * ((size_t)h.n_mu + h.n_ms) > nbytes || h.n_mu > 65535u || h.n_ms > 65535u)
+    return fail(SDX_EBANK, "bank blob: processing-order section out of range");
   HIPCHK(hipSetDevice(device));
   void* d = nullptr;
   HIPCHK(hipMalloc(&d, nbytes));

@@ -140,7 +140,7 @@ SDX_DEV M<NW> m_occ(const uint64_t* bm, uint64_t tgt, int tlen) {
 // pattern_exists (pattern_utils.py:34-136) for one lane; fast path = one candidate per value
 // ---------------------------------------------------------------------------------------------
 template <int NW>
-SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const double* norm, uint64_t ids, int npat, const uint64_t* bm,
+SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
                             int minpos) {
   PexRes res{false, -1, 0};
   const int nu = cld(&sp->nuniq), slen = cld(&sp->len);
@@ -152,29 +152,33 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const double* norm, uint64_t 
     cand[u] = 0;
     cnt[u] = 1;
     if (u < nu) {
-      const double v = cld(&sp->uval[u]), tol = cld(&sp->utol[u]);
+      // candidates (pattern_utils.py:53-61) as an exact integer interval test on k (bank.py
+      // _k_interval); kq[j] == SDX_K_NONE for j >= npat
+      const int klo = cld(&sp->klo[u]), khi = cld(&sp->khi[u]);
       uint32_t okm = 0;
 #pragma unroll
-      for (int j = 0; j < SDX_MAXPAT; ++j) {
-        const double g = fabs(norm[j] - v);
-        if (j < npat && (g <= 0.001 || g <= tol)) okm |= 1u << j;
-      }
+      for (int j = 0; j < SDX_MAXPAT; ++j) okm |= (k_in(kq[j], klo, khi) ? 1u : 0u) << j;
       const int c = __popc(okm);
       if (c == 0) return res;  // pattern_utils.py:78-80
       if (c == 1) {
         cand[u] = (uint64_t)(__ffs(okm) - 1);
-      } else {  // stable sort by gap, ties in dict order (list.sort is stable)
+      } else {  // stable sort by the fp64 gap of k/10, ties in dict order (list.sort is stable)
+        const double v = cld(&sp->uval[u]);
         uint64_t packed = 0;
         for (uint32_t mj = okm; mj; mj &= mj - 1) {
           const int j = __ffs(mj) - 1;
-          double gj = 0.0;
+          int kj = 0;
 #pragma unroll
-          for (int k = 0; k < SDX_MAXPAT; ++k) gj = (k == j) ? fabs(norm[k] - v) : gj;
+          for (int k = 0; k < SDX_MAXPAT; ++k) kj = (k == j) ? kq[k] : kj;
+          const double gj = fabs((double)kj / 10.0 - v);
           int rank = 0;
+          for (uint32_t mk = okm; mk; mk &= mk - 1) {
+            const int k = __ffs(mk) - 1;
+            int kk = 0;
 #pragma unroll
-          for (int k = 0; k < SDX_MAXPAT; ++k) {
-            const double gk = fabs(norm[k] - v);
-            rank += (((okm >> k) & 1u) && (gk < gj || (gk == gj && k < j))) ? 1 : 0;
+            for (int t = 0; t < SDX_MAXPAT; ++t) kk = (t == k) ? kq[t] : kk;
+            const double gk = fabs((double)kk / 10.0 - v);
+            rank += (gk < gj || (gk == gj && k < j)) ? 1 : 0;
           }
           packed |= (uint64_t)j << (4 * rank);
         }
