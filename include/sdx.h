@@ -97,7 +97,8 @@ typedef struct sdx_bank sdx_bank;
 
 int sdx_abi_version(void);
 const char* sdx_last_error(void);
-/* sizeof() of the bank records, for host layout checks: 0 hdr, 1 patspec, 2 mu, 3 ms, 4 mc, 5 result, 6 desc */
+/* sizeof() of the bank records, for host layout checks: 0 hdr, 1 patspec, 2 mu, 3 ms, 4 mc, 5 result, 6 desc,
+ * 7 mu_desc */
 int sdx_layout_size(int which);
 
 /* bank: compiled by pysignalduino_amd/bank.py (protocols.json -> blob) and uploaded once per device */

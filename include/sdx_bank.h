@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 4u
+#define SDX_BANK_VERSION 6u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -31,11 +31,14 @@ typedef struct {
   /* the same test on the integer k of a normalised value k/10 (round(x/clock, 1)):
    * candidate  <=>  klo[u] <= k <= khi[u]  (exact; computed by bank.py _k_interval) */
   int32_t klo[SDX_MAXUNIQ], khi[SDX_MAXUNIQ];
+  /* candidate ordering (stable sort by fp64 gap, pattern_utils.py:61-63): rank of k in the u16
+   * table at ranks[rk_off[u] + k - klo[u]]; equal gaps share a rank */
+  uint32_t rk_off[SDX_MAXUNIQ];
   uint8_t len;   /* search length; 0 = key absent/falsy */
   uint8_t nuniq; /* number of distinct values */
   uint8_t pad[6];
   uint8_t uidx[SDX_MAXSEARCH]; /* search position -> unique index */
-} sdx_patspec;                 /* 120 bytes */
+} sdx_patspec;                 /* 136 bytes */
 
 enum sdx_postdemo {
   SDX_PD_NONE = 0, SDX_PD_EM, SDX_PD_REVOLT, SDX_PD_FS20, SDX_PD_FHT80, SDX_PD_FHT80TF,
@@ -88,6 +91,22 @@ typedef struct {
   uint8_t has_lmin, has_lmax, lmax_is_str, invert, has_cr, res[3];
 } sdx_mc_proto;
 
+/* MU decode descriptor: the fields the compacted MU decode reads for one (message, protocol)
+ * pair (message_unsynced.py:146-290), staged in LDS once per tile (the first SDX_MUDESC_LDS).
+ * mm_on: 0 no modulematch; 1 LDS tables: st = mmtab[(mm_base + st) * 16 + digit] per hex digit,
+ * then st = mmtab[17 * S + mm_post + st] for the postamble, accept on flags mmtab[16 * S + mm_base
+ * + st] (ACC_NOW and DEAD are absorbing); 2 byte walk through the blob's t256 table. */
+#define SDX_MUDESC_LDS 160
+#define SDX_MMTAB_LDS 10240
+typedef struct {
+  uint8_t pre[16], post[2];             /* preamble / postamble bytes (longer ones: string heap) */
+  uint8_t pre_len, post_len;
+  uint8_t width, len_s, recon, dispatch_bin, remove_zero, postdemo, pad_bits, mm_on;
+  uint16_t lmin, lmax;                  /* chunk-count limits, 65535 = none */
+  uint16_t mm_base, mm_post;
+  uint8_t pre_state, res[3];
+} sdx_mu_desc;                          /* 40 bytes */
+
 /* modulematch DFA (search semantics of re.search over the payload).
  * flags: bit0 = a match has been found (absorbing), bit1 = match if the payload
  * ends here ('$'), bit2 = dead (no match possible any more). */
@@ -102,7 +121,11 @@ typedef struct {
   uint32_t off_mu, off_ms, off_mc, off_dfa, off_cls, off_trans, off_flags, off_str;
   uint32_t total_bytes, off_t256;
   uint32_t off_order; /* u16 processing order: n_mu MU record indices, then n_ms MS indices */
-  uint32_t res;
+  uint32_t off_rank;  /* u16 candidate gap-rank tables (sdx_patspec.rk_off) */
+  uint32_t off_mudesc;  /* sdx_mu_desc[n_mu] */
+  uint32_t off_mmtab;   /* u8 modulematch tables for the MU decode (see sdx_mu_desc) */
+  uint32_t mmtab_bytes; /* <= SDX_MMTAB_LDS, multiple of 16 */
+  uint32_t mm_states;   /* S: hex[S][16] at 0, flags[S] at 16*S, post tables at 17*S */
 } sdx_bank_hdr;
 
 #endif

@@ -28,11 +28,11 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 4
+MAGIC, VERSION = 0x4B4E4253, 6
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("klo", "<i4", (MAXUNIQ,)),
-                    ("khi", "<i4", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
+                    ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
                     ("pad", "u1", (6,)), ("uidx", "u1", (MAXSEARCH,))], align=True)
 MU_REC = np.dtype([("clock", "<f8"), ("start", PATSPEC), ("one", PATSPEC), ("zero", PATSPEC), ("flt", PATSPEC),
                    ("proto_index", "<i4"), ("length_min", "<i4"), ("length_max", "<i4"), ("width", "<i4"),
@@ -50,7 +50,16 @@ MC_REC = np.dtype([("cr_lo", "<f8"), ("cr_hi", "<f8"), ("proto_index", "<i4"), (
                    ("has_cr", "u1"), ("res", "u1", (3,))], align=True)
 DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4"),
                     ("t256_off", "<i4"), ("res", "<i4", (3,))])
-HDR_FMT = "<" + "I" * 20  # sdx_bank_hdr: 20 uint32
+HDR_FMT = "<" + "I" * 24  # sdx_bank_hdr: 24 uint32
+# MU decode descriptor (sdx_mu_desc): what the compacted decode reads per (message, protocol) pair,
+# staged in LDS once per tile
+MU_DESC = np.dtype([("pre", "u1", (16,)), ("post", "u1", (2,)), ("pre_len", "u1"), ("post_len", "u1"),
+                    ("width", "u1"), ("len_s", "u1"), ("recon", "u1"), ("dispatch_bin", "u1"),
+                    ("remove_zero", "u1"), ("postdemo", "u1"), ("pad_bits", "u1"), ("mm_on", "u1"),
+                    ("lmin", "<u2"), ("lmax", "<u2"), ("mm_base", "<u2"), ("mm_post", "<u2"),
+                    ("pre_state", "u1"), ("res", "u1", (3,))])
+MUDESC_LDS = 160      # SDX_MUDESC_LDS: descriptors held in LDS (the rest are read from the blob)
+MMTAB_LDS = 10240     # SDX_MMTAB_LDS: bytes of modulematch tables held in LDS
 
 POSTDEMO = {"postDemo_EM": 1, "postDemo_Revolt": 2, "postDemo_FS20": 3, "postDemo_FHT80": 4,
             "postDemo_FHT80TF": 5, "postDemo_WS2000": 6, "postDemo_WS7035": 7, "postDemo_WS7053": 8,
@@ -119,6 +128,15 @@ def _k_interval(v: float, tol: float):
     return acc[0], acc[-1]
 
 
+def _gap_ranks(v: float, klo: int, khi: int) -> List[int]:
+    """Rank of each k in [klo, khi] by its fp64 gap abs(k/10 - v) (pattern_utils.py:61-63 sorts the
+    candidates by that gap, stably): equal gaps share a rank, so the device orders candidates by
+    (rank, dict position) exactly as list.sort does."""
+    gaps = [abs(k / 10 - v) for k in range(klo, khi + 1)]
+    order = {g: i for i, g in enumerate(sorted(set(gaps)))}
+    return [order[g] for g in gaps]
+
+
 class Bank:
     """A compiled bank: the device blob plus host-side metadata for result building."""
 
@@ -153,7 +171,13 @@ class Bank:
             if not t >= 0.001:
                 raise NotImplementedError(f"{what}: tolerance below 0.001")
             rec["utol"][i] = t
-            rec["klo"][i], rec["khi"][i] = _k_interval(v, t)
+            klo, khi = _k_interval(v, t)
+            rec["klo"][i], rec["khi"][i] = klo, khi
+            key = (v, t)
+            if key not in self._rank_off:
+                self._rank_off[key] = len(self._ranks)
+                self._ranks.extend(_gap_ranks(v, klo, khi))
+            rec["rk_off"][i] = self._rank_off[key]
         for i, v in enumerate(search):
             rec["uidx"][i] = uniq.index(v)
 
@@ -177,6 +201,8 @@ class Bank:
     def compile(self) -> None:
         P = self.protocols
         self._heap = bytearray()
+        self._ranks: List[int] = []                 # u16 gap-rank tables (sdx_patspec.rk_off)
+        self._rank_off: Dict[Any, int] = {}
         self.mu_pids = [pid for pid, p in P.items() if "clockabs" in p]
         self.ms_pids = [pid for pid, p in P.items() if "sync" in p]
         self.mc_pids = [pid for pid, p in P.items() if "clockrange" in p]
@@ -356,21 +382,23 @@ class Bank:
             toff += t.size
             foff += len(flags)
             t2off += nst * 256
+        mudesc, mmtab, mm_states = self._mu_desc(mu, dfas, cls_of)
         trans_all = np.concatenate(trans_parts) if trans_parts else np.zeros(0, np.uint16)
         t256_all = np.concatenate(t256_parts) if t256_parts else np.zeros(0, np.uint8)
         flags_all = np.concatenate(flag_parts) if flag_parts else np.zeros(0, np.uint8)
         cls_arr = np.asarray(cls_of, dtype=np.uint8)
 
-        # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings | t256 | order  (16-B aligned)
+        # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings | t256 | order | ranks | mudesc | mmtab
         hdr_size = struct.calcsize(HDR_FMT)
         # processing orders (results are placed by protocol index, so any order is exact):
         # MU sorted by clock so consecutive protocols reuse the normalised patterns
         self.mu_order = sorted(range(len(self.mu_pids)), key=lambda r: float(mu[r]["clock"]))
         self.ms_order = list(range(len(self.ms_pids)))
         order = np.asarray(self.mu_order + self.ms_order, dtype=np.uint16)
+        ranks = np.asarray(self._ranks, dtype=np.uint16)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
                     trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
-                    order.tobytes()]
+                    order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
         for s in sections:
@@ -379,12 +407,92 @@ class Bank:
         total = cur
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
-                          len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], 0)
+                          len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], offs[10], offs[11], offs[12],
+                          len(mmtab), mm_states)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s
         self.blob = bytes(blob)
         self.mu_table, self.ms_table, self.mc_table = mu, ms, mc
+
+    def _mu_desc(self, mu, dfas, cls_of):
+        """MU decode descriptors + the LDS modulematch tables.
+
+        mm tables (u8): hex[S][16] (DFA step on hex digit v, local state ids), flags[S], then per
+        protocol post[nstates] (state after its postamble).  ACC_NOW and DEAD are absorbing, so
+        walking every character and testing the final flags equals message_unsynced.py:277-280's
+        re.search.  A DFA that does not fit MMTAB_LDS (or is not absorbing) keeps mm_on = 2: the
+        device walks it byte by byte through the blob's t256 table instead.
+        """
+        P = self.protocols
+        d = np.zeros(len(self.mu_pids), MU_DESC)
+        hexc = [ord(c) for c in "0123456789ABCDEF"]
+        base_of: Dict[int, int] = {}
+        hex_rows: List[np.ndarray] = []
+        flag_rows: List[np.ndarray] = []
+        post_rows: List[int] = []
+        S = 0
+
+        def absorbing(nst, trans, flags):
+            t = np.asarray(trans)
+            for st in range(nst):
+                for bit in (regex_dfa.ACC_NOW, regex_dfa.DEAD):
+                    if flags[st] & bit and not all(flags[x] & bit for x in t[st]):
+                        return False
+            return True
+
+        def walk(dfa, st, data: bytes) -> int:
+            nst, start, trans, flags = dfa
+            for b in data:
+                st = int(trans[st][cls_of[b]])
+            return st
+
+        for r, pid in enumerate(self.mu_pids):
+            rec, p = mu[r], P[pid]
+            x = d[r]
+            pre = f"{p.get('preamble', '')}".encode("latin-1")
+            post = f"{p.get('postamble', '')}".encode("latin-1")
+            x["pre_len"], x["post_len"] = min(len(pre), 255), min(len(post), 255)
+            x["pre"][:min(len(pre), 16)] = list(pre[:16])
+            x["post"][:min(len(post), 2)] = list(post[:2])
+            x["width"] = int(rec["width"])
+            x["len_s"] = int(rec["start"]["len"]) if rec["has_start"] else 0
+            x["recon"], x["dispatch_bin"] = int(rec["recon"]), int(rec["dispatch_bin"])
+            x["remove_zero"], x["postdemo"] = int(rec["remove_zero"]), int(rec["postdemo"])
+            if int(rec["pad_bits"]) > 255:
+                raise NotImplementedError(f"MU {pid}: paddingbits > 255")
+            x["pad_bits"] = int(rec["pad_bits"])
+            x["lmin"] = min(int(rec["length_min"]), 65535)
+            x["lmax"] = min(int(rec["length_max"]), 65535)  # chunk counts never exceed 4096
+            k = int(rec["mm_dfa"])
+            if k < 0:
+                continue
+            x["mm_on"] = 2
+            x["pre_state"] = int(rec["mm_pre_state"])
+            nst, start, trans, flags = dfas[k]
+            if not absorbing(nst, trans, flags):
+                continue
+            if k not in base_of:
+                if 17 * (S + nst) + len(post_rows) + nst > MMTAB_LDS:
+                    continue
+                base_of[k] = S
+                t = np.asarray(trans, dtype=np.int64)
+                hex_rows.append(t[:, [cls_of[c] for c in hexc]].astype(np.uint8))
+                flag_rows.append(np.asarray(flags, dtype=np.uint8))
+                S += nst
+            if 17 * S + len(post_rows) + nst > MMTAB_LDS:
+                continue
+            x["mm_on"] = 1
+            x["mm_base"] = base_of[k]
+            x["mm_post"] = len(post_rows)
+            post_rows.extend(walk(dfas[k], st, post) for st in range(nst))
+        hexs = np.concatenate(hex_rows).reshape(-1) if hex_rows else np.zeros(0, np.uint8)
+        fls = np.concatenate(flag_rows) if flag_rows else np.zeros(0, np.uint8)
+        tab = np.concatenate([hexs, fls, np.asarray(post_rows, dtype=np.uint8)])
+        tab = np.concatenate([tab, np.zeros((-len(tab)) % 16, np.uint8)])
+        assert len(tab) <= MMTAB_LDS
+        self.mu_desc = d
+        return d, tab, S
 
     # -- host-side metadata used when turning device records into reference dicts -------------
     def class_pid(self, kind: str, rec_index: int) -> str:

@@ -57,6 +57,21 @@ SDX_DEV int py_round1_k(double q) {
   else k = (fmod(f, 2.0) == 0.0) ? f : f + 1.0;
   return (int)k;
 }
+// 10-key sorting network (29 comparators, depth 8; Knuth TAOCP 5.3.4), ascending
+SDX_DEV void sort10(uint32_t* a) {
+#define SDX_CE(i, j)                      \
+  {                                       \
+    const uint32_t x = a[i], y = a[j];    \
+    a[i] = x < y ? x : y;                 \
+    a[j] = x < y ? y : x;                 \
+  }
+  SDX_CE(4, 9) SDX_CE(3, 8) SDX_CE(2, 7) SDX_CE(1, 6) SDX_CE(0, 5) SDX_CE(1, 4) SDX_CE(6, 9) SDX_CE(0, 3)
+  SDX_CE(5, 8) SDX_CE(0, 2) SDX_CE(3, 6) SDX_CE(7, 9) SDX_CE(0, 1) SDX_CE(2, 4) SDX_CE(5, 7) SDX_CE(8, 9)
+  SDX_CE(1, 2) SDX_CE(4, 6) SDX_CE(7, 8) SDX_CE(3, 5) SDX_CE(2, 5) SDX_CE(6, 8) SDX_CE(1, 3) SDX_CE(4, 7)
+  SDX_CE(2, 3) SDX_CE(6, 7) SDX_CE(3, 4) SDX_CE(5, 6) SDX_CE(4, 5)
+#undef SDX_CE
+}
+
 // klo <= k <= khi (SDX_K_NONE never passes: the unsigned difference exceeds any interval width)
 SDX_DEV bool k_in(int k, int klo, int khi) { return (uint32_t)k - (uint32_t)klo <= (uint32_t)khi - (uint32_t)klo; }
 
@@ -496,6 +511,9 @@ struct BankView {
   const uint8_t* dflags;
   const uint8_t* str;
   const uint16_t* order;  // processing order: MU indices, then MS indices
+  const uint16_t* rank;   // candidate gap-rank tables
+  const sdx_mu_desc* mudesc;
+  const uint8_t* mmtab;
 };
 
 SDX_DEV BankView bank_view(const void* blob) {
@@ -512,6 +530,9 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.dflags = v.base + v.hdr->off_flags;
   v.str = v.base + v.hdr->off_str;
   v.order = (const uint16_t*)(v.base + v.hdr->off_order);
+  v.rank = (const uint16_t*)(v.base + v.hdr->off_rank);
+  v.mudesc = (const sdx_mu_desc*)(v.base + v.hdr->off_mudesc);
+  v.mmtab = v.base + v.hdr->off_mmtab;
   v.hdr = uniform_ptr(v.hdr);
   v.mu = uniform_ptr(v.mu);
   v.ms = uniform_ptr(v.ms);
@@ -523,6 +544,9 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.dflags = uniform_ptr(v.dflags);
   v.str = uniform_ptr(v.str);
   v.order = uniform_ptr(v.order);
+  v.rank = uniform_ptr(v.rank);
+  v.mudesc = uniform_ptr(v.mudesc);
+  v.mmtab = uniform_ptr(v.mmtab);
   return v;
 }
 

@@ -35,9 +35,16 @@ __device__ unsigned long long g_prof[32];
   do {                                                                                      \
     if (__lane_id() == 0) L.prof[wave][slot] += (unsigned long long)(x);                   \
   } while (0)
+// divergent code: the lowest active lane accounts the wave's time
+#define PROF_ADDD(slot, v)                                                                  \
+  do {                                                                                      \
+    if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_read_exec()) - 1)       \
+      L.prof[wave][slot] += __builtin_amdgcn_s_memtime() - (v);                             \
+  } while (0)
 #else
 #define PROF_T(v)
 #define PROF_ADD(slot, v)
+#define PROF_ADDD(slot, v)
 #define PROF_CNT(slot, x)
 #endif
 
@@ -59,14 +66,16 @@ struct StageRec {
 // MU (NW <= 4): a (message, protocol) pair that passed the pattern filters, queued for the
 // compacted decode (lane = pair)
 struct MuItem {
-  uint64_t st, u0, u1, u2;  // start / one / zero / float target strings (nibbles)
+  uint32_t st_lo, st_hi;    // start target string (nibbles)
+  uint16_t u0, u1, u2;      // one / zero / float target strings (width <= 4 -> 4 nibbles)
   uint16_t idx, p;          // search start position, protocol index
   uint8_t mi, fmask;        // tile message, found-key mask
-  uint16_t pad;
 };
 constexpr int QCAP = 128;  // per-wave ring: < 64 pending before a push of <= 64
 
-template <int NW, int TM>
+// LM: the lane-decode MU variant (NW <= 4) -- no per-wave byte scratch, but the MU decode
+// descriptors and modulematch tables staged in LDS
+template <int NW, int TM, bool LM>
 struct TileLds {
   static constexpr int WS = NW;              // words per id bitmap
   static constexpr int MSTRIDE = 10 * NW + 1;  // odd stride: fewer LDS bank conflicts across lanes
@@ -87,10 +96,13 @@ struct TileLds {
   uint32_t rec_base, heap_base, tile_bad, tot_rec;
   uint32_t wheap_pre[4];
   uint32_t mbase[TM];
-  Wave w[4];
+  Wave w[LM ? 1 : 4];
   StageRec rec[POOL_REC];
-  uint8_t heap[POOL_HEAP];
+  alignas(16) uint8_t heap[POOL_HEAP];
   int pool_nrec, pool_nheap, ovf, next_p;
+  int mm_states;
+  alignas(16) sdx_mu_desc desc[LM ? SDX_MUDESC_LDS : 1];
+  alignas(16) uint8_t mmtab[LM ? SDX_MMTAB_LDS : 16];
 #ifdef SDX_PROF
   unsigned long long prof[4][32];
 #endif
@@ -195,8 +207,8 @@ SDX_DEV void raise_msg(T& L, int msg_local, int proto, int kind) {
 // ---------------------------------------------------------------------------------------------
 // MU: finish one match (message_unsynced.py:230-290)
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM>
-SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
+template <int NW, int TM, bool LM>
+SDX_DEV void finish_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
                        int nb) {
   auto& W = L.w[wave];
   uint8_t* buf = W.bits;
@@ -303,10 +315,10 @@ SDX_DEV void finish_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
 // MU: decode one surviving (message, protocol) pair with the whole wave
 // (message_unsynced.py:146-290; re.finditer emulated exactly)
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM>
-SDX_DEV void decode_mu(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
+template <int NW, int TM, bool LM>
+SDX_DEV void decode_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
                        int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1, uint64_t ut2, int fmask) {
-  using T = TileLds<NW, TM>;
+  using T = TileLds<NW, TM, LM>;
   auto& W = L.w[wave];
   const int lane = lane_id();
   const uint64_t* bm = &L.bm[s * T::MSTRIDE];
@@ -471,32 +483,72 @@ SDX_DEV M<NW> m_range(int a, int b) {  // positions [a, b)
   return r;
 }
 
-template <int NW, int TM>
-SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int mi,
+// little-endian byte stream into 8-byte aligned LDS words (the tail word is zero-padded)
+struct ByteWriter {
+  uint64_t* dst;
+  uint64_t acc = 0;
+  int n = 0;
+  SDX_DEV explicit ByteWriter(uint64_t* d) : dst(d) {}
+  // append the low `cnt` (<= 8) bytes of `chunk` (its higher bytes are zero)
+  SDX_DEV void put(uint64_t chunk, int cnt) {
+    acc |= chunk << (8 * n);
+    const uint64_t spill = n ? chunk >> (64 - 8 * n) : 0ull;
+    n += cnt;
+    if (n >= 8) {
+      *dst++ = acc;
+      acc = spill;
+      n -= 8;
+    }
+  }
+  SDX_DEV void flush() {
+    if (n) *dst = acc;
+  }
+};
+
+// 8 hex digits (nibble i of x = digit i) -> 8 ASCII bytes '0'-'9','A'-'F' (byte i); only the low
+// `cnt` bytes are kept
+SDX_DEV uint64_t hex8(uint64_t x, int cnt) {
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  const uint64_t ge10 = ((x + 0x0606060606060606ull) >> 4) & 0x0101010101010101ull;
+  x += 0x3030303030303030ull + ge10 * 7ull;
+  return cnt >= 8 ? x : x & ((1ull << (8 * cnt)) - 1);
+}
+
+template <int NW, class T>
+SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
+                            int mi,
                             int q, int k, int Lw, bool emf, uint8_t esym, const M<NW>& V1, const M<NW>& VF) {
   constexpr int NB = 64 * NW + 64;
+  PROF_T(t_x);
   int nb = k + ((emf && Lw > 1) ? 1 : 0);
   // the chunk symbols as two packed bitstrings: P1 = symbol '1', PF = symbol 'F'
-  M<NW> P1 = m_stride_extract(V1, q, Lw, k), PF = m_stride_extract(VF, q, Lw, k);
+  M<NW> P1 = m_stride_extract(V1, q, Lw, k), PF = m_zero<NW>();
+  if (m_any(VF)) PF = m_stride_extract(VF, q, Lw, k);  // most protocols have no float symbol
   if (nb > k) {
     if (esym == 1) m_set(P1, k);
     if (esym == 2) m_set(PF, k);
   }
   bool anyf = m_any(PF);
+  PROF_ADDD(6, t_x);
+  PROF_T(t_pd);
   uint8_t pout[NB];
   bool usearr = false;
-  if (cld(&rec->postdemo) != SDX_PD_NONE && !anyf) {  // 'F' -> int() ValueError caught -> unchanged
+  if (d.postdemo != SDX_PD_NONE && !anyf) {  // 'F' -> int() ValueError caught -> unchanged
     uint8_t pin[NB];
     for (int b = 0; b < nb; ++b) pin[b] = m_test(P1, b) ? 1 : 0;
     int no = 0;
-    const int rc = run_postdemo(cld(&rec->postdemo), pin, nb, pout, &no);
+    const int rc = run_postdemo(d.postdemo, pin, nb, pout, &no);
     if (rc == 0) return;  // rcode < 1: match dropped
     if (rc == 1) {
       usearr = true;
       nb = no;
     }
   }
-  const int pad = cld(&rec->pad_bits);
+  PROF_ADDD(7, t_pd);
+  PROF_T(t_fmt);
+  const int pad = d.pad_bits;
   int nbp = nb;
   while (nbp % pad) ++nbp;
   const int nd = (nbp + 3) >> 2;
@@ -519,22 +571,31 @@ SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
     for (int i = a; i < e; ++i) v = (v << 1) | (i < nb ? pout[i] : 0);
     return v;
   };
+  const bool binm = d.dispatch_bin != 0;
+  // fast path: plain hex digits straight from the nibble-reversed words H
+  const bool fast = !usearr && !anyf && !binm;
   int dlen, skip = 0;
-  if (cld(&rec->dispatch_bin)) {
+  if (binm) {
     dlen = nbp;
   } else if (anyf) {
-    if (cld(&rec->remove_zero)) {  // None.lstrip('0') -> AttributeError (:269)
+    if (d.remove_zero) {  // None.lstrip('0') -> AttributeError (:269)
       atomicMin(&L.raise_key[mi], ((uint32_t)p << 8) | SDX_RAISE_ATTRIBUTE);
       return;
     }
     dlen = 4;
   } else {
-    if (cld(&rec->remove_zero))
-      while (skip < nd && digit(skip) == 0) ++skip;
+    if (d.remove_zero) {
+      if (fast) {  // first non-zero nibble (H holds no bits past digit nd)
+        const int f = m_first(H, 0);
+        skip = (f < 0 || (f >> 2) >= nd) ? nd : (f >> 2);
+      } else {
+        while (skip < nd && digit(skip) == 0) ++skip;
+      }
+    }
     dlen = nd - skip;
   }
   auto dchar = [&](int i) -> uint8_t {
-    if (cld(&rec->dispatch_bin)) {
+    if (binm) {
       if (usearr) return (uint8_t)(i < nb ? (pout[i] == 2 ? 'F' : '0' + pout[i]) : '0');
       return m_test(PF, i) ? 'F' : (uint8_t)('0' + (m_test(P1, i) ? 1 : 0));
     }
@@ -542,32 +603,78 @@ SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
     const int v = digit(i + skip);
     return (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
   };
-  if (cld(&rec->mm_dfa) >= 0) {  // re.search(modulematch, payload) (:277-280)
+  const int pre_len = d.pre_len, post_len = d.post_len;
+  const uint8_t* pre_g = pre_len > 16 ? bv.str + cld(&rec->pre_off) : nullptr;     // long strings: heap
+  const uint8_t* post_g = post_len > 2 ? bv.str + cld(&rec->post_off) : nullptr;
+  uint64_t pre0, pre1;  // the inline strings as words (no dynamic indexing into the descriptor)
+  __builtin_memcpy(&pre0, d.pre, 8);
+  __builtin_memcpy(&pre1, d.pre + 8, 8);
+  const uint64_t post16 = (uint64_t)d.post[0] | ((uint64_t)d.post[1] << 8);
+  auto post_c = [&](int i) -> uint8_t { return post_g ? post_g[i] : (uint8_t)(post16 >> (8 * i)); };
+  if (d.mm_on == 1 && fast) {  // re.search(modulematch, payload) (:277-280) on the LDS hex tables
+    const uint8_t* hx = L.mmtab + 16 * (int)d.mm_base;
+    int st = d.pre_state;
+    uint64_t cur = 0;
+    for (int i = 0; i < dlen; ++i) {
+      const int dd = skip + i;
+      if (i == 0 || (dd & 15) == 0) cur = m_word(H, dd >> 4) >> (4 * (dd & 15));
+      st = hx[16 * st + (int)(cur & 15ull)];
+      cur >>= 4;
+    }
+    st = L.mmtab[17 * L.mm_states + d.mm_post + st];
+    const uint8_t f = L.mmtab[16 * L.mm_states + d.mm_base + st];
+    if (!((f & 1) || (!(f & 4) && (f & 2)))) return;
+  } else if (d.mm_on) {  // byte walk through the blob's t256 table
     const sdx_dfa D = bv.dfa[cld(&rec->mm_dfa)];
     const uint8_t* t256 = bv.t256 + D.t256_off;
     const uint8_t* fl = bv.dflags + D.flags_off;
-    int st = cld(&rec->mm_pre_state);
-    const int tot = dlen + cld(&rec->post_len);
+    int st = d.pre_state;
+    const int tot = dlen + post_len;
     int i = 0;
     for (; i < tot; ++i) {
       if (fl[st] & 5) break;
-      const uint8_t c = i < dlen ? dchar(i) : bv.str[cld(&rec->post_off) + i - dlen];
+      const uint8_t c = i < dlen ? dchar(i) : post_c(i - dlen);
       st = t256[st * 256 + c];
     }
     const uint8_t f = fl[st];
     if (!((f & 1) || (!(f & 4) && i == tot && (f & 2)))) return;
   }
-  const int total = cld(&rec->pre_len) + dlen + cld(&rec->post_len);
+  PROF_ADDD(9, t_fmt);
+  PROF_T(t_wr);
+  // payload (:271-274): preamble + digits + postamble into an 8-byte aligned pool slot
+  const int total = pre_len + dlen + post_len;
+  const int span = (total + 7) & ~7;
   const int slot = atomicAdd(&L.pool_nrec, 1);
-  const int off = atomicAdd(&L.pool_nheap, total);
-  if (slot >= POOL_REC || off + total > POOL_HEAP) {
+  const int off = atomicAdd(&L.pool_nheap, span);
+  if (slot >= POOL_REC || off + span > POOL_HEAP) {
     L.ovf = 1;
     return;
   }
-  uint8_t* dst = L.heap + off;
-  for (int i = 0; i < cld(&rec->pre_len); ++i) dst[i] = bv.str[cld(&rec->pre_off) + i];
-  for (int i = 0; i < dlen; ++i) dst[cld(&rec->pre_len) + i] = dchar(i);
-  for (int i = 0; i < cld(&rec->post_len); ++i) dst[cld(&rec->pre_len) + dlen + i] = bv.str[cld(&rec->post_off) + i];
+  ByteWriter w(reinterpret_cast<uint64_t*>(L.heap + off));
+  if (pre_g) {
+    for (int i = 0; i < pre_len; ++i) w.put(pre_g[i], 1);
+  } else {
+    auto lowb = [](uint64_t x, int c) { return c >= 8 ? x : x & ((1ull << (8 * c)) - 1); };
+    if (pre_len) w.put(lowb(pre0, pre_len), pre_len < 8 ? pre_len : 8);
+    if (pre_len > 8) w.put(lowb(pre1, pre_len - 8), pre_len - 8);
+  }
+  if (fast) {
+    for (int t = 0; t < dlen; t += 8) {  // 8 digits per step: nibbles -> bytes -> ASCII hex
+      const int b = 4 * (skip + t), wi = b >> 6, sh = b & 63;
+      uint64_t x = m_word(H, wi) >> sh;
+      if (sh > 32) x |= m_word(H, wi + 1) << (64 - sh);
+      const int cnt = (dlen - t < 8) ? dlen - t : 8;
+      w.put(hex8(x & 0xFFFFFFFFull, cnt), cnt);
+    }
+  } else {
+    for (int i = 0; i < dlen; ++i) w.put(dchar(i), 1);
+  }
+  if (post_g) {
+    for (int i = 0; i < post_len; ++i) w.put(post_g[i], 1);
+  } else if (post_len) {
+    w.put(post_len == 1 ? (post16 & 0xFFull) : post16, post_len);
+  }
+  w.flush();
   StageRec r;
   r.off = (uint32_t)off;
   r.len = (uint16_t)total;
@@ -577,15 +684,17 @@ SDX_DEV void finish_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
   r.wave = (uint8_t)wave;
   r.rank = (uint16_t)atomicAdd(&L.cnt[mi], 1u);
   L.rec[slot] = r;
+  PROF_ADDD(8, t_wr);
 }
 
 // MU, lane = message: exact re.finditer emulation on register bitmasks (message_unsynced.py:146-290)
-template <int NW, int TM>
-SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p,
+template <int NW, class T>
+SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
                             int mi, const uint64_t* bm, int n, int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1,
                             uint64_t ut2, int fmask) {
-  const int Lw = cld(&rec->width);
-  const int lenS = cld(&rec->has_start) ? (int)cld(&rec->start.len) : 0;
+  PROF_T(t_setup);
+  const int Lw = d.width;
+  const int lenS = d.len_s;
   const uint64_t ut[3] = {ut0, ut1, ut2};
   const uint8_t SYM[3] = {1, 0, 2};
   M<NW> U = m_zero<NW>(), V1 = m_zero<NW>(), VF = m_zero<NW>();
@@ -606,7 +715,7 @@ SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
   //  prefix -- first writer wins -- which is the insertion-ordered dict without dynamic indexing)
   bool elive[3] = {false, false, false};
   uint64_t ekey[3] = {0, 0, 0};
-  if (cld(&rec->recon) && Lw > 1) {
+  if (d.recon && Lw > 1) {
     const uint64_t msk = (Lw - 1 >= 16) ? ~0ull : ((1ull << (4 * (Lw - 1))) - 1);
 #pragma unroll
     for (int kk = 0; kk < 3; ++kk) {
@@ -618,13 +727,15 @@ SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
     }
   }
   const M<NW> S = lenS ? m_occ<NW>(bm, st_tgt, lenS) : m_all<NW>();
-  const int lmin = cld(&rec->length_min);
+  const int lmin = d.lmin;
   // s: START at s and >= length_min units at s+lenS (with length_min 0 every START qualifies,
   // including one that ends exactly at the end of the data: empty group -> IndexError)
   const M<NW> V = lmin > 0 ? m_and(S, m_shr(m_runs(U, lmin, Lw), lenS)) : S;
   const M<NW> NU = m_not(U);
   int pos = idx;
+  PROF_ADDD(4, t_setup);
   while (true) {
+    PROF_T(t_scan);
     const int s = m_first(V, pos);
     if (s < 0 || s > n) break;
     const int q = s + lenS;
@@ -653,8 +764,9 @@ SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
     }
     pos = q + G;
     const int nch = k + (emf ? 1 : 0);
-    if (nch > cld(&rec->length_max)) continue;  // (:217-218)
-    finish_mu_lane(L, wave, bv, rec, p, mi, q, k, Lw, emf, esym, V1, VF);
+    PROF_ADDD(5, t_scan);
+    if (nch > (int)d.lmax) continue;  // (:217-218); 65535 = none
+    finish_mu_lane<NW>(L, wave, bv, rec, d, p, mi, q, k, Lw, emf, esym, V1, VF);
     if ((L.raise_key[mi] >> 8) <= (uint32_t)p) return;
   }
 }
@@ -662,8 +774,8 @@ SDX_DEV void decode_mu_lane(TileLds<NW, TM>& L, int wave, const BankView& bv, co
 // ---------------------------------------------------------------------------------------------
 // MS: finish (message_synced.py:191-241)
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM>
-SDX_DEV void finish_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
+template <int NW, int TM, bool LM>
+SDX_DEV void finish_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
                        int nb) {
   auto& W = L.w[wave];
   uint8_t* buf = W.bits;
@@ -710,10 +822,10 @@ SDX_DEV void finish_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
 }
 
 // MS decode loop (:172-189) for one surviving pair, wave-cooperative over chunks
-template <int NW, int TM>
-SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
+template <int NW, int TM, bool LM>
+SDX_DEV void decode_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
                        int start, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3, int fmask) {
-  using T = TileLds<NW, TM>;
+  using T = TileLds<NW, TM, LM>;
   auto& W = L.w[wave];
   const int lane = lane_id();
   const uint64_t* bm = &L.bm[s * T::MSTRIDE];
@@ -802,8 +914,8 @@ SDX_DEV void decode_ms(TileLds<NW, TM>& L, int wave, const BankView& bv, const s
 // message with a smaller (protocol, rank) key -- rank is the per-message atomic counter, which
 // increases monotonically along one (message, protocol) pair's finditer loop.
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM>
-SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
+template <int NW, int TM, bool LM>
+SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
   const int tid = threadIdx.x;
   // flush scratch aliases the id bitmaps (dead once every wave has left the protocol loop)
   static_assert(sizeof(L.bm) >= TM * 4 + POOL_REC * 2, "flush scratch does not fit the bitmaps");
@@ -893,7 +1005,8 @@ SDX_DEV void flush_tile(TileLds<NW, TM>& L, const int* msg_of, int nvalid, const
 // ---------------------------------------------------------------------------------------------
 template <int KIND, int NW, int TM>
 __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
-  using T = TileLds<NW, TM>;
+  constexpr bool LANE_MU = KIND == SDX_KIND_MU && NW <= 4;
+  using T = TileLds<NW, TM, LANE_MU>;
   __shared__ T L;
   const BankView bv = bank_view(bank);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -911,6 +1024,18 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     L.pool_nrec = 0;
     L.pool_nheap = 0;
     L.ovf = 0;
+  }
+  if constexpr (LANE_MU) {  // MU decode descriptors + modulematch tables -> LDS (16-B pieces)
+    const int ndesc = (int)bv.hdr->n_mu < SDX_MUDESC_LDS ? (int)bv.hdr->n_mu : SDX_MUDESC_LDS;
+    const int n16 = (ndesc * (int)sizeof(sdx_mu_desc) + 15) >> 4;
+    const uint4* src = reinterpret_cast<const uint4*>(bv.mudesc);
+    uint4* dst = reinterpret_cast<uint4*>(L.desc);
+    for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
+    const int m16 = (int)bv.hdr->mmtab_bytes >> 4;
+    const uint4* msrc = reinterpret_cast<const uint4*>(bv.mmtab);
+    uint4* mdst = reinterpret_cast<uint4*>(L.mmtab);
+    for (int i = tid; i < m16; i += blockDim.x) mdst[i] = msrc[i];
+    if (tid == 0) L.mm_states = (int)bv.hdr->mm_states;
   }
 #ifdef SDX_PROF
   if (lane < 32) L.prof[wave][lane] = 0;
@@ -991,7 +1116,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     }
   }
   auto PEX = [&](const sdx_patspec* sp, int minpos) -> PexRes {
-    if constexpr (NW <= 4) return pexists_lane<NW>(sp, kq, ids, npat, bmine, minpos);
+    if constexpr (NW <= 4) return pexists_lane<NW>(sp, kq, ids, npat, bmine, minpos, bv.rank);
     else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
   };
   // ---- protocol loop: waves take protocols one at a time, in the bank's processing order
@@ -1013,9 +1138,17 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
         const MuItem it = Q[(head + lane) & (QCAP - 1)];
         const int qm = it.mi, qp = it.p;
         const uint32_t rk = L.raise_key[qm];
-        if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp)
-          decode_mu_lane(L, wave, bv, bv.mu + qp, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx, it.st,
-                         it.u0, it.u1, it.u2, it.fmask);
+#ifndef SDX_X_NODECODE
+        if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp) {
+#else
+        if (rk == 0x12345u) {
+#endif
+          sdx_mu_desc d;
+          if (qp < SDX_MUDESC_LDS) d = L.desc[qp];
+          else d = bv.mudesc[qp];
+          decode_mu_lane<NW>(L, wave, bv, bv.mu + qp, d, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx,
+                             ((uint64_t)it.st_hi << 32) | it.st_lo, it.u0, it.u1, it.u2, it.fmask);
+        }
       }
     }
     wave_sync();
@@ -1074,10 +1207,11 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
         if (pass) {
           if (alive) {
             MuItem it;
-            it.st = st_tgt;
-            it.u0 = ut0;
-            it.u1 = ut1;
-            it.u2 = ut2;
+            it.st_lo = (uint32_t)st_tgt;
+            it.st_hi = (uint32_t)(st_tgt >> 32);
+            it.u0 = (uint16_t)ut0;
+            it.u1 = (uint16_t)ut1;
+            it.u2 = (uint16_t)ut2;
             it.idx = (uint16_t)idx;
             it.p = (uint16_t)p;
             it.mi = (uint8_t)mi;
@@ -1649,6 +1783,7 @@ int sdx_layout_size(int which) {
     case 4: return (int)sizeof(sdx_mc_proto);
     case 5: return (int)sizeof(sdx_result);
     case 6: return (int)sizeof(sdx_desc);
+    case 7: return (int)sizeof(sdx_mu_desc);
   }
   return -1;
 }
@@ -1659,7 +1794,10 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
   std::memcpy(&h, blob, sizeof h);
   if (h.magic != SDX_BANK_MAGIC || h.version != SDX_BANK_VERSION || h.total_bytes != nbytes)
     return fail(SDX_EBANK, "bank blob magic/version/size mismatch (rebuild the bank and the library)");
-  if ((size_t)h.off_order + 2u * ((size_t)h.n_mu + h.n_ms) > nbytes || h.n_mu > 65535u || h.n_ms > 65535u)
+  if ((size_t)h.off_order + 2u * ((size_t)h.n_mu + h.n_ms) > nbytes || h.off_rank > nbytes || h.n_mu > 65535u ||
+      h.n_ms > 65535u || (size_t)h.off_mudesc + sizeof(sdx_mu_desc) * h.n_mu > nbytes ||
+      (size_t)h.off_mmtab + h.mmtab_bytes > nbytes || h.mmtab_bytes > SDX_MMTAB_LDS || (h.mmtab_bytes & 15u) ||
+      (h.off_mudesc & 15u) || (h.off_mmtab & 15u) || 17u * h.mm_states > h.mmtab_bytes)
     return fail(SDX_EBANK, "bank blob: processing-order section out of range");
   HIPCHK(hipSetDevice(device));
   void* d = nullptr;

@@ -141,8 +141,11 @@ SDX_DEV M<NW> m_occ(const uint64_t* bm, uint64_t tgt, int tlen) {
 // ---------------------------------------------------------------------------------------------
 template <int NW>
 SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
-                            int minpos) {
+                            int minpos, const uint16_t* ranks) {
   PexRes res{false, -1, 0};
+#ifdef SDX_X_NOCAND
+  return PexRes{true, minpos, 0};
+#endif
   const int nu = cld(&sp->nuniq), slen = cld(&sp->len);
   uint64_t cand[SDX_MAXUNIQ];
   int cnt[SDX_MAXUNIQ];
@@ -162,26 +165,20 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, 
       if (c == 0) return res;  // pattern_utils.py:78-80
       if (c == 1) {
         cand[u] = (uint64_t)(__ffs(okm) - 1);
-      } else {  // stable sort by the fp64 gap of k/10, ties in dict order (list.sort is stable)
-        const double v = cld(&sp->uval[u]);
-        uint64_t packed = 0;
-        for (uint32_t mj = okm; mj; mj &= mj - 1) {
-          const int j = __ffs(mj) - 1;
-          int kj = 0;
+      } else {  // stable sort by the fp64 gap of k/10 (bank gap-rank table), ties in dict order
+        const uint16_t* rt = ranks + cld(&sp->rk_off[u]);
+        uint32_t key[SDX_MAXPAT];
 #pragma unroll
-          for (int k = 0; k < SDX_MAXPAT; ++k) kj = (k == j) ? kq[k] : kj;
-          const double gj = fabs((double)kj / 10.0 - v);
-          int rank = 0;
-          for (uint32_t mk = okm; mk; mk &= mk - 1) {
-            const int k = __ffs(mk) - 1;
-            int kk = 0;
-#pragma unroll
-            for (int t = 0; t < SDX_MAXPAT; ++t) kk = (t == k) ? kq[t] : kk;
-            const double gk = fabs((double)kk / 10.0 - v);
-            rank += (gk < gj || (gk == gj && k < j)) ? 1 : 0;
-          }
-          packed |= (uint64_t)j << (4 * rank);
+        for (int j = 0; j < SDX_MAXPAT; ++j) {
+          const bool okj = (okm >> j) & 1u;
+          const uint32_t r = rt[okj ? kq[j] - klo : 0];  // index always inside [0, khi - klo]
+          key[j] = okj ? (r << 4) | (uint32_t)j : 0xFFFFFFFFu;
         }
+        sort10(key);
+        uint64_t packed = 0;
+#pragma unroll
+        for (int i = 0; i < SDX_MAXPAT; ++i)
+          packed |= (i < c) ? (uint64_t)(key[i] & 15u) << (4 * i) : 0ull;
         cand[u] = packed;
       }
       cnt[u] = c;
@@ -190,6 +187,9 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, 
     }
   }
   if (nu == 0 || total > 10000) return res;
+#ifdef SDX_X_NOCOMBO
+  return PexRes{true, minpos, cand[0]};
+#endif
   int digit[SDX_MAXUNIQ];
 #pragma unroll
   for (int u = 0; u < SDX_MAXUNIQ; ++u) digit[u] = 0;

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import struct
 from ctypes import POINTER, Structure, c_char_p, c_int, c_int32, c_size_t, c_uint32, c_void_p
 from typing import Dict, Optional, Tuple
 
@@ -93,8 +94,8 @@ def load_library(path: Optional[str] = None):
 
 def check_layout(lib) -> None:
     """The numpy mirrors of the C structs must match sizeof() on the C side."""
-    want = {0: 80, 1: bankmod.PATSPEC.itemsize, 2: bankmod.MU_REC.itemsize, 3: bankmod.MS_REC.itemsize,
-            4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize}
+    want = {0: struct.calcsize(bankmod.HDR_FMT), 1: bankmod.PATSPEC.itemsize, 2: bankmod.MU_REC.itemsize, 3: bankmod.MS_REC.itemsize,
+            4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize}
     for k, v in want.items():
         got = lib.sdx_layout_size(k)
         if got != v:

@@ -26,6 +26,39 @@ def test_bank_classes(bk):
     assert set(bk.mc_pids) == {"52", "10", "57", "119", "58", "43", "11", "129", "18", "47", "12", "96"}
 
 
+def _all_patspecs(bk):
+    for r in bk.mu_table:
+        for f in ("start", "one", "zero", "flt"):
+            yield r[f]
+    for r in bk.ms_table:
+        for q in range(4):
+            yield r["key"][q]
+
+
+def test_k_intervals_and_gap_ranks_match_fp64(bk):
+    """The device's integer candidate test (klo <= k <= khi) and candidate order ((rank, dict
+    position) from the bank's gap-rank tables) reproduce pattern_utils.py:53-63's fp64 test and
+    stable gap sort for every k, including both interval borders."""
+    ranks = np.asarray(bk._ranks)
+    rng = random.Random(5)
+    seen = 0
+    for ps in _all_patspecs(bk):
+        for u in range(int(ps["nuniq"])):
+            v, tol = float(ps["uval"][u]), float(ps["utol"][u])
+            klo, khi, off = int(ps["klo"][u]), int(ps["khi"][u]), int(ps["rk_off"][u])
+            for k in range(klo - 30, khi + 31):
+                g = abs(k / 10 - v)
+                assert (g <= 0.001 or g <= tol) == (klo <= k <= khi), (v, k)
+            ks = list(range(klo, khi + 1))
+            for _ in range(20):  # random candidate sets in random dict order
+                cand = rng.sample(ks, min(len(ks), rng.randint(2, 10)))
+                ref = [j for _, j in sorted(((abs(k / 10 - v), j) for j, k in enumerate(cand)), key=lambda t: t[0])]
+                dev = [j for _, j in sorted((int(ranks[off + k - klo]), j) for j, k in enumerate(cand))]
+                assert ref == dev, (v, cand)
+            seen += 1
+    assert seen > 100
+
+
 def test_bank_search_lists_and_tolerances(bk):
     P = bk.protocols
     for r, pid in enumerate(bk.mu_pids):
@@ -75,9 +108,43 @@ def test_preamble_prestate(bk):
                 re.search(p["modulematch"], pre + dm + post))
 
 
+def test_mu_desc_modulematch_tables(bk):
+    """The LDS modulematch tables (hex-digit steps, postamble step, final flags) accept exactly
+    the payloads re.search(modulematch, preamble + digits + postamble) accepts
+    (message_unsynced.py:271-280), for every MU protocol on the table path."""
+    import struct
+    h = struct.unpack(bankmod.HDR_FMT, bk.blob[:struct.calcsize(bankmod.HDR_FMT)])
+    off_tab, nbytes, S = h[21], h[22], h[23]
+    tab = np.frombuffer(bk.blob[off_tab:off_tab + nbytes], dtype=np.uint8)
+    rng = random.Random(11)
+    P = bk.protocols
+    checked = 0
+    for r, pid in enumerate(bk.mu_pids):
+        d = bk.mu_desc[r]
+        if int(d["mm_on"]) != 1:
+            continue
+        p = P[pid]
+        pre, post = f"{p.get('preamble', '')}", f"{p.get('postamble', '')}"
+        for _ in range(60):
+            n = rng.randint(0, 24)
+            digits = "".join(rng.choice("0123456789ABCDEF") for _ in range(n))
+            if rng.random() < 0.3:  # bias towards the pattern's own literal digits
+                lit = "".join(c for c in p["modulematch"] if c in "0123456789ABCDEF")
+                digits = (lit + digits)[:max(n, len(lit))]
+            st = int(d["pre_state"])
+            for c in digits:
+                st = int(tab[16 * (int(d["mm_base"]) + st) + int(c, 16)])
+            st = int(tab[17 * S + int(d["mm_post"]) + st])
+            f = int(tab[16 * S + int(d["mm_base"]) + st])
+            dev = bool(f & 1) or (not (f & 4) and bool(f & 2))
+            assert dev == bool(re.search(p["modulematch"], pre + digits + post)), (pid, digits)
+            checked += 1
+    assert checked > 1000
+
+
 def test_blob_header(bk):
     import struct
-    h = struct.unpack(bankmod.HDR_FMT, bk.blob[:80])
+    h = struct.unpack(bankmod.HDR_FMT, bk.blob[:struct.calcsize(bankmod.HDR_FMT)])
     assert h[0] == bankmod.MAGIC and h[1] == bankmod.VERSION and h[16] == len(bk.blob)
     assert (h[3], h[4], h[5]) == (129, 66, 12)
 

@@ -1,0 +1,40 @@
+"""Kernel time of k_pulses<MU> / <MS> for the library named by SDX_LIB (variant timing).
+usage: SDX_LIB=path/to/libsdx_variant.so python tools/time_mu.py [n] [reps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from pysignalduino_amd import bank as bankmod, runtime, synth
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 333333
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    runtime.load_library()
+    bk = bankmod.Bank()
+    eng = runtime.Engine(bk, 0)
+    res = []
+    for kind, gen in (("MU", synth.mu_corpus), ("MS", synth.ms_corpus)):
+        pb = gen(bk.protocols, n, seed=42)
+        bd = eng.to_device_pulses(pb)
+        out = eng.alloc_out(pb.n, 8 * pb.n + 4096, 200 * pb.n + 65536)
+        k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
+        eng.launch_pulses(k, bd, out)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ts = []
+        for _ in range(reps):
+            out["cursor"].zero_()
+            e0.record()
+            eng.launch_pulses(k, bd, out)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        res.append(f"{kind} {min(ts):.3f} ms")
+    print(os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")), " | ".join(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
