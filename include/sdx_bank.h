@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 6u
+#define SDX_BANK_VERSION 7u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -38,7 +38,8 @@ typedef struct {
   uint8_t nuniq; /* number of distinct values */
   uint8_t pad[6];
   uint8_t uidx[SDX_MAXSEARCH]; /* search position -> unique index */
-} sdx_patspec;                 /* 136 bytes */
+  uint64_t uidx_pk;            /* the same, nibble i = uidx[i] */
+} sdx_patspec;                 /* 144 bytes */
 
 enum sdx_postdemo {
   SDX_PD_NONE = 0, SDX_PD_EM, SDX_PD_REVOLT, SDX_PD_FS20, SDX_PD_FHT80, SDX_PD_FHT80TF,

@@ -28,12 +28,12 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 6
+MAGIC, VERSION = 0x4B4E4253, 7
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("klo", "<i4", (MAXUNIQ,)),
                     ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
-                    ("pad", "u1", (6,)), ("uidx", "u1", (MAXSEARCH,))], align=True)
+                    ("pad", "u1", (6,)), ("uidx", "u1", (MAXSEARCH,)), ("uidx_pk", "<u8")], align=True)
 MU_REC = np.dtype([("clock", "<f8"), ("start", PATSPEC), ("one", PATSPEC), ("zero", PATSPEC), ("flt", PATSPEC),
                    ("proto_index", "<i4"), ("length_min", "<i4"), ("length_max", "<i4"), ("width", "<i4"),
                    ("pad_bits", "<i4"), ("postdemo", "<i4"), ("mm_dfa", "<i4"), ("mm_pre_state", "<i4"), ("pre_off", "<i4"),
@@ -178,8 +178,11 @@ class Bank:
                 self._rank_off[key] = len(self._ranks)
                 self._ranks.extend(_gap_ranks(v, klo, khi))
             rec["rk_off"][i] = self._rank_off[key]
+        pk = 0
         for i, v in enumerate(search):
             rec["uidx"][i] = uniq.index(v)
+            pk |= uniq.index(v) << (4 * i)
+        rec["uidx_pk"] = pk
 
     @staticmethod
     def _float_list(spec):

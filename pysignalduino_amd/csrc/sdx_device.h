@@ -35,7 +35,7 @@ SDX_DEV double py_round1(double q) {
   double k;
   if (r > 0.0) k = f + 1.0;
   else if (r < 0.0) k = f;
-  else k = (fmod(f, 2.0) == 0.0) ? f : f + 1.0;
+  else k = (((long long)f & 1) == 0) ? f : f + 1.0;  // |f| < 2^53: exact parity
   double res = k / 10.0;
   if (res == 0.0) res = copysign(0.0, q);
   return res;
@@ -54,7 +54,7 @@ SDX_DEV int py_round1_k(double q) {
   double k;
   if (r > 0.0) k = f + 1.0;
   else if (r < 0.0) k = f;
-  else k = (fmod(f, 2.0) == 0.0) ? f : f + 1.0;
+  else k = (((long long)f & 1) == 0) ? f : f + 1.0;  // |f| < 2^53: exact parity
   return (int)k;
 }
 // 10-key sorting network (29 comparators, depth 8; Knuth TAOCP 5.3.4), ascending

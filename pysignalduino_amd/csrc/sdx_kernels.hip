@@ -54,6 +54,8 @@ constexpr int REC_CAP = 160;     // MC: staged results per wave
 constexpr int HEAP_CAP = 4096;   // MC: staged payload bytes per wave
 constexpr int POOL_REC = 640;    // MU/MS: staged results per tile (shared by the 4 waves)
 constexpr int POOL_HEAP = 16384; // MU/MS: staged payload bytes per tile
+constexpr int POOL_REC_MS = 256;   // short MS tiles: ~1 result per message; smaller LDS -> more tiles/CU
+constexpr int POOL_HEAP_MS = 8192;
 
 struct StageRec {
   uint32_t off;
@@ -89,6 +91,7 @@ struct TileLds {
     uint8_t bits2[NBITS];
   };
   uint64_t bm[TM * MSTRIDE];
+  uint64_t pairs[TM][2];  // id-pair presence per message: bit 10a+b <=> "ab" occurs
   int32_t nlen[TM];
   uint32_t raise_key[TM];
   uint32_t digit_ok[TM];
@@ -97,8 +100,12 @@ struct TileLds {
   uint32_t wheap_pre[4];
   uint32_t mbase[TM];
   Wave w[LM ? 1 : 4];
-  StageRec rec[POOL_REC];
-  alignas(16) uint8_t heap[POOL_HEAP];
+  // short MS tiles (NW <= 4, not the MU lane variant) stage few results; overflow re-runs on the
+  // long variant
+  static constexpr int PREC = (NW <= 4 && !LM) ? POOL_REC_MS : POOL_REC;
+  static constexpr int PHEAP = (NW <= 4 && !LM) ? POOL_HEAP_MS : POOL_HEAP;
+  StageRec rec[PREC];
+  alignas(16) uint8_t heap[PHEAP];
   int pool_nrec, pool_nheap, ovf, next_p;
   int mm_states;
   alignas(16) sdx_mu_desc desc[LM ? SDX_MUDESC_LDS : 1];
@@ -129,7 +136,7 @@ SDX_DEV int pool_alloc(T& L, int total, int* rec_slot) {
   if (lane_id() == 0) {
     r = atomicAdd(&L.pool_nrec, 1);
     h = atomicAdd(&L.pool_nheap, total);
-    if (r >= POOL_REC || h + total > POOL_HEAP) {
+    if (r >= T::PREC || h + total > T::PHEAP) {
       L.ovf = 1;
       h = -1;
     }
@@ -646,7 +653,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   const int span = (total + 7) & ~7;
   const int slot = atomicAdd(&L.pool_nrec, 1);
   const int off = atomicAdd(&L.pool_nheap, span);
-  if (slot >= POOL_REC || off + span > POOL_HEAP) {
+  if (slot >= T::PREC || off + span > T::PHEAP) {
     L.ovf = 1;
     return;
   }
@@ -918,7 +925,7 @@ template <int NW, int TM, bool LM>
 SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
   const int tid = threadIdx.x;
   // flush scratch aliases the id bitmaps (dead once every wave has left the protocol loop)
-  static_assert(sizeof(L.bm) >= TM * 4 + POOL_REC * 2, "flush scratch does not fit the bitmaps");
+  static_assert(sizeof(L.bm) >= TM * 4 + TileLds<NW, TM, LM>::PREC * 2, "flush scratch does not fit the bitmaps");
   uint32_t* fill = reinterpret_cast<uint32_t*>(L.bm);          // bucket fill per message
   uint16_t* bidx = reinterpret_cast<uint16_t*>(fill + TM);     // pool records bucketed by message
   if (tid < TM) fill[tid] = 0;
@@ -1063,6 +1070,26 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       if (lane < 10) L.bm[mi * T::MSTRIDE + lane * T::WS + w] = mine;
     }
     const uint64_t nd = ballot(nondigit);
+    if constexpr (NW <= 4) {  // pair presence: lane = id pair (a, b), a = q / 10, b = q % 10
+      wave_sync();
+      uint64_t pr[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = lane + 64 * h;
+        uint64_t acc = 0;
+        if (q < 100) {
+          const uint64_t* A = &L.bm[mi * T::MSTRIDE + (q / 10) * T::WS];
+          const uint64_t* B = &L.bm[mi * T::MSTRIDE + (q % 10) * T::WS];
+#pragma unroll
+          for (int w = 0; w < NW; ++w) acc |= A[w] & ((B[w] >> 1) | (w + 1 < NW ? B[w + 1] << 63 : 0ull));
+        }
+        pr[h] = ballot(acc != 0);
+      }
+      if (lane == 0) {
+        L.pairs[mi][0] = pr[0];
+        L.pairs[mi][1] = pr[1];
+      }
+    }
     if (lane == 0) {
       L.nlen[mi] = n;
       L.digit_ok[mi] = (nd == 0 && n > 0) ? 1u : 0u;
@@ -1097,6 +1124,13 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     n = L.nlen[mi];
     lane_ok = n > 0;  // empty D -> [] (message_unsynced.py:22-25 / message_synced.py:23-25)
   }
+  uint64_t P0 = 0, P1 = 0;
+  if constexpr (NW <= 4) {
+    if (mvalid) {
+      P0 = L.pairs[mi][0];
+      P1 = L.pairs[mi][1];
+    }
+  }
   const uint64_t* bmine = &L.bm[(mvalid ? mi : 0) * T::MSTRIDE];
   const int nw = (n + 63) >> 6;
   double clock = 0.0;
@@ -1115,8 +1149,8 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
         if (k < npat) kq[k] = py_round1_k(val[k] / clock);
     }
   }
-  auto PEX = [&](const sdx_patspec* sp, int minpos) -> PexRes {
-    if constexpr (NW <= 4) return pexists_lane<NW>(sp, kq, ids, npat, bmine, minpos, bv.rank);
+  auto PEX = [&](const sdx_patspec* sp, int minpos, bool need_pos) -> PexRes {
+    if constexpr (NW <= 4) return pexists_lane<NW>(sp, kq, ids, npat, bmine, minpos, bv.rank, P0, P1, need_pos);
     else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
   };
   // ---- protocol loop: waves take protocols one at a time, in the bank's processing order
@@ -1178,7 +1212,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       PROF_T(t_st);
       if (alive) {
         if (cld(&rec->has_start)) {
-          const PexRes r = PEX(&rec->start, 0);
+          const PexRes r = PEX(&rec->start, 0, true);
           alive = r.found;
           idx = r.pos;
           st_tgt = r.tgt;
@@ -1187,15 +1221,15 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       PROF_ADD(2, t_st);
       PROF_T(t_ozf);
       if (alive && cld(&rec->one.len)) {
-        const PexRes r = PEX(&rec->one, idx);
+        const PexRes r = PEX(&rec->one, idx, false);
         if (r.found) { ut0 = r.tgt; fmask |= 1; } else alive = false;
       }
       if (alive && cld(&rec->zero.len)) {
-        const PexRes r = PEX(&rec->zero, idx);
+        const PexRes r = PEX(&rec->zero, idx, false);
         if (r.found) { ut1 = r.tgt; fmask |= 2; } else alive = false;
       }
       if (alive && cld(&rec->flt.len)) {
-        const PexRes r = PEX(&rec->flt, idx);
+        const PexRes r = PEX(&rec->flt, idx, false);
         if (r.found) { ut2 = r.tgt; fmask |= 4; }
       }
       alive = alive && fmask != 0;
@@ -1244,7 +1278,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
       uint64_t kt0 = 0, kt1 = 0, kt2 = 0, kt3 = 0;
       int fmask = 0;
       if (alive && cld(&rec->key[0].len)) {  // sync (:140-158)
-        const PexRes r = PEX(&rec->key[0], 0);
+        const PexRes r = PEX(&rec->key[0], 0, true);
         if (r.found) {
           kt0 = r.tgt;
           fmask |= 1;
@@ -1254,15 +1288,15 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
         } else alive = false;
       }
       if (alive && cld(&rec->key[1].len)) {
-        const PexRes r = PEX(&rec->key[1], 0);
+        const PexRes r = PEX(&rec->key[1], 0, false);
         if (r.found) { kt1 = r.tgt; fmask |= 2; } else alive = false;
       }
       if (alive && cld(&rec->key[2].len)) {
-        const PexRes r = PEX(&rec->key[2], 0);
+        const PexRes r = PEX(&rec->key[2], 0, false);
         if (r.found) { kt2 = r.tgt; fmask |= 4; } else alive = false;
       }
       if (alive && cld(&rec->key[3].len)) {
-        const PexRes r = PEX(&rec->key[3], 0);
+        const PexRes r = PEX(&rec->key[3], 0, false);
         if (r.found) { kt3 = r.tgt; fmask |= 8; }
       }
       alive = alive && fmask != 0;

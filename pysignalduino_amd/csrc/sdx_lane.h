@@ -139,9 +139,15 @@ SDX_DEV M<NW> m_occ(const uint64_t* bm, uint64_t tgt, int tlen) {
 // ---------------------------------------------------------------------------------------------
 // pattern_exists (pattern_utils.py:34-136) for one lane; fast path = one candidate per value
 // ---------------------------------------------------------------------------------------------
+// pair-presence bit of ids (a, b): set iff "ab" occurs in the message (TileLds::pairs)
+SDX_DEV bool pair_bit(uint64_t P0, uint64_t P1, int a, int b) {
+  const int q = 10 * a + b;
+  return ((q < 64 ? P0 >> q : P1 >> (q - 64)) & 1ull) != 0;
+}
+
 template <int NW>
 SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
-                            int minpos, const uint16_t* ranks) {
+                            int minpos, const uint16_t* ranks, uint64_t P0, uint64_t P1, bool need_pos) {
   PexRes res{false, -1, 0};
 #ifdef SDX_X_NOCAND
   return PexRes{true, minpos, 0};
@@ -163,7 +169,11 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, 
       for (int j = 0; j < SDX_MAXPAT; ++j) okm |= (k_in(kq[j], klo, khi) ? 1u : 0u) << j;
       const int c = __popc(okm);
       if (c == 0) return res;  // pattern_utils.py:78-80
+#ifdef SDX_X_NOSORT
+      if (true) {
+#else
       if (c == 1) {
+#endif
         cand[u] = (uint64_t)(__ffs(okm) - 1);
       } else {  // stable sort by the fp64 gap of k/10 (bank gap-rank table), ties in dict order
         const uint16_t* rt = ranks + cld(&sp->rk_off[u]);
@@ -171,7 +181,11 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, 
 #pragma unroll
         for (int j = 0; j < SDX_MAXPAT; ++j) {
           const bool okj = (okm >> j) & 1u;
+#ifdef SDX_X_NORANKLOAD
+          const uint32_t r = (uint32_t)(kq[j] - klo) & 0xFFFu;
+#else
           const uint32_t r = rt[okj ? kq[j] - klo : 0];  // index always inside [0, khi - klo]
+#endif
           key[j] = okj ? (r << 4) | (uint32_t)j : 0xFFFFFFFFu;
         }
         sort10(key);
@@ -206,9 +220,16 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, 
       }
     }
     if (!dup) {
+      const uint64_t upk = cld(&sp->uidx_pk);
       uint64_t tgt = 0;
-      for (int i = 0; i < slen; ++i) tgt |= (uint64_t)((uid >> (4 * cld(&sp->uidx[i]))) & 15) << (4 * i);
-      const int p = m_first(m_occ<NW>(bm, tgt, slen), minpos);
+      for (int i = 0; i < slen; ++i) tgt |= (uint64_t)((uid >> (4 * (int)((upk >> (4 * i)) & 15))) & 15) << (4 * i);
+      // every adjacent id pair of the target must occur in the message: exact for a 2-id target
+      // searched from position 0, a necessary condition otherwise
+      bool ok = true;
+      for (int i = 0; i + 1 < slen; ++i)
+        ok = ok && pair_bit(P0, P1, (int)((tgt >> (4 * i)) & 15), (int)((tgt >> (4 * i + 4)) & 15));
+      int p = -1;
+      if (ok) p = (slen == 2 && minpos == 0 && !need_pos) ? 0 : m_first(m_occ<NW>(bm, tgt, slen), minpos);
       if (p >= 0) {
         res.found = true;
         res.pos = p;
