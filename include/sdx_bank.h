@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 7u
+#define SDX_BANK_VERSION 8u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -121,12 +121,15 @@ typedef struct {
   uint32_t n_proto, n_mu, n_ms, n_mc, n_dfa, n_class;
   uint32_t off_mu, off_ms, off_mc, off_dfa, off_cls, off_trans, off_flags, off_str;
   uint32_t total_bytes, off_t256;
-  uint32_t off_order; /* u16 processing order: n_mu MU record indices, then n_ms MS indices */
+  uint32_t off_order; /* u16 processing order: n_mu MU record indices (grouped by clock), then n_ms MS
+                       * indices, then n_mu_groups + 1 MU group starts */
   uint32_t off_rank;  /* u16 candidate gap-rank tables (sdx_patspec.rk_off) */
   uint32_t off_mudesc;  /* sdx_mu_desc[n_mu] */
   uint32_t off_mmtab;   /* u8 modulematch tables for the MU decode (see sdx_mu_desc) */
   uint32_t mmtab_bytes; /* <= SDX_MMTAB_LDS, multiple of 16 */
   uint32_t mm_states;   /* S: hex[S][16] at 0, flags[S] at 16*S, post tables at 17*S */
+  uint32_t n_mu_groups; /* MU clock groups: order[n_mu + n_ms + g] .. [+ g + 1] bound group g */
+  uint32_t res;
 } sdx_bank_hdr;
 
 #endif

@@ -28,7 +28,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 7
+MAGIC, VERSION = 0x4B4E4253, 8
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("klo", "<i4", (MAXUNIQ,)),
@@ -50,7 +50,7 @@ MC_REC = np.dtype([("cr_lo", "<f8"), ("cr_hi", "<f8"), ("proto_index", "<i4"), (
                    ("has_cr", "u1"), ("res", "u1", (3,))], align=True)
 DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4"),
                     ("t256_off", "<i4"), ("res", "<i4", (3,))])
-HDR_FMT = "<" + "I" * 24  # sdx_bank_hdr: 24 uint32
+HDR_FMT = "<" + "I" * 26  # sdx_bank_hdr: 26 uint32
 # MU decode descriptor (sdx_mu_desc): what the compacted decode reads per (message, protocol) pair,
 # staged in LDS once per tile
 MU_DESC = np.dtype([("pre", "u1", (16,)), ("post", "u1", (2,)), ("pre_len", "u1"), ("post_len", "u1"),
@@ -395,9 +395,16 @@ class Bank:
         hdr_size = struct.calcsize(HDR_FMT)
         # processing orders (results are placed by protocol index, so any order is exact):
         # MU sorted by clock so consecutive protocols reuse the normalised patterns
-        self.mu_order = sorted(range(len(self.mu_pids)), key=lambda r: float(mu[r]["clock"]))
+        # MU: clock groups (one normalisation per group and tile), largest group first so that the
+        # waves' dynamic grabbing ends on small groups; group g = mu_order[gstart[g]:gstart[g+1]]
+        groups: Dict[float, List[int]] = {}
+        for r in range(len(self.mu_pids)):
+            groups.setdefault(float(mu[r]["clock"]), []).append(r)
+        glist = sorted(groups.values(), key=lambda g: -len(g))
+        self.mu_order = [r for g in glist for r in g]
+        self.mu_gstart = list(np.cumsum([0] + [len(g) for g in glist]))
         self.ms_order = list(range(len(self.ms_pids)))
-        order = np.asarray(self.mu_order + self.ms_order, dtype=np.uint16)
+        order = np.asarray(self.mu_order + self.ms_order + self.mu_gstart, dtype=np.uint16)
         ranks = np.asarray(self._ranks, dtype=np.uint16)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
                     trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
@@ -411,7 +418,7 @@ class Bank:
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
                           len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], offs[10], offs[11], offs[12],
-                          len(mmtab), mm_states)
+                          len(mmtab), mm_states, len(glist), 0)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s

@@ -1187,12 +1187,26 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     }
     wave_sync();
   };
+  // MU: a wave takes a whole clock group (one normalisation per group); MS: one protocol
+  const int ngrab = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu_groups : nproto;
+  const uint16_t* gstart = bv.order + bv.hdr->n_mu + bv.hdr->n_ms;
+  int cur = 0, cend = 0;
   while (true) {
-    int g = 0;
-    if (lane == 0) g = atomicAdd(&L.next_p, 1);
-    g = __builtin_amdgcn_readfirstlane(g);
-    if (g >= nproto) break;
-    const int p = cld(&order[g]);
+    if (cur == cend) {
+      int g = 0;
+      if (lane == 0) g = atomicAdd(&L.next_p, 1);
+      g = __builtin_amdgcn_readfirstlane(g);
+      if (g >= ngrab) break;
+      if (KIND == SDX_KIND_MU) {
+        cur = cld(&gstart[g]);
+        cend = cld(&gstart[g + 1]);
+      } else {
+        cur = g;
+        cend = g + 1;
+      }
+    }
+    const int p = cld(&order[cur]);
+    ++cur;
     if (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
       if (cld(&rec->never) || !cld(&rec->active)) continue;
@@ -1828,7 +1842,7 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
   std::memcpy(&h, blob, sizeof h);
   if (h.magic != SDX_BANK_MAGIC || h.version != SDX_BANK_VERSION || h.total_bytes != nbytes)
     return fail(SDX_EBANK, "bank blob magic/version/size mismatch (rebuild the bank and the library)");
-  if ((size_t)h.off_order + 2u * ((size_t)h.n_mu + h.n_ms) > nbytes || h.off_rank > nbytes || h.n_mu > 65535u ||
+  if ((size_t)h.off_order + 2u * ((size_t)h.n_mu + h.n_ms + h.n_mu_groups + 1) > nbytes || h.off_rank > nbytes || h.n_mu > 65535u ||
       h.n_ms > 65535u || (size_t)h.off_mudesc + sizeof(sdx_mu_desc) * h.n_mu > nbytes ||
       (size_t)h.off_mmtab + h.mmtab_bytes > nbytes || h.mmtab_bytes > SDX_MMTAB_LDS || (h.mmtab_bytes & 15u) ||
       (h.off_mudesc & 15u) || (h.off_mmtab & 15u) || 17u * h.mm_states > h.mmtab_bytes)
