@@ -106,7 +106,8 @@ struct TileLds {
   static constexpr int PHEAP = (NW <= 4 && !LM) ? POOL_HEAP_MS : POOL_HEAP;
   StageRec rec[PREC];
   alignas(16) uint8_t heap[PHEAP];
-  int pool_nrec, pool_nheap, ovf, next_p;
+  unsigned long long pool_ctr;  // low 32: staged records, high 32: staged heap bytes (one LDS atomic)
+  int ovf, next_p;
   int mm_states;
   alignas(16) sdx_mu_desc desc[LM ? SDX_MUDESC_LDS : 1];
   alignas(16) uint8_t mmtab[LM ? SDX_MMTAB_LDS : 16];
@@ -134,8 +135,9 @@ template <class T>
 SDX_DEV int pool_alloc(T& L, int total, int* rec_slot) {
   int h = -1, r = -1;
   if (lane_id() == 0) {
-    r = atomicAdd(&L.pool_nrec, 1);
-    h = atomicAdd(&L.pool_nheap, total);
+    const unsigned long long o = atomicAdd(&L.pool_ctr, ((unsigned long long)total << 32) | 1ull);
+    r = (int)(uint32_t)o;
+    h = (int)(o >> 32);
     if (r >= T::PREC || h + total > T::PHEAP) {
       L.ovf = 1;
       h = -1;
@@ -525,7 +527,7 @@ SDX_DEV uint64_t hex8(uint64_t x, int cnt) {
 
 template <int NW, class T>
 SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
-                            int mi,
+                            int mi, int j,
                             int q, int k, int Lw, bool emf, uint8_t esym, const M<NW>& V1, const M<NW>& VF) {
   constexpr int NB = 64 * NW + 64;
   PROF_T(t_x);
@@ -651,8 +653,8 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   // payload (:271-274): preamble + digits + postamble into an 8-byte aligned pool slot
   const int total = pre_len + dlen + post_len;
   const int span = (total + 7) & ~7;
-  const int slot = atomicAdd(&L.pool_nrec, 1);
-  const int off = atomicAdd(&L.pool_nheap, span);
+  const unsigned long long o = atomicAdd(&L.pool_ctr, ((unsigned long long)span << 32) | 1ull);
+  const int slot = (int)(uint32_t)o, off = (int)(o >> 32);
   if (slot >= T::PREC || off + span > T::PHEAP) {
     L.ovf = 1;
     return;
@@ -689,7 +691,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   r.bitlen = (uint32_t)nbp;
   r.msg = (uint8_t)mi;
   r.wave = (uint8_t)wave;
-  r.rank = (uint16_t)atomicAdd(&L.cnt[mi], 1u);
+  r.rank = (uint16_t)j;  // match index within this (message, protocol) pair: monotone
   L.rec[slot] = r;
   PROF_ADDD(8, t_wr);
 }
@@ -739,7 +741,7 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   // including one that ends exactly at the end of the data: empty group -> IndexError)
   const M<NW> V = lmin > 0 ? m_and(S, m_shr(m_runs(U, lmin, Lw), lenS)) : S;
   const M<NW> NU = m_not(U);
-  int pos = idx;
+  int pos = idx, nfin = 0;
   PROF_ADDD(4, t_setup);
   while (true) {
     PROF_T(t_scan);
@@ -773,7 +775,7 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
     const int nch = k + (emf ? 1 : 0);
     PROF_ADDD(5, t_scan);
     if (nch > (int)d.lmax) continue;  // (:217-218); 65535 = none
-    finish_mu_lane<NW>(L, wave, bv, rec, d, p, mi, q, k, Lw, emf, esym, V1, VF);
+    finish_mu_lane<NW>(L, wave, bv, rec, d, p, mi, nfin++, q, k, Lw, emf, esym, V1, VF);
     if ((L.raise_key[mi] >> 8) <= (uint32_t)p) return;
   }
 }
@@ -925,18 +927,29 @@ template <int NW, int TM, bool LM>
 SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
   const int tid = threadIdx.x;
   // flush scratch aliases the id bitmaps (dead once every wave has left the protocol loop)
-  static_assert(sizeof(L.bm) >= TM * 4 + TileLds<NW, TM, LM>::PREC * 2, "flush scratch does not fit the bitmaps");
-  uint32_t* fill = reinterpret_cast<uint32_t*>(L.bm);          // bucket fill per message
-  uint16_t* bidx = reinterpret_cast<uint16_t*>(fill + TM);     // pool records bucketed by message
-  if (tid < TM) fill[tid] = 0;
+  static_assert(sizeof(L.bm) >= TM * 8 + TileLds<NW, TM, LM>::PREC * 2, "flush scratch does not fit the bitmaps");
+  uint32_t* fill = reinterpret_cast<uint32_t*>(L.bm);       // bucket fill per message
+  uint32_t* cntm = fill + TM;                               // staged records per message
+  uint16_t* bidx = reinterpret_cast<uint16_t*>(cntm + TM);  // pool records bucketed by message
+  if (tid < TM) {
+    fill[tid] = 0;
+    cntm[tid] = 0;
+  }
+  __syncthreads();
+  const int nr = (int)(uint32_t)L.pool_ctr;
+  const int nh = (int)(L.pool_ctr >> 32);
+  const bool ovf = L.ovf != 0;
+  if (!ovf)
+    for (int r = tid; r < nr; r += blockDim.x) atomicAdd(&cntm[L.rec[r].msg], 1u);
+  __syncthreads();
   if (tid == 0) {
-    int bad = L.ovf ? 1 : 0;
+    int bad = ovf ? 1 : 0;
     uint32_t nrec = 0;
     for (int m = 0; m < nvalid; ++m) {
       L.mbase[m] = nrec;
-      if (L.raise_key[m] == 0xFFFFFFFFu && !bad) nrec += L.cnt[m];
+      if (L.raise_key[m] == 0xFFFFFFFFu && !bad) nrec += cntm[m];
     }
-    const uint32_t nheap = bad ? 0u : (uint32_t)L.pool_nheap;
+    const uint32_t nheap = bad ? 0u : (uint32_t)nh;
     uint32_t rb = 0, hb = 0;
     if (!bad) {
       rb = atomicAdd(&out.cursor_dev[0], nrec);
@@ -956,7 +969,6 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
   __syncthreads();
   const int bad = L.tile_bad;  // block-uniform
   if (!bad) {
-    const int nr = L.pool_nrec;
     for (int r = tid; r < nr; r += blockDim.x) {
       const int m = L.rec[r].msg;
       if (L.raise_key[m] != 0xFFFFFFFFu) continue;
@@ -968,7 +980,7 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
     for (int j = tid; j < nt; j += blockDim.x) {
       const StageRec sr = L.rec[bidx[j]];
       const uint32_t key = ((uint32_t)sr.proto << 16) | sr.rank;
-      const uint32_t b0 = L.mbase[sr.msg], b1 = b0 + L.cnt[sr.msg];
+      const uint32_t b0 = L.mbase[sr.msg], b1 = b0 + cntm[sr.msg];
       uint32_t rk = 0;
       for (uint32_t i = b0; i < b1; ++i) {
         const StageRec& o = L.rec[bidx[i]];
@@ -983,7 +995,6 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       out.rec_dev[L.rec_base + b0 + rk] = o;
     }
     uint8_t* hd = out.heap_dev + L.heap_base;
-    const int nh = L.pool_nheap;
     for (int i = tid; i < nh; i += blockDim.x) hd[i] = L.heap[i];
   }
   for (int m = tid; m < nvalid; m += blockDim.x) {
@@ -1001,7 +1012,7 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
     } else {
       d.status = SDX_ST_OK;
       d.raise_kind = 0;
-      d.n_rec = (uint16_t)L.cnt[m];
+      d.n_rec = (uint16_t)cntm[m];
     }
     out.desc_dev[msg_of[m]] = d;
   }
@@ -1028,8 +1039,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   }
   if (tid == 0) {
     L.next_p = 0;
-    L.pool_nrec = 0;
-    L.pool_nheap = 0;
+    L.pool_ctr = 0;
     L.ovf = 0;
   }
   if constexpr (LANE_MU) {  // MU decode descriptors + modulematch tables -> LDS (16-B pieces)
@@ -1210,6 +1220,9 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     if (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
       if (cld(&rec->never) || !cld(&rec->active)) continue;
+#ifdef SDX_X_NOSTARTPROTO
+      if (cld(&rec->has_start)) continue;
+#endif
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
       int idx = 0;
       uint64_t st_tgt = 0, ut0 = 0, ut1 = 0, ut2 = 0;
@@ -1230,6 +1243,9 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
           alive = r.found;
           idx = r.pos;
           st_tgt = r.tgt;
+#ifdef SDX_X_STARTONLY
+          alive = false;
+#endif
         }
       }
       PROF_ADD(2, t_st);
