@@ -43,7 +43,7 @@ def cpu_baseline(P, budget_s: float):
     from oracle import sd_oracle as O
     from pysignalduino_amd import synth
     ob = O.OracleBank()
-    NS = 6000
+    NS = 12000
     mu = synth.mu_corpus(P, NS, seed=9001)
     ms = synth.ms_corpus(P, NS, seed=9002)
     mc = synth.mc_corpus(P, NS, seed=9003)
@@ -148,6 +148,13 @@ def main():
 
     # roofline of the dominant kernel (MU): algorithmic bytes / measured kernel time
     kt = {k: float(np.mean(v)) for k, v in ktimes.items()}
+    # HBM traffic of the same kernel/launch from the committed PMC passes (tools/pmc.sh ->
+    # tools/pmc_traffic.py); null when absent or recorded for another launch size
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
+            tj = json.load(fh)
     dom = max(kt, key=kt.get)
     bd = {"MU": bmu, "MS": bms, "MC": bmc}[dom]
     o = outs[dom]
@@ -160,6 +167,10 @@ def main():
     out_bytes = n * runtime.DESC_DT.itemsize + int(cur[0]) * runtime.RES_DT.itemsize + int(cur[1])
     alg = in_bytes + out_bytes + len(bk.blob)
     achieved = alg / kt[dom]
+    if os.path.exists(tpath):
+        tag = f"k_pulses<{dom}>" if dom != "MC" else "k_mc"
+        if tj.get("_config", {}).get("msgs_per_gpu") == args.msgs and tj.get(tag, {}).get("traffic_bytes"):
+            traffic = float(tj[tag]["traffic_bytes"])
     res = {
         "metric": "RF messages/sec demodulated (MU+MS+MC, full protocol bank)",
         "value": value, "unit": "msgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -172,7 +183,7 @@ def main():
         "per_kernel_ms": {k: 1e3 * v for k, v in kt.items()},
         "per_type_msgs_per_s": {"MU": mu.n / kt["MU"], "MS": ms.n / kt["MS"], "MC": mc.n / kt["MC"]},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": None, "kernel": f"k_pulses<{dom}>" if dom != "MC" else "k_mc",
+                     "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": f"k_pulses<{dom}>" if dom != "MC" else "k_mc",
                      "alg_bytes_per_launch": alg},
     }
     if rank == 0 and not args.no_cpu:

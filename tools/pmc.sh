@@ -22,3 +22,4 @@ for p in "${passes[@]}"; do
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$p.log"; exit $rc; fi
 done
 python3 tools/pmc_summary.py "$OUT"
+python3 tools/pmc_traffic.py "$OUT" gpurun_out/pmc_traffic.json > /dev/null
