@@ -32,41 +32,43 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--msgs", type=int, default=1_000_000, help="messages per rank (1/3 MU, 1/3 MS, 1/3 MC)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(P, budget_s: float):
-    """The CPU oracle (pure-Python restatement of the reference path, kind 'port') on a bounded
-    sample of the same workload, 1 core; MU:MS:MC in the same 1:1:1 mix."""
-    from oracle import sd_oracle as O
-    from pysignalduino_amd import synth
-    ob = O.OracleBank()
-    NS = 12000
-    mu = synth.mu_corpus(P, NS, seed=9001)
-    ms = synth.ms_corpus(P, NS, seed=9002)
-    mc = synth.mc_corpus(P, NS, seed=9003)
-    t0 = time.perf_counter()
-    done = 0
-    i = 0
-    while time.perf_counter() - t0 < budget_s and i < NS:
-        for kind, b in (("MU", mu), ("MS", ms)):
-            try:
-                O.demod(ob, b.to_msg_dict(i), kind)
-            except Exception:
-                pass
-        try:
-            O.demod_mc_fixed(ob, mc.hex(i), int(mc.clock[i]), int(mc.mcbitnum[i]),
-                             "Mc" if mc.mtype[i] else "MC", "V 3.2.0" if mc.v32[i] else None)
-        except Exception:
-            pass
-        done += 3
-        i += 1
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "msgs/s", "cores": 1, "kind": "port",
-            "sample": f"{done} messages (1:1:1 MU/MS/MC, seeds 9001-9003) through oracle/sd_oracle.py, "
-                      f"{dt:.1f} s, 1 thread, {platform.processor() or platform.machine()}"}
+def cpu_baseline(mu, ms, mc, budget_s: float):
+    """The plain-C oracle (oracle/sd_oracle_c.c, a restatement of the reference path: kind 'port')
+    timed on this host over a bounded 1:1:1 MU/MS/MC sample of the SAME corpora the GPU
+    demodulates: once on one core, once on all cores this process may use.  Each message is
+    fully demodulated against the whole bank, with results written, as on the GPU."""
+    from oracle import c_oracle as CO
+    CO.build()
+    bank = CO.CBank()
+    cores = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():  # the box's CPU share (16 per GPU)
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
+    cores = max(1, min(cores, 64))
+
+    def timed(k, threads):
+        idx = np.arange(k)
+        packs = [("MU", CO.pack_batch(mu.subset(idx))), ("MS", CO.pack_batch(ms.subset(idx))),
+                 ("MC", CO.mc_batch(mc.subset(idx)))]
+        t0 = time.perf_counter()
+        for kind, pk in packs:
+            CO.run(kind, pk, threads)
+        return 3 * k / (time.perf_counter() - t0)
+
+    # size the samples from a short probe so the whole leg stays within ~budget_s seconds
+    probe = timed(min(300, mu.n, ms.n, mc.n), 1)
+    k1 = int(max(300, min(mu.n, ms.n, mc.n, probe * budget_s * 0.35 / 3)))
+    v1 = timed(k1, 1)
+    kn = int(max(300, min(mu.n, ms.n, mc.n, v1 * cores * budget_s * 0.5 / 3)))
+    vn = timed(kn, cores)
+    return {"value": vn, "unit": "msgs/s", "cores": cores, "kind": "port", "value_1core": v1,
+            "sample": f"oracle/sd_oracle_c.c (plain C, gcc -O2): {3 * kn} messages (1:1:1 MU/MS/MC, the "
+                      f"first {kn} of each bench corpus) on {cores} threads; 1-core rate on {3 * k1} messages; "
+                      f"{platform.processor() or platform.machine()}"}
 
 
 def main():
@@ -187,7 +189,7 @@ def main():
                      "alg_bytes_per_launch": alg},
     }
     if rank == 0 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(P, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(mu, ms, mc, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

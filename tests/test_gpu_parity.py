@@ -140,3 +140,46 @@ def test_size_independent_properties(proto):
     half = pb.subset(np.arange(10000, 20000))
     d3, r3, h3 = eng.run(runtime.KIND_MU, eng.to_device_pulses(half))
     assert per_msg(d3, r3, h3) == a[10000:]
+
+
+@pytest.mark.parametrize("kind,n,seed", [("MU", 50000, 9101), ("MS", 100000, 9102), ("MC", 100000, 9103)])
+def test_large_corpus_vs_c_oracle(kind, n, seed):
+    """Record-level, bit-exact: the device path (runtime.Engine through the C-ABI) against the
+    plain-C oracle on large seeded corpora -- statuses/raise kinds, protocol ids, payload bytes
+    and bit lengths of every result, in order."""
+    import os
+    from oracle import c_oracle as CO
+    from pysignalduino_amd import bank as B, runtime, synth
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    cb = CO.CBank()
+    gen = {"MU": synth.mu_corpus, "MS": synth.ms_corpus, "MC": synth.mc_corpus}[kind]
+    batch = gen(bk.protocols, n, seed=seed)
+    if kind == "MC":
+        d_desc, d_rec, d_heap = eng.run(runtime.KIND_MC, eng.to_device_mc(batch))
+        packed = CO.mc_batch(batch)
+        cls_pids = bk.mc_pids
+    else:
+        d_desc, d_rec, d_heap = eng.run(runtime.KIND_MU if kind == "MU" else runtime.KIND_MS,
+                                        eng.to_device_pulses(batch))
+        packed = CO.pack_batch(batch)
+        cls_pids = bk.mu_pids if kind == "MU" else bk.ms_pids
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    st, rk, rb, nr, rec, heap = CO.run(kind, packed, threads)
+    dh, ch = d_heap.tobytes(), heap.tobytes()
+    assert np.array_equal(d_desc["status"] == runtime.ST_RAISED, st == 1)
+    assert np.array_equal(np.where(st == 1, d_desc["raise_kind"], 0), np.where(st == 1, rk, 0))
+    ok = st == 0
+    assert np.array_equal(d_desc["n_rec"][ok], nr[ok])
+    bad = []
+    for i in np.nonzero(ok & (nr > 0))[0]:
+        a = d_rec[int(d_desc["rec_begin"][i]):int(d_desc["rec_begin"][i]) + int(nr[i])]
+        b = rec[int(rb[i]):int(rb[i]) + int(nr[i])]
+        for x, y in zip(a, b):
+            same = (cls_pids[int(x["proto"])] == cb.pids[int(y["proto"])] and
+                    dh[int(x["payload_off"]):int(x["payload_off"]) + int(x["payload_len"])] ==
+                    ch[int(y["off"]):int(y["off"]) + int(y["len"])] and
+                    (kind == "MC" or int(x["bit_length"]) == int(y["bitlen"])))
+            if not same:
+                bad.append((int(i), x, y))
+    assert not bad, f"{len(bad)} record mismatches; first: {bad[:2]}"
