@@ -41,11 +41,14 @@ __device__ unsigned long long g_prof[32];
     if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_read_exec()) - 1)       \
       L.prof[wave][slot] += __builtin_amdgcn_s_memtime() - (v);                             \
   } while (0)
+// per-lane event count (divergent code)
+#define PROF_CNTL(slot) atomicAdd(&L.prof[wave][slot], 1ull)
 #else
 #define PROF_T(v)
 #define PROF_ADD(slot, v)
 #define PROF_ADDD(slot, v)
 #define PROF_CNT(slot, x)
+#define PROF_CNTL(slot)
 #endif
 
 namespace sdx {
@@ -75,6 +78,17 @@ struct MuItem {
 };
 constexpr int QCAP = 128;  // per-wave ring: < 64 pending before a push of <= 64
 
+// MU (NW <= 4): one finditer match, finished after the protocol loop with lane = match
+struct MuMatch {
+  uint16_t q, k;         // first unit position, number of full units
+  uint16_t u0, u1, u2;   // one / zero / float target strings
+  uint16_t p;            // protocol index
+  uint8_t mi;            // tile message
+  uint8_t flags;         // bit0 tail matched, bits1-2 tail symbol, bits3-5 found-key mask
+  uint8_t j;             // match index within the (message, protocol) pair
+};
+constexpr int MATCH_CAP = 512;  // per tile; more -> tile overflow -> exact re-run (long variant)
+
 // LM: the lane-decode MU variant (NW <= 4) -- no per-wave byte scratch, but the MU decode
 // descriptors and modulematch tables staged in LDS
 template <int NW, int TM, bool LM>
@@ -102,15 +116,21 @@ struct TileLds {
   Wave w[LM ? 1 : 4];
   // short MS tiles (NW <= 4, not the MU lane variant) stage few results; overflow re-runs on the
   // long variant
-  static constexpr int PREC = (NW <= 4 && !LM) ? POOL_REC_MS : POOL_REC;
-  static constexpr int PHEAP = (NW <= 4 && !LM) ? POOL_HEAP_MS : POOL_HEAP;
+  static constexpr int PREC = LM ? 512 : (NW <= 4 ? POOL_REC_MS : POOL_REC);
+  static constexpr int PHEAP = LM ? 14336 : (NW <= 4 ? POOL_HEAP_MS : POOL_HEAP);
   StageRec rec[PREC];
   alignas(16) uint8_t heap[PHEAP];
   unsigned long long pool_ctr;  // low 32: staged records, high 32: staged heap bytes (one LDS atomic)
   int ovf, next_p;
-  int mm_states;
+  int mm_states, nmatch;
+  MuMatch mlist[LM ? MATCH_CAP : 1];
   alignas(16) sdx_mu_desc desc[LM ? SDX_MUDESC_LDS : 1];
-  alignas(16) uint8_t mmtab[LM ? SDX_MMTAB_LDS : 16];
+  // the decode queues live only during the protocol loop, the modulematch tables only in the
+  // finish phase after it: one region
+  union alignas(16) {
+    MuItem q[4][LM ? QCAP : 1];
+    uint8_t mmtab[LM ? SDX_MMTAB_LDS : 16];
+  } u;
 #ifdef SDX_PROF
   unsigned long long prof[4][32];
 #endif
@@ -525,6 +545,30 @@ SDX_DEV uint64_t hex8(uint64_t x, int cnt) {
   return cnt >= 8 ? x : x & ((1ull << (8 * cnt)) - 1);
 }
 
+// pattern_lookup (message_unsynced.py:113-123): U = every unit occurrence; V1 / VF = occurrences
+// whose symbol is '1' / 'F' (the LAST writer of an identical unit string decides its symbol)
+template <int NW>
+SDX_DEV void sym_masks(const uint64_t* bm, uint64_t ut0, uint64_t ut1, uint64_t ut2, int fmask, int Lw, M<NW>* U,
+                       M<NW>* V1, M<NW>* VF) {
+  const uint64_t ut[3] = {ut0, ut1, ut2};
+  const uint8_t SYM[3] = {1, 0, 2};
+  *U = m_zero<NW>();
+  if (V1) *V1 = m_zero<NW>();
+  if (VF) *VF = m_zero<NW>();
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    if (!((fmask >> kk) & 1)) continue;
+    uint8_t fs = SYM[kk];
+#pragma unroll
+    for (int j = kk + 1; j < 3; ++j)
+      if (((fmask >> j) & 1) && ut[j] == ut[kk]) fs = SYM[j];
+    const M<NW> occ = m_occ<NW>(bm, ut[kk], Lw);
+    *U = m_or(*U, occ);
+    if (V1 && fs == 1) *V1 = m_or(*V1, occ);
+    if (VF && fs == 2) *VF = m_or(*VF, occ);
+  }
+}
+
 template <int NW, class T>
 SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
                             int mi, int j,
@@ -621,7 +665,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   const uint64_t post16 = (uint64_t)d.post[0] | ((uint64_t)d.post[1] << 8);
   auto post_c = [&](int i) -> uint8_t { return post_g ? post_g[i] : (uint8_t)(post16 >> (8 * i)); };
   if (d.mm_on == 1 && fast) {  // re.search(modulematch, payload) (:277-280) on the LDS hex tables
-    const uint8_t* hx = L.mmtab + 16 * (int)d.mm_base;
+    const uint8_t* hx = L.u.mmtab + 16 * (int)d.mm_base;
     int st = d.pre_state;
     uint64_t cur = 0;
     for (int i = 0; i < dlen; ++i) {
@@ -630,8 +674,8 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
       st = hx[16 * st + (int)(cur & 15ull)];
       cur >>= 4;
     }
-    st = L.mmtab[17 * L.mm_states + d.mm_post + st];
-    const uint8_t f = L.mmtab[16 * L.mm_states + d.mm_base + st];
+    st = L.u.mmtab[17 * L.mm_states + d.mm_post + st];
+    const uint8_t f = L.u.mmtab[16 * L.mm_states + d.mm_base + st];
     if (!((f & 1) || (!(f & 4) && (f & 2)))) return;
   } else if (d.mm_on) {  // byte walk through the blob's t256 table
     const sdx_dfa D = bv.dfa[cld(&rec->mm_dfa)];
@@ -692,6 +736,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   r.msg = (uint8_t)mi;
   r.wave = (uint8_t)wave;
   r.rank = (uint16_t)j;  // match index within this (message, protocol) pair: monotone
+  PROF_CNTL(20);
   L.rec[slot] = r;
   PROF_ADDD(8, t_wr);
 }
@@ -706,19 +751,8 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   const int lenS = d.len_s;
   const uint64_t ut[3] = {ut0, ut1, ut2};
   const uint8_t SYM[3] = {1, 0, 2};
-  M<NW> U = m_zero<NW>(), V1 = m_zero<NW>(), VF = m_zero<NW>();
-#pragma unroll
-  for (int kk = 0; kk < 3; ++kk) {
-    if (!((fmask >> kk) & 1)) continue;
-    uint8_t fs = SYM[kk];  // dict: the LAST writer of an identical string decides the symbol (:122)
-#pragma unroll
-    for (int j = kk + 1; j < 3; ++j)
-      if (((fmask >> j) & 1) && ut[j] == ut[kk]) fs = SYM[j];
-    const M<NW> occ = m_occ<NW>(bm, ut[kk], Lw);
-    U = m_or(U, occ);
-    if (fs == 1) V1 = m_or(V1, occ);
-    if (fs == 2) VF = m_or(VF, occ);
-  }
+  M<NW> U;
+  sym_masks<NW>(bm, ut0, ut1, ut2, fmask, Lw, &U, nullptr, nullptr);
   // end_pattern_lookup: pstr[:-1], first writer wins (:124-127); regex tail only with reconstructBit
   // (kept per source key kk: key kk is live iff found and no earlier found key has the same
   //  prefix -- first writer wins -- which is the insertion-ordered dict without dynamic indexing)
@@ -775,8 +809,24 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
     const int nch = k + (emf ? 1 : 0);
     PROF_ADDD(5, t_scan);
     if (nch > (int)d.lmax) continue;  // (:217-218); 65535 = none
-    finish_mu_lane<NW>(L, wave, bv, rec, d, p, mi, nfin++, q, k, Lw, emf, esym, V1, VF);
-    if ((L.raise_key[mi] >> 8) <= (uint32_t)p) return;
+    PROF_CNTL(22);
+    const int slot = atomicAdd(&L.nmatch, 1);  // finished after the protocol loop, lane = match
+    if (slot >= MATCH_CAP) {
+      L.ovf = 1;
+      return;
+    }
+    MuMatch mm;
+    mm.q = (uint16_t)q;
+    mm.k = (uint16_t)k;
+    mm.u0 = (uint16_t)ut0;
+    mm.u1 = (uint16_t)ut1;
+    mm.u2 = (uint16_t)ut2;
+    mm.mi = (uint8_t)mi;
+    mm.p = (uint16_t)p;
+    mm.flags = (uint8_t)((emf ? 1 : 0) | (esym << 1) | (fmask << 3));
+    mm.j = (uint8_t)(nfin < 255 ? nfin : 255);
+    ++nfin;
+    L.mlist[slot] = mm;
   }
 }
 
@@ -1039,6 +1089,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   }
   if (tid == 0) {
     L.next_p = 0;
+    L.nmatch = 0;
     L.pool_ctr = 0;
     L.ovf = 0;
   }
@@ -1048,10 +1099,6 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     const uint4* src = reinterpret_cast<const uint4*>(bv.mudesc);
     uint4* dst = reinterpret_cast<uint4*>(L.desc);
     for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
-    const int m16 = (int)bv.hdr->mmtab_bytes >> 4;
-    const uint4* msrc = reinterpret_cast<const uint4*>(bv.mmtab);
-    uint4* mdst = reinterpret_cast<uint4*>(L.mmtab);
-    for (int i = tid; i < m16; i += blockDim.x) mdst[i] = msrc[i];
     if (tid == 0) L.mm_states = (int)bv.hdr->mm_states;
   }
 #ifdef SDX_PROF
@@ -1171,10 +1218,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   double last_clock = __builtin_nan("");  // NaN != anything: the first protocol normalises
   MuItem* Q = nullptr;
   int q_head = 0, q_tail = 0;
-  if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
-    __shared__ MuItem Qs[4][QCAP];
-    Q = Qs[wave];
-  }
+  if constexpr (KIND == SDX_KIND_MU && NW <= 4) Q = L.u.q[wave];
   auto drain = [&](int head, int cnt) {
     wave_sync();
     if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
@@ -1190,6 +1234,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
           sdx_mu_desc d;
           if (qp < SDX_MUDESC_LDS) d = L.desc[qp];
           else d = bv.mudesc[qp];
+          PROF_CNTL(21);
           decode_mu_lane<NW>(L, wave, bv, bv.mu + qp, d, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx,
                              ((uint64_t)it.st_hi << 32) | it.st_lo, it.u0, it.u1, it.u2, it.fmask);
         }
@@ -1351,6 +1396,33 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   PROF_T(t_bar);
   __syncthreads();
   PROF_ADD(14, t_bar);
+  if constexpr (LANE_MU) {  // finish every match of the tile: lane = match (message_unsynced.py:197-290)
+    PROF_T(t_fin);
+    {  // modulematch tables -> LDS, over the (now dead) decode queues
+      const int m16 = (int)bv.hdr->mmtab_bytes >> 4;
+      const uint4* msrc = reinterpret_cast<const uint4*>(bv.mmtab);
+      uint4* mdst = reinterpret_cast<uint4*>(L.u.mmtab);
+      for (int i = tid; i < m16; i += blockDim.x) mdst[i] = msrc[i];
+      __syncthreads();
+    }
+    const int nm = L.nmatch < MATCH_CAP ? L.nmatch : MATCH_CAP;
+    for (int m = tid; m < nm; m += blockDim.x) {
+      const MuMatch mm = L.mlist[m];
+      const int qm = mm.mi, qp = mm.p;
+      const uint32_t rk = L.raise_key[qm];
+      if (rk != 0xFFFFFFFFu && (rk >> 8) < (uint32_t)qp) continue;  // an earlier protocol raised
+      sdx_mu_desc d;
+      if (qp < SDX_MUDESC_LDS) d = L.desc[qp];
+      else d = bv.mudesc[qp];
+      const uint64_t* bmm = &L.bm[qm * T::MSTRIDE];
+      M<NW> U, V1, VF;
+      sym_masks<NW>(bmm, mm.u0, mm.u1, mm.u2, (mm.flags >> 3) & 7, d.width, &U, &V1, &VF);
+      finish_mu_lane<NW>(L, wave, bv, bv.mu + qp, d, qp, qm, mm.j, mm.q, mm.k, d.width, (mm.flags & 1) != 0,
+                         (uint8_t)((mm.flags >> 1) & 3), V1, VF);
+    }
+    __syncthreads();
+    PROF_ADD(16, t_fin);
+  }
   PROF_T(t_fl);
   flush_tile(L, msg_of, nvalid, out);
   PROF_ADD(13, t_fl);

@@ -14,7 +14,7 @@ from pysignalduino_amd import bank as bankmod, runtime, synth
 NAMES = {0: "stage bitmaps", 1: "MU normalise", 2: "MU pexists(start)", 3: "MU pexists(one/zero/float)",
          4: "MU decode setup", 5: "MU finditer scan", 6: "MU chunk->bits", 7: "MU postDemod",
          8: "MU payload write", 9: "MU format+DFA", 10: "MS decode", 11: "MS finish", 12: "MU decode total",
-         13: "flush", 14: "end barrier wait", 15: "kernel total", 20: "#results(MU)", 21: "#survivors(MU)",
+         13: "flush", 14: "end barrier wait", 15: "kernel total", 16: "MU finish phase (lane = match)", 20: "#results(MU)", 21: "#survivors(MU)",
          22: "#matches(MU)", 23: "#survivors(MS)"}
 
 
