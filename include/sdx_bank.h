@@ -97,7 +97,7 @@ typedef struct {
  * mm_on: 0 no modulematch; 1 LDS tables: st = mmtab[(mm_base + st) * 16 + digit] per hex digit,
  * then st = mmtab[17 * S + mm_post + st] for the postamble, accept on flags mmtab[16 * S + mm_base
  * + st] (ACC_NOW and DEAD are absorbing); 2 byte walk through the blob's t256 table. */
-#define SDX_MUDESC_LDS 160
+#define SDX_MUDESC_LDS 144
 #define SDX_MMTAB_LDS 10240
 typedef struct {
   uint8_t pre[16], post[2];             /* preamble / postamble bytes (longer ones: string heap) */

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #ifdef SDX_PROF
 __device__ unsigned long long g_prof[32];
@@ -77,6 +78,7 @@ struct MuItem {
   uint8_t mi, fmask;        // tile message, found-key mask
 };
 constexpr int QCAP = 128;  // per-wave ring: < 64 pending before a push of <= 64
+constexpr int LANE_WAVES = 8;  // lane-decode MU variant: 8 waves (512 threads) share one tile
 
 // MU (NW <= 4): one finditer match, finished after the protocol loop with lane = match
 struct MuMatch {
@@ -111,9 +113,13 @@ struct TileLds {
   uint32_t digit_ok[TM];
   uint32_t cnt[TM];    // staged results per message (atomic; the old value is the record's rank)
   uint32_t rec_base, heap_base, tile_bad, tot_rec;
-  uint32_t wheap_pre[4];
   uint32_t mbase[TM];
-  Wave w[LM ? 1 : 4];
+  struct WaveScratch4 {
+    Wave w[4];
+  };
+  struct NoScratch {};
+  // per-wave byte scratch: MS and the long MU variant only (the lane-decode MU variant has none)
+  typename std::conditional<LM, NoScratch, WaveScratch4>::type wa;
   // short MS tiles (NW <= 4, not the MU lane variant) stage few results; overflow re-runs on the
   // long variant
   static constexpr int PREC = LM ? 512 : (NW <= 4 ? POOL_REC_MS : POOL_REC);
@@ -128,11 +134,11 @@ struct TileLds {
   // the decode queues live only during the protocol loop, the modulematch tables only in the
   // finish phase after it: one region
   union alignas(16) {
-    MuItem q[4][LM ? QCAP : 1];
+    MuItem q[LM ? LANE_WAVES : 1][LM ? QCAP : 1];
     uint8_t mmtab[LM ? SDX_MMTAB_LDS : 16];
   } u;
 #ifdef SDX_PROF
-  unsigned long long prof[4][32];
+  unsigned long long prof[LM ? LANE_WAVES : 4][32];
 #endif
 };
 
@@ -239,7 +245,7 @@ SDX_DEV void raise_msg(T& L, int msg_local, int proto, int kind) {
 template <int NW, int TM, bool LM>
 SDX_DEV void finish_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
                        int nb) {
-  auto& W = L.w[wave];
+  auto& W = L.wa.w[wave];
   uint8_t* buf = W.bits;
   PROF_T(t_pd);
   // postDemodulation (:231-250): 'F' -> int() ValueError caught -> bits unchanged
@@ -348,7 +354,7 @@ template <int NW, int TM, bool LM>
 SDX_DEV void decode_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
                        int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1, uint64_t ut2, int fmask) {
   using T = TileLds<NW, TM, LM>;
-  auto& W = L.w[wave];
+  auto& W = L.wa.w[wave];
   const int lane = lane_id();
   const uint64_t* bm = &L.bm[s * T::MSTRIDE];
   const int n = L.nlen[s], nw = (n + 63) >> 6;
@@ -836,7 +842,7 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
 template <int NW, int TM, bool LM>
 SDX_DEV void finish_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
                        int nb) {
-  auto& W = L.w[wave];
+  auto& W = L.wa.w[wave];
   uint8_t* buf = W.bits;
   if (nb == 0) return;                                      // (:191-192)
   if (cld(&rec->lir_min) != -1 && nb < cld(&rec->lir_min)) return;      // length_in_range (:194-196)
@@ -885,7 +891,7 @@ template <int NW, int TM, bool LM>
 SDX_DEV void decode_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
                        int start, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3, int fmask) {
   using T = TileLds<NW, TM, LM>;
-  auto& W = L.w[wave];
+  auto& W = L.wa.w[wave];
   const int lane = lane_id();
   const uint64_t* bm = &L.bm[s * T::MSTRIDE];
   const int n = L.nlen[s];
@@ -1071,8 +1077,17 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
 // ---------------------------------------------------------------------------------------------
 // MU / MS tile kernel
 // ---------------------------------------------------------------------------------------------
+// the lane-decode MU variant runs 8 waves per tile; (512, 2) asks for 2 such tiles per CU,
+// i.e. 4 waves/SIMD (<= 128 VGPRs)
+template <int KIND, int NW>
+constexpr int pulses_threads() { return (KIND == SDX_KIND_MU && NW <= 4) ? 64 * LANE_WAVES : 256; }
+template <int KIND, int NW>
+constexpr int pulses_min_blocks() { return (KIND == SDX_KIND_MU && NW <= 4) ? 2 : 1; }
+
 template <int KIND, int NW, int TM>
-__global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
+__global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
+    (pulses_min_blocks<KIND, NW>() == 2 ? 4 : 1)))) void k_pulses(
+    const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
   constexpr bool LANE_MU = KIND == SDX_KIND_MU && NW <= 4;
   using T = TileLds<NW, TM, LANE_MU>;
   __shared__ T L;
@@ -1108,7 +1123,8 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
   PROF_T(t_kernel);
   PROF_T(t_stage);
   // ---- stage: per-id position bitmaps (coalesced 64-character rows, 10 ballots each)
-  for (int mi = wave; mi < nvalid; mi += 4) {
+  constexpr int NWAVE = pulses_threads<KIND, NW>() / 64;
+  for (int mi = wave; mi < nvalid; mi += NWAVE) {
     const int msg = msg_of[mi];
     const int64_t off = b.offsets_dev[msg];
     int n = (int)(b.offsets_dev[msg + 1] - off);
@@ -1262,7 +1278,7 @@ __global__ __launch_bounds__(256) void k_pulses(const void* __restrict__ bank, s
     }
     const int p = cld(&order[cur]);
     ++cur;
-    if (KIND == SDX_KIND_MU) {
+    if constexpr (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
       if (cld(&rec->never) || !cld(&rec->active)) continue;
 #ifdef SDX_X_NOSTARTPROTO
@@ -1970,7 +1986,8 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   constexpr int TM = 64;
   const int grid = (ntot + TM - 1) / TM;
   if (kind == SDX_KIND_MU)
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), dim3(sdx::pulses_threads<SDX_KIND_MU, 4>()),
+                       0, st, bank->dev, *batch, *out);
   else
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
   HIPCHK(hipGetLastError());
