@@ -89,7 +89,7 @@ struct MuMatch {
   uint8_t flags;         // bit0 tail matched, bits1-2 tail symbol, bits3-5 found-key mask
   uint8_t j;             // match index within the (message, protocol) pair
 };
-constexpr int MATCH_CAP = 512;  // per tile; more -> tile overflow -> exact re-run (long variant)
+constexpr int MATCH_CAP = 768;  // per tile (bench corpus: mean 290, max 513); more -> tile overflow -> exact re-run
 
 // LM: the lane-decode MU variant (NW <= 4) -- no per-wave byte scratch, but the MU decode
 // descriptors and modulematch tables staged in LDS
@@ -123,7 +123,7 @@ struct TileLds {
   // short MS tiles (NW <= 4, not the MU lane variant) stage few results; overflow re-runs on the
   // long variant
   static constexpr int PREC = LM ? 512 : (NW <= 4 ? POOL_REC_MS : POOL_REC);
-  static constexpr int PHEAP = LM ? 14336 : (NW <= 4 ? POOL_HEAP_MS : POOL_HEAP);
+  static constexpr int PHEAP = LM ? 10240 : (NW <= 4 ? POOL_HEAP_MS : POOL_HEAP);  // MU bench tiles: <= 8.1 KB
   StageRec rec[PREC];
   alignas(16) uint8_t heap[PHEAP];
   unsigned long long pool_ctr;  // low 32: staged records, high 32: staged heap bytes (one LDS atomic)
