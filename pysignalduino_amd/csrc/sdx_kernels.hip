@@ -30,20 +30,20 @@ __device__ unsigned long long g_prof[32];
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, v)                                                                   \
   do {                                                                                      \
-    if (__lane_id() == 0) L.prof[wave][slot] += __builtin_amdgcn_s_memtime() - (v);        \
+    if (__lane_id() == 0) L.prof[wave][slot] += (unsigned)(__builtin_amdgcn_s_memtime() - (v)); \
   } while (0)
 #define PROF_CNT(slot, x)                                                                   \
   do {                                                                                      \
-    if (__lane_id() == 0) L.prof[wave][slot] += (unsigned long long)(x);                   \
+    if (__lane_id() == 0) L.prof[wave][slot] += (unsigned)(x);                              \
   } while (0)
 // divergent code: the lowest active lane accounts the wave's time
 #define PROF_ADDD(slot, v)                                                                  \
   do {                                                                                      \
     if (__lane_id() == __ffsll((unsigned long long)__builtin_amdgcn_read_exec()) - 1)       \
-      L.prof[wave][slot] += __builtin_amdgcn_s_memtime() - (v);                             \
+      L.prof[wave][slot] += (unsigned)(__builtin_amdgcn_s_memtime() - (v));                 \
   } while (0)
 // per-lane event count (divergent code)
-#define PROF_CNTL(slot) atomicAdd(&L.prof[wave][slot], 1ull)
+#define PROF_CNTL(slot) atomicAdd(&L.prof[wave][slot], 1u)
 #else
 #define PROF_T(v)
 #define PROF_ADD(slot, v)
@@ -138,7 +138,7 @@ struct TileLds {
     uint8_t mmtab[LM ? SDX_MMTAB_LDS : 16];
   } u;
 #ifdef SDX_PROF
-  unsigned long long prof[LM ? LANE_WAVES : 4][32];
+  unsigned int prof[LM ? LANE_WAVES : 4][24];  // s_memtime deltas per wave (< 2^32 per kernel)
 #endif
 };
 
@@ -1117,7 +1117,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     if (tid == 0) L.mm_states = (int)bv.hdr->mm_states;
   }
 #ifdef SDX_PROF
-  if (lane < 32) L.prof[wave][lane] = 0;
+  if (lane < 24) L.prof[wave][lane] = 0;
 #endif
   __syncthreads();
   PROF_T(t_kernel);
@@ -1409,16 +1409,27 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     }
     PROF_ADD(12, t_dec);
   }
+  // modulematch tables for the finish phase: loaded into registers now, so that the global
+  // load latency overlaps the end barrier; stored over the (then dead) decode queues after it
+  static_assert(SDX_MMTAB_LDS <= 2 * 16 * 64 * LANE_WAVES, "prefetch covers the LDS table cap");
+  uint4 mm_pf[2];
+  const int m16 = LANE_MU ? (int)bv.hdr->mmtab_bytes >> 4 : 0;
+  if constexpr (LANE_MU) {
+    const uint4* msrc = reinterpret_cast<const uint4*>(bv.mmtab);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (tid + k * (int)blockDim.x < m16) mm_pf[k] = msrc[tid + k * blockDim.x];
+  }
   PROF_T(t_bar);
   __syncthreads();
   PROF_ADD(14, t_bar);
   if constexpr (LANE_MU) {  // finish every match of the tile: lane = match (message_unsynced.py:197-290)
     PROF_T(t_fin);
-    {  // modulematch tables -> LDS, over the (now dead) decode queues
-      const int m16 = (int)bv.hdr->mmtab_bytes >> 4;
-      const uint4* msrc = reinterpret_cast<const uint4*>(bv.mmtab);
+    {
       uint4* mdst = reinterpret_cast<uint4*>(L.u.mmtab);
-      for (int i = tid; i < m16; i += blockDim.x) mdst[i] = msrc[i];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (tid + k * (int)blockDim.x < m16) mdst[tid + k * blockDim.x] = mm_pf[k];
       __syncthreads();
     }
     const int nm = L.nmatch < MATCH_CAP ? L.nmatch : MATCH_CAP;
@@ -1444,7 +1455,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   PROF_ADD(13, t_fl);
   PROF_ADD(15, t_kernel);
 #ifdef SDX_PROF
-  if (lane < 32) atomicAdd(&g_prof[lane], L.prof[wave][lane]);
+  if (lane < 24) atomicAdd(&g_prof[lane], (unsigned long long)L.prof[wave][lane]);
 #endif
 }
 
