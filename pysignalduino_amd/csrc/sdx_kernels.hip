@@ -1433,8 +1433,44 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       __syncthreads();
     }
     const int nm = L.nmatch < MATCH_CAP ? L.nmatch : MATCH_CAP;
-    for (int m = tid; m < nm; m += blockDim.x) {
-      const MuMatch mm = L.mlist[m];
+    // group the matches by protocol (counting sort into the free half of the queue region):
+    // lanes of one wave then follow the same postDemod / modulematch / formatting path
+    constexpr int NBIN = 256;
+    static_assert(sizeof(L.u) >= SDX_MMTAB_LDS + MATCH_CAP * 2 + NBIN * 4, "sort scratch fits the union");
+    uint16_t* perm = reinterpret_cast<uint16_t*>(L.u.mmtab + SDX_MMTAB_LDS);
+    uint32_t* bin = reinterpret_cast<uint32_t*>(perm + MATCH_CAP);
+    const bool sorted = (int)bv.hdr->n_mu <= NBIN;
+    if (sorted) {
+      for (int i = tid; i < NBIN; i += blockDim.x) bin[i] = 0;
+      __syncthreads();
+      for (int m = tid; m < nm; m += blockDim.x) atomicAdd(&bin[L.mlist[m].p], 1u);
+      __syncthreads();
+      if (wave == 0) {  // exclusive prefix over the bins, 4 per lane
+        uint32_t v[4], t = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k] = bin[4 * lane + k];
+          t += v[k];
+        }
+        uint32_t x = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o);
+          if (lane >= o) x += y;
+        }
+        uint32_t base = x - t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          bin[4 * lane + k] = base;
+          base += v[k];
+        }
+      }
+      __syncthreads();
+      for (int m = tid; m < nm; m += blockDim.x) perm[atomicAdd(&bin[L.mlist[m].p], 1u)] = (uint16_t)m;
+      __syncthreads();
+    }
+    for (int i = tid; i < nm; i += blockDim.x) {
+      const MuMatch mm = L.mlist[sorted ? perm[i] : i];
       const int qm = mm.mi, qp = mm.p;
       const uint32_t rk = L.raise_key[qm];
       if (rk != 0xFFFFFFFFu && (rk >> 8) < (uint32_t)qp) continue;  // an earlier protocol raised

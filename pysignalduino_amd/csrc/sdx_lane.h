@@ -204,6 +204,44 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, 
 #ifdef SDX_X_NOCOMBO
   return PexRes{true, minpos, cand[0]};
 #endif
+  const uint64_t upk = cld(&sp->uidx_pk);
+  // fast paths in exact itertools.product order for the common shapes: a 2-pulse search of two
+  // distinct values (width-2 one/zero keys, 2-pulse starts) and a 1-pulse search
+  if (nu == 2 && slen == 2 && upk == 0x10ull) {
+    for (int i = 0; i < cnt[0]; ++i) {
+      const int a = (int)((cand[0] >> (4 * i)) & 15), ida = (int)((ids >> (4 * a)) & 15);
+      for (int j = 0; j < cnt[1]; ++j) {
+        const int b = (int)((cand[1] >> (4 * j)) & 15);
+        if (b == a) continue;  // no id reused (pattern_utils.py:114-115)
+        const int idb = (int)((ids >> (4 * b)) & 15);
+        if (!pair_bit(P0, P1, ida, idb)) continue;  // "ab" occurs nowhere
+        const uint64_t tgt = (uint64_t)ida | ((uint64_t)idb << 4);
+        int p = 0;
+        if (minpos != 0 || need_pos) {
+          p = m_first(m_occ<NW>(bm, tgt, 2), minpos);
+          if (p < 0) continue;
+        }
+        res.found = true;
+        res.pos = p;
+        res.tgt = tgt;
+        return res;
+      }
+    }
+    return res;
+  }
+  if (nu == 1 && slen == 1) {
+    for (int i = 0; i < cnt[0]; ++i) {
+      const int a = (int)((cand[0] >> (4 * i)) & 15), ida = (int)((ids >> (4 * a)) & 15);
+      const int p = m_first(m_occ<NW>(bm, (uint64_t)ida, 1), minpos);
+      if (p >= 0) {
+        res.found = true;
+        res.pos = p;
+        res.tgt = (uint64_t)ida;
+        return res;
+      }
+    }
+    return res;
+  }
   int digit[SDX_MAXUNIQ];
 #pragma unroll
   for (int u = 0; u < SDX_MAXUNIQ; ++u) digit[u] = 0;
@@ -220,7 +258,6 @@ SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, 
       }
     }
     if (!dup) {
-      const uint64_t upk = cld(&sp->uidx_pk);
       uint64_t tgt = 0;
       for (int i = 0; i < slen; ++i) tgt |= (uint64_t)((uid >> (4 * (int)((upk >> (4 * i)) & 15))) & 15) << (4 * i);
       // every adjacent id pair of the target must occur in the message: exact for a 2-id target
