@@ -80,6 +80,16 @@ struct MuItem {
 constexpr int QCAP = 128;  // per-wave ring: < 64 pending before a push of <= 64
 constexpr int LANE_WAVES = 8;  // lane-decode MU variant: 8 waves (512 threads) share one tile
 
+// MS (NW <= 4): a (message, protocol) pair that passed the sync/one/zero/float lookups, queued
+// for the lane decode
+struct MsItem {
+  uint32_t k0_lo, k0_hi;  // sync target string (nibbles)
+  uint16_t k1, k2, k3;    // one / zero / float target strings (width <= 4)
+  uint16_t start;         // first chunk position (after the sync)
+  uint16_t p;             // protocol index
+  uint8_t mi, fmask;      // tile message, found-key mask
+};
+
 // MU (NW <= 4): one finditer match, finished after the protocol loop with lane = match
 struct MuMatch {
   uint16_t q, k;         // first unit position, number of full units
@@ -91,9 +101,11 @@ struct MuMatch {
 };
 constexpr int MATCH_CAP = 768;  // per tile (bench corpus: mean 290, max 513); more -> tile overflow -> exact re-run
 
-// LM: the lane-decode MU variant (NW <= 4) -- no per-wave byte scratch, but the MU decode
+// LM: 0 = wave-cooperative decode (the long variants), 1 = lane-decode MU (NW <= 4: decode
+// descriptors, modulematch tables, match list), 2 = lane-decode MS (NW <= 4).  The lane variants
+// have no per-wave byte scratch; the MU one keeps the MU decode
 // descriptors and modulematch tables staged in LDS
-template <int NW, int TM, bool LM>
+template <int NW, int TM, int LM>
 struct TileLds {
   static constexpr int WS = NW;              // words per id bitmap
   static constexpr int MSTRIDE = 10 * NW + 1;  // odd stride: fewer LDS bank conflicts across lanes
@@ -119,26 +131,27 @@ struct TileLds {
   };
   struct NoScratch {};
   // per-wave byte scratch: MS and the long MU variant only (the lane-decode MU variant has none)
-  typename std::conditional<LM, NoScratch, WaveScratch4>::type wa;
+  typename std::conditional<LM != 0, NoScratch, WaveScratch4>::type wa;
   // short MS tiles (NW <= 4, not the MU lane variant) stage few results; overflow re-runs on the
   // long variant
-  static constexpr int PREC = LM ? 512 : (NW <= 4 ? POOL_REC_MS : POOL_REC);
-  static constexpr int PHEAP = LM ? 10240 : (NW <= 4 ? POOL_HEAP_MS : POOL_HEAP);  // MU bench tiles: <= 8.1 KB
+  static constexpr int PREC = LM == 1 ? 512 : (NW <= 4 ? POOL_REC_MS : POOL_REC);
+  static constexpr int PHEAP = LM == 1 ? 10240 : (NW <= 4 ? POOL_HEAP_MS : POOL_HEAP);  // MU bench tiles: <= 8.1 KB
   StageRec rec[PREC];
   alignas(16) uint8_t heap[PHEAP];
   unsigned long long pool_ctr;  // low 32: staged records, high 32: staged heap bytes (one LDS atomic)
   int ovf, next_p;
   int mm_states, nmatch;
-  MuMatch mlist[LM ? MATCH_CAP : 1];
-  alignas(16) sdx_mu_desc desc[LM ? SDX_MUDESC_LDS : 1];
+  MuMatch mlist[LM == 1 ? MATCH_CAP : 1];
+  alignas(16) sdx_mu_desc desc[LM == 1 ? SDX_MUDESC_LDS : 1];
   // the decode queues live only during the protocol loop, the modulematch tables only in the
   // finish phase after it: one region
   union alignas(16) {
-    MuItem q[LM ? LANE_WAVES : 1][LM ? QCAP : 1];
-    uint8_t mmtab[LM ? SDX_MMTAB_LDS : 16];
+    MuItem q[LM == 1 ? LANE_WAVES : 1][LM == 1 ? QCAP : 1];
+    uint8_t mmtab[LM == 1 ? SDX_MMTAB_LDS : 16];
   } u;
+  MsItem msq[LM == 2 ? LANE_WAVES : 1][LM == 2 ? QCAP : 1];  // MS decode queues
 #ifdef SDX_PROF
-  unsigned int prof[LM ? LANE_WAVES : 4][24];  // s_memtime deltas per wave (< 2^32 per kernel)
+  unsigned int prof[LM != 0 ? LANE_WAVES : 4][24];  // s_memtime deltas per wave (< 2^32 per kernel)
 #endif
 };
 
@@ -242,7 +255,7 @@ SDX_DEV void raise_msg(T& L, int msg_local, int proto, int kind) {
 // ---------------------------------------------------------------------------------------------
 // MU: finish one match (message_unsynced.py:230-290)
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM, bool LM>
+template <int NW, int TM, int LM>
 SDX_DEV void finish_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
                        int nb) {
   auto& W = L.wa.w[wave];
@@ -350,7 +363,7 @@ SDX_DEV void finish_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, con
 // MU: decode one surviving (message, protocol) pair with the whole wave
 // (message_unsynced.py:146-290; re.finditer emulated exactly)
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM, bool LM>
+template <int NW, int TM, int LM>
 SDX_DEV void decode_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_mu_proto* rec, int p, int s,
                        int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1, uint64_t ut2, int fmask) {
   using T = TileLds<NW, TM, LM>;
@@ -839,7 +852,7 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
 // ---------------------------------------------------------------------------------------------
 // MS: finish (message_synced.py:191-241)
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM, bool LM>
+template <int NW, int TM, int LM>
 SDX_DEV void finish_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
                        int nb) {
   auto& W = L.wa.w[wave];
@@ -887,7 +900,7 @@ SDX_DEV void finish_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, con
 }
 
 // MS decode loop (:172-189) for one surviving pair, wave-cooperative over chunks
-template <int NW, int TM, bool LM>
+template <int NW, int TM, int LM>
 SDX_DEV void decode_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, const sdx_ms_proto* rec, int p, int s,
                        int start, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3, int fmask) {
   using T = TileLds<NW, TM, LM>;
@@ -973,13 +986,193 @@ SDX_DEV void decode_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, con
 }
 
 // ---------------------------------------------------------------------------------------------
+// MS, lane = (message, protocol) survivor (message_synced.py:160-241) on register bitmasks
+// ---------------------------------------------------------------------------------------------
+// finish one MS result from its packed bits (P1 = '1', PF = 'F', nb bits): length_in_range,
+// padding BEFORE postDemod, postDemod without try, hex (None -> skipped), payload
+template <int NW, class T>
+SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, int p, int mi, const M<NW>& P1,
+                            const M<NW>& PF, int nb) {
+  constexpr int NB = 64 * NW + 64;
+  if (nb == 0) return;  // (:191-192)
+  if (cld(&rec->lir_min) != -1 && nb < cld(&rec->lir_min)) return;  // length_in_range (:194-196)
+  if (nb > cld(&rec->lir_max)) return;
+  int nbits = nb;  // padding (:198-200): appended '0' bits (P1/PF hold zeros beyond nb)
+  const int pad = cld(&rec->pad_bits);
+  while (nbits % pad) ++nbits;
+  const bool anyf = m_any(PF);
+  const int pd = cld(&rec->postdemo);
+  uint8_t pout[NB];
+  bool usearr = false;
+  if (pd != SDX_PD_NONE) {  // (:203-219)
+    if (anyf) {  // int('F') -> ValueError, not caught
+      atomicMin(&L.raise_key[mi], ((uint32_t)p << 8) | SDX_RAISE_VALUE);
+      return;
+    }
+    uint8_t pin[NB];
+    for (int b = 0; b < nbits; ++b) pin[b] = m_test(P1, b) ? 1 : 0;
+    int no = 0;
+    const int rc = run_postdemo(pd, pin, nbits, pout, &no);
+    if (rc == -1) {
+      atomicMin(&L.raise_key[mi], ((uint32_t)p << 8) | SDX_RAISE_VALUE);
+      return;
+    }
+    if (rc == 0) return;
+    if (no > 0) {  // `if ret:` keeps the bits for an empty list
+      usearr = true;
+      nbits = no;
+    }
+  }
+  if (!usearr && anyf) return;  // bin_str_2_hex_str -> None -> skipped (:224-226)
+  const int nd = (nbits + 3) >> 2;
+  if (!usearr && 4 * nd > 64 * NW) {
+    for (int b = 0; b < nbits; ++b) pout[b] = m_test(P1, b) ? 1 : 0;
+    usearr = true;
+  }
+  M<NW> H = m_zero<NW>();  // hex digits: right-aligned to a nibble boundary, nibble-reversed
+  if (!usearr) {
+    H = m_shl_small(P1, 4 * nd - nbits);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) H.w[i] = nibrev(H.w[i]);
+  }
+  const int pre_len = cld(&rec->pre_len), post_len = cld(&rec->post_len);
+  const uint8_t* pre = bv.str + cld(&rec->pre_off);
+  const uint8_t* post = bv.str + cld(&rec->post_off);
+  const int total = pre_len + nd + post_len;
+  const int span = (total + 7) & ~7;
+  const unsigned long long o = atomicAdd(&L.pool_ctr, ((unsigned long long)span << 32) | 1ull);
+  const int slot = (int)(uint32_t)o, off = (int)(o >> 32);
+  if (slot >= T::PREC || off + span > T::PHEAP) {
+    L.ovf = 1;
+    return;
+  }
+  ByteWriter w(reinterpret_cast<uint64_t*>(L.heap + off));
+  for (int i = 0; i < pre_len; ++i) w.put(pre[i], 1);
+  if (!usearr) {
+    for (int t = 0; t < nd; t += 8) {
+      const int b = 4 * t, wi = b >> 6, sh = b & 63;
+      uint64_t x = m_word(H, wi) >> sh;
+      if (sh > 32) x |= m_word(H, wi + 1) << (64 - sh);
+      const int cnt = (nd - t < 8) ? nd - t : 8;
+      w.put(hex8(x & 0xFFFFFFFFull, cnt), cnt);
+    }
+  } else {
+    for (int d = 0; d < nd; ++d) {  // nibbles from the right (helpers.py:28-64)
+      const int e = nbits - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+      int v = 0;
+      for (int i = a; i < e; ++i) v = (v << 1) | pout[i];
+      w.put((uint64_t)(v < 10 ? '0' + v : 'A' + v - 10), 1);
+    }
+  }
+  for (int i = 0; i < post_len; ++i) w.put(post[i], 1);
+  w.flush();
+  StageRec r;
+  r.off = (uint32_t)off;
+  r.len = (uint16_t)total;
+  r.proto = (uint16_t)p;
+  r.bitlen = (uint32_t)nbits;
+  r.msg = (uint8_t)mi;
+  r.wave = 0;
+  r.rank = 0;  // one result per (message, protocol)
+  L.rec[slot] = r;
+}
+
+template <int NW, class T>
+SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, int p, int mi, const uint64_t* bm,
+                            int n, int start, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3, int fmask) {
+  const int Wd = cld(&rec->width);
+  const uint64_t kt[4] = {k0, k1, k2, k3};
+  const int klen[4] = {cld(&rec->key[0].len), cld(&rec->key[1].len), cld(&rec->key[2].len), cld(&rec->key[3].len)};
+  const uint8_t KSYM[4] = {3, 1, 0, 2};  // 3: the sync symbol '' (no bit)
+  const int span = start < n ? n - start : 0;
+  const int nfull = span / Wd, part = span - nfull * Wd;
+  // chunk-indexed masks (bit t = chunk at start + t*Wd): symbol '1', 'F', sync-skip, unit, tail
+  M<NW> C1 = m_zero<NW>(), CF = m_zero<NW>(), CS = m_zero<NW>(), CU = m_zero<NW>(), CT = m_zero<NW>();
+  // pattern_lookup (:122-135): distinct strings, value = the last writer's symbol
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    if (!((fmask >> kk) & 1) || klen[kk] != Wd) continue;
+    bool later = false;
+#pragma unroll
+    for (int j = kk + 1; j < 4; ++j) later |= ((fmask >> j) & 1) && klen[j] == klen[kk] && kt[j] == kt[kk];
+    if (later) continue;
+    const M<NW> C = m_stride_extract(m_occ<NW>(bm, kt[kk], Wd), start, Wd, nfull);
+    CU = m_or(CU, C);
+    if (KSYM[kk] == 1) C1 = m_or(C1, C);
+    if (KSYM[kk] == 2) CF = m_or(CF, C);
+    if (KSYM[kk] == 3) CS = m_or(CS, C);
+  }
+  // end_pattern_lookup (:124-127, reset after the sync :158): one/zero/float pstr[:-1], first
+  // writer wins; a full chunk that is no unit continues with chunk[:-1]'s symbol (:183-187)
+  const bool recon = cld(&rec->recon) != 0 && Wd > 1;
+  const uint64_t emsk = (Wd - 1 >= 16) ? ~0ull : ((1ull << (4 * (Wd - 1))) - 1);
+  if (recon) {
+#pragma unroll
+    for (int kk = 1; kk < 4; ++kk) {
+      if (!((fmask >> kk) & 1) || klen[kk] != Wd) continue;
+      const uint64_t key = kt[kk] & emsk;
+      bool earlier = false;
+#pragma unroll
+      for (int j = 1; j < kk; ++j) earlier |= ((fmask >> j) & 1) && klen[j] == Wd && (kt[j] & emsk) == key;
+      if (earlier) continue;
+      const M<NW> C = m_and(m_stride_extract(m_occ<NW>(bm, key, Wd - 1), start, Wd, nfull), m_not(CU));
+      CT = m_or(CT, C);
+      if (KSYM[kk] == 1) C1 = m_or(C1, C);
+      if (KSYM[kk] == 2) CF = m_or(CF, C);
+    }
+  }
+  // the first chunk that is neither ends the loop (:188-189)
+  int k = m_first(m_and(m_not(m_or(CU, CT)), m_range_lo<NW>(nfull)), 0);
+  if (k < 0) k = nfull;
+  // a partial last chunk: a unit of its length (last writer), else (recon) the chunk as a tail key
+  int extra = -1;
+  if (k == nfull && part > 0) {
+    const int x = start + nfull * Wd;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      if (((fmask >> kk) & 1) && klen[kk] == part && match_at(bm, NW, n, kt[kk], part, x)) extra = KSYM[kk];
+    if (extra < 0 && recon && part == Wd - 1) {
+#pragma unroll
+      for (int kk = 1; kk < 4; ++kk)
+        if (extra < 0 && ((fmask >> kk) & 1) && klen[kk] == Wd && match_at(bm, NW, n, kt[kk] & emsk, part, x))
+          extra = KSYM[kk];
+    }
+  }
+  // bits = chunks [0, k) without the sync-symbol ones, then the partial chunk's bit
+  const M<NW> R = m_range_lo<NW>(k);
+  M<NW> P1, PF;
+  int nb;
+  if (!m_any(m_and(CS, R))) {
+    P1 = m_and(C1, R);
+    PF = m_and(CF, R);
+    nb = k;
+  } else {  // a sync-string chunk inside the data (rare): compact serially
+    P1 = m_zero<NW>();
+    PF = m_zero<NW>();
+    nb = 0;
+    for (int t = 0; t < k; ++t) {
+      if (m_test(CS, t)) continue;
+      if (m_test(C1, t)) m_set(P1, nb);
+      if (m_test(CF, t)) m_set(PF, nb);
+      ++nb;
+    }
+  }
+  if (extra >= 0 && extra != 3) {
+    if (extra == 1) m_set(P1, nb);
+    if (extra == 2) m_set(PF, nb);
+    ++nb;
+  }
+  finish_ms_lane<NW>(L, bv, rec, p, mi, P1, PF, nb);
+}
+
+// ---------------------------------------------------------------------------------------------
 // tile flush: records in (message, protocol, match) order, one atomic per tile.
 // Records reach the pool in any order (waves and drained (message, protocol) items run
 // concurrently); a record's place inside its message is the number of records of the same
 // message with a smaller (protocol, rank) key -- rank is the per-message atomic counter, which
 // increases monotonically along one (message, protocol) pair's finditer loop.
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TM, bool LM>
+template <int NW, int TM, int LM>
 SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
   const int tid = threadIdx.x;
   // flush scratch aliases the id bitmaps (dead once every wave has left the protocol loop)
@@ -1080,16 +1273,17 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
 // the lane-decode MU variant runs 8 waves per tile; (512, 2) asks for 2 such tiles per CU,
 // i.e. 4 waves/SIMD (<= 128 VGPRs)
 template <int KIND, int NW>
-constexpr int pulses_threads() { return (KIND == SDX_KIND_MU && NW <= 4) ? 64 * LANE_WAVES : 256; }
+constexpr int pulses_threads() { return NW <= 4 ? 64 * LANE_WAVES : 256; }
 template <int KIND, int NW>
-constexpr int pulses_min_blocks() { return (KIND == SDX_KIND_MU && NW <= 4) ? 2 : 1; }
+constexpr int pulses_min_blocks() { return NW <= 4 ? 2 : 1; }
 
 template <int KIND, int NW, int TM>
 __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
     (pulses_min_blocks<KIND, NW>() == 2 ? 4 : 1)))) void k_pulses(
     const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
   constexpr bool LANE_MU = KIND == SDX_KIND_MU && NW <= 4;
-  using T = TileLds<NW, TM, LANE_MU>;
+  constexpr bool LANE_MS = KIND == SDX_KIND_MS && NW <= 4;
+  using T = TileLds<NW, TM, LANE_MU ? 1 : (LANE_MS ? 2 : 0)>;
   __shared__ T L;
   const BankView bv = bank_view(bank);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1233,8 +1427,10 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   const uint16_t* order = bv.order + (KIND == SDX_KIND_MU ? 0 : (int)bv.hdr->n_mu);
   double last_clock = __builtin_nan("");  // NaN != anything: the first protocol normalises
   MuItem* Q = nullptr;
+  MsItem* QS = nullptr;
   int q_head = 0, q_tail = 0;
-  if constexpr (KIND == SDX_KIND_MU && NW <= 4) Q = L.u.q[wave];
+  if constexpr (LANE_MU) Q = L.u.q[wave];
+  if constexpr (LANE_MS) QS = L.msq[wave];
   auto drain = [&](int head, int cnt) {
     wave_sync();
     if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
@@ -1254,6 +1450,16 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           decode_mu_lane<NW>(L, wave, bv, bv.mu + qp, d, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx,
                              ((uint64_t)it.st_hi << 32) | it.st_lo, it.u0, it.u1, it.u2, it.fmask);
         }
+      }
+    }
+    if constexpr (LANE_MS) {
+      if (lane < cnt) {
+        const MsItem it = QS[(head + lane) & (QCAP - 1)];
+        const int qm = it.mi, qp = it.p;
+        const uint32_t rk = L.raise_key[qm];
+        if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp)
+          decode_ms_lane<NW>(L, bv, bv.ms + qp, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.start,
+                             ((uint64_t)it.k0_hi << 32) | it.k0_lo, it.k1, it.k2, it.k3, it.fmask);
       }
     }
     wave_sync();
@@ -1391,16 +1597,40 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         if (r.found) { kt3 = r.tgt; fmask |= 8; }
       }
       alive = alive && fmask != 0;
-      uint64_t surv = ballot(alive);
-      while (surv) {
-        const int sl = ffs64(surv);
-        surv &= surv - 1;
-        decode_ms(L, wave, bv, rec, p, sl, bcast_i(start, sl), bcast_u64(kt0, sl), bcast_u64(kt1, sl),
-                  bcast_u64(kt2, sl), bcast_u64(kt3, sl), bcast_i(fmask, sl));
+      if constexpr (LANE_MS) {  // queue the survivors; drain 64 at a time, lane = (message, protocol)
+        const uint64_t pass = ballot(alive);
+        if (pass) {
+          if (alive) {
+            MsItem it;
+            it.k0_lo = (uint32_t)kt0;
+            it.k0_hi = (uint32_t)(kt0 >> 32);
+            it.k1 = (uint16_t)kt1;
+            it.k2 = (uint16_t)kt2;
+            it.k3 = (uint16_t)kt3;
+            it.start = (uint16_t)start;
+            it.p = (uint16_t)p;
+            it.mi = (uint8_t)mi;
+            it.fmask = (uint8_t)fmask;
+            QS[(q_tail + lanes_below(pass)) & (QCAP - 1)] = it;
+          }
+          q_tail += popc64(pass);
+          if (q_tail - q_head >= WAVE) {
+            drain(q_head, WAVE);
+            q_head += WAVE;
+          }
+        }
+      } else {
+        uint64_t surv = ballot(alive);
+        while (surv) {
+          const int sl = ffs64(surv);
+          surv &= surv - 1;
+          decode_ms(L, wave, bv, rec, p, sl, bcast_i(start, sl), bcast_u64(kt0, sl), bcast_u64(kt1, sl),
+                    bcast_u64(kt2, sl), bcast_u64(kt3, sl), bcast_i(fmask, sl));
+        }
       }
     }
   }
-  if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
+  if constexpr (LANE_MU || LANE_MS) {
     PROF_T(t_dec);
     while (q_head < q_tail) {
       const int c = (q_tail - q_head < WAVE) ? q_tail - q_head : WAVE;
@@ -2036,7 +2266,8 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), dim3(sdx::pulses_threads<SDX_KIND_MU, 4>()),
                        0, st, bank->dev, *batch, *out);
   else
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), dim3(sdx::pulses_threads<SDX_KIND_MS, 4>()),
+                       0, st, bank->dev, *batch, *out);
   HIPCHK(hipGetLastError());
   return SDX_OK;
 }
