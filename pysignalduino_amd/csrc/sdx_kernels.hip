@@ -1198,7 +1198,7 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       L.mbase[m] = nrec;
       if (L.raise_key[m] == 0xFFFFFFFFu && !bad) nrec += cntm[m];
     }
-    const uint32_t nheap = bad ? 0u : (uint32_t)nh;
+    const uint32_t nheap = bad ? 0u : (((uint32_t)nh + 15u) & ~15u);  // 16-B pieces: full-width copy
     uint32_t rb = 0, hb = 0;
     if (!bad) {
       rb = atomicAdd(&out.cursor_dev[0], nrec);
@@ -1244,7 +1244,14 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       out.rec_dev[L.rec_base + b0 + rk] = o;
     }
     uint8_t* hd = out.heap_dev + L.heap_base;
-    for (int i = tid; i < nh; i += blockDim.x) hd[i] = L.heap[i];
+    if ((((uintptr_t)hd) & 15u) == 0) {  // 16-B stores (every tile reserves a multiple of 16 B)
+      const int n16 = (nh + 15) >> 4;
+      const uint4* src = reinterpret_cast<const uint4*>(L.heap);
+      uint4* dst = reinterpret_cast<uint4*>(hd);
+      for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
+    } else {
+      for (int i = tid; i < nh; i += blockDim.x) hd[i] = L.heap[i];
+    }
   }
   for (int m = tid; m < nvalid; m += blockDim.x) {
     sdx_desc d;
