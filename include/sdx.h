@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 1
+#define SDX_ABI_VERSION 2
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -68,6 +68,8 @@ typedef struct {
   const double* pat_val_dev;   /* [n*10] float(P#) */
   const int8_t* cp_slot_dev;   /* [n] MS: slot of CP, -1 = CP not a pattern (NULL for MU) */
   const uint8_t* ms_ok_dev;    /* [n] MS: CP/SP/R string gates passed (NULL for MU) */
+  const int32_t* len_dev;      /* optional [n] message lengths: message i = data[offsets[i], +len[i])
+                                * (slot layout of sdx_parse_lines); NULL = offsets[i+1] - offsets[i] */
   const int32_t* sel_dev;      /* optional [n_sel] subset of message indices to run, NULL = all */
   int32_t n;                   /* messages in the batch */
   int32_t n_sel;               /* entries in sel_dev (ignored when sel_dev == NULL) */
@@ -80,6 +82,7 @@ typedef struct {
   const int32_t* clock_dev;    /* [n] C= */
   const int32_t* mcbitnum_dev; /* [n] L= */
   const uint8_t* flags_dev;    /* [n] bit0: message type 'Mc', bit1: version starts 'V 3.2.' */
+  const int32_t* len_dev;      /* optional [n] frame lengths (as sdx_pulse_batch.len_dev) */
   const int32_t* sel_dev;
   int32_t n, n_sel;
 } sdx_mc_batch;
@@ -114,6 +117,71 @@ int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch*
                           void* hip_stream);
 /* MC "fixed" chain: every frame x every clockrange protocol */
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream);
+
+/* ---- wire-line front end ------------------------------------------------------
+ * Raw firmware lines, byte for byte as the transport receives them (the reference decodes them
+ * latin-1, signalduino/transport.py:123).  One launch runs, per line, what
+ * SignalParser.parse_line does before demodulation (signalduino/parser/__init__.py:37-49):
+ * strip + STX/ETX framing (parser/base.py:188-206), decompress_payload (base.py:13-186), routing
+ * by payload[:2].upper(), the MU validity regex (parser/mu.py:48), _parse_to_dict and the "D"
+ * check (mu.py:82-94, ms.py:65-78), and the MC header validation (parser/mc.py:37-155).  The
+ * outputs of a line form message i of an sdx_pulse_batch (MU/MS) or sdx_mc_batch (MC) in slot
+ * layout (len_dev set): no host repacking. */
+enum sdx_line_kind { SDX_LINE_NONE = 0, SDX_LINE_MU = 1, SDX_LINE_MS = 2, SDX_LINE_MC = 3, SDX_LINE_MN = 4 };
+enum sdx_line_status {
+  SDX_LS_OK = 0,          /* routed to kind, ready for demodulation */
+  SDX_LS_NOFRAME = 1,     /* extract_payload() returned None: ignored */
+  SDX_LS_NOPARSER = 2,    /* no parser for the message type: ignored */
+  SDX_LS_INVALID = 3,     /* the parser rejects the line (MU regex, MC header, MC hex, R/F): ignored */
+  SDX_LS_NODATA = 4,      /* no D field: ignored */
+  SDX_LS_UNSUPPORTED = 5  /* outside the device contract (e.g. multi-digit P ids, non-integer P# values,
+                           * bytes >= 0x80 after decompression, MN): the caller must not guess */
+};
+
+typedef struct {
+  const uint8_t* bytes_dev;    /* all lines concatenated */
+  const int64_t* offsets_dev;  /* [n+1] line i = bytes[offsets[i], offsets[i+1]) */
+  int32_t n;
+} sdx_lines;
+
+typedef struct {
+  uint8_t* kind_dev;           /* [n] enum sdx_line_kind */
+  uint8_t* status_dev;         /* [n] enum sdx_line_status */
+  uint8_t* slot_dev;           /* [3 * offsets[n] + 16] per-line slots: line i owns [3*offsets[i], 3*offsets[i+1]) */
+  int64_t* doff_dev;           /* [n] start of the D (MU/MS) or hex (MC) characters in slot_dev */
+  int32_t* dlen_dev;           /* [n] their length */
+  uint8_t* npat_dev;           /* [n]   MU/MS: patterns (see sdx_pulse_batch) */
+  uint8_t* pat_id_dev;         /* [n*10] */
+  double* pat_val_dev;         /* [n*10] */
+  int8_t* cp_slot_dev;         /* [n]   MS */
+  uint8_t* ms_ok_dev;          /* [n]   MS */
+  int32_t* clock_dev;          /* [n]   MC: int(C) */
+  int32_t* mcbitnum_dev;       /* [n]   MC: int(L) */
+  uint8_t* mcflags_dev;        /* [n]   MC: sdx_mc_batch flags (MCParser: type "MC", no version) */
+  uint8_t* meta_dev;           /* [n*32] raw R (bytes 0-14, length at 15, 255 = absent) and F (16-30,
+                                * length at 31) strings, for meta.rssi / frame.rssi / frame.freq_afc */
+} sdx_lines_out;
+
+/* parse a batch of lines into out (device buffers, caller-owned; no allocation, no sync).  Lines
+ * longer than the kernels' contract (SDX_LONG_MAX pulses, SDX_MC_HEX_MAX hex characters) are
+ * reported SDX_LS_UNSUPPORTED. */
+int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out, void* hip_stream);
+
+#define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */
+#define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */
+#define SDX_MC_HEX_MAX 128  /* sdx_demod_mc */
+enum sdx_sel_class { SDX_SEL_MU_SHORT = 0, SDX_SEL_MU_LONG = 1, SDX_SEL_MS_SHORT = 2, SDX_SEL_MS_LONG = 3,
+                     SDX_SEL_MC = 4, SDX_SEL_NCLASS = 5 };
+#define SDX_SEL_CHUNK 1024  /* lines per selection workgroup */
+/* Selection lists for the demodulation launches, built on the device in line order: the OK lines
+ * of each class (MS lines whose string gates failed are left out -- they have no results).  Class
+ * k's line indices are sel_dev[start_k, start_k + counts[k]) with start_k = counts[0] + ... +
+ * counts[k-1]; counts_dev[0..4] receives the class sizes (the only value a host needs back, to size
+ * the launches).  scratch_dev: 8 * ceil(n / SDX_SEL_CHUNK) int32.  Pass each list as sel_dev of an
+ * sdx_pulse_batch / sdx_mc_batch whose arrays are the sdx_lines_out arrays (offsets = doff_dev,
+ * len = dlen_dev, data = slot_dev). */
+int sdx_select_lines(const sdx_lines_out* out, int32_t n, int32_t* sel_dev, int32_t* counts_dev,
+                     int32_t* scratch_dev, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -7,7 +7,8 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "sdx_kernels.hip")
+SRCS = [os.path.join(HERE, "csrc", "sdx_kernels.hip"),   # demodulation kernels + bank + C-ABI
+        os.path.join(HERE, "csrc", "sdx_lines.hip")]     # wire-line front end (sdx_parse_lines/select)
 OUT = os.path.join(HERE, "_lib", "libsdx.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
@@ -15,12 +16,12 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
 
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    deps = [SRC, os.path.join(HERE, "csrc", "sdx_device.h"),
+    deps = [*SRCS, os.path.join(HERE, "csrc", "sdx_device.h"), os.path.join(HERE, "csrc", "sdx_lane.h"),
             os.path.join(os.path.dirname(HERE), "include", "sdx.h"),
             os.path.join(os.path.dirname(HERE), "include", "sdx_bank.h")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = [HIPCC, *FLAGS, SRC, "-o", OUT + ".tmp"]
+    cmd = [HIPCC, *FLAGS, *SRCS, "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -1328,7 +1328,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   for (int mi = wave; mi < nvalid; mi += NWAVE) {
     const int msg = msg_of[mi];
     const int64_t off = b.offsets_dev[msg];
-    int n = (int)(b.offsets_dev[msg + 1] - off);
+    int n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
     if (n > 64 * NW) n = 64 * NW;  // host routes longer messages to the long variant
     bool nondigit = false;
     for (int w = 0; w < NW; ++w) {
@@ -2035,7 +2035,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   int clock = 0, mcbit = 0, flags = 0;
   if (valid) {
     const int64_t off = b.offsets_dev[msg];
-    const int hl = (int)(b.offsets_dev[msg + 1] - off);
+    const int hl = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
     clock = b.clock_dev[msg];
     mcbit = b.mcbitnum_dev[msg];
     flags = b.flags_dev[msg];
@@ -2188,6 +2188,10 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+namespace sdx {
+// the error text of sdx_last_error() for the other translation units (sdx_lines.hip)
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace sdx
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
     hipError_t e_ = (x);                                                                 \

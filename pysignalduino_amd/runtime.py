@@ -32,18 +32,20 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
                    ("msg", "<u4")])
 
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
-            "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc"]
+            "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_parse_lines",
+            "sdx_select_lines"]
 
 
 class SdxPulseBatch(Structure):
     _fields_ = [("data_dev", c_void_p), ("offsets_dev", c_void_p), ("npat_dev", c_void_p),
                 ("pat_id_dev", c_void_p), ("pat_val_dev", c_void_p), ("cp_slot_dev", c_void_p),
-                ("ms_ok_dev", c_void_p), ("sel_dev", c_void_p), ("n", c_int32), ("n_sel", c_int32)]
+                ("ms_ok_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p), ("n", c_int32),
+                ("n_sel", c_int32)]
 
 
 class SdxMcBatch(Structure):
     _fields_ = [("hex_dev", c_void_p), ("offsets_dev", c_void_p), ("clock_dev", c_void_p),
-                ("mcbitnum_dev", c_void_p), ("flags_dev", c_void_p), ("sel_dev", c_void_p),
+                ("mcbitnum_dev", c_void_p), ("flags_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p),
                 ("n", c_int32), ("n_sel", c_int32)]
 
 
@@ -51,6 +53,22 @@ class SdxOut(Structure):
     _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("cursor_dev", c_void_p),
                 ("rec_cap", c_uint32), ("heap_cap", c_uint32)]
 
+
+class SdxLines(Structure):
+    _fields_ = [("bytes_dev", c_void_p), ("offsets_dev", c_void_p), ("n", c_int32)]
+
+
+class SdxLinesOut(Structure):
+    _fields_ = [(f, c_void_p) for f in ("kind_dev", "status_dev", "slot_dev", "doff_dev", "dlen_dev", "npat_dev",
+                                         "pat_id_dev", "pat_val_dev", "cp_slot_dev", "ms_ok_dev", "clock_dev",
+                                         "mcbitnum_dev", "mcflags_dev", "meta_dev")]
+
+
+# include/sdx.h front-end constants
+LINE_NONE, LINE_MU, LINE_MS, LINE_MC, LINE_MN = 0, 1, 2, 3, 4
+LS_OK, LS_NOFRAME, LS_NOPARSER, LS_INVALID, LS_NODATA, LS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+SEL_MU_SHORT, SEL_MU_LONG, SEL_MS_SHORT, SEL_MS_LONG, SEL_MC, SEL_NCLASS = 0, 1, 2, 3, 4, 5
+SEL_CHUNK = 1024
 
 _LIB = None
 
@@ -84,7 +102,11 @@ def load_library(path: Optional[str] = None):
         f.restype = c_int
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mc.restype = c_int
-    if lib.sdx_abi_version() != 1:
+    lib.sdx_parse_lines.argtypes = [POINTER(SdxLines), POINTER(SdxLinesOut), c_void_p]
+    lib.sdx_parse_lines.restype = c_int
+    lib.sdx_select_lines.argtypes = [POINTER(SdxLinesOut), c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.sdx_select_lines.restype = c_int
+    if lib.sdx_abi_version() != 2:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -194,7 +216,8 @@ class Engine:
     # -- launches -------------------------------------------------------------------------------
     def launch_pulses(self, kind: int, bd, out, sel=None, long_variant: bool = False) -> None:
         b = SdxPulseBatch(_ptr(bd["data"]), _ptr(bd["offsets"]), _ptr(bd["npat"]), _ptr(bd["pat_id"]),
-                          _ptr(bd["pat_val"]), _ptr(bd["cp_slot"]), _ptr(bd["ms_ok"]), _ptr(sel), bd["n"],
+                          _ptr(bd["pat_val"]), _ptr(bd["cp_slot"]), _ptr(bd["ms_ok"]), _ptr(bd.get("len")),
+                          _ptr(sel), bd["n"],
                           0 if sel is None else int(sel.numel()))
         o = self._out_struct(out)
         fn = self.lib.sdx_demod_pulses_long if long_variant else self.lib.sdx_demod_pulses
@@ -202,7 +225,8 @@ class Engine:
 
     def launch_mc(self, bd, out, sel=None) -> None:
         b = SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
-                       _ptr(bd["flags"]), _ptr(sel), bd["n"], 0 if sel is None else int(sel.numel()))
+                       _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"],
+                       0 if sel is None else int(sel.numel()))
         o = self._out_struct(out)
         _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 
