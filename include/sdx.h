@@ -134,8 +134,10 @@ enum sdx_line_status {
   SDX_LS_NOPARSER = 2,    /* no parser for the message type: ignored */
   SDX_LS_INVALID = 3,     /* the parser rejects the line (MU regex, MC header, MC hex, R/F): ignored */
   SDX_LS_NODATA = 4,      /* no D field: ignored */
-  SDX_LS_UNSUPPORTED = 5  /* outside the device contract (e.g. multi-digit P ids, non-integer P# values,
+  SDX_LS_UNSUPPORTED = 5, /* outside the device contract (e.g. multi-digit P ids, non-integer P# values,
                            * bytes >= 0x80 after decompression, MN): the caller must not guess */
+  SDX_LS_RAISES = 6       /* handed to the demodulator, which raises (caught by the parser): no results
+                           * (MC: int(C) / int(L) of a hex-lettered value) */
 };
 
 typedef struct {
@@ -158,8 +160,11 @@ typedef struct {
   int32_t* clock_dev;          /* [n]   MC: int(C) */
   int32_t* mcbitnum_dev;       /* [n]   MC: int(L) */
   uint8_t* mcflags_dev;        /* [n]   MC: sdx_mc_batch flags (MCParser: type "MC", no version) */
-  uint8_t* meta_dev;           /* [n*32] raw R (bytes 0-14, length at 15, 255 = absent) and F (16-30,
-                                * length at 31) strings, for meta.rssi / frame.rssi / frame.freq_afc */
+  uint8_t* meta_dev;           /* [n*32] raw R (bytes 0-14, length at 15, 255 = absent; longer
+                                * values make the line SDX_LS_UNSUPPORTED) and
+                                * F (16-30, length at 31) strings, for meta.rssi / frame.rssi / frame.freq_afc */
+  int32_t* plen_dev;           /* [n] decompressed lines: payload length at slot_dev + 3*offsets[i] (RawFrame.line);
+                                * -1 = not decompressed (the payload is the stripped line between STX and ETX) */
 } sdx_lines_out;
 
 /* parse a batch of lines into out (device buffers, caller-owned; no allocation, no sync).  Lines

@@ -297,8 +297,8 @@ LD void put_meta(uint8_t* m, const Str& P, Field f) {
     return;
   }
   const int n = f.e - f.s;
-  m[15] = (uint8_t)(n > 15 ? 254 : n);  // 254: longer than the slot (value not kept)
-  for (int i = 0; i < 15 && i < n; ++i) m[i] = P.p[f.s + i];
+  m[15] = (uint8_t)n;  // <= 15 (longer values are SDX_LS_UNSUPPORTED)
+  for (int i = 0; i < n; ++i) m[i] = P.p[f.s + i];
 }
 
 __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out out) {
@@ -322,6 +322,7 @@ __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out
   uint8_t* meta = out.meta_dev + 32 * (int64_t)i;
   meta[15] = 255;
   meta[31] = 255;
+  out.plen_dev[i] = -1;
   auto done = [&]() {
     out.kind_dev[i] = kind;
     out.status_dev[i] = status;
@@ -360,6 +361,7 @@ __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out
       return;
     }
     P = Str{slot, w.n};
+    out.plen_dev[i] = w.n;
   }
   // ---- routing: payload[:2].upper()
   const uint8_t c0 = P.n > 0 ? up(P.p[0]) : 0, c1 = P.n > 1 ? up(P.p[1]) : 0;
@@ -469,7 +471,7 @@ __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out
     long long cv = 0, lv = 0;
     const int rc = parse_dec(P, fC.s, fC.e, &cv), rl = parse_dec(P, fL.s, fL.e, &lv);
     if (rc == 2 || rl == 2) {  // int(C) / int(L) raise inside demodulate_mc -> caught, nothing decoded
-      status = SDX_LS_INVALID;
+      status = SDX_LS_RAISES;
       done();
       return;
     }
@@ -575,6 +577,11 @@ __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out
       ms_ok = slotv >= 0;
     }
     out.ms_ok_dev[i] = ms_ok ? 1 : 0;
+  }
+  if ((fR.s >= 0 && fR.e - fR.s > 15) || (fF.s >= 0 && fF.e - fF.s > 15)) {  // meta_dev holds 15 bytes
+    status = SDX_LS_UNSUPPORTED;
+    done();
+    return;
   }
   // ---- the D (MU/MS) or hex (MC) characters: already in the slot when decompressed, else copied
   const int dn = fD.e - fD.s;
@@ -726,7 +733,7 @@ extern "C" int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out,
   if (!lines->bytes_dev || !lines->offsets_dev || !out->kind_dev || !out->status_dev || !out->slot_dev ||
       !out->doff_dev || !out->dlen_dev || !out->npat_dev || !out->pat_id_dev || !out->pat_val_dev ||
       !out->cp_slot_dev || !out->ms_ok_dev || !out->clock_dev || !out->mcbitnum_dev || !out->mcflags_dev ||
-      !out->meta_dev)
+      !out->meta_dev || !out->plen_dev)
     return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: null buffer");
   const int grid = (lines->n + 255) / 256;
   hipLaunchKernelGGL(sdxl::k_parse_lines, dim3(grid), dim3(256), 0, (hipStream_t)hip_stream, *lines, *out);

@@ -1,0 +1,278 @@
+"""Wire-line front end: raw SIGNALduino firmware lines -> DecodedMessage, on the GPU.
+
+Mirrors the reference's parser entry point, ``signalduino.parser.SignalParser``
+(signalduino/parser/__init__.py:18-77), and its data types ``RawFrame`` / ``DecodedMessage``
+(signalduino/types.py:13-32).  Per line the reference runs, in Python: strip + STX/ETX framing,
+Mred=1 decompression, routing by message type, the MU validity regex, ``_parse_to_dict``, the MC
+header checks, then ``SDProtocols.demodulate*``.  Here a batch of lines is uploaded once and
+  1. ``sdx_parse_lines``   (csrc/sdx_lines.hip) does all of the parsing, one lane per line, writing
+                           the demodulators' SoA batch in place (slot layout, ``len_dev``),
+  2. ``sdx_select_lines``  builds the per-kind selection lists (MU/MS short or long, MC) on the device,
+  3. the MU / MS (and, in mc_mode='fixed', MC) demodulation kernels run over those lists,
+and only the result records come back.  The host side assembles the Python objects.
+
+Observable behaviour per line is the reference's: ``parse_line`` returns the same
+``DecodedMessage`` list (protocol_id, payload, metadata, raw.line / message_type / rssi /
+freq_afc), and lines the reference ignores give ``[]`` (a demodulator exception is caught and
+logged by the reference's parsers, so it also gives ``[]``).  Lines outside the device contract
+(MN lines, multi-digit pattern ids, non-integer pattern values, non-ASCII characters after
+decompression, over-long messages) are never approximated: ``parse_line`` raises
+:class:`ContractError` and ``parse_lines`` returns the exception in that line's slot.
+There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from datetime import datetime
+from typing import Any, List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import runtime
+from .packing import ContractError
+from .sd_protocols import SDProtocols
+
+_KIND_NAME = {runtime.LINE_MU: "MU", runtime.LINE_MS: "MS", runtime.LINE_MC: "MC", runtime.LINE_MN: "MN"}
+
+
+@dataclass(slots=True)
+class RawFrame:
+    """signalduino/types.py:13-21."""
+
+    line: str
+    timestamp: datetime = field(default_factory=datetime.utcnow)
+    rssi: Optional[float] = None
+    freq_afc: Optional[float] = None
+    message_type: Optional[str] = None
+
+
+@dataclass(slots=True)
+class DecodedMessage:
+    """signalduino/types.py:24-31."""
+
+    protocol_id: str
+    payload: str
+    raw: RawFrame
+    metadata: dict = field(default_factory=dict)
+
+
+def calc_rssi(raw_rssi: int) -> float:
+    """parser/base.py calc_rssi."""
+    if raw_rssi >= 128:
+        return ((raw_rssi - 256) / 2) - 74
+    return (raw_rssi / 2) - 74
+
+
+def calc_afc(raw_afc: int) -> float:
+    """parser/base.py calc_afc."""
+    if raw_afc >= 128:
+        return (raw_afc - 256) / 2
+    return raw_afc / 2
+
+
+def _to_bytes(line: Union[str, bytes]) -> bytes:
+    if isinstance(line, (bytes, bytearray, memoryview)):
+        return bytes(line)
+    try:
+        return line.encode("latin-1")  # the transport's decoding (transport.py:123), inverted
+    except UnicodeEncodeError as e:
+        raise ContractError("characters above U+00FF cannot come from the firmware transport") from e
+
+
+class LineBatch:
+    """Device buffers of one parsed batch (sdx_lines / sdx_lines_out of include/sdx.h)."""
+
+    def __init__(self, eng: "runtime.Engine", data: np.ndarray, offsets: np.ndarray):
+        t = eng.torch
+        d = eng.dev
+        n = len(offsets) - 1
+        total = int(offsets[-1])
+        self.n = n
+        self.eng = eng
+        self.bytes = t.from_numpy(data if len(data) else np.zeros(1, np.uint8)).to(d)
+        self.offsets = t.from_numpy(offsets).to(d)
+        e = lambda k, dt: t.empty(max(k, 1), dtype=dt, device=d)  # noqa: E731
+        self.kind, self.status = e(n, t.uint8), e(n, t.uint8)
+        self.slot = t.empty(3 * total + 16, dtype=t.uint8, device=d)
+        self.doff, self.dlen = e(n, t.int64), e(n, t.int32)
+        self.npat, self.pat_id, self.pat_val = e(n, t.uint8), e(10 * n, t.uint8), e(10 * n, t.float64)
+        self.cp_slot, self.ms_ok = e(n, t.int8), e(n, t.uint8)
+        self.clock, self.mcbitnum, self.mcflags = e(n, t.int32), e(n, t.int32), e(n, t.uint8)
+        self.meta, self.plen = e(32 * n, t.uint8), e(n, t.int32)
+        self.sel = e(n, t.int32)
+        self.counts = t.zeros(8, dtype=t.int32, device=d)
+        self.scratch = e(8 * ((n + runtime.SEL_CHUNK - 1) // runtime.SEL_CHUNK), t.int32)
+        p = runtime._ptr
+        self.c_lines = runtime.SdxLines(p(self.bytes), p(self.offsets), n)
+        self.c_out = runtime.SdxLinesOut(p(self.kind), p(self.status), p(self.slot), p(self.doff), p(self.dlen),
+                                         p(self.npat), p(self.pat_id), p(self.pat_val), p(self.cp_slot),
+                                         p(self.ms_ok), p(self.clock), p(self.mcbitnum), p(self.mcflags),
+                                         p(self.meta), p(self.plen))
+
+    def launch(self) -> None:
+        """sdx_parse_lines + sdx_select_lines on the engine's current stream (no host sync)."""
+        import ctypes
+        lib, st = self.eng.lib, self.eng.stream_ptr()
+        runtime._check(lib, lib.sdx_parse_lines(ctypes.byref(self.c_lines), ctypes.byref(self.c_out), st))
+        runtime._check(lib, lib.sdx_select_lines(ctypes.byref(self.c_out), self.n, runtime._ptr(self.sel),
+                                                 runtime._ptr(self.counts), runtime._ptr(self.scratch), st))
+
+    def selections(self):
+        """Class sizes (one 32-byte read-back) -> device sub-lists of sel per class."""
+        cnt = self.counts.cpu().numpy()[: runtime.SEL_NCLASS]
+        start = np.concatenate([[0], np.cumsum(cnt)])
+        return [self.sel[int(start[k]): int(start[k + 1])] for k in range(runtime.SEL_NCLASS)], cnt
+
+    def pulse_batch(self):
+        return {"data": self.slot, "offsets": self.doff, "npat": self.npat, "pat_id": self.pat_id,
+                "pat_val": self.pat_val, "cp_slot": self.cp_slot, "ms_ok": self.ms_ok, "len": self.dlen, "n": self.n}
+
+    def mc_batch(self):
+        return {"hex": self.slot, "offsets": self.doff, "clock": self.clock, "mcbitnum": self.mcbitnum,
+                "flags": self.mcflags, "len": self.dlen, "n": self.n}
+
+
+def pack_lines(lines: Sequence[Union[str, bytes]]):
+    """Concatenate lines into (data uint8, offsets int64[n+1]); per-line ContractError where a line
+    cannot be represented (returned in ``bad``; such lines are replaced by an empty line)."""
+    bs, bad = [], {}
+    for i, ln in enumerate(lines):
+        try:
+            bs.append(_to_bytes(ln))
+        except ContractError as e:
+            bad[i] = e
+            bs.append(b"")
+    lens = np.fromiter((len(b) for b in bs), np.int64, len(bs))
+    offsets = np.zeros(len(bs) + 1, np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    data = np.frombuffer(b"".join(bs), np.uint8).copy()
+    return data, offsets, bad
+
+
+class SignalParser:
+    """signalduino/parser/__init__.py:18-77 with the whole line -> DecodedMessage path on the GPU."""
+
+    def __init__(self, protocols: Optional[SDProtocols] = None, logger: Optional[logging.Logger] = None,
+                 rfmode: Optional[str] = None):
+        self.protocols = protocols or SDProtocols()
+        self.logger = logger or logging.getLogger(__name__)
+        self.protocols.register_log_callback(self._log_adapter)
+        self.rfmode = rfmode
+
+    def _log_adapter(self, message: str, level: int):
+        if level <= 1:
+            self.logger.error(message)
+        elif level == 2:
+            self.logger.warning(message)
+        elif level == 3:
+            self.logger.info(message)
+        else:
+            self.logger.debug(message)
+
+    # ------------------------------------------------------------------------------------------
+    def parse_line(self, line: Union[str, bytes]) -> List[DecodedMessage]:
+        """SignalParser.parse_line (parser/__init__.py:37-49)."""
+        out = self.parse_lines([line])[0]
+        if isinstance(out, BaseException):
+            raise out
+        return out
+
+    def parse_lines(self, lines: Sequence[Union[str, bytes]]) -> List[Union[List[DecodedMessage], Exception]]:
+        """Batch form of parse_line: one upload, one parse launch, one launch per demodulation
+        variant, one read-back.  Returns one DecodedMessage list per line (or the ContractError
+        for a line outside the device contract)."""
+        n = len(lines)
+        if n == 0:
+            return []
+        data, offsets, bad = pack_lines(lines)
+        eng = self.protocols._ensure()
+        bk = self.protocols._bank
+        lb = LineBatch(eng, data, offsets)
+        lb.launch()
+        sels, cnt = lb.selections()
+        res = {}
+        pb = lb.pulse_batch()
+        if cnt[runtime.SEL_MU_SHORT] or cnt[runtime.SEL_MU_LONG]:
+            res["MU"] = eng.run(runtime.KIND_MU, pb, sel_short=sels[runtime.SEL_MU_SHORT],
+                                sel_long=sels[runtime.SEL_MU_LONG])
+        if cnt[runtime.SEL_MS_SHORT] or cnt[runtime.SEL_MS_LONG]:
+            res["MS"] = eng.run(runtime.KIND_MS, pb, sel_short=sels[runtime.SEL_MS_SHORT],
+                                sel_long=sels[runtime.SEL_MS_LONG])
+        if self.protocols.mc_mode == "fixed" and cnt[runtime.SEL_MC]:
+            res["MC"] = eng.run(runtime.KIND_MC, lb.mc_batch(), sel_short=sels[runtime.SEL_MC])
+        # read-back of the per-line fields the Python objects need
+        kind = lb.kind[:n].cpu().numpy()
+        status = lb.status[:n].cpu().numpy()
+        plen = lb.plen[:n].cpu().numpy()
+        meta = lb.meta[: 32 * n].cpu().numpy().reshape(n, 32)
+        need_slot = plen >= 0
+        slot = lb.slot.cpu().numpy() if need_slot.any() else None
+        ms_clock = None
+        if "MS" in res:
+            pv = lb.pat_val[: 10 * n].cpu().numpy().reshape(n, 10)
+            cps = lb.cp_slot[:n].cpu().numpy().astype(np.int64)
+            ms_clock = np.abs(pv[np.arange(n), np.maximum(cps, 0)])
+        hb = {k: v[2].tobytes() for k, v in res.items()}
+        out: List[Any] = []
+        for i in range(n):
+            if i in bad:
+                out.append(bad[i])
+                continue
+            st = int(status[i])
+            if st == runtime.LS_UNSUPPORTED:
+                out.append(ContractError(f"line {i} is outside the device contract of the front end "
+                                         f"(kind {_KIND_NAME.get(int(kind[i]), '?')})"))
+                continue
+            name = _KIND_NAME.get(int(kind[i]))
+            if st != runtime.LS_OK or name not in res:
+                out.append([])
+                continue
+            desc, rec, _ = res[name]
+            d = desc[i]
+            if d["status"] == runtime.ST_RAISED or int(d["n_rec"]) == 0:
+                out.append([])  # a demodulator exception is caught by the reference's parsers
+                continue
+            if d["status"] != runtime.ST_OK:
+                raise RuntimeError(f"device status {int(d['status'])} for line {i}")
+            fr = self._frame(lines[i], i, plen, offsets, slot, meta, name)
+            rssi_raw = self._meta_str(meta[i], 0)
+            msgs = []
+            for r in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
+                p = int(r["proto"])
+                off = int(r["payload_off"])
+                payload = hb[name][off: off + int(r["payload_len"])].decode("latin-1")
+                if name == "MC":
+                    pid = bk.mc_pids[p]
+                    md = {"protocol_id": pid, "rssi": None, "freq_afc": None}
+                else:
+                    pid = bk.mu_pids[p] if name == "MU" else bk.ms_pids[p]
+                    clock = bk.mu_clock[p] if name == "MU" else float(ms_clock[i])
+                    md = {"bit_length": int(r["bit_length"]), "rssi": rssi_raw, "clock": clock}
+                msgs.append(DecodedMessage(protocol_id=str(pid), payload=payload, raw=fr, metadata=md))
+            out.append(msgs)
+        return out
+
+    @staticmethod
+    def _meta_str(m: np.ndarray, base: int) -> Optional[str]:
+        ln = int(m[base + 15])
+        return None if ln == 255 else bytes(m[base: base + ln]).decode("latin-1")
+
+    def _frame(self, line, i, plen, offsets, slot, meta, name) -> RawFrame:
+        """RawFrame(line=payload, message_type) + _extract_metadata (mu.py:96-108, mc.py:141-155)."""
+        if plen[i] >= 0:
+            s0 = 3 * int(offsets[i])
+            payload = bytes(slot[s0: s0 + int(plen[i])]).decode("latin-1")
+        else:
+            s = line.decode("latin-1") if isinstance(line, (bytes, bytearray, memoryview)) else line
+            payload = s.strip()[1:-1]
+        fr = RawFrame(line=payload, message_type=name)
+        r, f = self._meta_str(meta[i], 0), self._meta_str(meta[i], 16)
+        for raw, attr, fn in ((r, "rssi", calc_rssi), (f, "freq_afc", calc_afc)):
+            if raw is None:
+                continue
+            try:
+                setattr(fr, attr, fn(int(raw)))
+            except ValueError:
+                self.logger.warning("Could not parse %s value: %s", "RSSI" if attr == "rssi" else "AFC", raw)
+        return fr

@@ -61,12 +61,12 @@ class SdxLines(Structure):
 class SdxLinesOut(Structure):
     _fields_ = [(f, c_void_p) for f in ("kind_dev", "status_dev", "slot_dev", "doff_dev", "dlen_dev", "npat_dev",
                                          "pat_id_dev", "pat_val_dev", "cp_slot_dev", "ms_ok_dev", "clock_dev",
-                                         "mcbitnum_dev", "mcflags_dev", "meta_dev")]
+                                         "mcbitnum_dev", "mcflags_dev", "meta_dev", "plen_dev")]
 
 
 # include/sdx.h front-end constants
 LINE_NONE, LINE_MU, LINE_MS, LINE_MC, LINE_MN = 0, 1, 2, 3, 4
-LS_OK, LS_NOFRAME, LS_NOPARSER, LS_INVALID, LS_NODATA, LS_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+LS_OK, LS_NOFRAME, LS_NOPARSER, LS_INVALID, LS_NODATA, LS_UNSUPPORTED, LS_RAISES = 0, 1, 2, 3, 4, 5, 6
 SEL_MU_SHORT, SEL_MU_LONG, SEL_MS_SHORT, SEL_MS_LONG, SEL_MC, SEL_NCLASS = 0, 1, 2, 3, 4, 5
 SEL_CHUNK = 1024
 
@@ -231,21 +231,38 @@ class Engine:
         _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 
     # -- full run with contract routing and overflow re-runs (all on the GPU) --------------------
-    def run(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None):
-        """Demodulate a device batch; returns host numpy (desc, rec, heap)."""
+    def run(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None,
+            sel_short=None, sel_long=None):
+        """Demodulate a device batch; returns host numpy (desc, rec, heap).
+
+        ``sel_short`` / ``sel_long``: device int32 lists of the messages to run with the short /
+        long variant (MC: ``sel_short`` only), as sdx_select_lines builds them; the other
+        messages keep an empty OK descriptor.  Without them every message runs, routed by length.
+        """
         t = self.torch
         n = bd["n"]
-        lengths = bd["lengths"]
-        if kind == KIND_MC:
-            if n and int(lengths.max(initial=0)) > MC_HEX_MAX:
-                raise NotImplementedError(f"MC frames longer than {MC_HEX_MAX} hex characters are outside "
-                                          "the device contract")
-        elif n and int(lengths.max(initial=0)) > LONG_MAX:
-            raise NotImplementedError(f"messages longer than {LONG_MAX} pulses are outside the device contract")
-        rec_cap = rec_cap or (8 * n + 1024)
-        heap_cap = heap_cap or (200 * n + 65536)
+        selected = sel_short is not None or sel_long is not None
+        if selected:
+            n_work = sum(int(s.numel()) for s in (sel_short, sel_long) if s is not None)
+        else:
+            n_work = n
+            lengths = bd["lengths"]
+            if kind == KIND_MC:
+                if n and int(lengths.max(initial=0)) > MC_HEX_MAX:
+                    raise NotImplementedError(f"MC frames longer than {MC_HEX_MAX} hex characters are outside "
+                                              "the device contract")
+            elif n and int(lengths.max(initial=0)) > LONG_MAX:
+                raise NotImplementedError(f"messages longer than {LONG_MAX} pulses are outside the device contract")
+        rec_cap = rec_cap or (8 * n_work + 1024)
+        heap_cap = heap_cap or (200 * n_work + 65536)
         out = self.alloc_out(n, rec_cap, heap_cap)
-        if kind == KIND_MC:
+        if selected:
+            if sel_short is not None and sel_short.numel():
+                (self.launch_mc(bd, out, sel=sel_short) if kind == KIND_MC else
+                 self.launch_pulses(kind, bd, out, sel=sel_short))
+            if sel_long is not None and sel_long.numel():
+                self.launch_pulses(kind, bd, out, sel=sel_long, long_variant=True)
+        elif kind == KIND_MC:
             self.launch_mc(bd, out)
         else:
             short = lengths <= SHORT_MAX

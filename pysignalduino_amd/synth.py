@@ -296,3 +296,165 @@ def mc_corpus(protocols: Dict[str, dict], n: int, seed: int = 44) -> McBatch:
     mtype = (rng.random(n) < 0.5).astype(np.uint8)
     v32 = (rng.random(n) < 0.1).astype(np.uint8)
     return McBatch(hexdata.copy(), offsets, clock, L, mtype, v32, choice.astype(np.int32))
+
+
+# ---------------------------------------------------------------------------------------------
+# Firmware lines: the wire format the front end (sdx_parse_lines) consumes.
+# A line is bytes: STX + payload + ETX (+ "\n"), latin-1 as the transport decodes it
+# (signalduino/transport.py:123).  Compressed lines use the firmware's Mred=1 encoding, i.e. the
+# inverse of the decompression the reference runs (signalduino/parser/base.py:13-186).
+STX, ETX = b"\x02", b"\x03"
+
+
+def _pint(v: float) -> str:
+    return str(int(v)) if float(v).is_integer() else repr(float(v))
+
+
+def _line_fields(pb: PulseBatch, i: int):
+    """(ids, vals, data, cp, sp) of message i with the pattern ids moved into 0..7 as the firmware
+    numbers them (ids and data digits renamed consistently; unchanged when more than 8 patterns)."""
+    n = int(pb.npat[i])
+    ids = [chr(pb.pat_id[i, k]) for k in range(n)]
+    vals = [float(pb.pat_val[i, k]) for k in range(n)]
+    msg = pb.message(i)
+    if pb.kind == "MS":
+        cp = ids[pb.cp_slot[i]] if pb.cp_slot[i] >= 0 else "9"
+        sp = ids[pb.sp_slot[i]] if pb.sp_slot[i] >= 0 else "9"
+    else:
+        cp, sp = (ids[0] if ids else "0"), None
+    if n <= 8 and any(c > "7" for c in ids):
+        free = [c for c in "01234567" if c not in ids]
+        ren = {}
+        for c in ids:
+            ren[c] = c if c <= "7" else free.pop(0)
+        ids = [ren[c] for c in ids]
+        msg = msg.translate(str.maketrans(ren))
+        cp = ren.get(cp, cp)
+        sp = ren.get(sp, sp) if sp is not None else None
+    return ids, vals, msg, cp, sp
+
+
+def pulse_payload(pb: PulseBatch, i: int) -> bytes:
+    """Uncompressed payload "MU;P0=..;D=..;CP=..;R=..;" (MS adds SP) in firmware field order."""
+    ids, vals, msg, cp, sp = _line_fields(pb, i)
+    parts = [pb.kind] + ["P%s=%s" % (c, _pint(v)) for c, v in zip(ids, vals)] + ["D=" + msg, "CP=" + cp]
+    if pb.kind == "MS":
+        parts.append("SP=" + sp)
+    if pb.rssi[i] >= 0:
+        parts.append("R=%d" % int(pb.rssi[i]))
+    return (";".join(parts) + ";").encode("latin-1")
+
+
+def compress_pulse_payload(pb: PulseBatch, i: int) -> Optional[bytes]:
+    """Mred=1 form of pulse_payload (None when the message is not representable: pattern values
+    that are not integers of magnitude <= 32767, ids > 7, or data digits > 7)."""
+    ids, vals, msg, cp, sp = _line_fields(pb, i)
+    if any(c > "7" for c in msg) or any(c > "7" for c in ids) or not msg:
+        return None
+    out = bytearray(("M" + pb.kind[1].lower() + ";").encode())
+    for pid, v in zip(ids, vals):
+        if not v.is_integer() or abs(v) > 32767:
+            return None
+        a = int(abs(v))
+        lo, hi = a & 0xFF, a >> 8
+        out += bytes([0x80 | int(pid) | (0x20 if v < 0 else 0) | (0x10 if lo >= 128 else 0),
+                      0x80 | (lo & 0x7F), 0x80 | hi]) + b";"
+    odd = len(msg) % 2
+    out += b"d" if odd else b"D"
+    digits = [int(c) for c in msg] + ([0] if odd else [])
+    out += bytes((digits[j] << 4) | digits[j + 1] for j in range(0, len(digits), 2)) + b";"
+    out += b"C" + cp.encode() + b";"
+    if pb.kind == "MS":
+        out += b"S" + sp.encode() + b";"
+    if 0 <= pb.rssi[i] <= 255:
+        out += b"R" + ("%X" % int(pb.rssi[i])).encode() + b";"
+    return bytes(out)
+
+
+def mc_payload(mb: McBatch, i: int, rssi: Optional[int] = None) -> bytes:
+    c = int(mb.clock[i])
+    s = "MC;LL=%d;LH=%d;SL=%d;SH=%d;D=%s;C=%d;L=%d;" % (-2 * c, 2 * c, -c, c, mb.hex(i), c, int(mb.mcbitnum[i]))
+    if rssi is not None:
+        s += "R=%d;" % rssi
+    return s.encode("latin-1")
+
+
+def frame(payload: bytes, newline: bool = True) -> bytes:
+    return STX + payload + ETX + (b"\n" if newline else b"")
+
+
+def line_corpus(protocols: Dict[str, dict], n: int, seed: int = 45, mix=(0.4, 0.4, 0.2),
+                compress_frac: float = 0.3, mu_npulse: int = 256):
+    """Config 5 (§8(f) 1): n framed firmware lines, MU/MS/MC in proportion ``mix``, a fraction
+    of the MU/MS lines Mred=1-compressed.  Returns (lines: List[bytes], kinds: np.ndarray)."""
+    rng = np.random.default_rng(seed)
+    kinds = rng.choice(3, size=n, p=np.asarray(mix, np.float64) / np.sum(mix))
+    cnt = [int((kinds == k).sum()) for k in range(3)]
+    mu = mu_corpus(protocols, max(cnt[0], 1), seed=seed + 1, npulse=mu_npulse)
+    ms = ms_corpus(protocols, max(cnt[1], 1), seed=seed + 2)
+    mc = mc_corpus(protocols, max(cnt[2], 1), seed=seed + 3)
+    comp = rng.random(n) < compress_frac
+    rssi = rng.integers(0, 256, size=n)
+    lines: List[bytes] = []
+    pos = [0, 0, 0]
+    for j in range(n):
+        k = int(kinds[j])
+        i = pos[k]
+        pos[k] += 1
+        if k == 2:
+            lines.append(frame(mc_payload(mc, i, int(rssi[j]))))
+            continue
+        pb = mu if k == 0 else ms
+        p = compress_pulse_payload(pb, i) if comp[j] else None
+        lines.append(frame(p if p is not None else pulse_payload(pb, i)))
+    return lines, kinds
+
+
+_JUNK = b";=;=-+0123456789ABCDEFabcdefPDCSRLMFOpewmu \t\r\n\x02\x03\x80\x91\xa0\xb5\xc3\xdf\xff"
+
+
+def mutate_line(rng: np.random.Generator, line: bytes) -> bytes:
+    """One seeded corruption of a firmware line (the fuzz cases of the front-end parity tests)."""
+    b = bytearray(line)
+    op = int(rng.integers(0, 14))
+    if not b:
+        return bytes(_JUNK[int(rng.integers(0, len(_JUNK)))] for _ in range(int(rng.integers(1, 8))))
+    j = int(rng.integers(0, len(b)))
+    if op == 0:                       # drop a byte
+        del b[j]
+    elif op == 1:                     # insert a byte
+        b.insert(j, _JUNK[int(rng.integers(0, len(_JUNK)))])
+    elif op == 2:                     # overwrite a byte
+        b[j] = _JUNK[int(rng.integers(0, len(_JUNK)))]
+    elif op == 3:                     # swap the case of the type character
+        k = b.find(b"M")
+        if 0 <= k + 1 < len(b):
+            b[k + 1] ^= 0x20
+    elif op == 4:                     # lose the framing
+        b = b.replace(STX, b"", 1) if rng.random() < 0.5 else b.replace(ETX, b"", 1)
+    elif op == 5:                     # whitespace around the frame
+        b = bytearray(b" \t"[: int(rng.integers(0, 3))] + bytes(b) + b"\r\n \x0b"[: int(rng.integers(0, 4))])
+    parts = bytes(b).split(b";")
+    if op >= 6 and len(parts) > 2:
+        q = int(rng.integers(1, len(parts) - 1))
+        if op == 6:                   # duplicate a field (last value wins)
+            parts.insert(q + int(rng.integers(0, 2)), parts[q])
+        elif op == 7:                 # drop a field
+            del parts[q]
+        elif op == 8:                 # empty the value of a field
+            parts[q] = parts[q].split(b"=")[0] + b"="
+        elif op == 9:                 # swap two fields
+            r = int(rng.integers(1, len(parts) - 1))
+            parts[q], parts[r] = parts[r], parts[q]
+        elif op == 10:                # an extra field the grammars may or may not accept
+            extra = [b"P05=-400", b"P10=300", b"P3=1e3", b"P3=4.5", b"F=12", b"V=1", b"O", b"e", b"p",
+                     b"w=1", b"M=AB", b"MC", b"X=1", b"SP=x", b"CP=", b"R=-5", b"D=", b"P8=200"]
+            parts.insert(q, extra[int(rng.integers(0, len(extra)))])
+        elif op == 11:                # a '=' removed
+            parts[q] = parts[q].replace(b"=", b"", 1)
+        elif op == 12:                # an empty part
+            parts.insert(q, b"")
+        else:                         # lowercase a key
+            parts[q] = parts[q][:1].lower() + parts[q][1:]
+        return b";".join(parts)
+    return bytes(b)

@@ -1,0 +1,258 @@
+"""Wire-line front end: sdx_parse_lines / sdx_select_lines / frontend.SignalParser.
+
+CPU tests pin the oracle (oracle/lines_oracle.py) to what the reference parser did on the same
+lines (tests/golden/lines_golden.json.gz, made by tests/golden/make_lines_golden.py).  GPU tests
+compare the device outputs with the oracle field by field (bit-exact) and the end-to-end
+DecodedMessage lists with the reference's own (the "e2e" records of the goldens)."""
+import numpy as np
+import pytest
+
+from oracle import lines_oracle as LO
+from pysignalduino_amd import bank as B
+from pysignalduino_amd import synth
+
+TYPE = {LO.MU: "MU", LO.MS: "MS", LO.MC: "MC"}
+
+
+def _lines(golden):
+    return [c["line"].encode("latin-1") for c in golden("lines_golden.json.gz")]
+
+
+def test_oracle_char_classes_are_pythons():
+    for c in range(256):
+        ch = chr(c)
+        assert (c in LO._WS) == ch.isspace(), c
+        assert LO._alpha(c) == ch.isalpha(), c
+
+
+def test_oracle_matches_reference_goldens(golden):
+    cases = golden("lines_golden.json.gz")
+    unsupported = 0
+    bad = []
+    for c in cases:
+        assert "raise" not in c
+        r = LO.parse_line(c["line"].encode("latin-1"))
+        if r["status"] == LO.UNSUPPORTED:
+            unsupported += 1
+            continue
+        exp_payload = c["payload"]
+        got_payload = None if r["payload"] is None else r["payload"].decode("latin-1")
+        ok = exp_payload == got_payload
+        if r["status"] in (LO.OK, LO.RAISES):
+            ok = ok and c["calls"] == [[TYPE[r["kind"]], [list(kv) for kv in r["msg"]]]]
+            fr = c["frame"]
+            ok = ok and fr is not None and fr[0] == got_payload and fr[1] == TYPE[r["kind"]] \
+                and fr[2] == r["rssi"] and fr[3] == r["freq_afc"]
+        else:
+            ok = ok and c["calls"] == []
+        if not ok:
+            bad.append((c["src"], c["line"], r["status"], c["calls"][:1], r.get("msg")))
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:3]}"
+    assert unsupported <= 0.05 * len(cases), unsupported
+    # the goldens cover every status the front end reports
+    st = {LO.parse_line(c["line"].encode("latin-1"))["status"] for c in cases}
+    assert st >= {LO.OK, LO.NOFRAME, LO.NOPARSER, LO.INVALID, LO.NODATA, LO.UNSUPPORTED, LO.RAISES}
+
+
+def test_reference_test_vectors_present(golden):
+    """The reference's own parser/decompression test inputs are in the fixture."""
+    srcs = {c["src"].split(":")[0] for c in golden("lines_golden.json.gz")}
+    assert {"test_mu_parser.py", "test_ms_parser.py", "test_mc_parser.py", "test_decompress_payload.py"} <= srcs
+
+
+def test_synth_lines_roundtrip():
+    """Compressed and plain synthetic lines parse back to the generating message (oracle)."""
+    P = B.Bank().protocols
+    lines, kinds = synth.line_corpus(P, 600, seed=7, compress_frac=0.5, mu_npulse=64)
+    ok = {LO.MU: 0, LO.MS: 0, LO.MC: 0}
+    for ln, k in zip(lines, kinds):
+        r = LO.parse_line(ln)
+        assert r["status"] in (LO.OK, LO.INVALID), (ln, r["status"])
+        if r["status"] == LO.OK:
+            ok[r["kind"]] += 1
+            assert r["kind"] == [LO.MU, LO.MS, LO.MC][k]
+    assert ok[LO.MU] > 150 and ok[LO.MS] > 150 and ok[LO.MC] > 80, ok
+
+
+def test_compressed_payload_decompresses_to_the_plain_one():
+    P = B.Bank().protocols
+    pb = synth.ms_corpus(P, 200, seed=3)
+    n = 0
+    for i in range(pb.n):
+        c = synth.compress_pulse_payload(pb, i)
+        if c is None:
+            continue
+        plain = synth.pulse_payload(pb, i)
+        got = dict(LO._kv(LO.decompress(c)))
+        exp = dict(LO._kv(plain))
+        # the firmware's compressed form carries the same fields (type spelled "Ms" -> "MS")
+        assert got == exp, (plain, c)
+        n += 1
+    assert n > 50
+
+
+# ---------------------------------------------------------------------------------- GPU ------
+def _fuzz(lines, n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        m = synth.mutate_line(rng, lines[int(rng.integers(0, len(lines)))])
+        if rng.random() < 0.4:
+            m = synth.mutate_line(rng, m)
+        out.append(m)
+    return out
+
+
+def _device_parse(lines):
+    from pysignalduino_amd import frontend, runtime
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    p = SDProtocols()
+    eng = p._ensure()
+    data, offsets, bad = frontend.pack_lines(lines)
+    assert not bad
+    lb = frontend.LineBatch(eng, data, offsets)
+    lb.launch()
+    sels, cnt = lb.selections()
+    n = len(lines)
+    g = lambda t, k=n: t[:k].cpu().numpy()  # noqa: E731
+    return dict(kind=g(lb.kind), status=g(lb.status), doff=g(lb.doff), dlen=g(lb.dlen), npat=g(lb.npat),
+                pat_id=g(lb.pat_id, 10 * n).reshape(n, 10), pat_val=g(lb.pat_val, 10 * n).reshape(n, 10),
+                cp_slot=g(lb.cp_slot), ms_ok=g(lb.ms_ok), clock=g(lb.clock), mcbitnum=g(lb.mcbitnum),
+                mcflags=g(lb.mcflags), meta=g(lb.meta, 32 * n).reshape(n, 32), plen=g(lb.plen),
+                slot=lb.slot.cpu().numpy(), offsets=offsets,
+                sels=[s.cpu().numpy() for s in sels], counts=cnt, runtime=runtime)
+
+
+def _meta(m, base):
+    ln = int(m[base + 15])
+    return None if ln == 255 else bytes(m[base: base + ln])
+
+
+def _compare(lines, dv):
+    bad = []
+    for i, ln in enumerate(lines):
+        r = LO.parse_line(ln)
+        e = []
+        if int(dv["kind"][i]) != r["kind"] or int(dv["status"][i]) != r["status"]:
+            e.append(("kind/status", int(dv["kind"][i]), int(dv["status"][i]), r["kind"], r["status"]))
+        elif r["status"] == LO.OK:
+            s0 = int(dv["doff"][i])
+            d = bytes(dv["slot"][s0: s0 + int(dv["dlen"][i])])
+            if d != r["data"]:
+                e.append(("data", d[:40], r["data"][:40]))
+            if _meta(dv["meta"][i], 0) != r["R"] or _meta(dv["meta"][i], 16) != r["F"]:
+                e.append(("meta", _meta(dv["meta"][i], 0), r["R"], _meta(dv["meta"][i], 16), r["F"]))
+            if int(dv["plen"][i]) != r["plen"]:
+                e.append(("plen", int(dv["plen"][i]), r["plen"]))
+            elif r["plen"] >= 0:
+                s0 = 3 * int(dv["offsets"][i])
+                if bytes(dv["slot"][s0: s0 + r["plen"]]) != r["payload"]:
+                    e.append(("payload",))
+            if r["kind"] == LO.MC:
+                if (int(dv["clock"][i]), int(dv["mcbitnum"][i]), int(dv["mcflags"][i])) != \
+                        (r["clock"], r["mcbitnum"], r["mcflags"]):
+                    e.append(("mc", int(dv["clock"][i]), int(dv["mcbitnum"][i]), r["clock"], r["mcbitnum"]))
+            else:
+                npat = int(dv["npat"][i])
+                ids = [int(chr(c)) for c in dv["pat_id"][i][:npat]]
+                vals = list(dv["pat_val"][i][:npat])
+                if ids != r["ids"] or vals != r["vals"]:
+                    e.append(("patterns", ids, vals, r["ids"], r["vals"]))
+                if r["kind"] == LO.MS and (int(dv["ms_ok"][i]) != r["ms_ok"] or
+                                           (r["ms_ok"] and int(dv["cp_slot"][i]) != r["cp_slot"])):
+                    e.append(("ms", int(dv["ms_ok"][i]), int(dv["cp_slot"][i]), r["ms_ok"], r["cp_slot"]))
+        if e:
+            bad.append((i, ln[:80], e))
+    return bad
+
+
+def _check_selection(lines, dv):
+    classes = [LO.sel_class(LO.parse_line(ln)) for ln in lines]
+    for k in range(5):
+        exp = [i for i, c in enumerate(classes) if c == k]
+        assert int(dv["counts"][k]) == len(exp), k
+        assert list(dv["sels"][k]) == exp, k
+
+
+@pytest.mark.gpu
+def test_parse_lines_matches_oracle_on_goldens(golden):
+    lines = _lines(golden)
+    dv = _device_parse(lines)
+    bad = _compare(lines, dv)
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:3]}"
+    _check_selection(lines, dv)
+
+
+@pytest.mark.gpu
+def test_parse_lines_matches_oracle_fuzz():
+    P = B.Bank().protocols
+    base, _ = synth.line_corpus(P, 4000, seed=11, compress_frac=0.4)
+    lines = base + _fuzz(base, 30000, seed=12) + [b"", b"\x02\x03", b"\x02MU;;\x03", b" \x02MC;;\x03 ",
+                                                  b"\x02Ms;\x80;\x03", b"\x02MN;D=AB;\x03"]
+    dv = _device_parse(lines)
+    bad = _compare(lines, dv)
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:3]}"
+    _check_selection(lines, dv)
+
+
+@pytest.mark.gpu
+def test_parse_lines_long_and_multi_chunk():
+    """Lines beyond the short variant, > SDX_LONG_MAX, and a batch spanning many select chunks."""
+    P = B.Bank().protocols
+    base, _ = synth.line_corpus(P, 3000, seed=21, compress_frac=0.3, mu_npulse=200)
+    longs = [b"\x02MU;P0=-500;P1=500;D=" + b"01" * k + b";CP=1;\x03" for k in (100, 129, 1000, 2048, 2049, 3000)]
+    longs += [b"\x02MS;P0=-500;P1=500;P2=-5000;D=2" + b"01" * k + b";CP=1;SP=2;\x03" for k in (127, 128, 500)]
+    lines = base + longs + base
+    dv = _device_parse(lines)
+    bad = _compare(lines, dv)
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:3]}"
+    _check_selection(lines, dv)
+
+
+def _flat_msgs(res):
+    return [[d.protocol_id, d.payload, d.metadata, [d.raw.line, d.raw.message_type, d.raw.rssi, d.raw.freq_afc]]
+            for d in res]
+
+
+@pytest.mark.gpu
+def test_signal_parser_end_to_end_matches_reference(golden):
+    from pysignalduino_amd.frontend import SignalParser
+    cases = golden("lines_golden.json.gz")
+    sp = SignalParser()
+    got = sp.parse_lines([c["line"] for c in cases])
+    bad = []
+    nres = 0
+    for c, g in zip(cases, got):
+        if isinstance(g, Exception):
+            assert LO.parse_line(c["line"].encode("latin-1"))["status"] == LO.UNSUPPORTED
+            continue
+        exp = c.get("e2e", [])
+        nres += len(exp)
+        if _flat_msgs(g) != exp:
+            bad.append((c["src"], c["line"][:80], exp[:2], _flat_msgs(g)[:2]))
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:2]}"
+    assert nres > 1000
+    # parse_line (single) agrees with the batch
+    i = next(k for k, c in enumerate(cases) if c.get("e2e"))
+    assert _flat_msgs(sp.parse_line(cases[i]["line"])) == cases[i]["e2e"]
+
+
+@pytest.mark.gpu
+def test_signal_parser_matches_demodulate_batch_at_scale():
+    """200k lines: the fused line path == demodulate_batch of the oracle's msg_data (which the
+    demodulator parity tests pin to the reference)."""
+    from pysignalduino_amd.frontend import SignalParser
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    P = B.Bank().protocols
+    lines, _ = synth.line_corpus(P, 200_000, seed=31, compress_frac=0.3)
+    proto = SDProtocols()
+    got = SignalParser(proto).parse_lines(lines)
+    recs = [LO.parse_line(ln) for ln in lines]
+    for kind, name in ((LO.MU, "MU"), (LO.MS, "MS")):
+        idx = [i for i, r in enumerate(recs) if r["status"] == LO.OK and r["kind"] == kind]
+        exp = proto.demodulate_batch([dict(recs[i]["msg"]) for i in idx], name)
+        for i, e in zip(idx, exp):
+            e = [] if isinstance(e, BaseException) else e
+            g = got[i]
+            assert [(d.protocol_id, d.payload, d.metadata) for d in g] == \
+                [(x["protocol_id"], x["payload"], x["meta"]) for x in e], (i, lines[i][:80])
