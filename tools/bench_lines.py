@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Front-end benchmark: raw firmware lines/s, line bytes -> decoded records.
+
+One step = one pass over a batch of ``--lines`` framed firmware lines resident in HBM
+(pysignalduino_amd.synth.line_corpus: MU/MS/MC 1/3 each, 30 % of the MU/MS lines Mred=1
+compressed): sdx_parse_lines, sdx_select_lines, the class-count read-back, then the MU/MS
+short/long and MC ('fixed' chain) demodulation launches over the selection lists -- exactly
+frontend.SignalParser.parse_lines minus the Python object assembly.  Prints ONE JSON line in the
+bench.py format: value = lines/s of the whole step; roofline of the parse kernel (algorithmic
+bytes: line bytes + offsets read, per-line SoA fields + D characters written, DESIGN.md
+"Front end"); cpu_baseline = the CPU oracle of the same path (oracle/lines_oracle.py parse +
+oracle/sd_oracle_c.c demodulation, one core) on a bounded sample.
+
+usage: python tools/bench_lines.py [--lines 1000000 --steps 5 --warmup 2]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+HBM_PEAK = 8.0e12
+
+
+def cpu_baseline(lines, budget_s):
+    """oracle/lines_oracle.py (Python) for the parse + the plain-C oracle for demodulation."""
+    from oracle import c_oracle as CO
+    from oracle import lines_oracle as LO
+    from pysignalduino_amd import packing
+    CO.build()
+    cbank = CO.CBank()
+
+    def run(sample):
+        t0 = time.perf_counter()
+        recs = [LO.parse_line(ln) for ln in sample]
+        mu = [dict(r["msg"]) for r in recs if r["status"] == LO.OK and r["kind"] == LO.MU]
+        ms = [dict(r["msg"]) for r in recs if r["status"] == LO.OK and r["kind"] == LO.MS and r["ms_ok"]]
+        mc = [(r["data"].decode(), r["clock"], r["mcbitnum"], "MC", None) for r in recs
+              if r["status"] == LO.OK and r["kind"] == LO.MC]
+        for kind, msgs in (("MU", mu), ("MS", ms)):
+            if msgs:
+                pk = packing.PulsePacker(kind)
+                for m in msgs:
+                    pk.add(m)
+                CO.run(kind, CO.pack_batch(pk.batch()), 1)
+        if mc:
+            CO.run("MC", CO.pack_mc(mc), 1)
+        return len(sample) / (time.perf_counter() - t0)
+
+    probe = run(lines[:300])
+    k = int(max(300, min(len(lines), probe * budget_s)))
+    v = run(lines[:k])
+    return {"value": v, "unit": "lines/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/lines_oracle.py parse (Python) + oracle/sd_oracle_c.c demodulation (C, 1 thread) "
+                      f"of the first {k} bench lines; {platform.processor() or platform.machine()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lines", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    import torch
+    from pysignalduino_amd import bank as bankmod, frontend, runtime, synth
+    torch.cuda.set_device(0)
+    bk = bankmod.Bank()
+    eng = runtime.Engine(bk, 0)
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"sdx_lines_{args.lines}_45.npz")
+    if os.path.exists(cache):  # the same seeded corpus, built once per box (profiling re-runs)
+        z = np.load(cache)
+        data, offsets = z["data"], z["offsets"]
+        lines = [data[offsets[i]: offsets[i + 1]].tobytes() for i in range(len(offsets) - 1)]
+    else:
+        lines, _ = synth.line_corpus(bk.protocols, args.lines, seed=45, mix=(1, 1, 1), compress_frac=0.3)
+        data, offsets, bad = frontend.pack_lines(lines)
+        assert not bad
+        np.savez(cache, data=data, offsets=offsets)
+    n = len(lines)
+    lb = frontend.LineBatch(eng, data, offsets)
+    pb, mb = lb.pulse_batch(), lb.mc_batch()
+    outs = {"MU": eng.alloc_out(n, 4 * n + 4096, 100 * n + 65536), "MS": eng.alloc_out(n, 2 * n + 4096, 40 * n + 65536),
+            "MC": eng.alloc_out(n, 2 * n + 4096, 40 * n + 65536)}
+    stream = torch.cuda.current_stream()
+    names = ["parse+select", "MU", "MS", "MC"]
+    ev = {k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in names}
+    ev_parse = torch.cuda.Event(enable_timing=True)
+    kt = {k: [] for k in names + ["parse"]}
+    import ctypes
+
+    def step(record=False):
+        for o in outs.values():
+            o["cursor"].zero_()
+        if record:
+            ev["parse+select"][0].record(stream)
+        lib, st = eng.lib, eng.stream_ptr()
+        runtime._check(lib, lib.sdx_parse_lines(ctypes.byref(lb.c_lines), ctypes.byref(lb.c_out), st))
+        if record:
+            ev_parse.record(stream)
+        runtime._check(lib, lib.sdx_select_lines(ctypes.byref(lb.c_out), n, runtime._ptr(lb.sel),
+                                                 runtime._ptr(lb.counts), runtime._ptr(lb.scratch), st))
+        if record:
+            ev["parse+select"][1].record(stream)
+        sels, cnt = lb.selections()  # 32-byte read-back: sizes the launches
+        for k, short, long_ in (("MU", runtime.SEL_MU_SHORT, runtime.SEL_MU_LONG),
+                                ("MS", runtime.SEL_MS_SHORT, runtime.SEL_MS_LONG), ("MC", runtime.SEL_MC, None)):
+            if record:
+                ev[k][0].record(stream)
+            if k == "MC":
+                if cnt[short]:
+                    eng.launch_mc(mb, outs[k], sel=sels[short])
+            else:
+                kind = runtime.KIND_MU if k == "MU" else runtime.KIND_MS
+                if cnt[short]:
+                    eng.launch_pulses(kind, pb, outs[k], sel=sels[short])
+                if cnt[long_]:
+                    eng.launch_pulses(kind, pb, outs[k], sel=sels[long_], long_variant=True)
+            if record:
+                ev[k][1].record(stream)
+        return cnt
+
+    for _ in range(args.warmup):
+        cnt = step()
+    torch.cuda.synchronize()
+    for k, o in outs.items():
+        cur = o["cursor"].cpu().numpy()
+        if cur[2] != 0:
+            raise SystemExit(f"{k}: result capacity overflow in the bench configuration ({cur})")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+        torch.cuda.synchronize()
+        for k in names:
+            kt[k].append(ev[k][0].elapsed_time(ev[k][1]) * 1e-3)
+        kt["parse"].append(ev["parse+select"][0].elapsed_time(ev_parse) * 1e-3)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    value = n * args.steps / dt
+    km = {k: float(np.mean(v)) for k, v in kt.items()}
+    # parse-kernel algorithmic bytes: every line byte + offsets read once; per line the SoA fields
+    # (kind 1, status 1, doff 8, dlen 4, npat 1, pat_id 10, pat_val 80, cp 1, ms_ok 1, clock 4,
+    # mcbitnum 4, mcflags 1, meta 32, plen 4 = 152 B) and the D characters written
+    dl = lb.dlen[:n].cpu().numpy().astype(np.int64)
+    stv = lb.status[:n].cpu().numpy()
+    alg = int(offsets[-1]) + 8 * (n + 1) + 152 * n + int(dl[stv == runtime.LS_OK].sum())
+    achieved = alg / km["parse"]
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "r01", "pmc_traffic_lines.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if tj.get("_config", {}).get("lines") == n and tj.get("k_parse_lines", {}).get("traffic_bytes"):
+            traffic = float(tj["k_parse_lines"]["traffic_bytes"])
+    res = {
+        "metric": "raw firmware lines/sec parsed + demodulated (wire-line front end, SURVEY §8(f) 1)",
+        "value": value, "unit": "lines/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8+f64", "data": "synthetic firmware lines (pysignalduino_amd/synth.py line_corpus)",
+        "config": {"workload": "framed firmware lines, MU/MS/MC 1/3 each (MU 256 pulses), 30% of MU/MS Mred=1 "
+                               "compressed; parse + select + MU/MS/MC ('fixed') demodulation",
+                   "lines": n, "line_bytes": int(offsets[-1]), "classes": [int(c) for c in cnt]},
+        "per_kernel_ms": {k: 1e3 * v for k, v in km.items()},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": "k_parse_lines",
+                     "alg_bytes_per_launch": alg},
+    }
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(lines, args.cpu_seconds)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

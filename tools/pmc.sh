@@ -3,9 +3,10 @@
 # with --pmc).  Output: gpurun_out/pmc/<pass>/..._counter_collection.csv + <pass>.log.
 # Usage: tools/pmc.sh [pass ...]   (default: all passes)
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+# PMC_BENCH / PMC_OUT / PMC_TRAFFIC / PMC_CONFIG select another workload (e.g. tools/bench_lines.py)
+OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
-BENCH="python3 bench.py --steps 3 --warmup 1 --no-cpu"
+BENCH=${PMC_BENCH:-"python3 bench.py --steps 3 --warmup 1 --no-cpu"}
 declare -A P
 P[sq1]="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
 P[sq2]="SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"
@@ -22,4 +23,4 @@ for p in "${passes[@]}"; do
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$p.log"; exit $rc; fi
 done
 python3 tools/pmc_summary.py "$OUT"
-python3 tools/pmc_traffic.py "$OUT" gpurun_out/pmc_traffic.json > /dev/null
+python3 tools/pmc_traffic.py "$OUT" "${PMC_TRAFFIC:-gpurun_out/pmc_traffic.json}" > /dev/null
