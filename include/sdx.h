@@ -169,7 +169,11 @@ typedef struct {
 
 /* parse a batch of lines into out (device buffers, caller-owned; no allocation, no sync).  Lines
  * longer than the kernels' contract (SDX_LONG_MAX pulses, SDX_MC_HEX_MAX hex characters) are
- * reported SDX_LS_UNSUPPORTED. */
+ * reported SDX_LS_UNSUPPORTED.  kind/status/doff/plen are written for every line; the other
+ * fields only where they mean something: dlen and meta for SDX_LS_OK lines, the pattern fields
+ * (npat, pat_id/pat_val[0..npat)) for OK MU/MS lines, cp_slot/ms_ok for OK MS lines, clock/
+ * mcbitnum/mcflags for OK MC lines, and plen plus the slot payload for OK decompressed lines.
+ * meta_dev must be 16-byte aligned. */
 int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out, void* hip_stream);
 
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */

@@ -194,9 +194,6 @@ def parse_line(line: bytes) -> Dict[str, Any]:
         return r
     items = _kv(q)
     kv = dict(items)
-    if sum(1 for k, _ in items if k[:1] == b"P" and len(k) > 1 and k[1:].isdigit()) > 16:
-        r["status"] = UNSUPPORTED                             # the kernel's P-key table holds 16
-        return r
     if b"D" not in kv:
         r["status"] = NODATA
         return r

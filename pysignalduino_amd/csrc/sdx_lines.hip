@@ -291,106 +291,105 @@ struct Field {
   int s, e;  // value range, s < 0: absent
 };
 
-LD void put_meta(uint8_t* m, const Str& P, Field f) {
-  if (f.s < 0) {
-    m[15] = 255;
-    return;
-  }
-  const int n = f.e - f.s;
-  m[15] = (uint8_t)n;  // <= 15 (longer values are SDX_LS_UNSUPPORTED)
-  for (int i = 0; i < n; ++i) m[i] = P.p[f.s + i];
+
+// ---- the parse kernel -------------------------------------------------------------------------
+// One lane per line.  A wave first stages the byte span of its (next) lines into its own LDS region
+// with coalesced 16-byte loads, then every lane scans its line in LDS; compressed payloads are
+// decompressed into a per-wave LDS area (prefix-sum allocated), and at the end of a round the
+// wave copies each line's D characters (or whole decompressed payload) to the slot with
+// byte-consecutive stores.  A line longer than the stage buffer, or a payload whose decompression
+// does not fit the LDS area, takes the same code on global memory (exact, slower).
+constexpr int PW = 2;         // waves per workgroup
+constexpr int STAGE = 8192;   // staged line bytes per wave and round
+constexpr int DECB = 4096;    // decompressed payload bytes per wave and round
+
+struct alignas(16) ParseLds {
+  uint8_t stage[STAGE + 32];
+  uint8_t dec[DECB];
+  uint32_t pv[10 * 64];  // fast P-key table [id][lane]: last value start | end << 16
+};
+
+struct LineRes {
+  uint8_t kind = SDX_LINE_NONE, status = SDX_LS_NOFRAME;
+  int dS = 0, dE = 0;  // D (MU/MS) or hex (MC) characters in the payload
+  Field fR{-1, -1}, fF{-1, -1};
+};
+
+LD void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= in.n) return;
-  const int64_t lo = in.offsets_dev[i], hi = in.offsets_dev[i + 1];
-  const uint8_t* L = in.bytes_dev + lo;
-  int a = 0, b = (int)(hi - lo);
-  uint8_t kind = SDX_LINE_NONE, status = SDX_LS_NOFRAME;
-  const int64_t slot0 = 3 * lo;
-  uint8_t* slot = out.slot_dev + slot0;
-  const int slot_cap = (int)(3 * (hi - lo));
-  out.doff_dev[i] = slot0;
-  out.dlen_dev[i] = 0;
-  out.npat_dev[i] = 0;
-  out.ms_ok_dev[i] = 0;
-  out.cp_slot_dev[i] = -1;
-  out.clock_dev[i] = 0;
-  out.mcbitnum_dev[i] = 0;
-  out.mcflags_dev[i] = 0;
-  uint8_t* meta = out.meta_dev + 32 * (int64_t)i;
-  meta[15] = 255;
-  meta[31] = 255;
-  out.plen_dev[i] = -1;
-  auto done = [&]() {
-    out.kind_dev[i] = kind;
-    out.status_dev[i] = status;
-  };
-  // ---- extract_payload (base.py:188-206)
+LD int64_t shfl64(int64_t v, int src) {
+  const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// extract_payload (base.py:188-206): payload = L[pa, pa + pn); also whether decompress_payload
+// runs on it (MS/MU/MO/MN with a byte >= 0x80 after the header).  One pass over the bytes.
+LD bool frame_line(const uint8_t* L, int len, int& pa, int& pn, bool& comp) {
+  int a = 0, b = len;
   while (a < b && py_space(L[a])) ++a;
   while (b > a && py_space(L[b - 1])) --b;
-  if (b - a < 6 || L[a] != 0x02 || L[b - 1] != 0x03 || L[a + 1] != 'M' || L[a + 3] != ';' || L[b - 2] != ';') {
-    done();
-    return;
+  if (b - a < 6 || L[a] != 0x02 || L[b - 1] != 0x03 || L[a + 1] != 'M' || L[a + 3] != ';' || L[b - 2] != ';')
+    return false;
+  const uint8_t t = L[a + 2];
+  if (!(t == 's' || t == 'S' || t == 'u' || t == 'U' || t == 'c' || t == 'C' || t == 'N' || t == 'O' || t == 'o'))
+    return false;
+  uint8_t any = 0;
+  for (int k = a + 4; k < b - 2; ++k) {  // '.' does not match a newline
+    const uint8_t c = L[k];
+    if (c == '\n') return false;
+    any |= c;
   }
-  {
-    const uint8_t t = L[a + 2];
-    if (!(t == 's' || t == 'S' || t == 'u' || t == 'U' || t == 'c' || t == 'C' || t == 'N' || t == 'O' ||
-          t == 'o')) {
-      done();
-      return;
-    }
-    for (int k = a + 4; k < b - 2; ++k)  // '.' does not match a newline
-      if (L[k] == '\n') {
-        done();
-        return;
-      }
-  }
-  Str P{L + a + 1, b - a - 2};
-  // ---- decompress_payload: MS/MU/MO/MN with a byte >= 0x80 after the header
-  const uint8_t t1 = up(P.p[1]);
-  bool comp = false;
-  if (t1 == 'S' || t1 == 'U' || t1 == 'O' || t1 == 'N')
-    for (int k = 3; k < P.n && !comp; ++k) comp = P.p[k] > 127;
-  if (comp) {
-    Writer w{slot, 0, slot_cap, false};
-    if (!decompress(P, w) || w.ovf) {
-      status = SDX_LS_UNSUPPORTED;
-      done();
-      return;
-    }
-    P = Str{slot, w.n};
-    out.plen_dev[i] = w.n;
-  }
+  const uint8_t t1 = up(t);
+  comp = (any & 0x80) && (t1 == 'S' || t1 == 'U' || t1 == 'O' || t1 == 'N');
+  pa = a + 1;
+  pn = b - a - 2;
+  return true;
+}
+
+LD bool same_key(const Str& P, int s1, int e1, int s2, int e2) {
+  if (e1 - s1 != e2 - s2) return false;
+  for (int k = 0; k < e1 - s1; ++k)
+    if (P.p[s1 + k] != P.p[s2 + k]) return false;
+  return true;
+}
+
+// routing + the per-type parser rules on a (decompressed) payload; writes the pattern / MS / MC
+// fields of line i, returns kind/status and the D/R/F ranges.  pvt = this lane's column of the
+// fast P-key table (stride 64 words).
+LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i, uint32_t* pvt) {
   // ---- routing: payload[:2].upper()
   const uint8_t c0 = P.n > 0 ? up(P.p[0]) : 0, c1 = P.n > 1 ? up(P.p[1]) : 0;
   if (c0 != 'M' || !(c1 == 'S' || c1 == 'U' || c1 == 'C' || c1 == 'N')) {
-    status = SDX_LS_NOPARSER;
-    done();
+    r.status = SDX_LS_NOPARSER;
     return;
   }
-  kind = c1 == 'U' ? SDX_LINE_MU : c1 == 'S' ? SDX_LINE_MS : c1 == 'C' ? SDX_LINE_MC : SDX_LINE_MN;
-  if (kind == SDX_LINE_MN) {  // the MN (FSK) path is not part of this build
-    status = SDX_LS_UNSUPPORTED;
-    done();
+  r.kind = c1 == 'U' ? SDX_LINE_MU : c1 == 'S' ? SDX_LINE_MS : c1 == 'C' ? SDX_LINE_MC : SDX_LINE_MN;
+  if (r.kind == SDX_LINE_MN) {  // the MN (FSK) path is not part of this build
+    r.status = SDX_LS_UNSUPPORTED;
     return;
   }
-  for (int k = 0; k < P.n; ++k)
-    if (P.p[k] > 127) {  // str methods on non-ASCII characters are not modelled
-      status = SDX_LS_UNSUPPORTED;
-      done();
+  {
+    uint8_t any = 0;
+    for (int k = 0; k < P.n; ++k) any |= P.p[k];
+    if (any & 0x80) {  // str methods on non-ASCII characters are not modelled
+      r.status = SDX_LS_UNSUPPORTED;
       return;
     }
-  if (kind == SDX_LINE_MU && !mu_valid(P)) {
-    status = SDX_LS_INVALID;
-    done();
+  }
+  if (r.kind == SDX_LINE_MU && !mu_valid(P)) {
+    r.status = SDX_LS_INVALID;
     return;
   }
-  Field fD{-1, -1}, fCP{-1, -1}, fSP{-1, -1}, fR{-1, -1}, fF{-1, -1}, fC{-1, -1}, fL{-1, -1}, fM{-1, -1};
-  if (kind == SDX_LINE_MC) {
+  Field fD{-1, -1}, fCP{-1, -1}, fSP{-1, -1}, fC{-1, -1}, fL{-1, -1};
+  Field& fR = r.fR;
+  Field& fF = r.fF;
+  if (r.kind == SDX_LINE_MC) {
     // ---- MCParser._parse_to_dict + key set + required fields (mc.py:37-56,95-139)
-    int pos = 0, s, e, nkeys = 0;
+    int pos = 0, s, e;
     uint32_t seen = 0;  // LL LH SL SH D C L R F M MC Mc
     while (next_part(P, pos, s, e)) {
       int eq = -1;
@@ -405,21 +404,18 @@ __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out
         bool keyok = kl >= 1 && kl <= 2;
         for (int k = s; k < eq && keyok; ++k) keyok = P.p[k] >= 'A' && P.p[k] <= 'Z';
         int v = eq + 1;
-        bool valok = true;
         if (v < e && (P.p[v] == '-' || P.p[v] == '+')) ++v;
-        valok = v < e;
+        bool valok = v < e;
         for (int k = v; k < e && valok; ++k) valok = hexc(P.p[k]);
         if (!keyok || !valok) {
-          status = SDX_LS_INVALID;
-          done();
+          r.status = SDX_LS_INVALID;
           return;
         }
         static const char* const KEYS[11] = {"LL", "LH", "SL", "SH", "D", "C", "L", "R", "F", "M", "MC"};
         for (int q = 0; q < 11 && bit < 0; ++q)
           if (keq(P, s, eq, KEYS[q])) bit = q;
         if (bit < 0) {  // a well-formed key outside the MC header set
-          status = SDX_LS_INVALID;
-          done();
+          r.status = SDX_LS_INVALID;
           return;
         }
         const Field f{eq + 1, e};
@@ -428,67 +424,57 @@ __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out
         if (bit == 6) fL = f;
         if (bit == 7) fR = f;
         if (bit == 8) fF = f;
-        if (bit == 9) fM = f;
       } else {
         if (keq(P, s, e, "MC")) bit = 10;
         else if (keq(P, s, e, "Mc")) bit = 11;
-        else if (nkeys > 0) {  // a non key=value part after the first one
-          status = SDX_LS_INVALID;
-          done();
-          return;
-        } else {  // first part: any type string, then outside the valid key set
-          status = SDX_LS_INVALID;
-          done();
+        else {  // not MC/Mc: invalid after the first part, and outside the key set as the first
+          r.status = SDX_LS_INVALID;
           return;
         }
       }
       if (seen & (1u << bit)) {  // duplicate key
-        status = SDX_LS_INVALID;
-        done();
+        r.status = SDX_LS_INVALID;
         return;
       }
       seen |= 1u << bit;
-      ++nkeys;
     }
     if (fD.s < 0 || fC.s < 0 || fL.s < 0) {
-      status = SDX_LS_INVALID;
-      done();
+      r.status = SDX_LS_INVALID;
       return;
     }
     for (int k = fD.s; k < fD.e; ++k)  // re.fullmatch(r"[0-9a-fA-F]+", raw_hex)
       if (!hexc(P.p[k])) {
-        status = SDX_LS_INVALID;
-        done();
+        r.status = SDX_LS_INVALID;
         return;
       }
     long long v;
     const int rr = fR.s >= 0 ? parse_dec(P, fR.s, fR.e, &v) : 1, rf = fF.s >= 0 ? parse_dec(P, fF.s, fF.e, &v) : 1;
     if ((rr != 1 && rr != 3) || (rf != 1 && rf != 3)) {  // int(R) / int(F) raise -> ignored (mc.py:141-155)
-      status = SDX_LS_INVALID;
-      done();
+      r.status = SDX_LS_INVALID;
       return;
     }
     long long cv = 0, lv = 0;
     const int rc = parse_dec(P, fC.s, fC.e, &cv), rl = parse_dec(P, fL.s, fL.e, &lv);
     if (rc == 2 || rl == 2) {  // int(C) / int(L) raise inside demodulate_mc -> caught, nothing decoded
-      status = SDX_LS_RAISES;
-      done();
+      r.status = SDX_LS_RAISES;
       return;
     }
     if (rc != 1 || rl != 1 || fD.e - fD.s > SDX_MC_HEX_MAX) {  // outside the int32 / frame-length contract
-      status = SDX_LS_UNSUPPORTED;
-      done();
+      r.status = SDX_LS_UNSUPPORTED;
       return;
     }
     out.clock_dev[i] = (int32_t)cv;
     out.mcbitnum_dev[i] = (int32_t)lv;
     out.mcflags_dev[i] = 0;  // msg_data.get("M", "MC") is never "Mc" (mc.py:60); no version
   } else {
-    // ---- _parse_to_dict (mu.py:82-94, ms.py:65-78) and the demodulators' P#/CP/SP/R gates
+    // ---- _parse_to_dict (mu.py:82-94, ms.py:65-78): last value wins, first position counts.
+    // P-keys "P<d>" (one digit) go to the lane's LDS table; any longer P-key ("P05", "P10")
+    // switches to the general (nested-scan) form below.
     int pos = 0, s, e;
-    // msg_data P-keys: distinct key strings in first-occurrence order, last value
-    int pk_s[16], pk_e[16], pv_s[16], pv_e[16];
-    int npk = 0;
+    uint32_t seen = 0;
+    uint64_t order = 0;
+    int nord = 0;
+    bool slow = P.n > 0xFFFF;
     while (next_part(P, pos, s, e)) {
       int eq = -1;
       for (int k = s; k < e; ++k)
@@ -504,97 +490,318 @@ __global__ __launch_bounds__(256) void k_parse_lines(sdx_lines in, sdx_lines_out
       else if (keq(P, s, ke, "R")) fR = f;
       else if (keq(P, s, ke, "F")) fF = f;
       else if (P.p[s] == 'P' && ke - s >= 2 && all_digits(P, s + 1, ke)) {
-        int q = 0;
-        while (q < npk && !(pk_e[q] - pk_s[q] == ke - s && [&] {
-                 for (int k = 0; k < ke - s; ++k)
-                   if (P.p[pk_s[q] + k] != P.p[s + k]) return false;
-                 return true;
-               }()))
-          ++q;
-        if (q == npk) {
-          if (npk == 16) {
-            status = SDX_LS_UNSUPPORTED;
-            done();
-            return;
+        if (ke - s == 2 && !slow) {
+          const int d = P.p[s + 1] - '0';
+          if (!((seen >> d) & 1)) {
+            seen |= 1u << d;
+            order |= (uint64_t)d << (4 * nord);
+            ++nord;
           }
-          pk_s[npk] = s;
-          pk_e[npk] = ke;
-          ++npk;
+          pvt[64 * d] = (uint32_t)f.s | ((uint32_t)f.e << 16);
+        } else {
+          slow = true;
         }
-        pv_s[q] = f.s;
-        pv_e[q] = f.e;
       }
     }
     if (fD.s < 0) {  // "D" not in msg_data
-      status = SDX_LS_NODATA;
-      done();
+      r.status = SDX_LS_NODATA;
       return;
     }
     // message_synced.py:21-47 string gates (packing.PulsePacker.add); patterns are converted only
     // where the reference converts them (MS past the gates, MU with non-empty data)
-    bool ms_ok = kind == SDX_LINE_MS && all_digits(P, fD.s, fD.e) && fCP.s >= 0 && all_digits(P, fCP.s, fCP.e) &&
+    bool ms_ok = r.kind == SDX_LINE_MS && all_digits(P, fD.s, fD.e) && fCP.s >= 0 && all_digits(P, fCP.s, fCP.e) &&
                  fSP.s >= 0 && all_digits(P, fSP.s, fSP.e) && (fR.s < 0 || all_digits(P, fR.s, fR.e));
-    const bool want_pat = kind == SDX_LINE_MS ? ms_ok : fD.e > fD.s;
-    // _patterns (message_unsynced.py:28-35): id = str(int(k[1:])), value = float(v), ValueError skipped
+    const bool want_pat = r.kind == SDX_LINE_MS ? ms_ok : fD.e > fD.s;
+    // _patterns (message_unsynced.py:28-35): id = str(int(k[1:])), value = float(v), ValueError
+    // skipped; slot = first successful assignment of the id, value = the last one
     int nslot = 0;
-    uint8_t sid[10];
-    double sval[10];
-    for (int q = 0; q < npk && want_pat; ++q) {
-      long long idv = 0;
-      for (int k = pk_s[q] + 1; k < pk_e[q]; ++k)
-        if (idv < 1000) idv = 10 * idv + (P.p[k] - '0');
-      long long v;
-      const int r = parse_int15(P, pv_s[q], pv_e[q], &v);
-      if (r == 0) continue;  // float('') -> ValueError -> skipped
-      if (r == 2 || idv >= 10) {  // other float() syntax / a multi-character pattern id
-        status = SDX_LS_UNSUPPORTED;
-        done();
-        return;
-      }
+    uint64_t sidp = 0;  // slot z -> id in nibble z
+    double* pval = out.pat_val_dev + 10 * (int64_t)i;
+    uint8_t* pid = out.pat_id_dev + 10 * (int64_t)i;
+    auto assign = [&](int id, double v) {
       int z = 0;
-      while (z < nslot && sid[z] != (uint8_t)idv) ++z;
-      if (z == nslot) sid[nslot++] = (uint8_t)idv;
-      sval[z] = (double)v;
+      while (z < nslot && (int)((sidp >> (4 * z)) & 15) != id) ++z;
+      if (z == nslot) {
+        sidp |= (uint64_t)id << (4 * z);
+        pid[z] = (uint8_t)('0' + id);
+        ++nslot;
+      }
+      pval[z] = v;
+    };
+    if (want_pat && !slow) {
+      for (int q = 0; q < nord; ++q) {
+        const int d = (int)((order >> (4 * q)) & 15);
+        const uint32_t w = pvt[64 * d];
+        long long v;
+        const int rv = parse_int15(P, (int)(w & 0xFFFF), (int)(w >> 16), &v);
+        if (rv == 0) continue;  // float('') -> ValueError -> skipped
+        if (rv == 2) {          // other float() syntax: not modelled
+          r.status = SDX_LS_UNSUPPORTED;
+          return;
+        }
+        assign(d, (double)v);
+      }
+    } else if (want_pat) {
+      pos = 0;
+      while (next_part(P, pos, s, e)) {
+        int eq = -1;
+        for (int k = s; k < e; ++k)
+          if (P.p[k] == '=') {
+            eq = k;
+            break;
+          }
+        const int ke = eq >= 0 ? eq : e;
+        if (!(P.p[s] == 'P' && ke - s >= 2 && all_digits(P, s + 1, ke))) continue;
+        bool dup = false;  // msg_data holds each key string once, at its first position
+        int p2 = 0, s2, e2;
+        while (!dup && next_part(P, p2, s2, e2) && s2 < s) {
+          int k2 = s2;
+          while (k2 < e2 && P.p[k2] != '=') ++k2;
+          dup = same_key(P, s, ke, s2, k2);
+        }
+        if (dup) continue;
+        int vs = eq >= 0 ? eq + 1 : e, ve = e;  // ... with the value of its last occurrence
+        int p3 = pos, s3, e3;
+        while (next_part(P, p3, s3, e3)) {
+          int k3 = s3;
+          while (k3 < e3 && P.p[k3] != '=') ++k3;
+          if (same_key(P, s, ke, s3, k3)) {
+            vs = k3 < e3 ? k3 + 1 : e3;
+            ve = e3;
+          }
+        }
+        long long idv = 0;
+        for (int k = s + 1; k < ke; ++k)
+          if (idv < 1000) idv = 10 * idv + (P.p[k] - '0');
+        long long v;
+        const int rv = parse_int15(P, vs, ve, &v);
+        if (rv == 0) continue;
+        if (rv == 2 || idv >= 10) {  // other float() syntax / a multi-character pattern id
+          r.status = SDX_LS_UNSUPPORTED;
+          return;
+        }
+        assign((int)idv, (double)v);
+      }
     }
     if (fD.e - fD.s > SDX_LONG_MAX) {  // longer than the long demodulation variant takes
-      status = SDX_LS_UNSUPPORTED;
-      done();
+      r.status = SDX_LS_UNSUPPORTED;
       return;
     }
     out.npat_dev[i] = (uint8_t)nslot;
-    for (int z = 0; z < 10; ++z) {
-      out.pat_id_dev[10 * (int64_t)i + z] = z < nslot ? (uint8_t)('0' + sid[z]) : 0;
-      out.pat_val_dev[10 * (int64_t)i + z] = z < nslot ? sval[z] : 0.0;
-    }
-    if (ms_ok) {  // str(int(CP)) in the pattern ids, else no demodulation
-      long long cp = 0;
-      for (int k = fCP.s; k < fCP.e; ++k)
-        if (cp < 1000) cp = 10 * cp + (P.p[k] - '0');
+    if (r.kind == SDX_LINE_MS) {
       int8_t slotv = -1;
-      for (int z = 0; z < nslot; ++z)
-        if (cp < 10 && sid[z] == (uint8_t)cp) slotv = (int8_t)z;
+      if (ms_ok) {  // str(int(CP)) in the pattern ids, else no demodulation
+        long long cp = 0;
+        for (int k = fCP.s; k < fCP.e; ++k)
+          if (cp < 1000) cp = 10 * cp + (P.p[k] - '0');
+        for (int z = 0; z < nslot; ++z)
+          if (cp < 10 && (int)((sidp >> (4 * z)) & 15) == cp) slotv = (int8_t)z;
+        ms_ok = slotv >= 0;
+      }
       out.cp_slot_dev[i] = slotv;
-      ms_ok = slotv >= 0;
+      out.ms_ok_dev[i] = ms_ok ? 1 : 0;
     }
-    out.ms_ok_dev[i] = ms_ok ? 1 : 0;
   }
   if ((fR.s >= 0 && fR.e - fR.s > 15) || (fF.s >= 0 && fF.e - fF.s > 15)) {  // meta_dev holds 15 bytes
-    status = SDX_LS_UNSUPPORTED;
-    done();
+    r.status = SDX_LS_UNSUPPORTED;
     return;
   }
-  // ---- the D (MU/MS) or hex (MC) characters: already in the slot when decompressed, else copied
-  const int dn = fD.e - fD.s;
-  if (comp) {
-    out.doff_dev[i] = slot0 + (P.p + fD.s - slot);
+  r.dS = fD.s;
+  r.dE = fD.e;
+  r.status = SDX_LS_OK;
+}
+
+// 16 bytes of meta_dev: value characters, length at byte 15 (255 = absent)
+LD uint4 meta16(const Str& P, Field f) {
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  if (f.s < 0) {
+    w3 = 255u << 24;
   } else {
-    for (int k = 0; k < dn; ++k) slot[k] = P.p[fD.s + k];
+    const int n = f.e - f.s;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const uint32_t c = k < n ? (uint32_t)P.p[f.s + k] << (8 * (k & 3)) : 0u;
+      if (k < 4) w0 |= c;
+      else if (k < 8) w1 |= c;
+      else if (k < 12) w2 |= c;
+      else w3 |= c;
+    }
+    w3 |= (uint32_t)n << 24;
   }
-  out.dlen_dev[i] = dn;
-  put_meta(meta, P, fR);
-  put_meta(meta + 16, P, fF);
-  status = SDX_LS_OK;
-  done();
+  return make_uint4(w0, w1, w2, w3);
+}
+
+LD void finish_fields(const Str& P, const LineRes& r, const sdx_lines_out& out, int i) {
+  uint4* m = reinterpret_cast<uint4*>(out.meta_dev + 32 * (int64_t)i);
+  m[0] = meta16(P, r.fR);
+  m[1] = meta16(P, r.fF);
+  out.dlen_dev[i] = r.dE - r.dS;
+}
+
+// a line on global memory only (longer than the stage buffer): same rules, lane-serial copy
+LD void line_global(const sdx_lines& in, const sdx_lines_out& out, int i, int64_t lo, int64_t hi, uint32_t* pvt) {
+  const uint8_t* L = in.bytes_dev + lo;
+  LineRes r;
+  int pa = 0, pn = 0;
+  bool comp = false;
+  int plen = -1;
+  int64_t doff = 3 * lo;
+  if (frame_line(L, (int)(hi - lo), pa, pn, comp)) {
+    Str P{L + pa, pn};
+    uint8_t* slot = out.slot_dev + 3 * lo;
+    bool ok = true;
+    if (comp) {
+      Writer w{slot, 0, (int)(3 * (hi - lo)), false};
+      ok = decompress(P, w) && !w.ovf;
+      P = Str{slot, w.n};
+      plen = w.n;
+    }
+    if (!ok) {
+      r.status = SDX_LS_UNSUPPORTED;
+    } else {
+      parse_payload(P, r, out, i, pvt);
+      if (r.status == SDX_LS_OK) {
+        if (comp) {
+          doff = 3 * lo + r.dS;
+        } else {
+          for (int k = 0; k < r.dE - r.dS; ++k) slot[k] = P.p[r.dS + k];
+        }
+        finish_fields(P, r, out, i);
+      }
+    }
+  }
+  out.doff_dev[i] = doff;
+  out.plen_dev[i] = plen;
+  out.kind_dev[i] = r.kind;
+  out.status_dev[i] = r.status;
+}
+
+__global__ __launch_bounds__(64 * PW) void k_parse_lines(sdx_lines in, sdx_lines_out out) {
+  __shared__ ParseLds sm[PW];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  ParseLds& S = sm[wave];
+  const int first = (blockIdx.x * PW + wave) * 64;
+  if (first >= in.n) return;  // wave-uniform
+  const int nv = min(64, in.n - first);
+  const int i = first + lane;
+  const bool valid = lane < nv;
+  const int64_t total = in.offsets_dev[in.n];
+  int64_t lo = 0, hi = 0;
+  if (valid) {
+    lo = in.offsets_dev[i];
+    hi = in.offsets_dev[i + 1];
+  }
+  uint32_t* pvt = S.pv + lane;
+  uint8_t* const sbase = reinterpret_cast<uint8_t*>(&S);
+  int next = 0;
+  while (next < nv) {
+    const int64_t base = shfl64(lo, next);
+    const bool fits = valid && lane >= next && hi - base <= STAGE;
+    const int k = next + __popcll(__ballot(fits));  // hi is monotone: the fitting lanes are next..k-1
+    if (k == next) {  // line `next` alone exceeds the stage buffer
+      if (lane == next) line_global(in, out, i, lo, hi, pvt);
+      ++next;
+      continue;
+    }
+    // ---- stage bytes [base, end) with 16-byte loads: LDS byte j <-> global byte (ga + j)
+    const int64_t end = shfl64(hi, k - 1);
+    const uint8_t* gb = in.bytes_dev + base;
+    const int sh = (int)((uintptr_t)gb & 15);
+    const uint8_t* ga = gb - sh;
+    const int nch = (int)((end - base + sh + 15) >> 4);
+    const uint8_t* glo = in.bytes_dev;
+    const uint8_t* ghi = in.bytes_dev + total;
+    for (int c = lane; c < nch; c += 64) {
+      const uint8_t* src = ga + 16 * c;
+      if (src >= glo && src + 16 <= ghi) {
+        *reinterpret_cast<uint4*>(S.stage + 16 * c) = *reinterpret_cast<const uint4*>(src);
+      } else {
+        for (int q = 0; q < 16; ++q) S.stage[16 * c + q] = (src + q >= glo && src + q < ghi) ? src[q] : 0;
+      }
+    }
+    wave_sync();
+    const bool mine = lane >= next && lane < k;
+    LineRes r;
+    int pa = 0, pn = 0;
+    bool comp = false, framed = false;
+    const uint8_t* L = S.stage + sh + (lo - base);
+    if (mine) framed = frame_line(L, (int)(hi - lo), pa, pn, comp);
+    // decompression targets: prefix-sum allocation in the wave's LDS area, else the global slot
+    const int ub = (mine && framed && comp) ? 3 * pn + 16 : 0;
+    int incl = ub;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    const int doff_l = incl - ub;
+    const bool dec_lds = incl <= DECB;
+    int plen = -1;
+    int64_t doff = 3 * lo;
+    uint32_t cp_src = 0;
+    int cp_len = 0;
+    if (mine && framed) {
+      const Str Ps{L + pa, pn};
+      if (comp && !dec_lds) {  // the LDS area is full: decompress into the slot and parse there
+        uint8_t* slot = out.slot_dev + 3 * lo;
+        Writer w{slot, 0, (int)(3 * (hi - lo)), false};
+        if (!decompress(Ps, w) || w.ovf) {
+          r.status = SDX_LS_UNSUPPORTED;
+        } else {
+          const Str P{slot, w.n};
+          plen = w.n;
+          parse_payload(P, r, out, i, pvt);
+          if (r.status == SDX_LS_OK) {
+            doff = 3 * lo + r.dS;
+            finish_fields(P, r, out, i);
+          }
+        }
+      } else {
+        bool ok = true;
+        Str P = Ps;
+        if (comp) {
+          Writer w{S.dec + doff_l, 0, ub, false};
+          ok = decompress(Ps, w) && !w.ovf;
+          P = Str{S.dec + doff_l, w.n};
+          plen = w.n;
+        }
+        if (!ok) {
+          r.status = SDX_LS_UNSUPPORTED;
+        } else {
+          parse_payload(P, r, out, i, pvt);
+          if (r.status == SDX_LS_OK) {
+            finish_fields(P, r, out, i);
+            if (comp) {  // the whole payload goes to the slot (RawFrame.line), D inside it
+              doff = 3 * lo + r.dS;
+              cp_src = (uint32_t)(P.p - sbase);
+              cp_len = P.n;
+            } else {
+              cp_src = (uint32_t)(P.p + r.dS - sbase);
+              cp_len = r.dE - r.dS;
+            }
+          }
+        }
+      }
+    }
+    if (mine) {
+      out.doff_dev[i] = doff;
+      out.plen_dev[i] = plen;
+      out.kind_dev[i] = r.kind;
+      out.status_dev[i] = r.status;
+    }
+    wave_sync();
+    // ---- copy-out: one line at a time, 64 consecutive bytes per store instruction
+    uint64_t cm = __ballot(cp_len > 0);
+    while (cm) {
+      const int j = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      const uint8_t* src = sbase + __shfl((int)cp_src, j);
+      uint8_t* dst = out.slot_dev + 3 * shfl64(lo, j);
+      const int len = __shfl(cp_len, j);
+      for (int q = lane; q < len; q += 64) dst[q] = src[q];
+    }
+    wave_sync();
+    next = k;
+  }
 }
 
 // ---- selection lists (sdx_select_lines): class of a parsed line, -1 = not demodulated
@@ -735,8 +942,11 @@ extern "C" int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out,
       !out->cp_slot_dev || !out->ms_ok_dev || !out->clock_dev || !out->mcbitnum_dev || !out->mcflags_dev ||
       !out->meta_dev || !out->plen_dev)
     return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: null buffer");
-  const int grid = (lines->n + 255) / 256;
-  hipLaunchKernelGGL(sdxl::k_parse_lines, dim3(grid), dim3(256), 0, (hipStream_t)hip_stream, *lines, *out);
+  if (((uintptr_t)out->meta_dev & 15) != 0)
+    return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: meta_dev must be 16-byte aligned");
+  const int per_block = 64 * sdxl::PW;
+  const int grid = (lines->n + per_block - 1) / per_block;
+  hipLaunchKernelGGL(sdxl::k_parse_lines, dim3(grid), dim3(per_block), 0, (hipStream_t)hip_stream, *lines, *out);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("sdx_parse_lines: ") + hipGetErrorString(e));
   return SDX_OK;

@@ -212,7 +212,9 @@ class SignalParser:
         if "MS" in res:
             pv = lb.pat_val[: 10 * n].cpu().numpy().reshape(n, 10)
             cps = lb.cp_slot[:n].cpu().numpy().astype(np.int64)
-            ms_clock = np.abs(pv[np.arange(n), np.maximum(cps, 0)])
+            ok_ms = (kind == runtime.LINE_MS) & (status == runtime.LS_OK)  # cp_slot is written for these
+            cps = np.where(ok_ms, np.clip(cps, 0, 9), 0)
+            ms_clock = np.abs(pv[np.arange(n), cps])
         hb = {k: v[2].tobytes() for k, v in res.items()}
         out: List[Any] = []
         for i in range(n):
