@@ -141,7 +141,8 @@ enum sdx_line_status {
 };
 
 typedef struct {
-  const uint8_t* bytes_dev;    /* all lines concatenated */
+  const uint8_t* bytes_dev;    /* all lines concatenated; 8-byte aligned and readable 16 bytes past
+                                * offsets[n] (the kernel reads whole aligned 8-byte words) */
   const int64_t* offsets_dev;  /* [n+1] line i = bytes[offsets[i], offsets[i+1]) */
   int32_t n;
 } sdx_lines;
@@ -149,7 +150,8 @@ typedef struct {
 typedef struct {
   uint8_t* kind_dev;           /* [n] enum sdx_line_kind */
   uint8_t* status_dev;         /* [n] enum sdx_line_status */
-  uint8_t* slot_dev;           /* [3 * offsets[n] + 16] per-line slots: line i owns [3*offsets[i], 3*offsets[i+1]) */
+  uint8_t* slot_dev;           /* [3 * offsets[n] + 16], 8-byte aligned; per-line slots: line i owns
+                                * [3*offsets[i], 3*offsets[i+1]) */
   int64_t* doff_dev;           /* [n] start of the D (MU/MS) or hex (MC) characters in slot_dev */
   int32_t* dlen_dev;           /* [n] their length */
   uint8_t* npat_dev;           /* [n]   MU/MS: patterns (see sdx_pulse_batch) */
@@ -173,7 +175,7 @@ typedef struct {
  * fields only where they mean something: dlen and meta for SDX_LS_OK lines, the pattern fields
  * (npat, pat_id/pat_val[0..npat)) for OK MU/MS lines, cp_slot/ms_ok for OK MS lines, clock/
  * mcbitnum/mcflags for OK MC lines, and plen plus the slot payload for OK decompressed lines.
- * meta_dev must be 16-byte aligned. */
+ * meta_dev must be 16-byte aligned; bytes_dev and slot_dev 8-byte aligned. */
 int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out, void* hip_stream);
 
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */

@@ -214,7 +214,7 @@ def parse_line(line: bytes) -> Dict[str, Any]:
                 if not _INT15.fullmatch(v) or int(k[1:]) >= 10:
                     r["status"] = UNSUPPORTED
                     return r
-                slot[int(k[1:])] = float(int(v))
+                slot[int(k[1:])] = float(v)                  # "-0" -> -0.0, as the reference
         ids, vals = list(slot.keys()), list(slot.values())
     if len(data) > LONG_MAX:
         r["status"] = UNSUPPORTED

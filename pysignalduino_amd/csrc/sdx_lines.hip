@@ -46,14 +46,38 @@ LD bool py_alnum_ascii(uint8_t c) { return c < 128 && (digit(c) || ((c | 32) >= 
 LD uint8_t up(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
 LD int hexv(uint8_t c) { return digit(c) ? c - '0' : ((c | 32) - 'a' + 10); }
 
-struct Writer {
-  uint8_t* d;
+// appends bytes to global memory, one 8-byte store per aligned word; the first and the last
+// (partial) words are written byte by byte, so no byte outside [d, d + n) is touched
+struct Writer8 {
+  uint8_t* w;    // aligned word being filled
   int n, cap;
   bool ovf;
+  uint64_t acc;
+  int fill;      // bytes of the word filled (incl. the skipped head)
+  int head;      // bytes of the first word before d
+  LD Writer8(uint8_t* dst, int capacity)
+      : w(dst - ((uintptr_t)dst & 7)), n(0), cap(capacity), ovf(false), acc(0), fill((int)((uintptr_t)dst & 7)),
+        head((int)((uintptr_t)dst & 7)) {}
+  LD void flush() {
+    if (head) {
+      for (int k = head; k < 8; ++k) w[k] = (uint8_t)(acc >> (8 * k));
+      head = 0;
+    } else {
+      *reinterpret_cast<uint64_t*>(w) = acc;
+    }
+    w += 8;
+    acc = 0;
+    fill = 0;
+  }
   LD void put(uint8_t c) {
-    if (n < cap) d[n] = c;
-    else ovf = true;
+    if (n >= cap) {
+      ovf = true;
+      ++n;
+      return;
+    }
+    acc |= (uint64_t)c << (8 * fill);
     ++n;
+    if (++fill == 8) flush();
   }
   LD void put_uint(uint32_t v) {
     char t[10];
@@ -63,6 +87,10 @@ struct Writer {
       v /= 10;
     } while (v);
     while (k) put((uint8_t)t[--k]);
+  }
+  LD void finish() {
+    for (int k = head; k < fill; ++k) w[k] = (uint8_t)(acc >> (8 * k));
+    fill = head = 0;
   }
 };
 
@@ -96,82 +124,135 @@ LD bool d_field(const Str& P, int s, int e) {
 
 // decompress_payload (base.py:13-186) into w; returns false when an upper() of a non-ASCII
 // character would be needed (UNSUPPORTED)
-LD bool decompress(const Str& P, Writer& w) {
-  int pos = 0, s, e;
-  bool first = true;
-  while (next_part(P, pos, s, e)) {
-    const uint8_t m0 = P.p[s];
-    const int m1s = s + 1, m1n = e - s - 1;
-    const int mark = w.n;
-    if (!first) w.put(';');
-    bool emitted = true;
-    if (m0 == 'D' || m0 == 'd') {  // :59-140, with the merge of ';'-split binary data
-      w.put('D');
-      w.put('=');
-      const int d0 = w.n;
-      auto emit_byte = [&](uint8_t c) {
-        w.put_uint((c >> 4) & 0xF);
-        w.put((uint8_t)('0' + (c & 0x7)));
-      };
-      for (int i = m1s; i < e; ++i) emit_byte(P.p[i]);
-      int j = pos, s2, e2;
-      while (true) {
-        const int before = j;
-        if (!next_part(P, j, s2, e2)) {
-          pos = j;
-          break;
-        }
-        if (d_field(P, s2, e2)) {
-          pos = before;  // the loop resumes at this part
-          break;
-        }
-        emit_byte(';');  // cur += ';' + next_part (empty parts in between are dropped)
-        for (int i = s2; i < e2; ++i) emit_byte(P.p[i]);
-        pos = j;
-      }
-      if (m0 == 'd' && w.n > d0) w.n -= 1;  // :130-131
-      if (w.n > d0 && w.n <= w.cap && w.d[d0] == '8') {  // :134-135
-        for (int i = d0; i + 1 < w.n && i + 1 < w.cap; ++i) w.d[i] = w.d[i + 1];
-        w.n -= 1;
-      }
-    } else if (m0 == 'M') {  // :144-146
-      w.put('M');
-      for (int i = m1s; i < e; ++i) {
-        if (P.p[i] >= 128) return false;
-        w.put(up(P.p[i]));
-      }
-    } else if (m0 > 127) {  // :149-165
-      w.put('P');
-      w.put((uint8_t)('0' + (m0 & 7)));
-      w.put('=');
-      if (m1n == 2) {
-        uint32_t ml = P.p[m1s] & 127, mh = P.p[m1s + 1] & 127;
-        if (m0 & 32) w.put('-');
-        if (m0 & 16) ml += 128;
-        w.put_uint(mh * 256 + ml);
-      }
-    } else if ((m0 == 'C' || m0 == 'S') && m1n == 1) {  // :168-169
-      w.put(m0);
-      w.put('P');
-      w.put('=');
-      w.put(P.p[m1s]);
-    } else if (m0 == 'o' || m0 == 'm') {  // :172-173
-      for (int i = s; i < e; ++i) w.put(P.p[i]);
-    } else if (m1n >= 1 && m1n <= 2 && hexc(P.p[m1s]) && (m1n == 1 || hexc(P.p[m1s + 1]))) {  // :176-177
-      w.put(m0);
-      w.put('=');
-      w.put_uint(m1n == 1 ? hexv(P.p[m1s]) : 16 * hexv(P.p[m1s]) + hexv(P.p[m1s + 1]));
-    } else if (py_alnum_ascii(m0)) {  // :180-181
-      w.put(m0);
-      if (m1n) w.put('=');
-      for (int i = m1s; i < e; ++i) w.put(P.p[i]);
-    } else {
-      emitted = false;
+// one non-D part of decompress_payload (base.py:142-181); false: str.upper() of a non-ASCII byte
+LD bool dec_part(const Str& P, int s, int e, Writer8& w) {
+  const uint8_t m0 = P.p[s];
+  const int m1s = s + 1, m1n = e - s - 1;
+  if (m0 == 'M') {  // :144-146
+    w.put('M');
+    for (int i = m1s; i < e; ++i) {
+      if (P.p[i] >= 128) return false;
+      w.put(up(P.p[i]));
     }
-    if (emitted) first = false;
-    else w.n = mark;  // no part, no separator
+  } else if (m0 > 127) {  // :149-165
+    w.put('P');
+    w.put((uint8_t)('0' + (m0 & 7)));
+    w.put('=');
+    if (m1n == 2) {
+      uint32_t ml = P.p[m1s] & 127, mh = P.p[m1s + 1] & 127;
+      if (m0 & 32) w.put('-');
+      if (m0 & 16) ml += 128;
+      w.put_uint(mh * 256 + ml);
+    }
+  } else if ((m0 == 'C' || m0 == 'S') && m1n == 1) {  // :168-169
+    w.put(m0);
+    w.put('P');
+    w.put('=');
+    w.put(P.p[m1s]);
+  } else if (m0 == 'o' || m0 == 'm') {  // :172-173
+    for (int i = s; i < e; ++i) w.put(P.p[i]);
+  } else if (m1n >= 1 && m1n <= 2 && hexc(P.p[m1s]) && (m1n == 1 || hexc(P.p[m1s + 1]))) {  // :176-177
+    w.put(m0);
+    w.put('=');
+    w.put_uint(m1n == 1 ? hexv(P.p[m1s]) : 16 * hexv(P.p[m1s]) + hexv(P.p[m1s + 1]));
+  } else {  // :180-181 (ASCII alnum)
+    w.put(m0);
+    if (m1n) w.put('=');
+    for (int i = m1s; i < e; ++i) w.put(P.p[i]);
+  }
+  return true;
+}
+
+// does decompress_payload emit anything for this part (the branches of :59-181)
+LD bool dec_emits(const Str& P, int s, int e) {
+  const uint8_t m0 = P.p[s];
+  const int m1n = e - s - 1;
+  return m0 == 'D' || m0 == 'd' || m0 == 'M' || m0 > 127 || ((m0 == 'C' || m0 == 'S') && m1n == 1) || m0 == 'o' ||
+         m0 == 'm' || (m1n >= 1 && m1n <= 2 && hexc(P.p[s + 1]) && (m1n == 1 || hexc(P.p[s + 2]))) ||
+         py_alnum_ascii(m0);
+}
+
+// a D/d part (:59-140) starting at part [s, e); pos = where the part loop resumes
+LD void dec_data(const Str& P, int s, int e, int& pos, Writer8& w) {
+  const uint8_t m0 = P.p[s];
+  const int m1s = s + 1;
+  w.put('D');
+  w.put('=');
+  // extent: the first part plus the following parts that do not start a field
+  int lastend = e, j = pos, s2, e2;
+  while (true) {
+    const int before = j;
+    if (!next_part(P, j, s2, e2)) {
+      pos = j;
+      break;
+    }
+    if (d_field(P, s2, e2)) {
+      pos = before;  // the loop resumes at this part
+      break;
+    }
+    lastend = e2;
+    pos = j;
+  }
+  // f"{(c >> 4) & 15}{c & 7}" for every byte of m1 + (';' + part)*, runs of ';' collapsed (the empty
+  // parts in between are dropped); 'd' drops the last digit (:130-131), then a leading '8' is
+  // dropped (:134-135) -- both applied while streaming.  Bytes are read eight at a time.
+  bool firstc = true;
+  uint8_t prev = 0;
+  const uint8_t* q = P.p + m1s;
+  const int al = (int)((uintptr_t)q & 7);
+  const uint64_t* wp = reinterpret_cast<const uint64_t*>(q - al);
+  for (int k0 = m1s - al; k0 < lastend; k0 += 8) {
+    const uint64_t x = *wp++;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int k = k0 + b;
+      if (k < m1s || k >= lastend) continue;
+      const uint8_t c = (uint8_t)(x >> (8 * b));
+      const bool skip = c == ';' && k > m1s && prev == ';';
+      prev = c;
+      if (skip) continue;
+      const uint8_t h = (c >> 4) & 0xF;
+      uint8_t c1 = h >= 10 ? '1' : (uint8_t)('0' + h);
+      if (firstc) {
+        firstc = false;
+        if (c1 == '8') c1 = 0;  // the leading '8'
+      }
+      if (c1) w.put(c1);
+      if (h >= 10) w.put((uint8_t)('0' + h - 10));
+      if (!(m0 == 'd' && k == lastend - 1)) w.put((uint8_t)('0' + (c & 0x7)));
+    }
+  }
+}
+
+// decompress_payload (base.py:13-186) of a payload that has a byte > 127 after its header.  The
+// parts before the first D/d part, that part, and the rest are three loops, so that the lanes of
+// a wave expand their (long) data parts together.
+LD bool decompress(const Str& P, Writer8& w) {
+  int pos = 0, s = 0, e = 0;
+  bool first = true, dpart = false;
+  while (next_part(P, pos, s, e)) {  // parts before the data
+    if (P.p[s] == 'D' || P.p[s] == 'd') {
+      dpart = true;
+      break;
+    }
+    if (!dec_emits(P, s, e)) continue;
+    if (!first) w.put(';');
+    first = false;
+    if (!dec_part(P, s, e, w)) return false;
+  }
+  if (dpart) {
+    if (!first) w.put(';');
+    first = false;
+    dec_data(P, s, e, pos, w);
+    while (next_part(P, pos, s, e)) {  // the rest (a second data part is possible)
+      if (!dec_emits(P, s, e)) continue;
+      w.put(';');
+      if (P.p[s] == 'D' || P.p[s] == 'd') dec_data(P, s, e, pos, w);
+      else if (!dec_part(P, s, e, w)) return false;
+    }
   }
   w.put(';');  // :184
+  w.finish();
   return true;
 }
 
@@ -233,8 +314,9 @@ LD bool mu_valid(const Str& P) {
   return hasd;
 }
 
-// int value of [-+]?[0-9]{1,15} (exact as a double); 0 = empty, 1 = ok, 2 = something else
-LD int parse_int15(const Str& P, int s, int e, long long* v) {
+// float() of [-+]?[0-9]{1,15} (exact: |v| < 2^53; "-0" is -0.0 as in Python); 0 = empty,
+// 1 = ok, 2 = something else
+LD int parse_num15(const Str& P, int s, int e, double* v) {
   if (s == e) return 0;
   int i = s;
   bool neg = false;
@@ -248,7 +330,7 @@ LD int parse_int15(const Str& P, int s, int e, long long* v) {
     if (!digit(P.p[i])) return 2;
     x = 10 * x + (P.p[i] - '0');
   }
-  *v = neg ? -x : x;
+  *v = neg ? -(double)x : (double)x;
   return 1;
 }
 // int() of [-+]?[0-9]+ (any length): 0 = empty, 1 = ok, 2 = not decimal, 3 = ok but |v| >= 2^31
@@ -293,21 +375,14 @@ struct Field {
 
 
 // ---- the parse kernel -------------------------------------------------------------------------
-// One lane per line.  A wave first stages the byte span of its (next) lines into its own LDS region
-// with coalesced 16-byte loads, then every lane scans its line in LDS; compressed payloads are
-// decompressed into a per-wave LDS area (prefix-sum allocated), and at the end of a round the
-// wave copies each line's D characters (or whole decompressed payload) to the slot with
-// byte-consecutive stores.  A line longer than the stage buffer, or a payload whose decompression
-// does not fit the LDS area, takes the same code on global memory (exact, slower).
-constexpr int PW = 2;         // waves per workgroup
-constexpr int STAGE = 8192;   // staged line bytes per wave and round
-constexpr int DECB = 4096;    // decompressed payload bytes per wave and round
-
-struct alignas(16) ParseLds {
-  uint8_t stage[STAGE + 32];
-  uint8_t dec[DECB];
-  uint32_t pv[10 * 64];  // fast P-key table [id][lane]: last value start | end << 16
-};
+// One lane per line, reading its line straight from HBM: byte loads for the few positional checks,
+// aligned 8-byte loads with SWAR byte-class masks for every scan (framing, each field value).
+// Compressed payloads are decompressed into the line's own slot region (its final place,
+// RawFrame.line) and parsed there, by the same code.  Canonical payloads go through a one-pass
+// fast path; everything else through parse_payload (the reference's dict semantics in full).
+// The D characters of uncompressed lines are copied to the slot by the whole wave, one line at a
+// time with consecutive bytes per store instruction.
+constexpr int PT = 256;  // threads per workgroup
 
 struct LineRes {
   uint8_t kind = SDX_LINE_NONE, status = SDX_LS_NOFRAME;
@@ -315,45 +390,255 @@ struct LineRes {
   Field fR{-1, -1}, fF{-1, -1};
 };
 
-LD void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 LD int64_t shfl64(int64_t v, int src) {
   const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src);
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
-// extract_payload (base.py:188-206): payload = L[pa, pa + pn); also whether decompress_payload
-// runs on it (MS/MU/MO/MN with a byte >= 0x80 after the header).  One pass over the bytes.
-LD bool frame_line(const uint8_t* L, int len, int& pa, int& pn, bool& comp) {
-  int a = 0, b = len;
-  while (a < b && py_space(L[a])) ++a;
-  while (b > a && py_space(L[b - 1])) --b;
-  if (b - a < 6 || L[a] != 0x02 || L[b - 1] != 0x03 || L[a + 1] != 'M' || L[a + 3] != ';' || L[b - 2] != ';')
-    return false;
-  const uint8_t t = L[a + 2];
-  if (!(t == 's' || t == 'S' || t == 'u' || t == 'U' || t == 'c' || t == 'C' || t == 'N' || t == 'O' || t == 'o'))
-    return false;
-  uint8_t any = 0;
-  for (int k = a + 4; k < b - 2; ++k) {  // '.' does not match a newline
-    const uint8_t c = L[k];
-    if (c == '\n') return false;
-    any |= c;
-  }
-  const uint8_t t1 = up(t);
-  comp = (any & 0x80) && (t1 == 'S' || t1 == 'U' || t1 == 'O' || t1 == 'N');
-  pa = a + 1;
-  pn = b - a - 2;
-  return true;
 }
 
 LD bool same_key(const Str& P, int s1, int e1, int s2, int e2) {
   if (e1 - s1 != e2 - s2) return false;
   for (int k = 0; k < e1 - s1; ++k)
     if (P.p[s1 + k] != P.p[s2 + k]) return false;
+  return true;
+}
+
+constexpr uint64_t SW_L1 = 0x0101010101010101ull, SW_H = 0x8080808080808080ull;
+enum { CLS_DIGIT = 0, CLS_HEX = 1, CLS_ANY = 2 };
+
+LD uint64_t sw_digits(uint64_t x) {  // high bit of each byte: '0'..'9'
+  const uint64_t lo7 = x & ~SW_H;
+  const uint64_t ge = ((lo7 | SW_H) - SW_L1 * 0x30) & SW_H;
+  const uint64_t le = ((SW_L1 * 0x39 | SW_H) - lo7) & SW_H;
+  return ge & le & ~x;
+}
+LD uint64_t sw_hexalpha(uint64_t x) {  // 'a'..'f' / 'A'..'F'
+  const uint64_t lc = (x & ~SW_H) | (SW_L1 * 0x20);
+  const uint64_t ge = ((lc | SW_H) - SW_L1 * 0x61) & SW_H;
+  const uint64_t le = ((SW_L1 * 0x66 | SW_H) - lc) & SW_H;
+  return ge & le & ~x;
+}
+
+// position of the first ';' at or after s, or -1 when a byte outside the class comes first
+// (CLS_ANY: any ASCII byte).  P must end with ';'; the aligned 8-byte words around it are read.
+LD int scan_run(const uint8_t* P, int s, int cls) {
+  const uint8_t* q = P + s;
+  const int a = (int)((uintptr_t)q & 7);
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(q - a);
+  int base = s - a;
+  const uint64_t pre = a ? (~0ull >> (64 - 8 * a)) : 0ull;  // bytes before s: neutral '0'
+  uint64_t x = (*w & ~pre) | (SW_L1 * 0x30 & pre);
+  while (true) {
+    const uint64_t t = x ^ (SW_L1 * 0x3B);
+    const uint64_t semi = (t - SW_L1) & ~t & SW_H;
+    const uint64_t dg = sw_digits(x);
+    const uint64_t tn = x ^ (SW_L1 * 0x0A);  // CLS_ANY: ASCII, not a newline
+    const uint64_t nl = ((tn & ~SW_H) + ~SW_H | tn) & SW_H;  // high bit: byte != '\n'
+    const uint64_t ok = cls == CLS_DIGIT ? dg : cls == CLS_HEX ? (dg | sw_hexalpha(x)) : (~x & nl & SW_H);
+    const uint64_t bad = ~ok & SW_H;
+    if (semi) {
+      if (bad & ((semi & (0 - semi)) - 1)) return -1;  // a bad byte before the ';'
+      return base + (__builtin_ctzll(semi) >> 3);
+    }
+    if (bad) return -1;
+    base += 8;
+    x = *++w;
+  }
+}
+
+LD long long dec_value(const uint8_t* P, int s, int e) {
+  long long v = 0;
+  for (int k = s; k < e; ++k) v = 10 * v + (P[k] - '0');
+  return v;
+}
+
+// ---- fast path: canonical firmware payloads ------------------------------------------------
+// Sound but incomplete: it accepts only payloads in the firmware's canonical form -- per type a
+// fixed key set, each key at most once (pattern ids single digit, values plain decimal), no
+// non-ASCII bytes -- for which the reference's dict / gate semantics reduce to one left-to-right
+// pass; anything else returns false and parse_payload decides.  Every part costs one scan_run (so
+// the lanes of a wave share one loop whatever part they are in).
+enum {
+  KP = 1, KD, KCP, KSP, KR, KF, KC, KL, KLL, KLH, KSL, KSH, KM, KW, KIGN
+};
+
+LD bool fast_payload(const uint8_t* P, int n, LineRes& r, const sdx_lines_out& out, int i) {
+  if (n < 4 || P[0] != 'M' || P[2] != ';' || P[n - 1] != ';') return false;
+  const uint8_t t = P[1];
+  const bool mu = t == 'U', ms = t == 'S', mc = t == 'C';
+  if (!mu && !ms && !mc) return false;
+  uint32_t have = 0, ids = 0;
+  uint64_t idord = 0;
+  int np = 0;
+  int dS = 0, dE = 0, rS = -1, rE = -1, fS = -1, fE = -1, cpS = 0, cpE = 0;
+  long long cval = 0, lval = 0;
+  bool phase1 = false;  // MU: past the P items
+  double* pval = out.pat_val_dev + 10 * (int64_t)i;
+  uint8_t* pid = out.pat_id_dev + 10 * (int64_t)i;
+  int s = 3;
+  while (s < n) {
+    const uint8_t b0 = P[s];
+    if (b0 == ';') {  // an empty part: skipped by the parsers, a mismatch for the MU regex
+      if (mu) return false;
+      ++s;
+      continue;
+    }
+    const uint8_t b1 = P[s + 1], b2 = s + 2 < n ? P[s + 2] : 0;
+    // 1. the key, where its value starts, the value's byte class
+    int key = 0, vs = s, cls = CLS_ANY;
+    bool sign = false;
+    if (b0 == 'P' && digit(b1) && b2 == '=') {
+      key = KP, vs = s + 3, cls = CLS_DIGIT, sign = true;
+    } else if (b1 == '=') {
+      vs = s + 2;
+      if (b0 == 'D') key = KD, cls = mc ? CLS_HEX : CLS_DIGIT;
+      else if (b0 == 'R') key = KR, cls = CLS_DIGIT, sign = mc;
+      else if (b0 == 'F') key = KF, cls = mc ? CLS_DIGIT : CLS_ANY, sign = mc;
+      else if (mc && b0 == 'C') key = KC, cls = CLS_DIGIT;
+      else if (mc && b0 == 'L') key = KL, cls = CLS_DIGIT;
+      else if (mc && b0 == 'M') key = KM, cls = CLS_HEX, sign = true;
+      else if (mu && b0 == 'w') key = KW, cls = CLS_DIGIT;
+    } else if (b2 == '=') {
+      vs = s + 3, cls = CLS_DIGIT;
+      if (b0 == 'C' && b1 == 'P' && !mc) key = KCP;
+      else if (b0 == 'S' && b1 == 'P' && ms) key = KSP;
+      else if (mc && b0 == 'L' && (b1 == 'L' || b1 == 'H')) key = b1 == 'L' ? KLL : KLH, cls = CLS_HEX, sign = true;
+      else if (mc && b0 == 'S' && (b1 == 'L' || b1 == 'H')) key = b1 == 'L' ? KSL : KSH, cls = CLS_HEX, sign = true;
+    }
+    if (!key) {  // a part no rule of this path names: MU O;/e;/p;, MS parts no gate reads
+      if (mc) return false;
+      if (ms && (b0 == 'P' || b0 == 'D' || b0 == 'C' || b0 == 'S' || b0 == 'R' || b0 == 'F')) return false;
+      if (mu && !((b0 == 'O' || b0 == 'e' || b0 == 'p') && b1 == ';')) return false;
+      key = KIGN, vs = s, cls = CLS_ANY;
+    }
+    int v0 = vs;
+    bool neg = false;
+    if (sign && (P[v0] == '-' || P[v0] == '+')) {
+      if (P[v0] == '+' && key == KP) return false;  // float("+5"): left to parse_payload
+      neg = P[v0] == '-';
+      ++v0;
+    }
+    // 2. one scan for every kind of part
+    const int e = scan_run(P, v0, cls);
+    if (e < 0) return false;
+    const int nv = e - v0;
+    // 3. the key's rule
+    const uint32_t bit = 1u << key;
+    if (key != KP && key != KIGN && key != KW) {
+      if (have & bit) return false;  // a repeated key: dict semantics left to parse_payload
+      have |= bit;
+    }
+    if (mu && key != KP) {
+      if (np < 2) return false;
+      phase1 = true;
+    }
+    switch (key) {
+      case KP: {
+        if (mc || (mu && (phase1 || b1 > '7' || np == 8))) return false;
+        const int id = b1 - '0';
+        if (((ids >> id) & 1) || nv < 1 || nv > (mu ? 5 : 15)) return false;
+        const double v = (double)dec_value(P, v0, e);
+        pval[np] = neg ? -v : v;
+        pid[np] = b1;
+        ids |= 1u << id;
+        idord |= (uint64_t)id << (4 * np);
+        ++np;
+        break;
+      }
+      case KD:
+        if (nv < (mu ? 2 : 1)) return false;
+        dS = v0, dE = e;
+        break;
+      case KCP:
+        if (nv < 1 || nv > (mu ? 1 : 9)) return false;
+        cpS = v0, cpE = e;
+        break;
+      case KSP:
+      case KLL:
+      case KLH:
+      case KSL:
+      case KSH:
+      case KM:
+        if (nv < 1) return false;
+        break;
+      case KR:
+        if (nv < 1) return false;
+        rS = vs, rE = e;
+        break;
+      case KF:
+        if (mu || (mc && nv < 1)) return false;
+        fS = vs, fE = e;
+        break;
+      case KC:
+      case KL:
+        if (nv < 1 || nv > 9) return false;
+        (key == KC ? cval : lval) = dec_value(P, v0, e);
+        break;
+      case KW:
+        if (nv != 1) return false;
+        break;
+      default:  // KIGN
+        if (mu && e != s + 1) return false;
+        break;
+    }
+    s = e + 1;
+  }
+  if (!(have & (1u << KD))) return false;
+  if ((rS >= 0 && rE - rS > 15) || (fS >= 0 && fE - fS > 15)) return false;
+  if (mc) {
+    if ((have & ((1u << KC) | (1u << KL))) != ((1u << KC) | (1u << KL)) || dE - dS > SDX_MC_HEX_MAX) return false;
+    out.clock_dev[i] = (int32_t)cval;
+    out.mcbitnum_dev[i] = (int32_t)lval;
+    out.mcflags_dev[i] = 0;
+  } else {
+    if (dE - dS > SDX_LONG_MAX) return false;
+    if (ms) {
+      if ((have & ((1u << KCP) | (1u << KSP))) != ((1u << KCP) | (1u << KSP))) return false;
+      const long long cp = dec_value(P, cpS, cpE);
+      int8_t slotv = -1;
+      for (int z = 0; z < np; ++z)
+        if (cp < 10 && (int)((idord >> (4 * z)) & 15) == cp) slotv = (int8_t)z;
+      out.cp_slot_dev[i] = slotv;
+      out.ms_ok_dev[i] = slotv >= 0 ? 1 : 0;
+    }
+    out.npat_dev[i] = (uint8_t)np;
+  }
+  r.kind = mu ? SDX_LINE_MU : ms ? SDX_LINE_MS : SDX_LINE_MC;
+  r.status = SDX_LS_OK;
+  r.dS = dS;
+  r.dE = dE;
+  r.fR = Field{rS, rE};
+  r.fF = Field{fS, fE};
+  return true;
+}
+
+// extract_payload (base.py:188-206) on the stripped line L[a, b): the positional checks, then one
+// SWAR pass for '.' not matching a newline and for the bytes > 127 that make decompress_payload
+// run (MS/MU/MO/MN).  Reads the aligned 8-byte words around the range.
+LD bool frame_check(const uint8_t* L, int a, int b, bool& comp) {
+  if (b - a < 6 || L[a] != 0x02 || L[b - 1] != 0x03 || L[a + 1] != 'M' || L[a + 3] != ';' || L[b - 2] != ';')
+    return false;
+  const uint8_t t = L[a + 2];
+  if (!(t == 's' || t == 'S' || t == 'u' || t == 'U' || t == 'c' || t == 'C' || t == 'N' || t == 'O' || t == 'o'))
+    return false;
+  const int s = a + 4, e = b - 2;
+  uint64_t acc = 0;
+  if (s < e) {
+    const uint8_t* q = L + s;
+    const int al = (int)((uintptr_t)q & 7);
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(q - al);
+    int rem = e - s + al;
+    uint64_t m = al ? ~(~0ull >> (64 - 8 * al)) : ~0ull;
+    for (; rem > 0; rem -= 8, ++w) {
+      if (rem < 8) m &= ~0ull >> (64 - 8 * rem);
+      const uint64_t x = *w & m;
+      const uint64_t tt = x ^ (SW_L1 * 0x0A);
+      if ((tt - SW_L1) & ~tt & SW_H) return false;
+      acc |= x;
+      m = ~0ull;
+    }
+  }
+  const uint8_t t1 = up(t);
+  comp = (acc & SW_H) && (t1 == 'S' || t1 == 'U' || t1 == 'O' || t1 == 'N');
   return true;
 }
 
@@ -532,14 +817,14 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
       for (int q = 0; q < nord; ++q) {
         const int d = (int)((order >> (4 * q)) & 15);
         const uint32_t w = pvt[64 * d];
-        long long v;
-        const int rv = parse_int15(P, (int)(w & 0xFFFF), (int)(w >> 16), &v);
+        double v;
+        const int rv = parse_num15(P, (int)(w & 0xFFFF), (int)(w >> 16), &v);
         if (rv == 0) continue;  // float('') -> ValueError -> skipped
         if (rv == 2) {          // other float() syntax: not modelled
           r.status = SDX_LS_UNSUPPORTED;
           return;
         }
-        assign(d, (double)v);
+        assign(d, v);
       }
     } else if (want_pat) {
       pos = 0;
@@ -573,14 +858,14 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
         long long idv = 0;
         for (int k = s + 1; k < ke; ++k)
           if (idv < 1000) idv = 10 * idv + (P.p[k] - '0');
-        long long v;
-        const int rv = parse_int15(P, vs, ve, &v);
+        double v;
+        const int rv = parse_num15(P, vs, ve, &v);
         if (rv == 0) continue;
         if (rv == 2 || idv >= 10) {  // other float() syntax / a multi-character pattern id
           r.status = SDX_LS_UNSUPPORTED;
           return;
         }
-        assign((int)idv, (double)v);
+        assign((int)idv, v);
       }
     }
     if (fD.e - fD.s > SDX_LONG_MAX) {  // longer than the long demodulation variant takes
@@ -611,24 +896,25 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
   r.status = SDX_LS_OK;
 }
 
-// 16 bytes of meta_dev: value characters, length at byte 15 (255 = absent)
+// 16 bytes of meta_dev: value characters, length at byte 15 (255 = absent); the value (<= 15
+// bytes) is read as aligned 8-byte words and funnel-shifted
 LD uint4 meta16(const Str& P, Field f) {
-  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-  if (f.s < 0) {
-    w3 = 255u << 24;
+  if (f.s < 0) return make_uint4(0, 0, 0, 255u << 24);
+  const int n = f.e - f.s;
+  const uint8_t* q = P.p + f.s;
+  const int al = (int)((uintptr_t)q & 7);
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(q - al);
+  const uint64_t w0 = w[0], w1 = n + al > 8 ? w[1] : 0, w2 = n + al > 16 ? w[2] : 0;
+  uint64_t lo = al ? (w0 >> (8 * al)) | (w1 << (64 - 8 * al)) : w0;
+  uint64_t hi = al ? (w1 >> (8 * al)) | (w2 << (64 - 8 * al)) : w1;
+  if (n < 8) {
+    lo &= n ? (~0ull >> (64 - 8 * n)) : 0ull;
+    hi = 0;
   } else {
-    const int n = f.e - f.s;
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-      const uint32_t c = k < n ? (uint32_t)P.p[f.s + k] << (8 * (k & 3)) : 0u;
-      if (k < 4) w0 |= c;
-      else if (k < 8) w1 |= c;
-      else if (k < 12) w2 |= c;
-      else w3 |= c;
-    }
-    w3 |= (uint32_t)n << 24;
+    hi &= n > 8 ? (~0ull >> (64 - 8 * (n - 8))) : 0ull;
   }
-  return make_uint4(w0, w1, w2, w3);
+  hi = (hi & 0x00FFFFFFFFFFFFFFull) | ((uint64_t)n << 56);
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
 LD void finish_fields(const Str& P, const LineRes& r, const sdx_lines_out& out, int i) {
@@ -638,170 +924,126 @@ LD void finish_fields(const Str& P, const LineRes& r, const sdx_lines_out& out, 
   out.dlen_dev[i] = r.dE - r.dS;
 }
 
-// a line on global memory only (longer than the stage buffer): same rules, lane-serial copy
-LD void line_global(const sdx_lines& in, const sdx_lines_out& out, int i, int64_t lo, int64_t hi, uint32_t* pvt) {
-  const uint8_t* L = in.bytes_dev + lo;
-  LineRes r;
-  int pa = 0, pn = 0;
-  bool comp = false;
-  int plen = -1;
-  int64_t doff = 3 * lo;
-  if (frame_line(L, (int)(hi - lo), pa, pn, comp)) {
-    Str P{L + pa, pn};
-    uint8_t* slot = out.slot_dev + 3 * lo;
-    bool ok = true;
-    if (comp) {
-      Writer w{slot, 0, (int)(3 * (hi - lo)), false};
-      ok = decompress(P, w) && !w.ovf;
-      P = Str{slot, w.n};
-      plen = w.n;
-    }
-    if (!ok) {
-      r.status = SDX_LS_UNSUPPORTED;
-    } else {
-      parse_payload(P, r, out, i, pvt);
-      if (r.status == SDX_LS_OK) {
-        if (comp) {
-          doff = 3 * lo + r.dS;
-        } else {
-          for (int k = 0; k < r.dE - r.dS; ++k) slot[k] = P.p[r.dS + k];
+constexpr uint8_t ST_RARE = 0xFF;  // internal: compressed, but not recognisably at its first byte
+
+__global__ __launch_bounds__(PT) void k_parse_lines(sdx_lines in, sdx_lines_out out) {
+  __shared__ uint32_t pv[PT / 64][10 * 64];  // parse_payload's P-key table, per lane
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * PT + threadIdx.x;
+  const bool valid = i < in.n;
+  uint32_t* pvt = pv[threadIdx.x >> 6] + lane;
+  int64_t cp_src = 0, cp_dst = 0;  // uncompressed OK lines: the D characters, copied by the wave
+  int cp_len = 0;
+  if (valid) {
+    const int64_t lo = in.offsets_dev[i], hi = in.offsets_dev[i + 1];
+    const uint8_t* L = in.bytes_dev + lo;
+    const int len = (int)(hi - lo);
+    LineRes r;
+    int64_t doff = 3 * lo;
+    int plen = -1;
+    int a = 0, b = len;  // str.strip() (transport.py:123)
+    while (a < b && py_space(L[a])) ++a;
+    while (b > a && py_space(L[b - 1])) --b;
+    // attempt 0: the fast path on the raw payload (its success implies the framing: every payload
+    // byte was checked to be ASCII and not a newline); attempt 1: extract_payload's checks, the
+    // decompression, and the general parser
+    const bool hdr = b - a >= 6 && L[a] == 0x02 && L[b - 1] == 0x03 && L[a + 1] == 'M' && L[a + 3] == ';' &&
+                     L[b - 2] == ';';
+    Str P{L + a + 1, b - a - 2};
+    const uint8_t t1 = hdr ? up(L[a + 2]) : 0;
+    // A payload whose first byte after the header has the high bit set is (the firmware's) Mred=1
+    // form: extract_payload's checks and the decompression into the slot region run first, then
+    // every lane runs the fast path on its payload (raw or decompressed) together.  Other lines
+    // reach extract_payload's checks only when the fast path declines (its success implies them:
+    // every payload byte was checked to be ASCII and not a newline); one that turns out to be
+    // compressed after all is finished by k_parse_rare.
+    const bool likely = hdr && (t1 == 'S' || t1 == 'U' || t1 == 'O' || t1 == 'N') && (L[a + 4] & 0x80);
+    bool framed = hdr, comp = false, decided = !hdr;
+    if (likely) {
+      framed = frame_check(L, a, b, comp);
+      decided = !framed;
+      if (framed && comp) {  // decompress_payload into the slot region, parsed there
+        Writer8 w(out.slot_dev + 3 * lo, 3 * len);
+        const bool ok = decompress(P, w) && !w.ovf;
+        P = Str{out.slot_dev + 3 * lo, w.n};
+        plen = ok ? w.n : -1;
+        if (!ok) {
+          r.status = SDX_LS_UNSUPPORTED;
+          decided = true;
         }
-        finish_fields(P, r, out, i);
       }
     }
+    if (!decided) {
+      const uint8_t ty = P.n > 1 ? P.p[1] : 0;
+      if (!((ty == 'U' || ty == 'S' || ty == 'C') && fast_payload(P.p, P.n, r, out, i))) {
+        bool c2 = false;
+        if (!likely && !frame_check(L, a, b, c2)) {
+          r.status = SDX_LS_NOFRAME;
+        } else if (c2) {
+          r.status = ST_RARE;
+        } else {
+          parse_payload(P, r, out, i, pvt);
+        }
+      }
+    }
+    if (r.status == SDX_LS_OK) {
+      finish_fields(P, r, out, i);
+      if (comp) {
+        doff = 3 * lo + r.dS;
+      } else {
+        doff = (3 * lo + 3) & ~3ll;  // word-aligned, inside the slot region (D < line length)
+        cp_src = (P.p + r.dS) - in.bytes_dev;
+        cp_dst = doff;
+        cp_len = r.dE - r.dS;
+      }
+    }
+    out.doff_dev[i] = doff;
+    out.plen_dev[i] = plen;
+    out.kind_dev[i] = r.kind;
+    out.status_dev[i] = r.status;
   }
-  out.doff_dev[i] = doff;
+  // the D characters of the wave's uncompressed OK lines, one line at a time: 4 bytes per lane
+  // (aligned source words realigned with v_alignbyte), 256 bytes per store instruction
+  uint64_t cm = __ballot(cp_len > 0);
+  while (cm) {
+    const int j = __builtin_ctzll(cm);
+    cm &= cm - 1;
+    const int64_t src = shfl64(cp_src, j);
+    const int sh = (int)(((uintptr_t)in.bytes_dev + src) & 3);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(in.bytes_dev + src - sh);
+    uint32_t* dw = reinterpret_cast<uint32_t*>(out.slot_dev + shfl64(cp_dst, j));
+    const int nw = (__shfl(cp_len, j) + 3) >> 2;
+    for (int q = lane; q < nw; q += 64) dw[q] = __builtin_amdgcn_alignbyte(sw[q + 1], sw[q], sh);
+  }
+}
+
+// the lines k_parse_lines left to it (ST_RARE): the whole extract_payload / decompress_payload /
+// parser sequence on global memory, general parser only
+__global__ __launch_bounds__(64) void k_parse_rare(sdx_lines in, sdx_lines_out out) {
+  __shared__ uint32_t pv[10 * 64];
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= in.n || out.status_dev[i] != ST_RARE) return;
+  const int64_t lo = in.offsets_dev[i];
+  const int len = (int)(in.offsets_dev[i + 1] - lo);
+  const uint8_t* L = in.bytes_dev + lo;
+  int a = 0, b = len;
+  while (a < b && py_space(L[a])) ++a;
+  while (b > a && py_space(L[b - 1])) --b;
+  LineRes r;
+  int plen = -1;
+  Writer8 w(out.slot_dev + 3 * lo, 3 * len);
+  if (!(decompress(Str{L + a + 1, b - a - 2}, w) && !w.ovf)) {
+    r.status = SDX_LS_UNSUPPORTED;
+  } else {
+    plen = w.n;
+    const Str P{out.slot_dev + 3 * lo, w.n};
+    parse_payload(P, r, out, i, pv + threadIdx.x);
+    if (r.status == SDX_LS_OK) finish_fields(P, r, out, i);
+  }
+  out.doff_dev[i] = 3 * lo + (r.status == SDX_LS_OK ? r.dS : 0);
   out.plen_dev[i] = plen;
   out.kind_dev[i] = r.kind;
   out.status_dev[i] = r.status;
-}
-
-__global__ __launch_bounds__(64 * PW) void k_parse_lines(sdx_lines in, sdx_lines_out out) {
-  __shared__ ParseLds sm[PW];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  ParseLds& S = sm[wave];
-  const int first = (blockIdx.x * PW + wave) * 64;
-  if (first >= in.n) return;  // wave-uniform
-  const int nv = min(64, in.n - first);
-  const int i = first + lane;
-  const bool valid = lane < nv;
-  const int64_t total = in.offsets_dev[in.n];
-  int64_t lo = 0, hi = 0;
-  if (valid) {
-    lo = in.offsets_dev[i];
-    hi = in.offsets_dev[i + 1];
-  }
-  uint32_t* pvt = S.pv + lane;
-  uint8_t* const sbase = reinterpret_cast<uint8_t*>(&S);
-  int next = 0;
-  while (next < nv) {
-    const int64_t base = shfl64(lo, next);
-    const bool fits = valid && lane >= next && hi - base <= STAGE;
-    const int k = next + __popcll(__ballot(fits));  // hi is monotone: the fitting lanes are next..k-1
-    if (k == next) {  // line `next` alone exceeds the stage buffer
-      if (lane == next) line_global(in, out, i, lo, hi, pvt);
-      ++next;
-      continue;
-    }
-    // ---- stage bytes [base, end) with 16-byte loads: LDS byte j <-> global byte (ga + j)
-    const int64_t end = shfl64(hi, k - 1);
-    const uint8_t* gb = in.bytes_dev + base;
-    const int sh = (int)((uintptr_t)gb & 15);
-    const uint8_t* ga = gb - sh;
-    const int nch = (int)((end - base + sh + 15) >> 4);
-    const uint8_t* glo = in.bytes_dev;
-    const uint8_t* ghi = in.bytes_dev + total;
-    for (int c = lane; c < nch; c += 64) {
-      const uint8_t* src = ga + 16 * c;
-      if (src >= glo && src + 16 <= ghi) {
-        *reinterpret_cast<uint4*>(S.stage + 16 * c) = *reinterpret_cast<const uint4*>(src);
-      } else {
-        for (int q = 0; q < 16; ++q) S.stage[16 * c + q] = (src + q >= glo && src + q < ghi) ? src[q] : 0;
-      }
-    }
-    wave_sync();
-    const bool mine = lane >= next && lane < k;
-    LineRes r;
-    int pa = 0, pn = 0;
-    bool comp = false, framed = false;
-    const uint8_t* L = S.stage + sh + (lo - base);
-    if (mine) framed = frame_line(L, (int)(hi - lo), pa, pn, comp);
-    // decompression targets: prefix-sum allocation in the wave's LDS area, else the global slot
-    const int ub = (mine && framed && comp) ? 3 * pn + 16 : 0;
-    int incl = ub;
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
-    }
-    const int doff_l = incl - ub;
-    const bool dec_lds = incl <= DECB;
-    int plen = -1;
-    int64_t doff = 3 * lo;
-    uint32_t cp_src = 0;
-    int cp_len = 0;
-    if (mine && framed) {
-      const Str Ps{L + pa, pn};
-      if (comp && !dec_lds) {  // the LDS area is full: decompress into the slot and parse there
-        uint8_t* slot = out.slot_dev + 3 * lo;
-        Writer w{slot, 0, (int)(3 * (hi - lo)), false};
-        if (!decompress(Ps, w) || w.ovf) {
-          r.status = SDX_LS_UNSUPPORTED;
-        } else {
-          const Str P{slot, w.n};
-          plen = w.n;
-          parse_payload(P, r, out, i, pvt);
-          if (r.status == SDX_LS_OK) {
-            doff = 3 * lo + r.dS;
-            finish_fields(P, r, out, i);
-          }
-        }
-      } else {
-        bool ok = true;
-        Str P = Ps;
-        if (comp) {
-          Writer w{S.dec + doff_l, 0, ub, false};
-          ok = decompress(Ps, w) && !w.ovf;
-          P = Str{S.dec + doff_l, w.n};
-          plen = w.n;
-        }
-        if (!ok) {
-          r.status = SDX_LS_UNSUPPORTED;
-        } else {
-          parse_payload(P, r, out, i, pvt);
-          if (r.status == SDX_LS_OK) {
-            finish_fields(P, r, out, i);
-            if (comp) {  // the whole payload goes to the slot (RawFrame.line), D inside it
-              doff = 3 * lo + r.dS;
-              cp_src = (uint32_t)(P.p - sbase);
-              cp_len = P.n;
-            } else {
-              cp_src = (uint32_t)(P.p + r.dS - sbase);
-              cp_len = r.dE - r.dS;
-            }
-          }
-        }
-      }
-    }
-    if (mine) {
-      out.doff_dev[i] = doff;
-      out.plen_dev[i] = plen;
-      out.kind_dev[i] = r.kind;
-      out.status_dev[i] = r.status;
-    }
-    wave_sync();
-    // ---- copy-out: one line at a time, 64 consecutive bytes per store instruction
-    uint64_t cm = __ballot(cp_len > 0);
-    while (cm) {
-      const int j = __builtin_ctzll(cm);
-      cm &= cm - 1;
-      const uint8_t* src = sbase + __shfl((int)cp_src, j);
-      uint8_t* dst = out.slot_dev + 3 * shfl64(lo, j);
-      const int len = __shfl(cp_len, j);
-      for (int q = lane; q < len; q += 64) dst[q] = src[q];
-    }
-    wave_sync();
-    next = k;
-  }
 }
 
 // ---- selection lists (sdx_select_lines): class of a parsed line, -1 = not demodulated
@@ -944,9 +1186,12 @@ extern "C" int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out,
     return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: null buffer");
   if (((uintptr_t)out->meta_dev & 15) != 0)
     return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: meta_dev must be 16-byte aligned");
-  const int per_block = 64 * sdxl::PW;
-  const int grid = (lines->n + per_block - 1) / per_block;
-  hipLaunchKernelGGL(sdxl::k_parse_lines, dim3(grid), dim3(per_block), 0, (hipStream_t)hip_stream, *lines, *out);
+  if (((uintptr_t)lines->bytes_dev & 7) != 0 || ((uintptr_t)out->slot_dev & 7) != 0)
+    return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: bytes_dev and slot_dev must be 8-byte aligned");
+  const int grid = (lines->n + sdxl::PT - 1) / sdxl::PT;
+  hipLaunchKernelGGL(sdxl::k_parse_lines, dim3(grid), dim3(sdxl::PT), 0, (hipStream_t)hip_stream, *lines, *out);
+  hipLaunchKernelGGL(sdxl::k_parse_rare, dim3((lines->n + 63) / 64), dim3(64), 0, (hipStream_t)hip_stream, *lines,
+                     *out);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("sdx_parse_lines: ") + hipGetErrorString(e));
   return SDX_OK;

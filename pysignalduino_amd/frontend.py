@@ -90,7 +90,8 @@ class LineBatch:
         total = int(offsets[-1])
         self.n = n
         self.eng = eng
-        self.bytes = t.from_numpy(data if len(data) else np.zeros(1, np.uint8)).to(d)
+        # 16 bytes of padding: the kernel reads whole aligned 8-byte words (include/sdx.h)
+        self.bytes = t.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(d)
         self.offsets = t.from_numpy(offsets).to(d)
         e = lambda k, dt: t.empty(max(k, 1), dtype=dt, device=d)  # noqa: E731
         self.kind, self.status = e(n, t.uint8), e(n, t.uint8)

@@ -155,8 +155,8 @@ def _compare(lines, dv):
             else:
                 npat = int(dv["npat"][i])
                 ids = [int(chr(c)) for c in dv["pat_id"][i][:npat]]
-                vals = list(dv["pat_val"][i][:npat])
-                if ids != r["ids"] or vals != r["vals"]:
+                vals = dv["pat_val"][i][:npat]
+                if ids != r["ids"] or vals.tobytes() != np.array(r["vals"], np.float64).tobytes():  # bitwise: -0.0
                     e.append(("patterns", ids, vals, r["ids"], r["vals"]))
                 if r["kind"] == LO.MS and (int(dv["ms_ok"][i]) != r["ms_ok"] or
                                            (r["ms_ok"] and int(dv["cp_slot"][i]) != r["cp_slot"])):

@@ -69,27 +69,31 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mix", default="1,1,1", help="MU,MS,MC proportions")
+    ap.add_argument("--compress-frac", type=float, default=0.3)
     args = ap.parse_args()
+    mix = tuple(float(x) for x in args.mix.split(","))
     import torch
     from pysignalduino_amd import bank as bankmod, frontend, runtime, synth
     torch.cuda.set_device(0)
     bk = bankmod.Bank()
     eng = runtime.Engine(bk, 0)
-    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"sdx_lines_{args.lines}_45.npz")
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                         f"sdx_lines_{args.lines}_45_{args.mix.replace(',', '-')}_{args.compress_frac}.npz")
     if os.path.exists(cache):  # the same seeded corpus, built once per box (profiling re-runs)
         z = np.load(cache)
         data, offsets = z["data"], z["offsets"]
         lines = [data[offsets[i]: offsets[i + 1]].tobytes() for i in range(len(offsets) - 1)]
     else:
-        lines, _ = synth.line_corpus(bk.protocols, args.lines, seed=45, mix=(1, 1, 1), compress_frac=0.3)
+        lines, _ = synth.line_corpus(bk.protocols, args.lines, seed=45, mix=mix, compress_frac=args.compress_frac)
         data, offsets, bad = frontend.pack_lines(lines)
         assert not bad
         np.savez(cache, data=data, offsets=offsets)
     n = len(lines)
     lb = frontend.LineBatch(eng, data, offsets)
     pb, mb = lb.pulse_batch(), lb.mc_batch()
-    outs = {"MU": eng.alloc_out(n, 4 * n + 4096, 100 * n + 65536), "MS": eng.alloc_out(n, 2 * n + 4096, 40 * n + 65536),
-            "MC": eng.alloc_out(n, 2 * n + 4096, 40 * n + 65536)}
+    outs = {"MU": eng.alloc_out(n, 8 * n + 4096, 160 * n + 65536), "MS": eng.alloc_out(n, 2 * n + 4096, 48 * n + 65536),
+            "MC": eng.alloc_out(n, 2 * n + 4096, 48 * n + 65536)}
     stream = torch.cuda.current_stream()
     names = ["parse+select", "MU", "MS", "MC"]
     ev = {k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in names}
@@ -165,8 +169,9 @@ def main():
         "value": value, "unit": "lines/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8+f64", "data": "synthetic firmware lines (pysignalduino_amd/synth.py line_corpus)",
-        "config": {"workload": "framed firmware lines, MU/MS/MC 1/3 each (MU 256 pulses), 30% of MU/MS Mred=1 "
-                               "compressed; parse + select + MU/MS/MC ('fixed') demodulation",
+        "config": {"workload": f"framed firmware lines, MU/MS/MC mix {args.mix} (MU 256 pulses), "
+                               f"{100 * args.compress_frac:.0f}% of MU/MS Mred=1 compressed; parse + select + "
+                               "MU/MS/MC ('fixed') demodulation",
                    "lines": n, "line_bytes": int(offsets[-1]), "classes": [int(c) for c in cnt]},
         "per_kernel_ms": {k: 1e3 * v for k, v in km.items()},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
