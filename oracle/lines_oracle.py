@@ -24,7 +24,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 NONE, MU, MS, MC, MN = 0, 1, 2, 3, 4
 OK, NOFRAME, NOPARSER, INVALID, NODATA, UNSUPPORTED, RAISES = 0, 1, 2, 3, 4, 5, 6
-SHORT_MAX, LONG_MAX, MC_HEX_MAX = 256, 4096, 128
+SHORT_MAX, LONG_MAX, MC_HEX_MAX, MN_HEX_MAX = 256, 4096, 128, 4096
 
 _WS = set(range(9, 14)) | set(range(0x1C, 0x21)) | {0x85, 0xA0}          # str.isspace() on latin-1
 _ALPHA_HI = {0xAA, 0xB5, 0xBA} | set(range(0xC0, 0xD7)) | set(range(0xD8, 0xF7)) | set(range(0xF8, 0x100))
@@ -124,6 +124,7 @@ _MC_VAL = re.compile(rb"[-+]?[0-9a-fA-F]+")
 _INT15 = re.compile(rb"[-+]?[0-9]{1,15}")
 _DEC = re.compile(rb"[-+]?[0-9]+")
 _MC_KEYS = {b"LL", b"LH", b"SL", b"SH", b"D", b"C", b"L", b"R", b"F", b"M", b"MC", b"Mc"}
+_MN_RE = re.compile(rb"^MN;D=(Y?)([0-9A-F]+);(?:R=([0-9]+);)?(?:A=(-?[0-9]{1,3});)?$")  # parser/mn.py:17
 
 
 def _kv(payload: bytes) -> List[Tuple[bytes, bytes]]:
@@ -184,7 +185,9 @@ def parse_line(line: bytes) -> Dict[str, Any]:
         r["status"] = NOPARSER
         return r
     r["kind"] = kind
-    if kind == MN or any(c > 127 for c in q):
+    if kind == MN:
+        return _mn(q, r)
+    if any(c > 127 for c in q):
         r["status"] = UNSUPPORTED
         return r
     if kind == MC:
@@ -281,6 +284,20 @@ def _mc(q: bytes, r: Dict[str, Any]) -> Dict[str, Any]:
     return r
 
 
+def _mn(q: bytes, r: Dict[str, Any]) -> Dict[str, Any]:
+    """parser/mn.py:33-51: ensure_message_type passes after routing; MN_PATTERN or ignored."""
+    m = _MN_RE.match(q)
+    if not m:
+        r["status"] = INVALID
+        return r
+    h, rr, a = m.group(2), m.group(3), m.group(4)
+    if len(h) > MN_HEX_MAX or (rr is not None and len(rr) > 15):
+        r["status"] = UNSUPPORTED
+        return r
+    r.update(status=OK, data=h, R=rr, F=a, rssi=None, freq_afc=None)
+    return r
+
+
 def sel_class(r: Dict[str, Any]) -> int:
     """sdx_select_lines class of a parsed line (-1: not demodulated)."""
     if r["status"] != OK:
@@ -290,4 +307,4 @@ def sel_class(r: Dict[str, Any]) -> int:
         return 0 if n <= SHORT_MAX else 1
     if r["kind"] == MS:
         return -1 if not r["ms_ok"] else (2 if n <= SHORT_MAX else 3)
-    return 4 if r["kind"] == MC else -1
+    return 4 if r["kind"] == MC else 5 if r["kind"] == MN else -1

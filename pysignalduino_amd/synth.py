@@ -458,3 +458,133 @@ def mutate_line(rng: np.random.Generator, line: bytes) -> bytes:
             parts[q] = parts[q][:1].lower() + parts[q][1:]
         return b";".join(parts)
     return bytes(b)
+
+
+# ---------------------------------------------------------------------------------------------
+# MN (FSK) frames: hex payloads that pass each 'modulation' protocol's regex,
+# length and checksum rules (the methods of sd_protocols/helpers.py:223-716), plus corrupted and
+# random ones.  Checksums are built with the generator-side helpers below (the product never uses
+# them: they construct inputs).
+# ---------------------------------------------------------------------------------------------
+_HEXD = "0123456789ABCDEF"
+
+
+def _hx(bs) -> str:
+    return "".join("%02X" % (int(b) & 0xFF) for b in bs)
+
+
+def _lfsr16_bytes(bs, gen: int, key: int) -> int:
+    acc = 0
+    for b in bs:
+        for i in range(7, -1, -1):
+            if (int(b) >> i) & 1:
+                acc ^= key
+            key = (key >> 1) ^ gen if key & 1 else key >> 1
+    return acc
+
+
+def _crc16_bytes(bs, poly: int) -> int:
+    crc = 0
+    for b in bs:
+        crc ^= int(b) << 8
+        for _ in range(8):
+            crc = ((crc << 1) ^ poly) & 0xFFFF if crc & 0x8000 else (crc << 1) & 0xFFFF
+    return crc
+
+
+def _crc8_bytes(bs) -> int:
+    crc = 0
+    for b in bs:
+        crc ^= int(b)
+        for _ in range(8):
+            crc = ((crc << 1) ^ 0x31) & 0xFF if crc & 0x80 else (crc << 1) & 0xFF
+    return crc
+
+
+def _xor_a(s: str) -> str:
+    return "".join(_HEXD[int(c, 16) ^ 0xA] for c in s)
+
+
+def _mn_valid(rng: np.random.Generator, kind: str) -> str:
+    """One frame that the named MN protocol family accepts (checksums valid)."""
+    rb = lambda k: rng.integers(0, 256, size=k)  # noqa: E731
+    tail = lambda: _hx(rb(int(rng.integers(0, 4))))  # noqa: E731
+    if kind == "lightning":            # helpers.py:223-280
+        body = rb(8)
+        x0 = _lfsr16_bytes(body, 0x8810, 0xABF9) ^ 0x899E
+        return _xor_a("%04X" % x0 + _hx(body)) + tail()
+    if kind == "5in1":                 # helpers.py:382-425
+        a = rb(13)
+        inv = [(~int(v)) & 0xFF for v in a]
+        inv[0] = sum(bin(v).count("1") for v in inv[1:])
+        a[0] = (~inv[0]) & 0xFF
+        return _hx(a) + _hx(inv) + tail()
+    if kind == "6in1":                 # helpers.py:427-471
+        mid = rb(15)
+        last = (0xFF - int(mid.sum())) & 0xFF
+        crc = _crc16_bytes(mid, 0x1021)
+        return "%04X" % crc + _hx(mid) + "%02X" % last + tail()
+    if kind == "7in1":                 # helpers.py:473-523
+        body = rb(21)
+        body[19] = body[19] if body[19] != 0xAA else 0xAB      # d[42:44] != '00'
+        x0 = _lfsr16_bytes(body, 0x8810, 0xBA95) ^ 0x6DF1
+        return _xor_a("%04X" % x0 + _hx(body)) + _hx(rb(int(rng.integers(0, 6))))
+    if kind == "pca301":               # helpers.py:525-579
+        body = rb(10)
+        return _hx(body) + "%04X" % _crc16_bytes(body, 0x8005) + _hx(rb(int(rng.integers(0, 21))))
+    if kind == "kopp":                 # helpers.py:581-628 (regexMatch ^0)
+        n = int(rng.integers(3, 16))
+        body = rb(n)
+        body[0] = n - 1
+        acc = 0xAA
+        for v in body:
+            acc ^= int(v)
+        return _hx(body) + "%02X" % acc + tail()
+    if kind == "lacrosse":             # helpers.py:630-716 (regexMatch ^9)
+        b = rb(4)
+        b[0] = 0x90 | (int(b[0]) & 0x0F)
+        if rng.random() < 0.8:         # a plausible temperature (the range check is tested too)
+            raw = int(rng.integers(1, 999))
+            b[1] = (int(b[1]) & 0xF0) | (raw // 100)
+            b[2] = ((raw // 10) % 10) << 4 | (raw % 10)
+        return _hx(b) + "%02X" % _crc8_bytes(b) + _hx(rb(int(rng.integers(0, 8))))
+    prefix, lo, hi = {"wh51": ("51", 28, 38), "wh57": ("57", 18, 38), "wh31": ("30", 22, 38),
+                      "wh31b": ("52", 22, 38), "wh40": ("40", 22, 38), "rojaflex": ("08", 18, 18),
+                      "avantek": ("", 16, 16), "ibs": ("D391", 36, 44), "wmbus": ("", 56, 300)}[kind]
+    n = int(rng.integers(lo, hi + 1))
+    return prefix + "".join(_HEXD[int(v)] for v in rng.integers(0, 16, size=n - len(prefix)))
+
+
+MN_KINDS = ("lightning", "5in1", "6in1", "7in1", "pca301", "kopp", "lacrosse", "wh51", "wh57", "wh31", "wh31b",
+            "wh40", "rojaflex", "avantek", "ibs", "wmbus")
+
+
+def mn_frames(n: int, seed: int = 46, noise_frac: float = 0.25, corrupt_frac: float = 0.15):
+    """n MN frames: (hex str, y_prefix bool, R int or None, A int or None).  Valid frames of every
+    protocol family, some with one nibble flipped (checksum failures), and random hex noise."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        u = rng.random()
+        if u < noise_frac:
+            k = int(rng.integers(1, 120))
+            h = "".join(_HEXD[int(v)] for v in rng.integers(0, 16, size=k))
+        else:
+            h = _mn_valid(rng, MN_KINDS[int(rng.integers(0, len(MN_KINDS)))])
+            if rng.random() < corrupt_frac / (1 - noise_frac):
+                j = int(rng.integers(0, len(h)))
+                h = h[:j] + _HEXD[int(h[j], 16) ^ int(rng.integers(1, 16))] + h[j + 1:]
+        y = bool(rng.random() < 0.1)
+        r = int(rng.integers(0, 256)) if rng.random() < 0.8 else None
+        a = int(rng.integers(-999, 1000)) if rng.random() < 0.6 else None
+        out.append((h, y, r, a))
+    return out
+
+
+def mn_payload(h: str, y: bool = False, r: Optional[int] = None, a: Optional[int] = None) -> bytes:
+    s = "MN;D=%s%s;" % ("Y" if y else "", h)
+    if r is not None:
+        s += "R=%d;" % r
+    if a is not None:
+        s += "A=%d;" % a
+    return s.encode("ascii")

@@ -38,7 +38,7 @@ def test_oracle_matches_reference_goldens(golden):
         exp_payload = c["payload"]
         got_payload = None if r["payload"] is None else r["payload"].decode("latin-1")
         ok = exp_payload == got_payload
-        if r["status"] in (LO.OK, LO.RAISES):
+        if r["status"] in (LO.OK, LO.RAISES) and r["kind"] != LO.MN:  # MNParser calls no demodulator
             ok = ok and c["calls"] == [[TYPE[r["kind"]], [list(kv) for kv in r["msg"]]]]
             fr = c["frame"]
             ok = ok and fr is not None and fr[0] == got_payload and fr[1] == TYPE[r["kind"]] \
