@@ -8,6 +8,9 @@
  *   SDProtocols.demodulate_ms(msg_data, msg_type)   sd_protocols/message_synced.py:10-243
  *   SDProtocols.demodulate_mc(msg_data, msg_type)   sd_protocols/sd_protocols.py:76-111
  *                                                   + manchester.py:49-144 ("fixed" mode)
+ *   MNParser.parse(frame) per-protocol loop         signalduino/parser/mn.py:79-191
+ *   SDProtocols.demodulate_mn / ConvBresser_* / ConvPCA301 / ConvKoppFreeControl / ConvLaCrosse
+ *                                                   sd_protocols/sd_protocols.py:113-154, helpers.py:190-716
  * The Python host mirror (pysignalduino_amd/sd_protocols.py) binds these with
  * ctypes; INTEGRATION.md shows the binding.  All pointers named *_dev are
  * device (HBM) pointers owned by the caller; the library never allocates in a
@@ -27,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 2
+#define SDX_ABI_VERSION 3
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -87,6 +90,22 @@ typedef struct {
   int32_t n, n_sel;
 } sdx_mc_batch;
 
+/* MN (FSK) batch: the hex characters of each frame (MN_PATTERN group 2, parser/mn.py:17) */
+typedef struct {
+  const uint8_t* hex_dev;      /* hex characters of all frames */
+  const int64_t* offsets_dev;  /* [n+1] frame i = hex[offsets[i], offsets[i+1]) (or + len[i]) */
+  const int32_t* len_dev;      /* optional [n] frame lengths (as sdx_pulse_batch.len_dev) */
+  const int32_t* sel_dev;      /* optional [n_sel] subset of frame indices to run, NULL = all */
+  int32_t n, n_sel;
+  uint64_t elig;               /* parser mode: bit k = MN protocol k (bank order) passes the rfmode filter
+                                * (parser/mn.py:83-93; the host folds MNParser.rfmode in) */
+  int32_t method;              /* -1: parser mode (MNParser.parse, results = bank protocols in order,
+                                * payload = preamble + decoded, a failed method gives "[]");
+                                * >= 1: method mode, enum sdx_mn_method: the method alone per frame
+                                * (SDProtocols.ConvX(msg_data)), 0 or 1 result with its payload */
+  int32_t res;
+} sdx_mn_batch;
+
 /* output buffers (caller-owned, device) */
 typedef struct {
   sdx_desc* desc_dev;          /* [n] */
@@ -117,6 +136,10 @@ int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch*
                           void* hip_stream);
 /* MC "fixed" chain: every frame x every clockrange protocol */
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream);
+/* MN (FSK): every frame x every 'modulation' protocol (parser mode) or one method (method mode).
+ * Frames must hold hex digits only ([0-9A-Fa-f]; the front end guarantees [0-9A-F]) and at most
+ * SDX_MN_HEX_MAX of them.  sdx_result.proto = MN table index (parser mode) / the method (method mode). */
+int sdx_demod_mn(const sdx_bank* bank, const sdx_mn_batch* batch, const sdx_out* out, void* hip_stream);
 
 /* ---- wire-line front end ------------------------------------------------------
  * Raw firmware lines, byte for byte as the transport receives them (the reference decodes them
@@ -126,7 +149,9 @@ int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out*
  * by payload[:2].upper(), the MU validity regex (parser/mu.py:48), _parse_to_dict and the "D"
  * check (mu.py:82-94, ms.py:65-78), and the MC header validation (parser/mc.py:37-155).  The
  * outputs of a line form message i of an sdx_pulse_batch (MU/MS) or sdx_mc_batch (MC) in slot
- * layout (len_dev set): no host repacking. */
+ * layout (len_dev set): no host repacking.  MN lines (parser/mn.py:31-51): MN_PATTERN is checked,
+ * the hex characters (without the 'Y' prefix) become frame i of an sdx_mn_batch, R and A are
+ * handed back raw in meta_dev (R at bytes 0-15, A at 16-31). */
 enum sdx_line_kind { SDX_LINE_NONE = 0, SDX_LINE_MU = 1, SDX_LINE_MS = 2, SDX_LINE_MC = 3, SDX_LINE_MN = 4 };
 enum sdx_line_status {
   SDX_LS_OK = 0,          /* routed to kind, ready for demodulation */
@@ -135,7 +160,7 @@ enum sdx_line_status {
   SDX_LS_INVALID = 3,     /* the parser rejects the line (MU regex, MC header, MC hex, R/F): ignored */
   SDX_LS_NODATA = 4,      /* no D field: ignored */
   SDX_LS_UNSUPPORTED = 5, /* outside the device contract (e.g. multi-digit P ids, non-integer P# values,
-                           * bytes >= 0x80 after decompression, MN): the caller must not guess */
+                           * bytes >= 0x80 after decompression): the caller must not guess */
   SDX_LS_RAISES = 6       /* handed to the demodulator, which raises (caught by the parser): no results
                            * (MC: int(C) / int(L) of a hex-lettered value) */
 };
@@ -181,13 +206,14 @@ int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out, void* hip_
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */
 #define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */
 #define SDX_MC_HEX_MAX 128  /* sdx_demod_mc */
+#define SDX_MN_HEX_MAX 4096 /* sdx_demod_mn */
 enum sdx_sel_class { SDX_SEL_MU_SHORT = 0, SDX_SEL_MU_LONG = 1, SDX_SEL_MS_SHORT = 2, SDX_SEL_MS_LONG = 3,
-                     SDX_SEL_MC = 4, SDX_SEL_NCLASS = 5 };
+                     SDX_SEL_MC = 4, SDX_SEL_MN = 5, SDX_SEL_NCLASS = 6 };
 #define SDX_SEL_CHUNK 1024  /* lines per selection workgroup */
 /* Selection lists for the demodulation launches, built on the device in line order: the OK lines
  * of each class (MS lines whose string gates failed are left out -- they have no results).  Class
  * k's line indices are sel_dev[start_k, start_k + counts[k]) with start_k = counts[0] + ... +
- * counts[k-1]; counts_dev[0..4] receives the class sizes (the only value a host needs back, to size
+ * counts[k-1]; counts_dev[0..5] receives the class sizes (the only value a host needs back, to size
  * the launches).  scratch_dev: 8 * ceil(n / SDX_SEL_CHUNK) int32.  Pass each list as sel_dev of an
  * sdx_pulse_batch / sdx_mc_batch whose arrays are the sdx_lines_out arrays (offsets = doff_dev,
  * len = dlen_dev, data = slot_dev). */

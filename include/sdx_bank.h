@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 8u
+#define SDX_BANK_VERSION 9u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -92,6 +92,29 @@ typedef struct {
   uint8_t has_lmin, has_lmax, lmax_is_str, invert, has_cr, res[3];
 } sdx_mc_proto;
 
+/* MN protocol = every id with 'modulation' (signalduino/parser/mn.py:80) */
+enum sdx_mn_method {
+  SDX_MN_RAW = 0,        /* no 'method': the payload is the hex data (mn.py:121) */
+  SDX_MN_LIGHTNING = 1,  /* helpers.py:223-280 ConvBresser_lightning */
+  SDX_MN_5IN1 = 2,       /* helpers.py:382-425 ConvBresser_5in1 */
+  SDX_MN_6IN1 = 3,       /* helpers.py:427-471 ConvBresser_6in1 */
+  SDX_MN_7IN1 = 4,       /* helpers.py:473-523 ConvBresser_7in1 */
+  SDX_MN_PCA301 = 5,     /* helpers.py:525-579 ConvPCA301 */
+  SDX_MN_KOPP = 6,       /* helpers.py:581-628 ConvKoppFreeControl */
+  SDX_MN_LACROSSE = 7,   /* helpers.py:630-716 ConvLaCrosse */
+  SDX_MN_MISSING = 255   /* a 'method' the reference class does not define: protocol skipped (mn.py:171-173) */
+};
+#define SDX_MN_MAX 64    /* MN protocols in a bank (sdx_mn_batch.elig is a 64-bit mask) */
+typedef struct {
+  int32_t proto_index;
+  int32_t lir_min;       /* length_in_range on len(hex) (helpers.py:124-166): -1 = none */
+  int32_t lir_max;       /* INT32_MAX = none */
+  int32_t dfa;           /* regexMatch search DFA (re.search, mn.py:104-113), -1 = no regexMatch */
+  int32_t method;        /* enum sdx_mn_method */
+  int32_t pre_off, pre_len;  /* preamble (mn.py:176-177) in the string heap */
+  int32_t res;
+} sdx_mn_proto;          /* 32 bytes */
+
 /* MU decode descriptor: the fields the compacted MU decode reads for one (message, protocol)
  * pair (message_unsynced.py:146-290), staged in LDS once per tile (the first SDX_MUDESC_LDS).
  * mm_on: 0 no modulematch; 1 LDS tables: st = mmtab[(mm_base + st) * 16 + digit] per hex digit,
@@ -129,6 +152,8 @@ typedef struct {
   uint32_t mmtab_bytes; /* <= SDX_MMTAB_LDS, multiple of 16 */
   uint32_t mm_states;   /* S: hex[S][16] at 0, flags[S] at 16*S, post tables at 17*S */
   uint32_t n_mu_groups; /* MU clock groups: order[n_mu + n_ms + g] .. [+ g + 1] bound group g */
+  uint32_t n_mn;        /* MN protocols (sdx_mn_proto[n_mn] at off_mn) */
+  uint32_t off_mn;
   uint32_t res;
 } sdx_bank_hdr;
 

@@ -28,7 +28,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 8
+MAGIC, VERSION = 0x4B4E4253, 9
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("klo", "<i4", (MAXUNIQ,)),
@@ -50,7 +50,9 @@ MC_REC = np.dtype([("cr_lo", "<f8"), ("cr_hi", "<f8"), ("proto_index", "<i4"), (
                    ("has_cr", "u1"), ("res", "u1", (3,))], align=True)
 DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4"),
                     ("t256_off", "<i4"), ("res", "<i4", (3,))])
-HDR_FMT = "<" + "I" * 26  # sdx_bank_hdr: 26 uint32
+MN_REC = np.dtype([("proto_index", "<i4"), ("lir_min", "<i4"), ("lir_max", "<i4"), ("dfa", "<i4"), ("method", "<i4"),
+                   ("pre_off", "<i4"), ("pre_len", "<i4"), ("res", "<i4")])
+HDR_FMT = "<" + "I" * 28  # sdx_bank_hdr: 28 uint32
 # MU decode descriptor (sdx_mu_desc): what the compacted decode reads per (message, protocol) pair,
 # staged in LDS once per tile
 MU_DESC = np.dtype([("pre", "u1", (16,)), ("post", "u1", (2,)), ("pre_len", "u1"), ("post_len", "u1"),
@@ -68,6 +70,16 @@ POSTDEMO = {"postDemo_EM": 1, "postDemo_Revolt": 2, "postDemo_FS20": 3, "postDem
 MC_METHODS = {"mcBit2Funkbus": 1, "mcBit2Sainlogic": 2, "mcBit2AS": 3, "mcBit2Hideki": 4, "mcBit2Maverick": 4,
               "mcBit2OSV1": 4, "mcBit2OSV2o3": 4, "mcBit2OSPIR": 4, "mcRaw": 5, "mcraw": 6, "mcBit2TFA": 7,
               "mcBit2Grothe": 8, "mcBit2SomfyRTS": 9}
+# MN methods (sd_protocols/helpers.py:223-716) -> enum sdx_mn_method; MN_MISSING: not on the class
+MN_METHODS = {"ConvBresser_lightning": 1, "ConvBresser_5in1": 2, "ConvBresser_6in1": 3, "ConvBresser_7in1": 4,
+              "ConvPCA301": 5, "ConvKoppFreeControl": 6, "ConvLaCrosse": 7}
+MN_MISSING = 255
+MN_MAX = 64
+# other methods the reference SDProtocols class defines: an MN protocol naming one of them would call
+# it with the wrong arguments (not modelled)
+_OTHER_METHODS = set(MC_METHODS) | set(POSTDEMO) | {"demodulate", "demodulate_mn", "demodulate_mc", "demodulate_mu",
+                                                    "demodulate_ms", "lfsr_digest16", "length_in_range",
+                                                    "mc2dmc", "bin_str_2_hex_str", "hex_to_bin_str"}
 
 
 def load_protocols(path: Optional[str] = None) -> Dict[str, dict]:
@@ -359,6 +371,48 @@ class Bank:
             self.mc_preamble.append(pre)
             rec["pre_off"], rec["pre_len"] = self._str(pre)
 
+        # MN = every id with 'modulation' (signalduino/parser/mn.py:80-191)
+        self.mn_pids = [pid for pid, p in P.items() if "modulation" in p]
+        if len(self.mn_pids) > MN_MAX:
+            raise NotImplementedError(f"more than {MN_MAX} MN protocols")
+        mn = np.zeros(len(self.mn_pids), MN_REC)
+        self.mn_rfmode: List[Any] = []
+        self.mn_modulation: List[Any] = []
+        self.mn_preamble: List[str] = []
+        for r, pid in enumerate(self.mn_pids):
+            p = P[pid]
+            rec = mn[r]
+            rec["proto_index"] = self.pids.index(pid)
+            self.mn_rfmode.append(p.get("rfmode", None))
+            self.mn_modulation.append(p.get("modulation", None))
+            lm = p.get("length_min", -1)             # helpers.py:144-164 on len(hex) (mn.py:98)
+            rec["lir_min"] = _int_exact(lm, f"MN {pid} length_min")
+            lx = p.get("length_max")
+            rec["lir_max"] = _int_exact(lx, f"MN {pid} length_max") if lx is not None else INT_NONE
+            rx = p.get("regexMatch", None)
+            if rx:
+                if not isinstance(rx, str):
+                    raise NotImplementedError(f"MN {pid}: regexMatch {rx!r}")
+                if rx not in mm_patterns:
+                    mm_patterns.append(rx)
+                rec["dfa"] = mm_patterns.index(rx)
+            else:
+                rec["dfa"] = -1
+            m = p.get("method")
+            if m:
+                if not isinstance(m, str):
+                    raise NotImplementedError(f"MN {pid}: method {m!r}")
+                name = m.split(".")[-1]
+                if name in MN_METHODS:
+                    rec["method"] = MN_METHODS[name]
+                elif name in _OTHER_METHODS:
+                    raise NotImplementedError(f"MN {pid}: method {name!r} called with MN arguments (not modelled)")
+                else:
+                    rec["method"] = MN_MISSING       # mn.py:171-173: not found -> skipped
+            pre = f"{p.get('preamble', '')}"
+            self.mn_preamble.append(pre)
+            rec["pre_off"], rec["pre_len"] = self._str(pre)
+
         if b"\n" in bytes(self._heap):
             raise NotImplementedError("newline inside a preamble/postamble ($ semantics)")
         cls_of, n_class, dfas = regex_dfa.compile_bank_dfas(mm_patterns)
@@ -391,7 +445,7 @@ class Bank:
         flags_all = np.concatenate(flag_parts) if flag_parts else np.zeros(0, np.uint8)
         cls_arr = np.asarray(cls_of, dtype=np.uint8)
 
-        # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings | t256 | order | ranks | mudesc | mmtab
+        # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings | t256 | order | ranks | mudesc | mmtab | mn
         hdr_size = struct.calcsize(HDR_FMT)
         # processing orders (results are placed by protocol index, so any order is exact):
         # MU sorted by clock so consecutive protocols reuse the normalised patterns
@@ -408,7 +462,7 @@ class Bank:
         ranks = np.asarray(self._ranks, dtype=np.uint16)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
                     trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
-                    order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes()]
+                    order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes(), mn.tobytes()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
         for s in sections:
@@ -418,12 +472,12 @@ class Bank:
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
                           len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], offs[10], offs[11], offs[12],
-                          len(mmtab), mm_states, len(glist), 0)
+                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], 0)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s
         self.blob = bytes(blob)
-        self.mu_table, self.ms_table, self.mc_table = mu, ms, mc
+        self.mu_table, self.ms_table, self.mc_table, self.mn_table = mu, ms, mc, mn
 
     def _mu_desc(self, mu, dfas, cls_of):
         """MU decode descriptors + the LDS modulematch tables.

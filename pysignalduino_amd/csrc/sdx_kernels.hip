@@ -2189,8 +2189,11 @@ static int fail(int code, const std::string& msg) {
   return code;
 }
 namespace sdx {
-// the error text of sdx_last_error() for the other translation units (sdx_lines.hip)
+// for the other translation units (sdx_lines.hip, sdx_mn.hip): the error text of sdx_last_error()
+// and the bank handle's fields
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
+const void* bank_dev_ptr(const sdx_bank* b) { return b->dev; }
+const sdx_bank_hdr* bank_hdr(const sdx_bank* b) { return &b->hdr; }
 }  // namespace sdx
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -2224,6 +2227,7 @@ int sdx_layout_size(int which) {
     case 5: return (int)sizeof(sdx_result);
     case 6: return (int)sizeof(sdx_desc);
     case 7: return (int)sizeof(sdx_mu_desc);
+    case 8: return (int)sizeof(sdx_mn_proto);
   }
   return -1;
 }
@@ -2237,7 +2241,8 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
   if ((size_t)h.off_order + 2u * ((size_t)h.n_mu + h.n_ms + h.n_mu_groups + 1) > nbytes || h.off_rank > nbytes || h.n_mu > 65535u ||
       h.n_ms > 65535u || (size_t)h.off_mudesc + sizeof(sdx_mu_desc) * h.n_mu > nbytes ||
       (size_t)h.off_mmtab + h.mmtab_bytes > nbytes || h.mmtab_bytes > SDX_MMTAB_LDS || (h.mmtab_bytes & 15u) ||
-      (h.off_mudesc & 15u) || (h.off_mmtab & 15u) || 17u * h.mm_states > h.mmtab_bytes)
+      (h.off_mudesc & 15u) || (h.off_mmtab & 15u) || 17u * h.mm_states > h.mmtab_bytes || h.n_mn > SDX_MN_MAX ||
+      (size_t)h.off_mn + sizeof(sdx_mn_proto) * h.n_mn > nbytes || (h.off_mn & 15u))
     return fail(SDX_EBANK, "bank blob: processing-order section out of range");
   HIPCHK(hipSetDevice(device));
   void* d = nullptr;

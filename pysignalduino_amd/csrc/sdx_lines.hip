@@ -9,11 +9,12 @@
 //   parser/mu.py:48-68          the MU validity regex, _parse_to_dict, "D" required
 //   parser/ms.py:35-41          _parse_to_dict, "D" required
 //   parser/mc.py:37-155         MC header validation, required D/C/L, hex D, int(R)/int(F)
+//   parser/mn.py:17,31-51       MN_PATTERN (the hex characters become an sdx_mn_batch frame)
 //   sd_protocols/message_*.py   the P#/CP/SP/R/data string gates the demodulators apply
 // The outputs of line i are message i of an sdx_pulse_batch / sdx_mc_batch in slot layout
 // (len_dev), so the demodulation kernels read them in place.  Anything whose exact Python meaning
 // this file does not model (bytes >= 0x80 after decompression, multi-digit pattern ids, non-integer
-// pattern values, MN lines) is reported SDX_LS_UNSUPPORTED instead of being approximated.
+// pattern values) is reported SDX_LS_UNSUPPORTED instead of being approximated.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -642,6 +643,52 @@ LD bool frame_check(const uint8_t* L, int a, int b, bool& comp) {
   return true;
 }
 
+// MNParser.parse up to the protocol loop (parser/mn.py:33-51):
+//   MN_PATTERN = ^MN;D=(Y?)([0-9A-F]+);(?:R=([0-9]+);)?(?:A=(-?[0-9]{1,3});)?$
+// matched deterministically ('Y' is no hex digit; an optional group that starts but does not
+// complete leaves text that '$' rejects).  '$' also matches before a final newline.
+LD void mn_line(const Str& P, LineRes& r) {
+  const uint8_t* p = P.p;
+  const int n = P.n;
+  r.status = SDX_LS_INVALID;
+  if (n < 7 || p[0] != 'M' || p[1] != 'N' || p[2] != ';' || p[3] != 'D' || p[4] != '=') return;
+  int k = 5;
+  if (p[k] == 'Y') ++k;
+  const int dS = k;
+  while (k < n && (digit(p[k]) || (p[k] >= 'A' && p[k] <= 'F'))) ++k;
+  if (k == dS || k >= n || p[k] != ';') return;
+  const int dE = k++;
+  Field fR{-1, -1}, fA{-1, -1};
+  if (k + 1 < n && p[k] == 'R' && p[k + 1] == '=') {
+    const int v = k + 2;
+    int e = v;
+    while (e < n && digit(p[e])) ++e;
+    if (e == v || e >= n || p[e] != ';') return;
+    fR = Field{v, e};
+    k = e + 1;
+  }
+  if (k + 1 < n && p[k] == 'A' && p[k + 1] == '=') {
+    const int v = k + 2;
+    int e = v;
+    if (e < n && p[e] == '-') ++e;
+    const int ds = e;
+    while (e < n && digit(p[e]) && e - ds < 3) ++e;
+    if (e == ds || e >= n || p[e] != ';') return;
+    fA = Field{v, e};
+    k = e + 1;
+  }
+  if (!(k == n || (k == n - 1 && p[k] == '\n'))) return;
+  if (dE - dS > SDX_MN_HEX_MAX || (fR.s >= 0 && fR.e - fR.s > 15)) {  // sdx_demod_mn / meta_dev contract
+    r.status = SDX_LS_UNSUPPORTED;
+    return;
+  }
+  r.status = SDX_LS_OK;
+  r.dS = dS;
+  r.dE = dE;
+  r.fR = fR;
+  r.fF = fA;  // A= travels in the F slot of meta_dev
+}
+
 // routing + the per-type parser rules on a (decompressed) payload; writes the pattern / MS / MC
 // fields of line i, returns kind/status and the D/R/F ranges.  pvt = this lane's column of the
 // fast P-key table (stride 64 words).
@@ -653,8 +700,8 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
     return;
   }
   r.kind = c1 == 'U' ? SDX_LINE_MU : c1 == 'S' ? SDX_LINE_MS : c1 == 'C' ? SDX_LINE_MC : SDX_LINE_MN;
-  if (r.kind == SDX_LINE_MN) {  // the MN (FSK) path is not part of this build
-    r.status = SDX_LS_UNSUPPORTED;
+  if (r.kind == SDX_LINE_MN) {
+    mn_line(P, r);
     return;
   }
   {
@@ -1057,6 +1104,7 @@ LD int sel_class(const sdx_lines_out& o, int i) {
     return n <= SDX_SHORT_MAX ? SDX_SEL_MS_SHORT : SDX_SEL_MS_LONG;
   }
   if (k == SDX_LINE_MC) return SDX_SEL_MC;
+  if (k == SDX_LINE_MN) return SDX_SEL_MN;
   return -1;
 }
 
@@ -1068,7 +1116,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sel_count(sdx_lines_out o, int 
   __shared__ int32_t c[SDX_SEL_NCLASS];
   if (threadIdx.x < SDX_SEL_NCLASS) c[threadIdx.x] = 0;
   __syncthreads();
-  int mine[SDX_SEL_NCLASS] = {0, 0, 0, 0, 0};
+  int mine[SDX_SEL_NCLASS] = {};
   const int base = blockIdx.x * SDX_SEL_CHUNK;
   for (int r = 0; r < SDX_SEL_CHUNK; r += SEL_THREADS) {
     const int i = base + r + threadIdx.x;
@@ -1093,7 +1141,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sel_write(sdx_lines_out o, int 
   if (threadIdx.x < SDX_SEL_NCLASS) tot[threadIdx.x] = pre[threadIdx.x] = 0;
   __syncthreads();
   {
-    int t[SDX_SEL_NCLASS] = {0, 0, 0, 0, 0}, p[SDX_SEL_NCLASS] = {0, 0, 0, 0, 0};
+    int t[SDX_SEL_NCLASS] = {}, p[SDX_SEL_NCLASS] = {};
     for (int b = threadIdx.x; b < nchunk; b += SEL_THREADS)
 #pragma unroll
       for (int q = 0; q < SDX_SEL_NCLASS; ++q) {

@@ -8,21 +8,22 @@ header checks, then ``SDProtocols.demodulate*``.  Here a batch of lines is uploa
   1. ``sdx_parse_lines``   (csrc/sdx_lines.hip) does all of the parsing, one lane per line, writing
                            the demodulators' SoA batch in place (slot layout, ``len_dev``),
   2. ``sdx_select_lines``  builds the per-kind selection lists (MU/MS short or long, MC) on the device,
-  3. the MU / MS (and, in mc_mode='fixed', MC) demodulation kernels run over those lists,
+  3. the MU / MS / MN (and, in mc_mode='fixed', MC) demodulation kernels run over those lists,
 and only the result records come back.  The host side assembles the Python objects.
 
 Observable behaviour per line is the reference's: ``parse_line`` returns the same
 ``DecodedMessage`` list (protocol_id, payload, metadata, raw.line / message_type / rssi /
 freq_afc), and lines the reference ignores give ``[]`` (a demodulator exception is caught and
 logged by the reference's parsers, so it also gives ``[]``).  Lines outside the device contract
-(MN lines, multi-digit pattern ids, non-integer pattern values, non-ASCII characters after
-decompression, over-long messages) are never approximated: ``parse_line`` raises
+(multi-digit pattern ids, non-integer pattern values, non-ASCII characters after decompression,
+over-long messages, an MN R= of more than 15 digits) are never approximated: ``parse_line`` raises
 :class:`ContractError` and ``parse_lines`` returns the exception in that line's slot.
 There is no CPU fallback.
 """
 from __future__ import annotations
 
 import logging
+import re
 from dataclasses import dataclass, field
 from datetime import datetime
 from typing import Any, List, Optional, Sequence, Union
@@ -69,6 +70,14 @@ def calc_afc(raw_afc: int) -> float:
     if raw_afc >= 128:
         return (raw_afc - 256) / 2
     return raw_afc / 2
+
+
+def calc_mn_afc(raw_afc: int) -> float:
+    """parser/mn.py:60-68 (the MN frame's A= field)."""
+    return round((26000000 / 16384 * raw_afc / 1000), 0)
+
+
+MN_PATTERN = re.compile(r"^MN;D=(Y?)([0-9A-F]+);(?:R=([0-9]+);)?(?:A=(-?[0-9]{1,3});)?$")  # parser/mn.py:17
 
 
 def _to_bytes(line: Union[str, bytes]) -> bytes:
@@ -128,6 +137,9 @@ class LineBatch:
     def pulse_batch(self):
         return {"data": self.slot, "offsets": self.doff, "npat": self.npat, "pat_id": self.pat_id,
                 "pat_val": self.pat_val, "cp_slot": self.cp_slot, "ms_ok": self.ms_ok, "len": self.dlen, "n": self.n}
+
+    def mn_batch(self):
+        return {"hex": self.slot, "offsets": self.doff, "len": self.dlen, "n": self.n}
 
     def mc_batch(self):
         return {"hex": self.slot, "offsets": self.doff, "clock": self.clock, "mcbitnum": self.mcbitnum,
@@ -202,6 +214,12 @@ class SignalParser:
                                 sel_long=sels[runtime.SEL_MS_LONG])
         if self.protocols.mc_mode == "fixed" and cnt[runtime.SEL_MC]:
             res["MC"] = eng.run(runtime.KIND_MC, lb.mc_batch(), sel_short=sels[runtime.SEL_MC])
+        if cnt[runtime.SEL_MN]:
+            # result space: <= (MN protocols) records of <= (preamble + frame) bytes per line
+            nmn = int(cnt[runtime.SEL_MN])
+            res["MN"] = eng.run(runtime.KIND_MN, lb.mn_batch(), sel_short=sels[runtime.SEL_MN],
+                                mn_elig=self.protocols.mn_eligibility(self.rfmode),
+                                rec_cap=len(bk.mn_pids) * nmn + 1024, heap_cap=int(4 * len(data) + 64 * nmn + 65536))
         # read-back of the per-line fields the Python objects need
         kind = lb.kind[:n].cpu().numpy()
         status = lb.status[:n].cpu().numpy()
@@ -238,6 +256,9 @@ class SignalParser:
                 continue
             if d["status"] != runtime.ST_OK:
                 raise RuntimeError(f"device status {int(d['status'])} for line {i}")
+            if name == "MN":
+                out.append(self._mn_messages(lines[i], i, plen, offsets, slot, meta, d, rec, hb["MN"]))
+                continue
             fr = self._frame(lines[i], i, plen, offsets, slot, meta, name)
             rssi_raw = self._meta_str(meta[i], 0)
             msgs = []
@@ -256,6 +277,31 @@ class SignalParser:
             out.append(msgs)
         return out
 
+    def _payload(self, line, i, plen, offsets, slot) -> str:
+        if plen[i] >= 0:
+            s0 = 3 * int(offsets[i])
+            return bytes(slot[s0: s0 + int(plen[i])]).decode("latin-1")
+        s = line.decode("latin-1") if isinstance(line, (bytes, bytearray, memoryview)) else line
+        return s.strip()[1:-1]
+
+    def _mn_messages(self, line, i, plen, offsets, slot, meta, d, rec, hb) -> List[DecodedMessage]:
+        """DecodedMessage list of an MN line (parser/mn.py:53-77,175-191): RawFrame(line=payload,
+        message_type='MN') without frame rssi/afc; metadata rssi / freq_afc / modulation / rfmode."""
+        bk = self.protocols._bank
+        fr = RawFrame(line=self._payload(line, i, plen, offsets, slot), message_type="MN")
+        r, a = self._meta_str(meta[i], 0), self._meta_str(meta[i], 16)
+        rssi = calc_rssi(int(r)) if r else None
+        afc = calc_mn_afc(int(a)) if a else None
+        msgs = []
+        for x in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
+            p = int(x["proto"])
+            off = int(x["payload_off"])
+            msgs.append(DecodedMessage(protocol_id=str(bk.mn_pids[p]),
+                                       payload=hb[off: off + int(x["payload_len"])].decode("latin-1"), raw=fr,
+                                       metadata={"rssi": rssi, "freq_afc": afc, "modulation": bk.mn_modulation[p],
+                                                 "rfmode": bk.mn_rfmode[p]}))
+        return msgs
+
     @staticmethod
     def _meta_str(m: np.ndarray, base: int) -> Optional[str]:
         ln = int(m[base + 15])
@@ -263,13 +309,7 @@ class SignalParser:
 
     def _frame(self, line, i, plen, offsets, slot, meta, name) -> RawFrame:
         """RawFrame(line=payload, message_type) + _extract_metadata (mu.py:96-108, mc.py:141-155)."""
-        if plen[i] >= 0:
-            s0 = 3 * int(offsets[i])
-            payload = bytes(slot[s0: s0 + int(plen[i])]).decode("latin-1")
-        else:
-            s = line.decode("latin-1") if isinstance(line, (bytes, bytearray, memoryview)) else line
-            payload = s.strip()[1:-1]
-        fr = RawFrame(line=payload, message_type=name)
+        fr = RawFrame(line=self._payload(line, i, plen, offsets, slot), message_type=name)
         r, f = self._meta_str(meta[i], 0), self._meta_str(meta[i], 16)
         for raw, attr, fn in ((r, "rssi", calc_rssi), (f, "freq_afc", calc_afc)):
             if raw is None:
@@ -279,3 +319,45 @@ class SignalParser:
             except ValueError:
                 self.logger.warning("Could not parse %s value: %s", "RSSI" if attr == "rssi" else "AFC", raw)
         return fr
+
+
+class MNParser:
+    """signalduino/parser/mn.py:20-191: MN frames -> DecodedMessage, the protocol loop on the GPU.
+
+    ``parse(frame)`` / ``parse_batch(frames)`` take RawFrames whose ``line`` is the payload (as the
+    reference's SignalParser hands them over).  MN_PATTERN is matched per frame on the host (the
+    batched line path, :class:`SignalParser`, does it on the device), then one ``sdx_demod_mn``
+    launch runs the rfmode / length / regexMatch / method loop for every matched frame."""
+
+    def __init__(self, protocols: SDProtocols, logger: Optional[logging.Logger] = None, rfmode: Optional[str] = None):
+        self.protocols = protocols
+        self.logger = logger or logging.getLogger(__name__)
+        self.rfmode = rfmode
+
+    def parse(self, frame: RawFrame) -> List[DecodedMessage]:
+        return self.parse_batch([frame])[0]
+
+    def parse_batch(self, frames: Sequence[RawFrame]) -> List[List[DecodedMessage]]:
+        rows, hexes, meta = [], [], []
+        for k, fr in enumerate(frames):
+            if not fr.line.upper().startswith("MN"):        # ensure_message_type (base.py:211-213)
+                self.logger.debug("Not an MN message: %s", fr.line[:2])
+                continue
+            m = MN_PATTERN.match(fr.line)
+            if not m:
+                self.logger.debug("MN message format mismatch: %s", fr.line)
+                continue
+            rows.append(k)
+            hexes.append(m.group(2))
+            meta.append((calc_rssi(int(m.group(3))) if m.group(3) else None,
+                         calc_mn_afc(int(m.group(4))) if m.group(4) else None))
+        out: List[List[DecodedMessage]] = [[] for _ in frames]
+        if not rows:
+            return out
+        bk = None
+        for k, res, (rssi, afc) in zip(rows, self.protocols.mn_parse_batch(hexes, self.rfmode), meta):
+            bk = bk or self.protocols._bank
+            out[k] = [DecodedMessage(protocol_id=str(pid), payload=payload, raw=frames[k],
+                                     metadata={"rssi": rssi, "freq_afc": afc, "modulation": bk.mn_modulation[p],
+                                               "rfmode": bk.mn_rfmode[p]}) for pid, payload, p in res]
+        return out

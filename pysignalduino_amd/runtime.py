@@ -21,19 +21,21 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libsdx.so")
 
 KIND_MU, KIND_MS, KIND_MC = 0, 1, 2
+KIND_MN = 3        # host-side tag for Engine.run (sdx_demod_mn)
 ST_OK, ST_RAISED, ST_OVF_TILE, ST_OVF_OUT = 0, 1, 2, 3
 RAISE_NAMES = {1: IndexError, 2: AttributeError, 3: ValueError, 4: TypeError, 5: ZeroDivisionError}
 SHORT_MAX = 256    # k_pulses<.., 4 words, 64 messages/tile>
 LONG_MAX = 4096    # k_pulses<.., 64 words, 4 messages/tile>
 MC_HEX_MAX = 128   # MC_MAXW * 16 hex characters
+MN_HEX_MAX = 4096  # SDX_MN_HEX_MAX
 
 DESC_DT = np.dtype([("rec_begin", "<u4"), ("n_rec", "<u2"), ("status", "u1"), ("raise_kind", "u1")])
 RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u2"), ("bit_length", "<u4"),
                    ("msg", "<u4")])
 
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
-            "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_parse_lines",
-            "sdx_select_lines"]
+            "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
+            "sdx_parse_lines", "sdx_select_lines"]
 
 
 class SdxPulseBatch(Structure):
@@ -47,6 +49,11 @@ class SdxMcBatch(Structure):
     _fields_ = [("hex_dev", c_void_p), ("offsets_dev", c_void_p), ("clock_dev", c_void_p),
                 ("mcbitnum_dev", c_void_p), ("flags_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p),
                 ("n", c_int32), ("n_sel", c_int32)]
+
+
+class SdxMnBatch(Structure):
+    _fields_ = [("hex_dev", c_void_p), ("offsets_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p),
+                ("n", c_int32), ("n_sel", c_int32), ("elig", ctypes.c_uint64), ("method", c_int32), ("res", c_int32)]
 
 
 class SdxOut(Structure):
@@ -67,7 +74,7 @@ class SdxLinesOut(Structure):
 # include/sdx.h front-end constants
 LINE_NONE, LINE_MU, LINE_MS, LINE_MC, LINE_MN = 0, 1, 2, 3, 4
 LS_OK, LS_NOFRAME, LS_NOPARSER, LS_INVALID, LS_NODATA, LS_UNSUPPORTED, LS_RAISES = 0, 1, 2, 3, 4, 5, 6
-SEL_MU_SHORT, SEL_MU_LONG, SEL_MS_SHORT, SEL_MS_LONG, SEL_MC, SEL_NCLASS = 0, 1, 2, 3, 4, 5
+SEL_MU_SHORT, SEL_MU_LONG, SEL_MS_SHORT, SEL_MS_LONG, SEL_MC, SEL_MN, SEL_NCLASS = 0, 1, 2, 3, 4, 5, 6
 SEL_CHUNK = 1024
 
 _LIB = None
@@ -102,11 +109,13 @@ def load_library(path: Optional[str] = None):
         f.restype = c_int
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mc.restype = c_int
+    lib.sdx_demod_mn.argtypes = [c_void_p, POINTER(SdxMnBatch), POINTER(SdxOut), c_void_p]
+    lib.sdx_demod_mn.restype = c_int
     lib.sdx_parse_lines.argtypes = [POINTER(SdxLines), POINTER(SdxLinesOut), c_void_p]
     lib.sdx_parse_lines.restype = c_int
     lib.sdx_select_lines.argtypes = [POINTER(SdxLinesOut), c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.sdx_select_lines.restype = c_int
-    if lib.sdx_abi_version() != 2:
+    if lib.sdx_abi_version() != 3:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -117,7 +126,8 @@ def load_library(path: Optional[str] = None):
 def check_layout(lib) -> None:
     """The numpy mirrors of the C structs must match sizeof() on the C side."""
     want = {0: struct.calcsize(bankmod.HDR_FMT), 1: bankmod.PATSPEC.itemsize, 2: bankmod.MU_REC.itemsize, 3: bankmod.MS_REC.itemsize,
-            4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize}
+            4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize,
+            8: bankmod.MN_REC.itemsize}
     for k, v in want.items():
         got = lib.sdx_layout_size(k)
         if got != v:
@@ -230,9 +240,27 @@ class Engine:
         o = self._out_struct(out)
         _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 
+    def to_device_mn(self, hexes) -> Dict[str, "object"]:
+        """MN frames (hex strings / bytes) -> device batch.  Contract: [0-9A-Fa-f]* and at most
+        MN_HEX_MAX characters (checked here; ContractError-free callers check before)."""
+        t = self.torch
+        bs = [h.encode("latin-1") if isinstance(h, str) else bytes(h) for h in hexes]
+        lens = np.fromiter((len(b) for b in bs), np.int64, len(bs))
+        offsets = np.zeros(len(bs) + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        data = np.frombuffer(b"".join(bs), np.uint8)
+        return {"hex": t.from_numpy(data.copy() if len(data) else np.zeros(1, np.uint8)).to(self.dev),
+                "offsets": t.from_numpy(offsets).to(self.dev), "n": len(bs), "lengths": lens}
+
+    def launch_mn(self, bd, out, elig: int = 0, method: int = -1, sel=None) -> None:
+        b = SdxMnBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd.get("len")), _ptr(sel), bd["n"],
+                       0 if sel is None else int(sel.numel()), elig, method, 0)
+        o = self._out_struct(out)
+        _check(self.lib, self.lib.sdx_demod_mn(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
+
     # -- full run with contract routing and overflow re-runs (all on the GPU) --------------------
     def run(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None,
-            sel_short=None, sel_long=None):
+            sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1):
         """Demodulate a device batch; returns host numpy (desc, rec, heap).
 
         ``sel_short`` / ``sel_long``: device int32 lists of the messages to run with the short /
@@ -247,7 +275,11 @@ class Engine:
         else:
             n_work = n
             lengths = bd["lengths"]
-            if kind == KIND_MC:
+            if kind == KIND_MN:
+                if n and int(lengths.max(initial=0)) > MN_HEX_MAX:
+                    raise NotImplementedError(f"MN frames longer than {MN_HEX_MAX} hex characters are outside "
+                                              "the device contract")
+            elif kind == KIND_MC:
                 if n and int(lengths.max(initial=0)) > MC_HEX_MAX:
                     raise NotImplementedError(f"MC frames longer than {MC_HEX_MAX} hex characters are outside "
                                               "the device contract")
@@ -255,8 +287,13 @@ class Engine:
                 raise NotImplementedError(f"messages longer than {LONG_MAX} pulses are outside the device contract")
         rec_cap = rec_cap or (8 * n_work + 1024)
         heap_cap = heap_cap or (200 * n_work + 65536)
+        if kind == KIND_MN and not selected:   # parser mode: <= n_mn results of <= preamble + frame bytes
+            rec_cap = max(rec_cap, 4 * n_work + 1024)
+            heap_cap = max(heap_cap, int(4 * int(np.sum(bd["lengths"])) + 160 * n_work + 65536))
         out = self.alloc_out(n, rec_cap, heap_cap)
-        if selected:
+        if kind == KIND_MN:
+            self.launch_mn(bd, out, elig=mn_elig, method=mn_method, sel=sel_short)
+        elif selected:
             if sel_short is not None and sel_short.numel():
                 (self.launch_mc(bd, out, sel=sel_short) if kind == KIND_MC else
                  self.launch_pulses(kind, bd, out, sel=sel_short))
@@ -286,7 +323,9 @@ class Engine:
             redo = np.concatenate([redo_out, redo_tile]).astype(np.int32)
             out2 = self.alloc_out(n, 2 * rec_cap + 64 * len(redo), 2 * heap_cap + 8192 * len(redo))
             sel = t.from_numpy(redo).to(self.dev)
-            if kind == KIND_MC:
+            if kind == KIND_MN:
+                self.launch_mn(bd, out2, elig=mn_elig, method=mn_method, sel=sel)
+            elif kind == KIND_MC:
                 self.launch_mc(bd, out2, sel=sel)
             else:
                 self.launch_pulses(kind, bd, out2, sel=sel, long_variant=True)

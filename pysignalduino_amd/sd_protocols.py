@@ -9,7 +9,11 @@ Mirrors the reference class RFD-FHEM/PySignalduino ``sd_protocols.SDProtocols``
   * demodulate / demodulate_mu / demodulate_ms / demodulate_mc (sd_protocols.py:60-111,
     message_unsynced.py:11, message_synced.py:10) -- packed and run by the HIP
     kernels in csrc/sdx_kernels.hip through the C-ABI include/sdx.h;
-  * demodulate_batch(list_of_msg_data, msg_type) -- the batched entry point.
+  * demodulate_batch(list_of_msg_data, msg_type) -- the batched entry point;
+  * MN (FSK): demodulate_mn (sd_protocols.py:113-154), the seven MN methods ConvBresser_lightning /
+    _5in1 / _6in1 / _7in1, ConvPCA301, ConvKoppFreeControl, ConvLaCrosse (helpers.py:223-716) and
+    mn_parse_batch (the protocol loop of signalduino/parser/mn.py:79-191) -- run by
+    csrc/sdx_mn.hip through sdx_demod_mn.
 
 It is injected where the reference injects its engine:
 ``SignalParser(protocols=SDProtocols())`` (signalduino/parser/__init__.py:21-27).
@@ -22,6 +26,7 @@ There is no CPU fallback: without the HIP library / a GPU every demodulate call 
 from __future__ import annotations
 
 import json
+import re
 from typing import Any, Dict, Iterable, List, Optional, Sequence
 
 import numpy as np
@@ -31,6 +36,7 @@ from . import packing
 from . import runtime
 
 _SENTINEL = object()
+_HEX_RE = re.compile(r"[0-9a-fA-F]*")
 
 
 class _Observed(dict):
@@ -177,8 +183,123 @@ class SDProtocols:
     def demodulate_ms(self, msg_data: Dict[str, Any], msg_type: str = "MS") -> list:
         return self._single(msg_data, "MS")
 
+    # ---------------------------------------------------------------- MN (FSK) -----------------
     def demodulate_mn(self, msg_data: Dict[str, Any], msg_type: str = "MN") -> list:
-        raise NotImplementedError("the MN (FSK) path is outside this build's scope (SURVEY.md §8(f) item 2)")
+        """sd_protocols.py:113-154: the protocol's MN method on msg_data['data'] (GPU)."""
+        if "protocol_id" not in msg_data:
+            self._logging(f"MN Demodulation failed: Missing protocol_id in msg_data: {msg_data}", 3)
+            return []
+        protocol_id = msg_data["protocol_id"]
+        if not self.protocol_exists(protocol_id):
+            self._logging(f"MN Demodulation: Protocol ID {protocol_id} not found.", 3)
+            return []
+        method_name_full = self.get_property(protocol_id, "method")
+        if not method_name_full:
+            self._logging(f"MN Demodulation: No method defined for protocol {protocol_id}. "
+                          f"Data: {msg_data.get('data', '')}", 3)
+            return []
+        name = method_name_full.split(".")[-1]
+        if name not in bankmod.MN_METHODS:
+            # a name the class does not define, or one called with the wrong arguments (TypeError)
+            self._logging(f"MN Demodulation: Unknown method {name} referenced by '{method_name_full}'.", 3)
+            return []
+        return self.mn_method_batch([msg_data], name, msg_type)[0]
+
+    def ConvBresser_lightning(self, msg_data, msg_type="MN"):  # noqa: N802  (helpers.py:223)
+        return self.mn_method_batch([msg_data], "ConvBresser_lightning", msg_type)[0]
+
+    def ConvBresser_5in1(self, msg_data, msg_type="MN"):  # noqa: N802  (helpers.py:382)
+        return self.mn_method_batch([msg_data], "ConvBresser_5in1", msg_type)[0]
+
+    def ConvBresser_6in1(self, msg_data, msg_type="MN"):  # noqa: N802  (helpers.py:427)
+        return self.mn_method_batch([msg_data], "ConvBresser_6in1", msg_type)[0]
+
+    def ConvBresser_7in1(self, msg_data, msg_type="MN"):  # noqa: N802  (helpers.py:473)
+        return self.mn_method_batch([msg_data], "ConvBresser_7in1", msg_type)[0]
+
+    def ConvPCA301(self, msg_data, msg_type="MN"):  # noqa: N802  (helpers.py:525)
+        return self.mn_method_batch([msg_data], "ConvPCA301", msg_type)[0]
+
+    def ConvKoppFreeControl(self, msg_data, msg_type="MN"):  # noqa: N802  (helpers.py:581)
+        return self.mn_method_batch([msg_data], "ConvKoppFreeControl", msg_type)[0]
+
+    def ConvLaCrosse(self, msg_data, msg_type="MN"):  # noqa: N802  (helpers.py:630)
+        return self.mn_method_batch([msg_data], "ConvLaCrosse", msg_type)[0]
+
+    _MN_META = {"ConvPCA301": {"is_raw": False}, "ConvKoppFreeControl": {"is_raw": False},
+                "ConvLaCrosse": {"is_raw": False}}
+
+    @staticmethod
+    def _mn_hex(d) -> str:
+        """The device contract of an MN frame: hex digits only, at most MN_HEX_MAX of them."""
+        if not isinstance(d, str) or len(d) > runtime.MN_HEX_MAX or not _HEX_RE.fullmatch(d):
+            raise packing.ContractError("MN data must be a string of at most "
+                                        f"{runtime.MN_HEX_MAX} hex digits for the device path")
+        return d
+
+    def mn_method_batch(self, messages: Sequence[Dict[str, Any]], name: str, msg_type: str = "MN") -> List[list]:
+        """One MN method (helpers.py:223-716) over many msg_data dicts in one launch: the
+        reference's list per message ([] or [{protocol_id, payload, meta}])."""
+        method = bankmod.MN_METHODS[name]
+        out: List[Any] = [[] for _ in messages]
+        idx, hexes = [], []
+        for i, m in enumerate(messages):
+            d = m.get("data")
+            if not d:                    # `if not hex_data: return []`
+                continue
+            hexes.append(self._mn_hex(d))
+            idx.append(i)
+        if not idx:
+            return out
+        eng = self._ensure()
+        desc, rec, heap = eng.run(runtime.KIND_MN, eng.to_device_mn(hexes), mn_method=method)
+        hb = heap.tobytes()
+        meta = self._MN_META.get(name, {})
+        for j, i in enumerate(idx):
+            d = desc[j]
+            if d["status"] != runtime.ST_OK:
+                raise RuntimeError(f"device status {int(d['status'])} for MN frame {i}")
+            if int(d["n_rec"]):
+                r = rec[int(d["rec_begin"])]
+                p = hb[int(r["payload_off"]): int(r["payload_off"]) + int(r["payload_len"])].decode("latin-1")
+                out[i] = [{"protocol_id": messages[i].get("protocol_id"), "payload": p, "meta": dict(meta)}]
+        return out
+
+    def mn_eligibility(self, rfmode: Optional[str]) -> int:
+        """parser/mn.py:83-93 as the 64-bit protocol mask of sdx_mn_batch.elig."""
+        self._ensure()
+        m = 0
+        for k, prf in enumerate(self._bank.mn_rfmode):
+            if prf and not (rfmode and prf != rfmode):
+                m |= 1 << k
+        return m
+
+    def mn_parse_batch(self, hexes: Sequence[str], rfmode: Optional[str] = None):
+        """The protocol loop of MNParser.parse (parser/mn.py:79-191) for many frames whose
+        MN_PATTERN matched: per frame the list of (protocol_id, payload, mn-table index)."""
+        for h in hexes:
+            self._mn_hex(h)
+        eng = self._ensure()
+        if not len(hexes):
+            return []
+        desc, rec, heap = eng.run(runtime.KIND_MN, eng.to_device_mn(hexes), mn_elig=self.mn_eligibility(rfmode))
+        return self._mn_results(desc, rec, heap, range(len(hexes)))
+
+    def _mn_results(self, desc, rec, heap, rows):
+        bk = self._bank
+        hb = heap.tobytes()
+        out = []
+        for i in rows:
+            d = desc[i]
+            if d["status"] != runtime.ST_OK:
+                raise RuntimeError(f"device status {int(d['status'])} for MN frame {i}")
+            res = []
+            for r in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
+                p = int(r["proto"])
+                off = int(r["payload_off"])
+                res.append((bk.mn_pids[p], hb[off: off + int(r["payload_len"])].decode("latin-1"), p))
+            out.append(res)
+        return out
 
     def _single(self, msg_data, kind):
         out = self.demodulate_batch([msg_data], kind, raise_errors=True)

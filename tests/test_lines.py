@@ -152,7 +152,7 @@ def _compare(lines, dv):
                 if (int(dv["clock"][i]), int(dv["mcbitnum"][i]), int(dv["mcflags"][i])) != \
                         (r["clock"], r["mcbitnum"], r["mcflags"]):
                     e.append(("mc", int(dv["clock"][i]), int(dv["mcbitnum"][i]), r["clock"], r["mcbitnum"]))
-            else:
+            elif r["kind"] != LO.MN:
                 npat = int(dv["npat"][i])
                 ids = [int(chr(c)) for c in dv["pat_id"][i][:npat]]
                 vals = dv["pat_val"][i][:npat]
@@ -168,7 +168,7 @@ def _compare(lines, dv):
 
 def _check_selection(lines, dv):
     classes = [LO.sel_class(LO.parse_line(ln)) for ln in lines]
-    for k in range(5):
+    for k in range(6):
         exp = [i for i, c in enumerate(classes) if c == k]
         assert int(dv["counts"][k]) == len(exp), k
         assert list(dv["sels"][k]) == exp, k
@@ -187,6 +187,8 @@ def test_parse_lines_matches_oracle_on_goldens(golden):
 def test_parse_lines_matches_oracle_fuzz():
     P = B.Bank().protocols
     base, _ = synth.line_corpus(P, 4000, seed=11, compress_frac=0.4)
+    base += [synth.frame(synth.mn_payload(*f)) for f in synth.mn_frames(1500, seed=13)]
+    base += [b"\x02MN;D=" + b"A" * k + b";R=7;\x03" for k in (4095, 4096, 4097)]
     lines = base + _fuzz(base, 30000, seed=12) + [b"", b"\x02\x03", b"\x02MU;;\x03", b" \x02MC;;\x03 ",
                                                   b"\x02Ms;\x80;\x03", b"\x02MN;D=AB;\x03"]
     dv = _device_parse(lines)
