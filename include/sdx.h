@@ -34,7 +34,7 @@ extern "C" {
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
-enum sdx_kind { SDX_KIND_MU = 0, SDX_KIND_MS = 1, SDX_KIND_MC = 2 };
+enum sdx_kind { SDX_KIND_MU = 0, SDX_KIND_MS = 1, SDX_KIND_MC = 2, SDX_KIND_MN = 3 };
 
 /* per-message status in sdx_desc.status */
 enum sdx_status {
@@ -202,6 +202,41 @@ typedef struct {
  * mcbitnum/mcflags for OK MC lines, and plen plus the slot payload for OK decompressed lines.
  * meta_dev must be 16-byte aligned; bytes_dev and slot_dev 8-byte aligned. */
 int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out, void* hip_stream);
+
+/* ---- publish-ready JSON ------------------------------------------------------
+ * The MQTT publication of a DecodedMessage, MqttPublisher._message_to_json (signalduino/mqtt.py:
+ * 227-245): json.dumps(asdict(message) minus "raw", indent=4), i.e.
+ *   {"protocol_id": ..., "payload": ..., "metadata": {...}} with Python's separators, indentation,
+ *   float repr and ensure_ascii escapes,
+ * built on the device from one demodulation launch's outputs and the front end's per-line fields
+ * (meta.rssi = the raw R string for MU/MS, meta.clock = float(clockabs) / abs(P[CP]); MC: protocol_id,
+ * rssi/freq_afc null; MN: calc_rssi(R), round(26000000/16384*A/1000, 0), modulation, rfmode).
+ * first_only = 1 gives the one message per line the controller publishes (decoded[0],
+ * signalduino/controller.py:254-257); 0 gives one JSON text per result record. */
+typedef struct {
+  int32_t kind;                /* enum sdx_kind of the demodulation launch */
+  int32_t first_only;
+  const sdx_desc* desc_dev;    /* [n] the launch's descriptors (indexed by line) */
+  const sdx_result* rec_dev;   /* its result records ... */
+  const uint32_t* cursor_dev;  /* ... and its cursor: cursor[0] = record count (read on the device) */
+  const uint8_t* heap_dev;     /* its payload heap */
+  const uint8_t* meta_dev;     /* sdx_lines_out.meta_dev [n*32] */
+  const double* pat_val_dev;   /* sdx_lines_out.pat_val_dev [n*10] (MS meta.clock) */
+  const int8_t* cp_slot_dev;   /* sdx_lines_out.cp_slot_dev [n] */
+  int32_t n;                   /* lines */
+  int32_t rec_max;             /* first_only = 0: capacity of the record-indexed outputs */
+} sdx_json_in;
+
+typedef struct {
+  uint8_t* json_dev;           /* JSON texts (ASCII), concatenated */
+  uint32_t* off_dev;           /* [n] (first_only) or [rec_max]: offset of the text in json_dev */
+  uint32_t* len_dev;           /* its length, 0 = no text (no result) */
+  uint32_t* cursor_dev;        /* [2] zeroed by the caller: bytes used, overflow flag (grow json_cap, re-run) */
+  uint32_t json_cap;
+  uint32_t res;
+} sdx_json_out;
+
+int sdx_serialize_json(const sdx_bank* bank, const sdx_json_in* in, const sdx_json_out* out, void* hip_stream);
 
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */
 #define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */

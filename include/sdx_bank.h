@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 9u
+#define SDX_BANK_VERSION 10u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -115,6 +115,15 @@ typedef struct {
   int32_t res;
 } sdx_mn_proto;          /* 32 bytes */
 
+/* JSON fragments of one protocol for sdx_serialize_json (the MQTT publication of a DecodedMessage,
+ * signalduino/mqtt.py:227-245: json.dumps(asdict(msg) minus raw, indent=4)), rendered on the host
+ * with Python's json module into the string heap: pid = json.dumps(protocol_id); s1 = MU:
+ * json.dumps(float(clockabs)) (meta.clock), MN: json.dumps(modulation); s2 = MN: json.dumps(rfmode). */
+typedef struct {
+  uint32_t pid_off, s1_off, s2_off;
+  uint16_t pid_len, s1_len, s2_len, res;
+} sdx_json_rec;          /* 20 bytes */
+
 /* MU decode descriptor: the fields the compacted MU decode reads for one (message, protocol)
  * pair (message_unsynced.py:146-290), staged in LDS once per tile (the first SDX_MUDESC_LDS).
  * mm_on: 0 no modulematch; 1 LDS tables: st = mmtab[(mm_base + st) * 16 + digit] per hex digit,
@@ -154,6 +163,7 @@ typedef struct {
   uint32_t n_mu_groups; /* MU clock groups: order[n_mu + n_ms + g] .. [+ g + 1] bound group g */
   uint32_t n_mn;        /* MN protocols (sdx_mn_proto[n_mn] at off_mn) */
   uint32_t off_mn;
+  uint32_t off_json;    /* sdx_json_rec[n_mu + n_ms + n_mc + n_mn], class-major (MU, MS, MC, MN) */
   uint32_t res;
 } sdx_bank_hdr;
 

@@ -28,7 +28,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 9
+MAGIC, VERSION = 0x4B4E4253, 10
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("klo", "<i4", (MAXUNIQ,)),
@@ -52,7 +52,9 @@ DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), 
                     ("t256_off", "<i4"), ("res", "<i4", (3,))])
 MN_REC = np.dtype([("proto_index", "<i4"), ("lir_min", "<i4"), ("lir_max", "<i4"), ("dfa", "<i4"), ("method", "<i4"),
                    ("pre_off", "<i4"), ("pre_len", "<i4"), ("res", "<i4")])
-HDR_FMT = "<" + "I" * 28  # sdx_bank_hdr: 28 uint32
+JSON_REC = np.dtype([("pid_off", "<u4"), ("s1_off", "<u4"), ("s2_off", "<u4"), ("pid_len", "<u2"), ("s1_len", "<u2"),
+                     ("s2_len", "<u2"), ("res", "<u2")])
+HDR_FMT = "<" + "I" * 29  # sdx_bank_hdr: 29 uint32
 # MU decode descriptor (sdx_mu_desc): what the compacted decode reads per (message, protocol) pair,
 # staged in LDS once per tile
 MU_DESC = np.dtype([("pre", "u1", (16,)), ("post", "u1", (2,)), ("pre_len", "u1"), ("post_len", "u1"),
@@ -413,6 +415,23 @@ class Bank:
             self.mn_preamble.append(pre)
             rec["pre_off"], rec["pre_len"] = self._str(pre)
 
+        # JSON fragments for sdx_serialize_json (signalduino/mqtt.py:227-245), rendered by Python's json
+        jrec = np.zeros(len(self.mu_pids) + len(self.ms_pids) + len(self.mc_pids) + len(self.mn_pids), JSON_REC)
+        j = 0
+        for cls_pids, extra in ((self.mu_pids, lambda r: (json.dumps(self.mu_clock[r]), None)),
+                                (self.ms_pids, lambda r: (None, None)), (self.mc_pids, lambda r: (None, None)),
+                                (self.mn_pids, lambda r: (json.dumps(self.mn_modulation[r]),
+                                                          json.dumps(self.mn_rfmode[r])))):
+            for r, pid in enumerate(cls_pids):
+                s1, s2 = extra(r)
+                jrec[j]["pid_off"], jrec[j]["pid_len"] = self._str(json.dumps(pid))
+                if s1 is not None:
+                    jrec[j]["s1_off"], jrec[j]["s1_len"] = self._str(s1)
+                if s2 is not None:
+                    jrec[j]["s2_off"], jrec[j]["s2_len"] = self._str(s2)
+                j += 1
+        self.json_table = jrec
+
         if b"\n" in bytes(self._heap):
             raise NotImplementedError("newline inside a preamble/postamble ($ semantics)")
         cls_of, n_class, dfas = regex_dfa.compile_bank_dfas(mm_patterns)
@@ -446,6 +465,7 @@ class Bank:
         cls_arr = np.asarray(cls_of, dtype=np.uint8)
 
         # blob: header | mu | ms | mc | dfa | cls | trans | flags | strings | t256 | order | ranks | mudesc | mmtab | mn
+        #       | json
         hdr_size = struct.calcsize(HDR_FMT)
         # processing orders (results are placed by protocol index, so any order is exact):
         # MU sorted by clock so consecutive protocols reuse the normalised patterns
@@ -462,7 +482,7 @@ class Bank:
         ranks = np.asarray(self._ranks, dtype=np.uint16)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
                     trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
-                    order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes(), mn.tobytes()]
+                    order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes(), mn.tobytes(), jrec.tobytes()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
         for s in sections:
@@ -472,7 +492,7 @@ class Bank:
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
                           len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], offs[10], offs[11], offs[12],
-                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], 0)
+                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], offs[14], 0)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s

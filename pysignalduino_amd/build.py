@@ -9,7 +9,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", "sdx_kernels.hip"),   # demodulation kernels + bank + C-ABI
         os.path.join(HERE, "csrc", "sdx_lines.hip"),     # wire-line front end (sdx_parse_lines/select)
-        os.path.join(HERE, "csrc", "sdx_mn.hip")]        # MN (FSK) engine (sdx_demod_mn)
+        os.path.join(HERE, "csrc", "sdx_mn.hip"),        # MN (FSK) engine (sdx_demod_mn)
+        os.path.join(HERE, "csrc", "sdx_json.hip")]      # publish-ready JSON (sdx_serialize_json)
 OUT = os.path.join(HERE, "_lib", "libsdx.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]

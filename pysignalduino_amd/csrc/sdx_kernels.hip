@@ -2228,6 +2228,7 @@ int sdx_layout_size(int which) {
     case 6: return (int)sizeof(sdx_desc);
     case 7: return (int)sizeof(sdx_mu_desc);
     case 8: return (int)sizeof(sdx_mn_proto);
+    case 9: return (int)sizeof(sdx_json_rec);
   }
   return -1;
 }
@@ -2242,7 +2243,8 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
       h.n_ms > 65535u || (size_t)h.off_mudesc + sizeof(sdx_mu_desc) * h.n_mu > nbytes ||
       (size_t)h.off_mmtab + h.mmtab_bytes > nbytes || h.mmtab_bytes > SDX_MMTAB_LDS || (h.mmtab_bytes & 15u) ||
       (h.off_mudesc & 15u) || (h.off_mmtab & 15u) || 17u * h.mm_states > h.mmtab_bytes || h.n_mn > SDX_MN_MAX ||
-      (size_t)h.off_mn + sizeof(sdx_mn_proto) * h.n_mn > nbytes || (h.off_mn & 15u))
+      (size_t)h.off_mn + sizeof(sdx_mn_proto) * h.n_mn > nbytes || (h.off_mn & 15u) ||
+      (size_t)h.off_json + sizeof(sdx_json_rec) * ((size_t)h.n_mu + h.n_ms + h.n_mc + h.n_mn) > nbytes)
     return fail(SDX_EBANK, "bank blob: processing-order section out of range");
   HIPCHK(hipSetDevice(device));
   void* d = nullptr;

@@ -368,11 +368,10 @@ __global__ __launch_bounds__(MN_THREADS) void k_mn(const void* __restrict__ bank
 
 }  // namespace sdxm
 
-struct sdx_bank;
-namespace sdx {
-const void* bank_dev_ptr(const sdx_bank* b);       // sdx_kernels.hip
+namespace sdx {  // sdx_kernels.hip
+const void* bank_dev_ptr(const sdx_bank* b);
 const sdx_bank_hdr* bank_hdr(const sdx_bank* b);
-}
+}  // namespace sdx
 
 extern "C" int sdx_demod_mn(const sdx_bank* bank, const sdx_mn_batch* batch, const sdx_out* out, void* hip_stream) {
   if (!bank || !batch || !out) return sdx::set_error(SDX_EINVAL, "sdx_demod_mn: null argument");

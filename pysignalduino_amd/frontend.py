@@ -302,6 +302,78 @@ class SignalParser:
                                                  "rfmode": bk.mn_rfmode[p]}))
         return msgs
 
+    # ------------------------------------------------------------------------------------------
+    def parse_lines_json(self, lines: Sequence[Union[str, bytes]]) -> List[Union[Optional[str], Exception]]:
+        """Per line, the MQTT message text the reference controller publishes for it:
+        ``MqttPublisher._message_to_json(parse_line(line)[0])`` (signalduino/controller.py:254-257,
+        mqtt.py:227-245), or None when the line decodes to nothing -- parse, demodulation and JSON
+        serialisation (sdx_serialize_json) all on the device; only the texts come back."""
+        n = len(lines)
+        if n == 0:
+            return []
+        data, offsets, bad = pack_lines(lines)
+        eng = self.protocols._ensure()
+        bk = self.protocols._bank
+        lb = LineBatch(eng, data, offsets)
+        lb.launch()
+        sels, cnt = lb.selections()
+        lo = {"meta": lb.meta, "pat_val": lb.pat_val, "cp_slot": lb.cp_slot}
+        pb = lb.pulse_batch()
+        jobs = []
+        if cnt[runtime.SEL_MU_SHORT] or cnt[runtime.SEL_MU_LONG]:
+            k = int(cnt[runtime.SEL_MU_SHORT] + cnt[runtime.SEL_MU_LONG])
+            jobs.append((runtime.KIND_MU, 8 * k + 1024, 200 * k + 65536, 600 * k + 65536,
+                         [(pb, sels[runtime.SEL_MU_SHORT], False), (pb, sels[runtime.SEL_MU_LONG], True)]))
+        if cnt[runtime.SEL_MS_SHORT] or cnt[runtime.SEL_MS_LONG]:
+            k = int(cnt[runtime.SEL_MS_SHORT] + cnt[runtime.SEL_MS_LONG])
+            jobs.append((runtime.KIND_MS, 4 * k + 1024, 64 * k + 65536, 300 * k + 65536,
+                         [(pb, sels[runtime.SEL_MS_SHORT], False), (pb, sels[runtime.SEL_MS_LONG], True)]))
+        if self.protocols.mc_mode == "fixed" and cnt[runtime.SEL_MC]:
+            k = int(cnt[runtime.SEL_MC])
+            jobs.append((runtime.KIND_MC, 4 * k + 1024, 96 * k + 65536, 400 * k + 65536,
+                         [(lb.mc_batch(), sels[runtime.SEL_MC], False)]))
+        if cnt[runtime.SEL_MN]:
+            k = int(cnt[runtime.SEL_MN])
+            jobs.append((runtime.KIND_MN, len(bk.mn_pids) * k + 1024, int(4 * len(data) + 64 * k + 65536),
+                         int(6 * len(data) + 400 * k + 65536), [(lb.mn_batch(), sels[runtime.SEL_MN], False)]))
+        elig = self.protocols.mn_eligibility(self.rfmode)
+        texts: List[Any] = [None] * n
+        for kind, rec_cap, heap_cap, json_cap, launches in jobs:
+            for _attempt in range(4):
+                out = eng.alloc_out(n, rec_cap, heap_cap)
+                for bd, sel, long_v in launches:
+                    if not sel.numel():
+                        continue
+                    if kind == runtime.KIND_MN:
+                        eng.launch_mn(bd, out, elig=elig, sel=sel)
+                    elif kind == runtime.KIND_MC:
+                        eng.launch_mc(bd, out, sel=sel)
+                    else:
+                        eng.launch_pulses(kind, bd, out, sel=sel, long_variant=long_v)
+                jo = eng.alloc_json(n, json_cap)
+                eng.launch_json(kind, out, lo, n, jo, first_only=True)
+                c1 = out["cursor"].cpu().numpy()
+                c2 = jo["cursor"].cpu().numpy()
+                if not c1[2] and not c2[1]:
+                    break
+                rec_cap, heap_cap, json_cap = 4 * rec_cap, 4 * heap_cap, 4 * json_cap
+            else:
+                raise RuntimeError("result / JSON capacity overflow persists")
+            lens = jo["len"][:n].cpu().numpy()
+            offs = jo["off"][:n].cpu().numpy()
+            blob = jo["json"][: int(c2[0])].cpu().numpy().tobytes()
+            for i in np.nonzero(lens > 0)[0]:
+                texts[int(i)] = blob[int(offs[i]): int(offs[i]) + int(lens[i])].decode("ascii")
+        status = lb.status[:n].cpu().numpy()
+        kinds = lb.kind[:n].cpu().numpy()
+        for i in range(n):
+            if i in bad:
+                texts[i] = bad[i]
+            elif int(status[i]) == runtime.LS_UNSUPPORTED:
+                texts[i] = ContractError(f"line {i} is outside the device contract of the front end "
+                                         f"(kind {_KIND_NAME.get(int(kinds[i]), '?')})")
+        return texts
+
     @staticmethod
     def _meta_str(m: np.ndarray, base: int) -> Optional[str]:
         ln = int(m[base + 15])

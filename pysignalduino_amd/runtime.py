@@ -35,7 +35,7 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
-            "sdx_parse_lines", "sdx_select_lines"]
+            "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json"]
 
 
 class SdxPulseBatch(Structure):
@@ -54,6 +54,17 @@ class SdxMcBatch(Structure):
 class SdxMnBatch(Structure):
     _fields_ = [("hex_dev", c_void_p), ("offsets_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p),
                 ("n", c_int32), ("n_sel", c_int32), ("elig", ctypes.c_uint64), ("method", c_int32), ("res", c_int32)]
+
+
+class SdxJsonIn(Structure):
+    _fields_ = [("kind", c_int32), ("first_only", c_int32), ("desc_dev", c_void_p), ("rec_dev", c_void_p),
+                ("cursor_dev", c_void_p), ("heap_dev", c_void_p), ("meta_dev", c_void_p), ("pat_val_dev", c_void_p),
+                ("cp_slot_dev", c_void_p), ("n", c_int32), ("rec_max", c_int32)]
+
+
+class SdxJsonOut(Structure):
+    _fields_ = [("json_dev", c_void_p), ("off_dev", c_void_p), ("len_dev", c_void_p), ("cursor_dev", c_void_p),
+                ("json_cap", c_uint32), ("res", c_uint32)]
 
 
 class SdxOut(Structure):
@@ -111,6 +122,8 @@ def load_library(path: Optional[str] = None):
     lib.sdx_demod_mc.restype = c_int
     lib.sdx_demod_mn.argtypes = [c_void_p, POINTER(SdxMnBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mn.restype = c_int
+    lib.sdx_serialize_json.argtypes = [c_void_p, POINTER(SdxJsonIn), POINTER(SdxJsonOut), c_void_p]
+    lib.sdx_serialize_json.restype = c_int
     lib.sdx_parse_lines.argtypes = [POINTER(SdxLines), POINTER(SdxLinesOut), c_void_p]
     lib.sdx_parse_lines.restype = c_int
     lib.sdx_select_lines.argtypes = [POINTER(SdxLinesOut), c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
@@ -127,7 +140,7 @@ def check_layout(lib) -> None:
     """The numpy mirrors of the C structs must match sizeof() on the C side."""
     want = {0: struct.calcsize(bankmod.HDR_FMT), 1: bankmod.PATSPEC.itemsize, 2: bankmod.MU_REC.itemsize, 3: bankmod.MS_REC.itemsize,
             4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize,
-            8: bankmod.MN_REC.itemsize}
+            8: bankmod.MN_REC.itemsize, 9: bankmod.JSON_REC.itemsize}
     for k, v in want.items():
         got = lib.sdx_layout_size(k)
         if got != v:
@@ -257,6 +270,23 @@ class Engine:
                        0 if sel is None else int(sel.numel()), elig, method, 0)
         o = self._out_struct(out)
         _check(self.lib, self.lib.sdx_demod_mn(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
+
+    def launch_json(self, kind: int, demod_out, lines_out, n: int, jout, first_only: bool = True) -> None:
+        """sdx_serialize_json over a demodulation launch's device outputs (no host sync)."""
+        ji = SdxJsonIn(kind, 1 if first_only else 0, _ptr(demod_out["desc"]), _ptr(demod_out["rec"]),
+                       _ptr(demod_out["cursor"]), _ptr(demod_out["heap"]), _ptr(lines_out["meta"]),
+                       _ptr(lines_out.get("pat_val")), _ptr(lines_out.get("cp_slot")), n,
+                       0 if first_only else demod_out["rec_cap"])
+        jo = SdxJsonOut(_ptr(jout["json"]), _ptr(jout["off"]), _ptr(jout["len"]), _ptr(jout["cursor"]),
+                        jout["cap"], 0)
+        _check(self.lib, self.lib.sdx_serialize_json(self.handle, ctypes.byref(ji), ctypes.byref(jo),
+                                                     self.stream_ptr()))
+
+    def alloc_json(self, items: int, cap: int):
+        t, d = self.torch, self.dev
+        return {"json": t.empty(max(cap, 8), dtype=t.uint8, device=d), "off": t.empty(max(items, 1), dtype=t.int32, device=d),
+                "len": t.empty(max(items, 1), dtype=t.int32, device=d), "cursor": t.zeros(2, dtype=t.int32, device=d),
+                "cap": cap, "items": items}
 
     # -- full run with contract routing and overflow re-runs (all on the GPU) --------------------
     def run(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None,
