@@ -1,0 +1,150 @@
+"""Batched controller loop: pysignalduino_amd.controller.BatchingParserTask vs the
+reference's per-line _parser_task (signalduino/controller.py:245-264).
+
+CPU tests drive the loop with a scripted parser (no GPU) and check it against a restatement of the
+reference loop: same callbacks / publications (first decoded message only) / command-response calls,
+in line order, with many lines per parse_lines call.  The GPU test runs the real SignalParser."""
+import asyncio
+import json
+import logging
+
+import pytest
+
+from pysignalduino_amd.controller import BatchingParserTask
+
+
+class FakeParser:
+    """parse_line(line) -> a scripted list; parse_lines = map of it (records the batch sizes)."""
+
+    def __init__(self):
+        self.batches = []
+
+    def parse_line(self, line):
+        if "boom" in line:
+            raise ValueError("contract")
+        k = sum(map(ord, line)) % 3
+        return [(line, j) for j in range(k)]
+
+    def parse_lines(self, lines):
+        self.batches.append(len(lines))
+        out = []
+        for ln in lines:
+            try:
+                out.append(self.parse_line(ln))
+            except ValueError as e:
+                out.append(e)
+        return out
+
+    def parse_lines_json(self, lines):
+        return [(json.dumps(r[0]) if r else None) if not isinstance(r, Exception) else r
+                for r in self.parse_lines(lines)]
+
+
+class Pub:
+    def __init__(self):
+        self.sent = []
+        self.base_topic = "t/v1"
+        self.client = self
+
+    async def publish(self, *a):
+        self.sent.append(a)
+
+
+class Ctl:
+    def __init__(self, parser, callback=True):
+        self._stop_event = asyncio.Event()
+        self._raw_message_queue = asyncio.Queue()
+        self.parser = parser
+        self.mqtt_publisher = Pub()
+        self.cb = []
+        self.cmd = []
+        self.message_callback = self._cb if callback else None
+        self.logger = logging.getLogger("test")
+
+    async def _cb(self, m):
+        self.cb.append(m)
+
+    async def _handle_as_command_response(self, line):
+        self.cmd.append(line)
+
+
+def reference_side_effects(parser, lines):
+    """controller.py:245-264 restated (the per-line loop's observable effects)."""
+    cb, sent, cmd = [], [], []
+    for line in lines:
+        if not line:
+            continue
+        try:
+            decoded = parser.parse_line(line)
+        except ValueError:
+            decoded = []          # in the reference the task would stop; lines outside the contract
+        if decoded:
+            cb.append(decoded[0])
+            sent.append((decoded[0],))
+        cmd.append(line)
+    return cb, sent, cmd
+
+
+async def _drive(ctl, task, lines, chunk=37):
+    runner = asyncio.create_task(task.run())
+    for i in range(0, len(lines), chunk):
+        for ln in lines[i:i + chunk]:
+            await ctl._raw_message_queue.put(ln)
+        await asyncio.sleep(0)
+    while not ctl._raw_message_queue.empty() or len(ctl.cmd) < len([x for x in lines if x]):
+        await asyncio.sleep(0.01)
+    ctl._stop_event.set()
+    runner.cancel()
+    await asyncio.gather(runner, return_exceptions=True)
+
+
+def test_batched_loop_matches_reference_loop():
+    lines = [f"MS;P0={i};D=01;" for i in range(500)] + ["", "boom"] + [f"MU;{i}" for i in range(300)]
+    parser = FakeParser()
+    ctl = Ctl(parser)
+    task = BatchingParserTask(ctl, max_batch=64, max_delay=0.01)
+    asyncio.run(_drive(ctl, task, lines))
+    cb, sent, cmd = reference_side_effects(FakeParser(), lines)
+    assert ctl.cb == cb and ctl.mqtt_publisher.sent == sent and ctl.cmd == cmd
+    assert max(parser.batches) > 1 and all(b <= 64 for b in parser.batches)
+    assert task.lines == 801
+
+
+def test_batched_loop_json_mode():
+    lines = [f"MC;D={i};" for i in range(200)]
+    parser = FakeParser()
+    ctl = Ctl(parser, callback=False)
+    task = BatchingParserTask(ctl, publish="json").install()
+    assert ctl._parser_task == task.run
+    asyncio.run(_drive(ctl, task, lines))
+    _, sent, _ = reference_side_effects(FakeParser(), lines)
+    assert ctl.mqtt_publisher.sent == [("t/v1/state/messages", json.dumps(s[0])) for s in sent]
+    with pytest.raises(ValueError):
+        BatchingParserTask(Ctl(parser), publish="json")
+
+
+@pytest.mark.gpu
+def test_batched_loop_with_the_gpu_parser():
+    """Real lines through the real SignalParser: the published messages are parse_line(line)[0]."""
+    from pysignalduino_amd import bank as B
+    from pysignalduino_amd import synth
+    from pysignalduino_amd.frontend import SignalParser
+    P = B.Bank().protocols
+    raw, _ = synth.line_corpus(P, 3000, seed=91)
+    raw += [synth.frame(synth.mn_payload(*f)) for f in synth.mn_frames(1000, seed=92)]
+    lines = [ln.decode("latin-1") for ln in raw]
+    sp = SignalParser()
+    ctl = Ctl(sp)
+    task = BatchingParserTask(ctl, max_batch=512)
+    asyncio.run(_drive(ctl, task, lines, chunk=200))
+    exp = [r[0] for r in sp.parse_lines(lines) if not isinstance(r, Exception) and r]
+    got = [m[0] for m in ctl.mqtt_publisher.sent]
+    key = lambda d: (d.protocol_id, d.payload, d.metadata, d.raw.line)  # noqa: E731
+    assert [key(d) for d in got] == [key(d) for d in exp]
+    assert [key(d) for d in ctl.cb] == [key(d) for d in exp]
+    assert ctl.cmd == lines and task.batches < len(lines) / 4
+    # json mode publishes the device texts of the same messages
+    from oracle import json_oracle as J
+    ctl2 = Ctl(sp, callback=False)
+    asyncio.run(_drive(ctl2, BatchingParserTask(ctl2, max_batch=512, publish="json"), lines, chunk=200))
+    assert [t for _, t in ctl2.mqtt_publisher.sent] == [J.published([d]) for d in exp]
