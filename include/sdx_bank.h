@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 10u
+#define SDX_BANK_VERSION 12u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -26,9 +26,8 @@
  * pattern_utils.py:34-136, with its unique values (first-appearance order)
  * and their tolerances (calculate_tolerance, pattern_utils.py:15-26) */
 typedef struct {
-  double uval[SDX_MAXUNIQ];
-  double utol[SDX_MAXUNIQ];
-  /* the same test on the integer k of a normalised value k/10 (round(x/clock, 1)):
+  /* hot part (one 64-byte line): what the lane filter reads per (message, protocol) */
+  /* the test on the integer k of a normalised value k/10 (round(x/clock, 1)):
    * candidate  <=>  klo[u] <= k <= khi[u]  (exact; computed by bank.py _k_interval) */
   int32_t klo[SDX_MAXUNIQ], khi[SDX_MAXUNIQ];
   /* candidate ordering (stable sort by fp64 gap, pattern_utils.py:61-63): rank of k in the u16
@@ -37,9 +36,12 @@ typedef struct {
   uint8_t len;   /* search length; 0 = key absent/falsy */
   uint8_t nuniq; /* number of distinct values */
   uint8_t pad[6];
-  uint8_t uidx[SDX_MAXSEARCH]; /* search position -> unique index */
-  uint64_t uidx_pk;            /* the same, nibble i = uidx[i] */
-} sdx_patspec;                 /* 144 bytes */
+  uint64_t uidx_pk;            /* search position -> unique index, nibble i */
+  /* cold part: the values themselves (the long-message variant's fp64 path) */
+  double uval[SDX_MAXUNIQ];
+  double utol[SDX_MAXUNIQ];
+  uint8_t uidx[SDX_MAXSEARCH]; /* the same as uidx_pk, one byte per position */
+} sdx_patspec;                 /* 144 bytes, 64-byte hot part first */
 
 enum sdx_postdemo {
   SDX_PD_NONE = 0, SDX_PD_EM, SDX_PD_REVOLT, SDX_PD_FS20, SDX_PD_FHT80, SDX_PD_FHT80TF,
@@ -49,6 +51,7 @@ enum sdx_postdemo {
 /* MU protocol = every id with 'clockabs' (message_unsynced.py:45) */
 typedef struct {
   double clock;                         /* float(clockabs)  (:59) */
+  uint8_t has_start, recon, dispatch_bin, remove_zero, active, never, res0, res1;
   sdx_patspec start, one, zero, flt;    /* (:67-141) */
   int32_t proto_index;                  /* index into the full bank (host: pid string) */
   int32_t length_min;                   /* regex {min,}  (:178) */
@@ -59,9 +62,27 @@ typedef struct {
   int32_t mm_dfa;                       /* modulematch DFA index, -1 = none (:277) */
   int32_t mm_pre_state;                 /* DFA state after consuming the (constant) preamble */
   int32_t pre_off, pre_len, post_off, post_len; /* string heap (:271-274) */
-  uint8_t has_start, recon, dispatch_bin, remove_zero, active, never, res0, res1;
   int32_t res2;
 } sdx_mu_proto;
+
+/* The MU lane filter's view of one protocol, packed into ONE 128-byte aligned record (the scalar
+ * data cache then fetches a protocol's filter state with two line reads instead of ~10): flags,
+ * clock and the four search lists with k bounds as int16 and rank offsets as uint16.  A list that
+ * does not fit (more than 3 distinct values, |k| > 32767, rank offset > 65535) sets `full`, and the
+ * filter reads sdx_mu_proto instead. */
+typedef struct {
+  uint32_t lohi[3];      /* unique value u: klo in the low 16 bits (two's complement), khi in the high 16 */
+  uint32_t rk01;         /* rk_off[0] | rk_off[1] << 16 */
+  uint32_t rk2_len_nu;   /* rk_off[2] | len << 16 | nuniq << 24 */
+  uint32_t upk;          /* uidx_pk (search lists of <= 8 positions; start: see start_upk) */
+} sdx_fspec;             /* 24 bytes */
+typedef struct {
+  double clock;          /* float(clockabs) */
+  uint64_t start_upk;    /* uidx_pk of the start list (<= 16 positions) */
+  uint32_t flags;        /* bit0 has_start, bit1 never, bit2 active, bit3 full */
+  sdx_fspec spec[4];     /* start, one, zero, float */
+  uint32_t res[3];
+} sdx_mu_filt;           /* 128 bytes */
 
 /* MS protocol = every id with 'sync' (message_synced.py:79) */
 typedef struct {
@@ -164,6 +185,7 @@ typedef struct {
   uint32_t n_mn;        /* MN protocols (sdx_mn_proto[n_mn] at off_mn) */
   uint32_t off_mn;
   uint32_t off_json;    /* sdx_json_rec[n_mu + n_ms + n_mc + n_mn], class-major (MU, MS, MC, MN) */
+  uint32_t off_mufilt;  /* sdx_mu_filt[n_mu], 128-byte aligned */
   uint32_t res;
 } sdx_bank_hdr;
 

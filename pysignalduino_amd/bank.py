@@ -28,18 +28,18 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 10
+MAGIC, VERSION = 0x4B4E4253, 12
 INT_NONE = 2147483647  # "no length_max" sentinel
 
-PATSPEC = np.dtype([("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("klo", "<i4", (MAXUNIQ,)),
-                    ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)), ("len", "u1"), ("nuniq", "u1"),
-                    ("pad", "u1", (6,)), ("uidx", "u1", (MAXSEARCH,)), ("uidx_pk", "<u8")], align=True)
-MU_REC = np.dtype([("clock", "<f8"), ("start", PATSPEC), ("one", PATSPEC), ("zero", PATSPEC), ("flt", PATSPEC),
+PATSPEC = np.dtype([("klo", "<i4", (MAXUNIQ,)), ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)),
+                    ("len", "u1"), ("nuniq", "u1"), ("pad", "u1", (6,)), ("uidx_pk", "<u8"),
+                    ("uval", "<f8", (MAXUNIQ,)), ("utol", "<f8", (MAXUNIQ,)), ("uidx", "u1", (MAXSEARCH,))], align=True)
+MU_REC = np.dtype([("clock", "<f8"), ("has_start", "u1"), ("recon", "u1"), ("dispatch_bin", "u1"),
+                   ("remove_zero", "u1"), ("active", "u1"), ("never", "u1"), ("res0", "u1"), ("res1", "u1"),
+                   ("start", PATSPEC), ("one", PATSPEC), ("zero", PATSPEC), ("flt", PATSPEC),
                    ("proto_index", "<i4"), ("length_min", "<i4"), ("length_max", "<i4"), ("width", "<i4"),
                    ("pad_bits", "<i4"), ("postdemo", "<i4"), ("mm_dfa", "<i4"), ("mm_pre_state", "<i4"), ("pre_off", "<i4"),
-                   ("pre_len", "<i4"), ("post_off", "<i4"), ("post_len", "<i4"), ("has_start", "u1"),
-                   ("recon", "u1"), ("dispatch_bin", "u1"), ("remove_zero", "u1"), ("active", "u1"),
-                   ("never", "u1"), ("res0", "u1"), ("res1", "u1"), ("res2", "<i4")], align=True)
+                   ("pre_len", "<i4"), ("post_off", "<i4"), ("post_len", "<i4"), ("res2", "<i4")], align=True)
 MS_REC = np.dtype([("pclock", "<f8"), ("key", PATSPEC, (4,)), ("proto_index", "<i4"), ("width", "<i4"),
                    ("lmin_sync", "<i4"), ("lir_min", "<i4"), ("lir_max", "<i4"), ("pad_bits", "<i4"),
                    ("postdemo", "<i4"), ("pre_off", "<i4"), ("pre_len", "<i4"), ("post_off", "<i4"),
@@ -54,7 +54,10 @@ MN_REC = np.dtype([("proto_index", "<i4"), ("lir_min", "<i4"), ("lir_max", "<i4"
                    ("pre_off", "<i4"), ("pre_len", "<i4"), ("res", "<i4")])
 JSON_REC = np.dtype([("pid_off", "<u4"), ("s1_off", "<u4"), ("s2_off", "<u4"), ("pid_len", "<u2"), ("s1_len", "<u2"),
                      ("s2_len", "<u2"), ("res", "<u2")])
-HDR_FMT = "<" + "I" * 29  # sdx_bank_hdr: 29 uint32
+FSPEC = np.dtype([("lohi", "<u4", (3,)), ("rk01", "<u4"), ("rk2_len_nu", "<u4"), ("upk", "<u4")])
+MU_FILT = np.dtype([("clock", "<f8"), ("start_upk", "<u8"), ("flags", "<u4"), ("spec", FSPEC, (4,)),
+                    ("res", "<u4", (3,))])
+HDR_FMT = "<" + "I" * 30  # sdx_bank_hdr: 30 uint32
 # MU decode descriptor (sdx_mu_desc): what the compacted decode reads per (message, protocol) pair,
 # staged in LDS once per tile
 MU_DESC = np.dtype([("pre", "u1", (16,)), ("post", "u1", (2,)), ("pre_len", "u1"), ("post_len", "u1"),
@@ -431,6 +434,7 @@ class Bank:
                     jrec[j]["s2_off"], jrec[j]["s2_len"] = self._str(s2)
                 j += 1
         self.json_table = jrec
+        mufilt = self._mu_filters(mu)
 
         if b"\n" in bytes(self._heap):
             raise NotImplementedError("newline inside a preamble/postamble ($ semantics)")
@@ -482,22 +486,58 @@ class Bank:
         ranks = np.asarray(self._ranks, dtype=np.uint16)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
                     trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
-                    order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes(), mn.tobytes(), jrec.tobytes()]
+                    order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes(), mn.tobytes(), jrec.tobytes(),
+                    mufilt.tobytes()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
-        for s in sections:
+        for k, s in enumerate(sections):
+            if k == 15:                      # sdx_mu_filt: whole 128-byte scalar-cache lines
+                cur = (cur + 127) // 128 * 128
             offs.append(cur)
             cur = (cur + len(s) + 15) // 16 * 16
         total = cur
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
                           len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], offs[10], offs[11], offs[12],
-                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], offs[14], 0)
+                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], offs[14], offs[15], 0)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s
         self.blob = bytes(blob)
         self.mu_table, self.ms_table, self.mc_table, self.mn_table = mu, ms, mc, mn
+
+    @staticmethod
+    def _mu_filters(mu) -> np.ndarray:
+        """sdx_mu_filt: the lane filter's compact copy of each MU record (include/sdx_bank.h)."""
+        f = np.zeros(len(mu), MU_FILT)
+        for r in range(len(mu)):
+            rec, x = mu[r], f[r]
+            x["clock"] = rec["clock"]
+            full = False
+            for i, key in enumerate(("start", "one", "zero", "flt")):
+                ps, fs = rec[key], x["spec"][i]
+                nu = int(ps["nuniq"])
+                if nu > 3:
+                    full = True
+                    continue
+                for u in range(nu):
+                    lo, hi, ro = int(ps["klo"][u]), int(ps["khi"][u]), int(ps["rk_off"][u])
+                    if not (-32768 <= lo <= 32767 and -32768 <= hi <= 32767 and 0 <= ro <= 65535):
+                        full = True
+                    fs["lohi"][u] = (lo & 0xFFFF) | ((hi & 0xFFFF) << 16)
+                rk = [int(ps["rk_off"][u]) & 0xFFFF for u in range(3)]
+                fs["rk01"] = rk[0] | (rk[1] << 16)
+                fs["rk2_len_nu"] = rk[2] | (int(ps["len"]) << 16) | (nu << 24)
+                upk = int(ps["uidx_pk"])
+                if key == "start":
+                    x["start_upk"] = upk
+                elif upk >= 1 << 32:
+                    full = True
+                else:
+                    fs["upk"] = upk
+            x["flags"] = (int(rec["has_start"]) | (int(rec["never"]) << 1) | (int(rec["active"]) << 2) |
+                          ((1 if full else 0) << 3))
+        return f
 
     def _mu_desc(self, mu, dfas, cls_of):
         """MU decode descriptors + the LDS modulematch tables.

@@ -514,6 +514,7 @@ struct BankView {
   const uint16_t* rank;   // candidate gap-rank tables
   const sdx_mu_desc* mudesc;
   const uint8_t* mmtab;
+  const sdx_mu_filt* mufilt;  // compact MU lane-filter records (128 B each)
 };
 
 SDX_DEV BankView bank_view(const void* blob) {
@@ -533,6 +534,7 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.rank = (const uint16_t*)(v.base + v.hdr->off_rank);
   v.mudesc = (const sdx_mu_desc*)(v.base + v.hdr->off_mudesc);
   v.mmtab = v.base + v.hdr->off_mmtab;
+  v.mufilt = (const sdx_mu_filt*)(v.base + v.hdr->off_mufilt);
   v.hdr = uniform_ptr(v.hdr);
   v.mu = uniform_ptr(v.mu);
   v.ms = uniform_ptr(v.ms);
@@ -547,6 +549,7 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.rank = uniform_ptr(v.rank);
   v.mudesc = uniform_ptr(v.mudesc);
   v.mmtab = uniform_ptr(v.mmtab);
+  v.mufilt = uniform_ptr(v.mufilt);
   return v;
 }
 

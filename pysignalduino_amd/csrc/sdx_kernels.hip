@@ -1423,8 +1423,14 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         if (k < npat) kq[k] = py_round1_k(val[k] / clock);
     }
   }
+  // pattern_exists: lane variant on a SpecV (compact MU filter record or full patspec), long
+  // variant on the full patspec
+  auto PEXV = [&](const SpecV& sv, const sdx_patspec* sp, int minpos, bool need_pos) -> PexRes {
+    if constexpr (NW <= 4) return pexists_lane<NW>(sv, kq, ids, npat, bmine, minpos, bv.rank, P0, P1, need_pos);
+    else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
+  };
   auto PEX = [&](const sdx_patspec* sp, int minpos, bool need_pos) -> PexRes {
-    if constexpr (NW <= 4) return pexists_lane<NW>(sp, kq, ids, npat, bmine, minpos, bv.rank, P0, P1, need_pos);
+    if constexpr (NW <= 4) return pexists_lane<NW>(spec_full(sp), kq, ids, npat, bmine, minpos, bv.rank, P0, P1, need_pos);
     else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
   };
   // ---- protocol loop: waves take protocols one at a time, in the bank's processing order
@@ -1493,27 +1499,38 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     ++cur;
     if constexpr (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
-      if (cld(&rec->never) || !cld(&rec->active)) continue;
+      const sdx_mu_filt* fr = uniform_ptr(bv.mufilt + p);  // the filter's state: two 64-byte lines
+      const uint32_t ff = cld(&fr->flags);
+      if ((ff & 2u) || !(ff & 4u)) continue;  // never / not active
 #ifdef SDX_X_NOSTARTPROTO
-      if (cld(&rec->has_start)) continue;
+      if (ff & 1u) continue;
 #endif
+      const bool full = (ff & 8u) != 0;
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
       int idx = 0;
       uint64_t st_tgt = 0, ut0 = 0, ut1 = 0, ut2 = 0;
       int fmask = 0;
       PROF_T(t_norm);
-      if (cld(&rec->clock) != last_clock) {  // wave-uniform: consecutive protocols often share a clock
-        last_clock = cld(&rec->clock);
-        const double ck = cld(&rec->clock);
+      const double pclk = cld(&fr->clock);
+      if (pclk != last_clock) {  // wave-uniform: consecutive protocols often share a clock
+        last_clock = pclk;
 #pragma unroll
         for (int k = 0; k < SDX_MAXPAT; ++k)
-          if (k < npat) kq[k] = py_round1_k(val[k] / ck);
+          if (k < npat) kq[k] = py_round1_k(val[k] / pclk);
       }
       PROF_ADD(1, t_norm);
+      auto SV = [&](int key, const sdx_patspec* sp) -> SpecV {
+        if constexpr (NW <= 4) {
+          if (!full) return spec_compact(&fr->spec[key], key == 0 ? cld(&fr->start_upk) : (uint64_t)cld(&fr->spec[key].upk));
+          return spec_full(sp);
+        } else {
+          return SpecV{};
+        }
+      };
       PROF_T(t_st);
       if (alive) {
-        if (cld(&rec->has_start)) {
-          const PexRes r = PEX(&rec->start, 0, true);
+        if (ff & 1u) {
+          const PexRes r = PEXV(SV(0, &rec->start), &rec->start, 0, true);
           alive = r.found;
           idx = r.pos;
           st_tgt = r.tgt;
@@ -1524,16 +1541,17 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       }
       PROF_ADD(2, t_st);
       PROF_T(t_ozf);
-      if (alive && cld(&rec->one.len)) {
-        const PexRes r = PEX(&rec->one, idx, false);
+      auto klen = [&](int key) -> int { return (int)((cld(&fr->spec[key].rk2_len_nu) >> 16) & 0xFF); };
+      if (alive && klen(1)) {
+        const PexRes r = PEXV(SV(1, &rec->one), &rec->one, idx, false);
         if (r.found) { ut0 = r.tgt; fmask |= 1; } else alive = false;
       }
-      if (alive && cld(&rec->zero.len)) {
-        const PexRes r = PEX(&rec->zero, idx, false);
+      if (alive && klen(2)) {
+        const PexRes r = PEXV(SV(2, &rec->zero), &rec->zero, idx, false);
         if (r.found) { ut1 = r.tgt; fmask |= 2; } else alive = false;
       }
-      if (alive && cld(&rec->flt.len)) {
-        const PexRes r = PEX(&rec->flt, idx, false);
+      if (alive && klen(3)) {
+        const PexRes r = PEXV(SV(3, &rec->flt), &rec->flt, idx, false);
         if (r.found) { ut2 = r.tgt; fmask |= 4; }
       }
       alive = alive && fmask != 0;
@@ -2229,6 +2247,7 @@ int sdx_layout_size(int which) {
     case 7: return (int)sizeof(sdx_mu_desc);
     case 8: return (int)sizeof(sdx_mn_proto);
     case 9: return (int)sizeof(sdx_json_rec);
+    case 10: return (int)sizeof(sdx_mu_filt);
   }
   return -1;
 }
@@ -2244,7 +2263,8 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
       (size_t)h.off_mmtab + h.mmtab_bytes > nbytes || h.mmtab_bytes > SDX_MMTAB_LDS || (h.mmtab_bytes & 15u) ||
       (h.off_mudesc & 15u) || (h.off_mmtab & 15u) || 17u * h.mm_states > h.mmtab_bytes || h.n_mn > SDX_MN_MAX ||
       (size_t)h.off_mn + sizeof(sdx_mn_proto) * h.n_mn > nbytes || (h.off_mn & 15u) ||
-      (size_t)h.off_json + sizeof(sdx_json_rec) * ((size_t)h.n_mu + h.n_ms + h.n_mc + h.n_mn) > nbytes)
+      (size_t)h.off_json + sizeof(sdx_json_rec) * ((size_t)h.n_mu + h.n_ms + h.n_mc + h.n_mn) > nbytes ||
+      (size_t)h.off_mufilt + sizeof(sdx_mu_filt) * h.n_mu > nbytes || (h.off_mufilt & 127u))
     return fail(SDX_EBANK, "bank blob: processing-order section out of range");
   HIPCHK(hipSetDevice(device));
   void* d = nullptr;

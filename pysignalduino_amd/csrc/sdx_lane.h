@@ -145,102 +145,178 @@ SDX_DEV bool pair_bit(uint64_t P0, uint64_t P1, int a, int b) {
   return ((q < 64 ? P0 >> q : P1 >> (q - 64)) & 1ull) != 0;
 }
 
+// one search list as the lane filter reads it (wave-uniform, scalar registers): from the full
+// sdx_patspec or from the compact sdx_fspec of an sdx_mu_filt record
+struct SpecV {
+  int nu, slen;
+  int klo[SDX_MAXUNIQ], khi[SDX_MAXUNIQ];
+  uint32_t rk_off[SDX_MAXUNIQ];
+  uint64_t upk;
+};
+SDX_DEV SpecV spec_full(const sdx_patspec* sp) {
+  SpecV v;
+  v.nu = cld(&sp->nuniq);
+  v.slen = cld(&sp->len);
+#pragma unroll
+  for (int u = 0; u < SDX_MAXUNIQ; ++u) {
+    v.klo[u] = cld(&sp->klo[u]);
+    v.khi[u] = cld(&sp->khi[u]);
+    v.rk_off[u] = cld(&sp->rk_off[u]);
+  }
+  v.upk = cld(&sp->uidx_pk);
+  return v;
+}
+SDX_DEV SpecV spec_compact(const sdx_fspec* fs, uint64_t upk) {
+  SpecV v;
+  const uint32_t w = cld(&fs->rk2_len_nu), rk01 = cld(&fs->rk01);
+  v.nu = (int)(w >> 24);
+  v.slen = (int)((w >> 16) & 0xFF);
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const uint32_t lh = cld(&fs->lohi[u]);
+    v.klo[u] = (int)(int16_t)(lh & 0xFFFF);
+    v.khi[u] = (int)(int16_t)(lh >> 16);
+  }
+  v.klo[3] = 0;
+  v.khi[3] = -1;
+  v.rk_off[0] = rk01 & 0xFFFF;
+  v.rk_off[1] = rk01 >> 16;
+  v.rk_off[2] = w & 0xFFFF;
+  v.rk_off[3] = 0;
+  v.upk = upk;
+  return v;
+}
+
+// rank key of candidate slot j for one search value: (gap rank << 4) | j -- the stable sort key of
+// pattern_utils.py:61-63 (equal fp64 gaps share a rank; ties keep dict order j)
+SDX_DEV uint32_t rank_key(const uint16_t* rt, int kqj, int klo, int j) {
+  return ((uint32_t)rt[kqj - klo] << 4) | (uint32_t)j;
+}
+// the candidate of mask m (non-empty) that comes first in the sorted candidate list: one rank load
+// per candidate, none when m has one bit
+SDX_DEV int first_cand(uint32_t m, const int* kq, int klo, const uint16_t* rt) {
+  if (!(m & (m - 1))) return __ffs(m) - 1;
+  uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < SDX_MAXPAT; ++j)
+    if ((m >> j) & 1u) {
+      const uint32_t k = rank_key(rt, kq[j], klo, j);
+      best = k < best ? k : best;
+    }
+  return (int)(best & 15u);
+}
+
 template <int NW>
-SDX_DEV PexRes pexists_lane(const sdx_patspec* sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
+SDX_DEV PexRes pexists_lane(const SpecV& sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
                             int minpos, const uint16_t* ranks, uint64_t P0, uint64_t P1, bool need_pos) {
   PexRes res{false, -1, 0};
 #ifdef SDX_X_NOCAND
   return PexRes{true, minpos, 0};
 #endif
-  const int nu = cld(&sp->nuniq), slen = cld(&sp->len);
-  uint64_t cand[SDX_MAXUNIQ];
+  const int nu = sp.nu, slen = sp.slen;
+  // candidate slots per unique search value (pattern_utils.py:53-61) as an exact integer interval
+  // test on k (bank.py _k_interval); kq[j] == SDX_K_NONE for j >= npat
+  uint32_t okm[SDX_MAXUNIQ];
   int cnt[SDX_MAXUNIQ];
   long long total = 1;
 #pragma unroll
   for (int u = 0; u < SDX_MAXUNIQ; ++u) {
-    cand[u] = 0;
+    okm[u] = 0;
     cnt[u] = 1;
     if (u < nu) {
-      // candidates (pattern_utils.py:53-61) as an exact integer interval test on k (bank.py
-      // _k_interval); kq[j] == SDX_K_NONE for j >= npat
-      const int klo = cld(&sp->klo[u]), khi = cld(&sp->khi[u]);
-      uint32_t okm = 0;
+      const int klo = sp.klo[u], khi = sp.khi[u];
+      uint32_t m = 0;
 #pragma unroll
-      for (int j = 0; j < SDX_MAXPAT; ++j) okm |= (k_in(kq[j], klo, khi) ? 1u : 0u) << j;
-      const int c = __popc(okm);
-      if (c == 0) return res;  // pattern_utils.py:78-80
-#ifdef SDX_X_NOSORT
-      if (true) {
-#else
-      if (c == 1) {
-#endif
-        cand[u] = (uint64_t)(__ffs(okm) - 1);
+      for (int j = 0; j < SDX_MAXPAT; ++j) m |= (k_in(kq[j], klo, khi) ? 1u : 0u) << j;
+      if (!m) return res;  // pattern_utils.py:78-80
+      okm[u] = m;
+      cnt[u] = __popc(m);
+      total *= cnt[u];
+      if (total > 10000) total = 10001;
+    }
+  }
+  if (nu == 0 || total > 10000) return res;  // pattern_utils.py:93-101
+  const uint64_t upk = sp.upk;
+  // The first hit in itertools.product order (lexicographic in the sorted candidate lists) is
+  // found without sorting for the two common shapes: (a) a 2-pulse search of two distinct values
+  // (width-2 one/zero keys, 2-pulse starts) -- a* = the first-sorted a that has any valid partner,
+  // b* = the first-sorted valid partner of a*; (b) a 1-pulse search -- the first-sorted a whose id
+  // occurs.  Ranks are loaded only for the candidates that compete.
+  if (nu == 2 && slen == 2 && upk == 0x10ull) {
+    const bool cheap = minpos == 0 && !need_pos;  // pair presence decides exactly
+    auto valid = [&](int a, int b, int* pos) -> bool {
+      const int ida = (int)((ids >> (4 * a)) & 15), idb = (int)((ids >> (4 * b)) & 15);
+      if (!pair_bit(P0, P1, ida, idb)) return false;  // "ab" occurs nowhere
+      if (cheap) {
+        *pos = 0;
+        return true;
+      }
+      *pos = m_first(m_occ<NW>(bm, (uint64_t)ida | ((uint64_t)idb << 4), 2), minpos);
+      return *pos >= 0;
+    };
+    uint32_t va = 0;
+    for (uint32_t ma = okm[0]; ma; ma &= ma - 1) {
+      const int a = __ffs(ma) - 1;
+      for (uint32_t mb = okm[1] & ~(1u << a); mb; mb &= mb - 1) {
+        int p;
+        if (valid(a, __ffs(mb) - 1, &p)) {
+          va |= 1u << a;
+          break;
+        }
+      }
+    }
+    if (!va) return res;
+    const int a = first_cand(va, kq, sp.klo[0], ranks + sp.rk_off[0]);
+    uint32_t vb = 0;
+    int pos_of_first = 0;
+    for (uint32_t mb = okm[1] & ~(1u << a); mb; mb &= mb - 1) {
+      int p;
+      if (valid(a, __ffs(mb) - 1, &p)) vb |= 1u << (__ffs(mb) - 1);
+    }
+    const int b = first_cand(vb, kq, sp.klo[1], ranks + sp.rk_off[1]);
+    valid(a, b, &pos_of_first);
+    const int ida = (int)((ids >> (4 * a)) & 15), idb = (int)((ids >> (4 * b)) & 15);
+    res.found = true;
+    res.tgt = (uint64_t)ida | ((uint64_t)idb << 4);
+    res.pos = pos_of_first;  // 0 when pair presence decided (minpos == 0, position not needed)
+    return res;
+  }
+  if (nu == 1 && slen == 1) {
+    uint32_t va = 0;
+    for (uint32_t ma = okm[0]; ma; ma &= ma - 1) {
+      const int a = __ffs(ma) - 1, ida = (int)((ids >> (4 * a)) & 15);
+      if (m_first(m_occ<NW>(bm, (uint64_t)ida, 1), minpos) >= 0) va |= 1u << a;
+    }
+    if (!va) return res;
+    const int a = first_cand(va, kq, sp.klo[0], ranks + sp.rk_off[0]);
+    res.found = true;
+    res.tgt = (ids >> (4 * a)) & 15;
+    res.pos = m_first(m_occ<NW>(bm, res.tgt, 1), minpos);
+    return res;
+  }
+  // general shape: the sorted candidate lists (packed nibbles), then the product loop
+  uint64_t cand[SDX_MAXUNIQ];
+#pragma unroll
+  for (int u = 0; u < SDX_MAXUNIQ; ++u) {
+    cand[u] = 0;
+    if (u < nu) {
+      if (cnt[u] == 1) {
+        cand[u] = (uint64_t)(__ffs(okm[u]) - 1);
       } else {  // stable sort by the fp64 gap of k/10 (bank gap-rank table), ties in dict order
-        const uint16_t* rt = ranks + cld(&sp->rk_off[u]);
+        const uint16_t* rt = ranks + sp.rk_off[u];
+        const int klo = sp.klo[u];
         uint32_t key[SDX_MAXPAT];
 #pragma unroll
-        for (int j = 0; j < SDX_MAXPAT; ++j) {
-          const bool okj = (okm >> j) & 1u;
-#ifdef SDX_X_NORANKLOAD
-          const uint32_t r = (uint32_t)(kq[j] - klo) & 0xFFFu;
-#else
-          const uint32_t r = rt[okj ? kq[j] - klo : 0];  // index always inside [0, khi - klo]
-#endif
-          key[j] = okj ? (r << 4) | (uint32_t)j : 0xFFFFFFFFu;
-        }
+        for (int j = 0; j < SDX_MAXPAT; ++j)
+          key[j] = ((okm[u] >> j) & 1u) ? rank_key(rt, kq[j], klo, j) : 0xFFFFFFFFu;
         sort10(key);
         uint64_t packed = 0;
 #pragma unroll
         for (int i = 0; i < SDX_MAXPAT; ++i)
-          packed |= (i < c) ? (uint64_t)(key[i] & 15u) << (4 * i) : 0ull;
+          packed |= (i < cnt[u]) ? (uint64_t)(key[i] & 15u) << (4 * i) : 0ull;
         cand[u] = packed;
       }
-      cnt[u] = c;
-      total *= c;
-      if (total > 10000) total = 10001;
     }
-  }
-  if (nu == 0 || total > 10000) return res;
-#ifdef SDX_X_NOCOMBO
-  return PexRes{true, minpos, cand[0]};
-#endif
-  const uint64_t upk = cld(&sp->uidx_pk);
-  // fast paths in exact itertools.product order for the common shapes: a 2-pulse search of two
-  // distinct values (width-2 one/zero keys, 2-pulse starts) and a 1-pulse search
-  if (nu == 2 && slen == 2 && upk == 0x10ull) {
-    for (int i = 0; i < cnt[0]; ++i) {
-      const int a = (int)((cand[0] >> (4 * i)) & 15), ida = (int)((ids >> (4 * a)) & 15);
-      for (int j = 0; j < cnt[1]; ++j) {
-        const int b = (int)((cand[1] >> (4 * j)) & 15);
-        if (b == a) continue;  // no id reused (pattern_utils.py:114-115)
-        const int idb = (int)((ids >> (4 * b)) & 15);
-        if (!pair_bit(P0, P1, ida, idb)) continue;  // "ab" occurs nowhere
-        const uint64_t tgt = (uint64_t)ida | ((uint64_t)idb << 4);
-        int p = 0;
-        if (minpos != 0 || need_pos) {
-          p = m_first(m_occ<NW>(bm, tgt, 2), minpos);
-          if (p < 0) continue;
-        }
-        res.found = true;
-        res.pos = p;
-        res.tgt = tgt;
-        return res;
-      }
-    }
-    return res;
-  }
-  if (nu == 1 && slen == 1) {
-    for (int i = 0; i < cnt[0]; ++i) {
-      const int a = (int)((cand[0] >> (4 * i)) & 15), ida = (int)((ids >> (4 * a)) & 15);
-      const int p = m_first(m_occ<NW>(bm, (uint64_t)ida, 1), minpos);
-      if (p >= 0) {
-        res.found = true;
-        res.pos = p;
-        res.tgt = (uint64_t)ida;
-        return res;
-      }
-    }
-    return res;
   }
   int digit[SDX_MAXUNIQ];
 #pragma unroll
