@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 12u
+#define SDX_BANK_VERSION 13u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -83,6 +83,16 @@ typedef struct {
   sdx_fspec spec[4];     /* start, one, zero, float */
   uint32_t res[3];
 } sdx_mu_filt;           /* 128 bytes */
+
+/* the MS lane filter's view of one protocol (as sdx_mu_filt; spec = sync, one, zero, float) */
+typedef struct {
+  double pclock;         /* float(clockabs or 0) */
+  uint64_t sync_upk;     /* uidx_pk of the sync list */
+  uint32_t flags;        /* bit1 never, bit3 full */
+  int32_t width, lmin_sync;
+  sdx_fspec spec[4];
+  uint32_t res;
+} sdx_ms_filt;           /* 128 bytes */
 
 /* MS protocol = every id with 'sync' (message_synced.py:79) */
 typedef struct {
@@ -186,6 +196,7 @@ typedef struct {
   uint32_t off_mn;
   uint32_t off_json;    /* sdx_json_rec[n_mu + n_ms + n_mc + n_mn], class-major (MU, MS, MC, MN) */
   uint32_t off_mufilt;  /* sdx_mu_filt[n_mu], 128-byte aligned */
+  uint32_t off_msfilt;  /* sdx_ms_filt[n_ms], 128-byte aligned */
   uint32_t res;
 } sdx_bank_hdr;
 

@@ -28,7 +28,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 12
+MAGIC, VERSION = 0x4B4E4253, 13
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("klo", "<i4", (MAXUNIQ,)), ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)),
@@ -57,7 +57,9 @@ JSON_REC = np.dtype([("pid_off", "<u4"), ("s1_off", "<u4"), ("s2_off", "<u4"), (
 FSPEC = np.dtype([("lohi", "<u4", (3,)), ("rk01", "<u4"), ("rk2_len_nu", "<u4"), ("upk", "<u4")])
 MU_FILT = np.dtype([("clock", "<f8"), ("start_upk", "<u8"), ("flags", "<u4"), ("spec", FSPEC, (4,)),
                     ("res", "<u4", (3,))])
-HDR_FMT = "<" + "I" * 30  # sdx_bank_hdr: 30 uint32
+MS_FILT = np.dtype([("pclock", "<f8"), ("sync_upk", "<u8"), ("flags", "<u4"), ("width", "<i4"), ("lmin_sync", "<i4"),
+                    ("spec", FSPEC, (4,)), ("res", "<u4")])
+HDR_FMT = "<" + "I" * 31  # sdx_bank_hdr: 31 uint32
 # MU decode descriptor (sdx_mu_desc): what the compacted decode reads per (message, protocol) pair,
 # staged in LDS once per tile
 MU_DESC = np.dtype([("pre", "u1", (16,)), ("post", "u1", (2,)), ("pre_len", "u1"), ("post_len", "u1"),
@@ -435,6 +437,7 @@ class Bank:
                 j += 1
         self.json_table = jrec
         mufilt = self._mu_filters(mu)
+        msfilt = self._ms_filters(ms)
 
         if b"\n" in bytes(self._heap):
             raise NotImplementedError("newline inside a preamble/postamble ($ semantics)")
@@ -487,11 +490,11 @@ class Bank:
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
                     trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
                     order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes(), mn.tobytes(), jrec.tobytes(),
-                    mufilt.tobytes()]
+                    mufilt.tobytes(), msfilt.tobytes()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
         for k, s in enumerate(sections):
-            if k == 15:                      # sdx_mu_filt: whole 128-byte scalar-cache lines
+            if k in (15, 16):                # sdx_mu_filt / sdx_ms_filt: whole 128-byte scalar-cache lines
                 cur = (cur + 127) // 128 * 128
             offs.append(cur)
             cur = (cur + len(s) + 15) // 16 * 16
@@ -499,7 +502,7 @@ class Bank:
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
                           len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], offs[10], offs[11], offs[12],
-                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], offs[14], offs[15], 0)
+                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], offs[14], offs[15], offs[16], 0)
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s
@@ -507,36 +510,55 @@ class Bank:
         self.mu_table, self.ms_table, self.mc_table, self.mn_table = mu, ms, mc, mn
 
     @staticmethod
-    def _mu_filters(mu) -> np.ndarray:
+    def _fspecs(specs, x, first_upk: str) -> bool:
+        """Fill x["spec"][0..3] (sdx_fspec) from four sdx_patspec; False if one does not fit."""
+        ok = True
+        for i, ps in enumerate(specs):
+            fs = x["spec"][i]
+            nu = int(ps["nuniq"])
+            fs["rk2_len_nu"] = (int(ps["len"]) << 16) | (min(nu, 255) << 24)  # len is read even when full
+            if nu > 3:
+                ok = False
+                continue
+            for u in range(nu):
+                lo, hi, ro = int(ps["klo"][u]), int(ps["khi"][u]), int(ps["rk_off"][u])
+                if not (-32768 <= lo <= 32767 and -32768 <= hi <= 32767 and 0 <= ro <= 65535):
+                    ok = False
+                fs["lohi"][u] = (lo & 0xFFFF) | ((hi & 0xFFFF) << 16)
+            rk = [int(ps["rk_off"][u]) & 0xFFFF for u in range(3)]
+            fs["rk01"] = rk[0] | (rk[1] << 16)
+            fs["rk2_len_nu"] = rk[2] | (int(ps["len"]) << 16) | (nu << 24)
+            upk = int(ps["uidx_pk"])
+            if i == 0:
+                x[first_upk] = upk
+            elif upk >= 1 << 32:
+                ok = False
+            else:
+                fs["upk"] = upk
+        return ok
+
+    @classmethod
+    def _mu_filters(cls, mu) -> np.ndarray:
         """sdx_mu_filt: the lane filter's compact copy of each MU record (include/sdx_bank.h)."""
         f = np.zeros(len(mu), MU_FILT)
         for r in range(len(mu)):
             rec, x = mu[r], f[r]
             x["clock"] = rec["clock"]
-            full = False
-            for i, key in enumerate(("start", "one", "zero", "flt")):
-                ps, fs = rec[key], x["spec"][i]
-                nu = int(ps["nuniq"])
-                if nu > 3:
-                    full = True
-                    continue
-                for u in range(nu):
-                    lo, hi, ro = int(ps["klo"][u]), int(ps["khi"][u]), int(ps["rk_off"][u])
-                    if not (-32768 <= lo <= 32767 and -32768 <= hi <= 32767 and 0 <= ro <= 65535):
-                        full = True
-                    fs["lohi"][u] = (lo & 0xFFFF) | ((hi & 0xFFFF) << 16)
-                rk = [int(ps["rk_off"][u]) & 0xFFFF for u in range(3)]
-                fs["rk01"] = rk[0] | (rk[1] << 16)
-                fs["rk2_len_nu"] = rk[2] | (int(ps["len"]) << 16) | (nu << 24)
-                upk = int(ps["uidx_pk"])
-                if key == "start":
-                    x["start_upk"] = upk
-                elif upk >= 1 << 32:
-                    full = True
-                else:
-                    fs["upk"] = upk
+            ok = cls._fspecs([rec[k] for k in ("start", "one", "zero", "flt")], x, "start_upk")
             x["flags"] = (int(rec["has_start"]) | (int(rec["never"]) << 1) | (int(rec["active"]) << 2) |
-                          ((1 if full else 0) << 3))
+                          ((0 if ok else 1) << 3))
+        return f
+
+    @classmethod
+    def _ms_filters(cls, ms) -> np.ndarray:
+        """sdx_ms_filt: the MS lane filter's compact copy of each MS record."""
+        f = np.zeros(len(ms), MS_FILT)
+        for r in range(len(ms)):
+            rec, x = ms[r], f[r]
+            x["pclock"] = rec["pclock"]
+            x["width"], x["lmin_sync"] = rec["width"], rec["lmin_sync"]
+            ok = cls._fspecs([rec["key"][k] for k in range(4)], x, "sync_upk")
+            x["flags"] = (int(rec["never"]) << 1) | ((0 if ok else 1) << 3)
         return f
 
     def _mu_desc(self, mu, dfas, cls_of):

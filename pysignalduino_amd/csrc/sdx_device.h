@@ -515,6 +515,7 @@ struct BankView {
   const sdx_mu_desc* mudesc;
   const uint8_t* mmtab;
   const sdx_mu_filt* mufilt;  // compact MU lane-filter records (128 B each)
+  const sdx_ms_filt* msfilt;  // compact MS lane-filter records
 };
 
 SDX_DEV BankView bank_view(const void* blob) {
@@ -535,6 +536,7 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.mudesc = (const sdx_mu_desc*)(v.base + v.hdr->off_mudesc);
   v.mmtab = v.base + v.hdr->off_mmtab;
   v.mufilt = (const sdx_mu_filt*)(v.base + v.hdr->off_mufilt);
+  v.msfilt = (const sdx_ms_filt*)(v.base + v.hdr->off_msfilt);
   v.hdr = uniform_ptr(v.hdr);
   v.mu = uniform_ptr(v.mu);
   v.ms = uniform_ptr(v.ms);
@@ -550,6 +552,7 @@ SDX_DEV BankView bank_view(const void* blob) {
   v.mudesc = uniform_ptr(v.mudesc);
   v.mmtab = uniform_ptr(v.mmtab);
   v.mufilt = uniform_ptr(v.mufilt);
+  v.msfilt = uniform_ptr(v.msfilt);
   return v;
 }
 

@@ -1429,10 +1429,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     if constexpr (NW <= 4) return pexists_lane<NW>(sv, kq, ids, npat, bmine, minpos, bv.rank, P0, P1, need_pos);
     else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
   };
-  auto PEX = [&](const sdx_patspec* sp, int minpos, bool need_pos) -> PexRes {
-    if constexpr (NW <= 4) return pexists_lane<NW>(spec_full(sp), kq, ids, npat, bmine, minpos, bv.rank, P0, P1, need_pos);
-    else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
-  };
   // ---- protocol loop: waves take protocols one at a time, in the bank's processing order
   // (MU: sorted by clock), from a tile counter -- results are ordered at the flush, so the
   // processing order is free and dynamic assignment balances the waves
@@ -1592,33 +1588,47 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       PROF_ADD(12, t_dec);
     } else {
       const sdx_ms_proto* rec = uniform_ptr(bv.ms + p);
-      if (cld(&rec->never)) continue;
+      const sdx_ms_filt* fr = uniform_ptr(bv.msfilt + p);  // the filter's state: two 64-byte lines
+      const uint32_t ff = cld(&fr->flags);
+      if (ff & 2u) continue;  // never
+      const bool full = (ff & 8u) != 0;
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
-      if (alive && cld(&rec->pclock) > 0.0)  // clock tolerance gate (:83-88)
-        alive = !(fabs(cld(&rec->pclock) - clock) > clock * 0.3);
+      const double pclk = cld(&fr->pclock);
+      if (alive && pclk > 0.0)  // clock tolerance gate (:83-88)
+        alive = !(fabs(pclk - clock) > clock * 0.3);
       int start = 0;
       uint64_t kt0 = 0, kt1 = 0, kt2 = 0, kt3 = 0;
       int fmask = 0;
-      if (alive && cld(&rec->key[0].len)) {  // sync (:140-158)
-        const PexRes r = PEX(&rec->key[0], 0, true);
+      auto SV = [&](int key) -> SpecV {
+        if constexpr (NW <= 4) {
+          if (!full) return spec_compact(&fr->spec[key], key == 0 ? cld(&fr->sync_upk) : (uint64_t)cld(&fr->spec[key].upk));
+          return spec_full(&rec->key[key]);
+        } else {
+          return SpecV{};
+        }
+      };
+      auto klen = [&](int key) -> int { return (int)((cld(&fr->spec[key].rk2_len_nu) >> 16) & 0xFF); };
+      if (alive && klen(0)) {  // sync (:140-158)
+        const PexRes r = PEXV(SV(0), &rec->key[0], 0, true);
         if (r.found) {
           kt0 = r.tgt;
           fmask |= 1;
-          start = r.pos + cld(&rec->key[0].len);
-          const double avail = cld(&rec->width) > 0 ? (double)(n - start) / (double)cld(&rec->width) : 0.0;
-          if ((double)cld(&rec->lmin_sync) > avail) alive = false;
+          start = r.pos + klen(0);
+          const int width = cld(&fr->width);
+          const double avail = width > 0 ? (double)(n - start) / (double)width : 0.0;
+          if ((double)cld(&fr->lmin_sync) > avail) alive = false;
         } else alive = false;
       }
-      if (alive && cld(&rec->key[1].len)) {
-        const PexRes r = PEX(&rec->key[1], 0, false);
+      if (alive && klen(1)) {
+        const PexRes r = PEXV(SV(1), &rec->key[1], 0, false);
         if (r.found) { kt1 = r.tgt; fmask |= 2; } else alive = false;
       }
-      if (alive && cld(&rec->key[2].len)) {
-        const PexRes r = PEX(&rec->key[2], 0, false);
+      if (alive && klen(2)) {
+        const PexRes r = PEXV(SV(2), &rec->key[2], 0, false);
         if (r.found) { kt2 = r.tgt; fmask |= 4; } else alive = false;
       }
-      if (alive && cld(&rec->key[3].len)) {
-        const PexRes r = PEX(&rec->key[3], 0, false);
+      if (alive && klen(3)) {
+        const PexRes r = PEXV(SV(3), &rec->key[3], 0, false);
         if (r.found) { kt3 = r.tgt; fmask |= 8; }
       }
       alive = alive && fmask != 0;
@@ -2248,6 +2258,7 @@ int sdx_layout_size(int which) {
     case 8: return (int)sizeof(sdx_mn_proto);
     case 9: return (int)sizeof(sdx_json_rec);
     case 10: return (int)sizeof(sdx_mu_filt);
+    case 11: return (int)sizeof(sdx_ms_filt);
   }
   return -1;
 }
@@ -2264,7 +2275,8 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
       (h.off_mudesc & 15u) || (h.off_mmtab & 15u) || 17u * h.mm_states > h.mmtab_bytes || h.n_mn > SDX_MN_MAX ||
       (size_t)h.off_mn + sizeof(sdx_mn_proto) * h.n_mn > nbytes || (h.off_mn & 15u) ||
       (size_t)h.off_json + sizeof(sdx_json_rec) * ((size_t)h.n_mu + h.n_ms + h.n_mc + h.n_mn) > nbytes ||
-      (size_t)h.off_mufilt + sizeof(sdx_mu_filt) * h.n_mu > nbytes || (h.off_mufilt & 127u))
+      (size_t)h.off_mufilt + sizeof(sdx_mu_filt) * h.n_mu > nbytes || (h.off_mufilt & 127u) ||
+      (size_t)h.off_msfilt + sizeof(sdx_ms_filt) * h.n_ms > nbytes || (h.off_msfilt & 127u))
     return fail(SDX_EBANK, "bank blob: processing-order section out of range");
   HIPCHK(hipSetDevice(device));
   void* d = nullptr;

@@ -140,7 +140,8 @@ def check_layout(lib) -> None:
     """The numpy mirrors of the C structs must match sizeof() on the C side."""
     want = {0: struct.calcsize(bankmod.HDR_FMT), 1: bankmod.PATSPEC.itemsize, 2: bankmod.MU_REC.itemsize, 3: bankmod.MS_REC.itemsize,
             4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize,
-            8: bankmod.MN_REC.itemsize, 9: bankmod.JSON_REC.itemsize, 10: bankmod.MU_FILT.itemsize}
+            8: bankmod.MN_REC.itemsize, 9: bankmod.JSON_REC.itemsize, 10: bankmod.MU_FILT.itemsize,
+            11: bankmod.MS_FILT.itemsize}
     for k, v in want.items():
         got = lib.sdx_layout_size(k)
         if got != v:

@@ -168,3 +168,34 @@ def test_bank_rejects_unmodelled():
     bad["999"] = {"clockabs": 100, "one": [1, -2], "zero": [2, -1], "length_min": "abc"}
     with pytest.raises(NotImplementedError):
         bankmod.Bank(bad)
+
+
+def test_compact_filter_records_roundtrip():
+    """sdx_mu_filt / sdx_ms_filt hold exactly the lane filter's fields of the full records (len and
+    nuniq even for a list that does not fit, flagged full)."""
+    bk = bankmod.Bank()
+
+    def dec(fs, u):
+        lh = int(fs["lohi"][u])
+        s16 = lambda v: v - 65536 if v >= 32768 else v  # noqa: E731
+        rk = [int(fs["rk01"]) & 0xFFFF, int(fs["rk01"]) >> 16, int(fs["rk2_len_nu"]) & 0xFFFF][u]
+        return s16(lh & 0xFFFF), s16(lh >> 16), rk
+
+    for table, filt, keys, upk0 in ((bk.mu_table, bankmod.Bank._mu_filters(bk.mu_table), ("start", "one", "zero", "flt"),
+                                     "start_upk"),
+                                    (bk.ms_table, bankmod.Bank._ms_filters(bk.ms_table), (0, 1, 2, 3), "sync_upk")):
+        nfull = 0
+        for rec, f in zip(table, filt):
+            full = bool(int(f["flags"]) & 8)
+            nfull += full
+            for i, k in enumerate(keys):
+                ps = rec[k] if isinstance(k, str) else rec["key"][k]
+                fs = f["spec"][i]
+                assert (int(fs["rk2_len_nu"]) >> 16) & 0xFF == int(ps["len"])
+                assert int(fs["rk2_len_nu"]) >> 24 == int(ps["nuniq"])
+                if full:
+                    continue
+                for u in range(int(ps["nuniq"])):
+                    assert dec(fs, u) == (int(ps["klo"][u]), int(ps["khi"][u]), int(ps["rk_off"][u]))
+                assert (int(f[upk0]) if i == 0 else int(fs["upk"])) == int(ps["uidx_pk"])
+        assert nfull < 10
