@@ -1325,15 +1325,43 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   PROF_T(t_stage);
   // ---- stage: per-id position bitmaps (coalesced 64-character rows, 10 ballots each)
   constexpr int NWAVE = pulses_threads<KIND, NW>() / 64;
-  for (int mi = wave; mi < nvalid; mi += NWAVE) {
-    const int msg = msg_of[mi];
-    const int64_t off = b.offsets_dev[msg];
-    int n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
-    if (n > 64 * NW) n = 64 * NW;  // host routes longer messages to the long variant
+  // short variants: a wave's messages are fetched up front -- lane k loads message k's offset and
+  // length, then every message's characters are loaded into registers -- so the global-load
+  // latencies of the wave's messages overlap instead of adding up message after message
+  constexpr int MPW = NW <= 4 ? (TM + NWAVE - 1) / NWAVE : 1;
+  int64_t pf_off = 0;
+  int pf_n = 0;
+  uint32_t pf_c[MPW][NW <= 4 ? NW : 1];
+  if constexpr (NW <= 4) {
+    if (lane < MPW && wave + lane * NWAVE < nvalid) {
+      const int msg = msg_of[wave + lane * NWAVE];
+      pf_off = b.offsets_dev[msg];
+      pf_n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - pf_off);
+      if (pf_n > 64 * NW) pf_n = 64 * NW;
+    }
+#pragma unroll
+    for (int k = 0; k < MPW; ++k) {
+      const int lo = __shfl((int)(uint32_t)pf_off, k), hi = __shfl((int)(uint32_t)((uint64_t)pf_off >> 32), k);
+      const int64_t off = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+      const int n = __shfl(pf_n, k);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int pos = w * 64 + lane;
+        pf_c[k][w] = pos < n ? (uint32_t)b.data_dev[off + pos] : 0xFFu;
+      }
+    }
+  }
+  if constexpr (NW <= 4) {
+#pragma unroll
+  for (int k = 0; k < MPW; ++k) {
+    const int mi = wave + k * NWAVE;
+    if (mi >= nvalid) break;
+    const int n = __shfl(pf_n, k);
     bool nondigit = false;
+#pragma unroll
     for (int w = 0; w < NW; ++w) {
       const int pos = w * 64 + lane;
-      const uint8_t c = pos < n ? b.data_dev[off + pos] : (uint8_t)0xFF;
+      const uint8_t c = (uint8_t)pf_c[k][w];
       nondigit |= pos < n && !((c >= '0' && c <= '9') || c == 0xFE);
       uint64_t mine = 0;
 #pragma unroll
@@ -1367,6 +1395,33 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     if (lane == 0) {
       L.nlen[mi] = n;
       L.digit_ok[mi] = (nd == 0 && n > 0) ? 1u : 0u;
+    }
+  }
+  }
+  if constexpr (NW > 4) {  // long variants: one message per wave
+    for (int mi = wave; mi < nvalid; mi += NWAVE) {
+      const int msg = msg_of[mi];
+      const int64_t off = b.offsets_dev[msg];
+      int n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
+      if (n > 64 * NW) n = 64 * NW;
+      bool nondigit = false;
+      for (int w = 0; w < NW; ++w) {
+        const int pos = w * 64 + lane;
+        const uint8_t c = pos < n ? b.data_dev[off + pos] : (uint8_t)0xFF;
+        nondigit |= pos < n && !((c >= '0' && c <= '9') || c == 0xFE);
+        uint64_t mine = 0;
+#pragma unroll
+        for (int id = 0; id < 10; ++id) {
+          const uint64_t bb = ballot(c == (uint8_t)('0' + id));
+          if (lane == id) mine = bb;
+        }
+        if (lane < 10) L.bm[mi * T::MSTRIDE + lane * T::WS + w] = mine;
+      }
+      const uint64_t nd = ballot(nondigit);
+      if (lane == 0) {
+        L.nlen[mi] = n;
+        L.digit_ok[mi] = (nd == 0 && n > 0) ? 1u : 0u;
+      }
     }
   }
   __syncthreads();
