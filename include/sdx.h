@@ -92,7 +92,8 @@ typedef struct {
 
 /* MN (FSK) batch: the hex characters of each frame (MN_PATTERN group 2, parser/mn.py:17) */
 typedef struct {
-  const uint8_t* hex_dev;      /* hex characters of all frames */
+  const uint8_t* hex_dev;      /* hex characters of all frames; readable 8 bytes past every frame's end
+                                * (k_mn stages frames with aligned 4-byte loads) */
   const int64_t* offsets_dev;  /* [n+1] frame i = hex[offsets[i], offsets[i+1]) (or + len[i]) */
   const int32_t* len_dev;      /* optional [n] frame lengths (as sdx_pulse_batch.len_dev) */
   const int32_t* sel_dev;      /* optional [n_sel] subset of frame indices to run, NULL = all */

@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 13u
+#define SDX_BANK_VERSION 15u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -136,6 +136,13 @@ enum sdx_mn_method {
   SDX_MN_MISSING = 255   /* a 'method' the reference class does not define: protocol skipped (mn.py:171-173) */
 };
 #define SDX_MN_MAX 64    /* MN protocols in a bank (sdx_mn_batch.elig is a 64-bit mask) */
+/* MN checksum tables (byte offsets inside the SDX_MNTAB_BYTES block at off_mntab) */
+#define SDX_MNTAB_CRC1021 0     /* u16[256] */
+#define SDX_MNTAB_CRC8005 512   /* u16[256] */
+#define SDX_MNTAB_CRC31 1024    /* u8[256] */
+#define SDX_MNTAB_LFSR8 1280    /* u16[16][16]: ConvBresser_lightning, key 0xABF9 */
+#define SDX_MNTAB_LFSR21 1792   /* u16[42][16]: ConvBresser_7in1, key 0xBA95 */
+#define SDX_MNTAB_BYTES 3136
 typedef struct {
   int32_t proto_index;
   int32_t lir_min;       /* length_in_range on len(hex) (helpers.py:124-166): -1 = none */
@@ -143,7 +150,7 @@ typedef struct {
   int32_t dfa;           /* regexMatch search DFA (re.search, mn.py:104-113), -1 = no regexMatch */
   int32_t method;        /* enum sdx_mn_method */
   int32_t pre_off, pre_len;  /* preamble (mn.py:176-177) in the string heap */
-  int32_t res;
+  int32_t dfa_slot;      /* distinct-regexMatch index (< 32): k_mn evaluates each pattern once per frame */
 } sdx_mn_proto;          /* 32 bytes */
 
 /* JSON fragments of one protocol for sdx_serialize_json (the MQTT publication of a DecodedMessage,
@@ -197,7 +204,7 @@ typedef struct {
   uint32_t off_json;    /* sdx_json_rec[n_mu + n_ms + n_mc + n_mn], class-major (MU, MS, MC, MN) */
   uint32_t off_mufilt;  /* sdx_mu_filt[n_mu], 128-byte aligned */
   uint32_t off_msfilt;  /* sdx_ms_filt[n_ms], 128-byte aligned */
-  uint32_t res;
+  uint32_t off_mntab;   /* MN checksum tables (SDX_MNTAB_BYTES, bank.py mn_tables) */
 } sdx_bank_hdr;
 
 #endif

@@ -28,7 +28,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 13
+MAGIC, VERSION = 0x4B4E4253, 15
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("klo", "<i4", (MAXUNIQ,)), ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)),
@@ -51,9 +51,52 @@ MC_REC = np.dtype([("cr_lo", "<f8"), ("cr_hi", "<f8"), ("proto_index", "<i4"), (
 DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4"),
                     ("t256_off", "<i4"), ("res", "<i4", (3,))])
 MN_REC = np.dtype([("proto_index", "<i4"), ("lir_min", "<i4"), ("lir_max", "<i4"), ("dfa", "<i4"), ("method", "<i4"),
-                   ("pre_off", "<i4"), ("pre_len", "<i4"), ("res", "<i4")])
+                   ("pre_off", "<i4"), ("pre_len", "<i4"), ("dfa_slot", "<i4")])
 JSON_REC = np.dtype([("pid_off", "<u4"), ("s1_off", "<u4"), ("s2_off", "<u4"), ("pid_len", "<u2"), ("s1_len", "<u2"),
                      ("s2_len", "<u2"), ("res", "<u2")])
+def mn_tables() -> bytes:
+    """Byte/nibble tables of the MN checksums (k_mn stages them in LDS): CRC-16 poly 0x1021 and
+    0x8005 and CRC-8 poly 0x31 (MSB first, init 0: helpers.py:281-309, 630-673), and the
+    LFSR-16 digests of ConvBresser_lightning / _7in1 (helpers.py:190-221, gen 0x8810 from keys
+    0xABF9 / 0xBA95 over 8 / 21 bytes) as per-nibble XOR tables: the key sequence does not depend
+    on the data, so byte k's contribution is the XOR of the keys at its set bits.
+    Layout (include/sdx_bank.h SDX_MNTAB_*): u16 crc1021[256] | u16 crc8005[256] | u8 crc31[256] |
+    u16 lfsr8[16 nibbles][16] | u16 lfsr21[42 nibbles][16]."""
+    def crc16_entry(t, poly):
+        c = t << 8
+        for _ in range(8):
+            c = ((c << 1) ^ poly) & 0xFFFF if c & 0x8000 else (c << 1) & 0xFFFF
+        return c
+
+    def crc8_entry(t):
+        c = t
+        for _ in range(8):
+            c = ((c << 1) ^ 0x31) & 0xFF if c & 0x80 else (c << 1) & 0xFF
+        return c
+
+    def lfsr_nibbles(key, nbytes):
+        keys = []
+        for _ in range(8 * nbytes):
+            keys.append(key)
+            key = (key >> 1) ^ 0x8810 if key & 1 else key >> 1
+        tab = np.zeros((2 * nbytes, 16), np.uint16)
+        for k in range(nbytes):
+            for v in range(16):
+                hi = lo = 0
+                for i in range(4):            # bit i of the nibble; the byte's bit 7 is step 8k
+                    if (v >> i) & 1:
+                        hi ^= keys[8 * k + (3 - i)]
+                        lo ^= keys[8 * k + 4 + (3 - i)]
+                tab[2 * k][v], tab[2 * k + 1][v] = hi, lo
+        return tab
+
+    parts = [np.array([crc16_entry(t, 0x1021) for t in range(256)], np.uint16).tobytes(),
+             np.array([crc16_entry(t, 0x8005) for t in range(256)], np.uint16).tobytes(),
+             np.array([crc8_entry(t) for t in range(256)], np.uint8).tobytes(),
+             lfsr_nibbles(0xABF9, 8).tobytes(), lfsr_nibbles(0xBA95, 21).tobytes()]
+    return b"".join(parts)
+
+
 FSPEC = np.dtype([("lohi", "<u4", (3,)), ("rk01", "<u4"), ("rk2_len_nu", "<u4"), ("upk", "<u4")])
 MU_FILT = np.dtype([("clock", "<f8"), ("start_upk", "<u8"), ("flags", "<u4"), ("spec", FSPEC, (4,)),
                     ("res", "<u4", (3,))])
@@ -386,6 +429,7 @@ class Bank:
         self.mn_rfmode: List[Any] = []
         self.mn_modulation: List[Any] = []
         self.mn_preamble: List[str] = []
+        mn_rx: List[str] = []
         for r, pid in enumerate(self.mn_pids):
             p = P[pid]
             rec = mn[r]
@@ -403,8 +447,12 @@ class Bank:
                 if rx not in mm_patterns:
                     mm_patterns.append(rx)
                 rec["dfa"] = mm_patterns.index(rx)
+                if rx not in mn_rx:
+                    mn_rx.append(rx)
+                rec["dfa_slot"] = mn_rx.index(rx)   # per-frame result cache slot (k_mn)
             else:
                 rec["dfa"] = -1
+                rec["dfa_slot"] = -1
             m = p.get("method")
             if m:
                 if not isinstance(m, str):
@@ -417,6 +465,8 @@ class Bank:
                 else:
                     rec["method"] = MN_MISSING       # mn.py:171-173: not found -> skipped
             pre = f"{p.get('preamble', '')}"
+            if len(mn_rx) > 32:
+                raise NotImplementedError("more than 32 distinct MN regexMatch patterns")
             self.mn_preamble.append(pre)
             rec["pre_off"], rec["pre_len"] = self._str(pre)
 
@@ -490,7 +540,7 @@ class Bank:
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
                     trans_all.tobytes(), flags_all.tobytes(), bytes(self._heap), t256_all.tobytes(),
                     order.tobytes(), ranks.tobytes(), mudesc.tobytes(), mmtab.tobytes(), mn.tobytes(), jrec.tobytes(),
-                    mufilt.tobytes(), msfilt.tobytes()]
+                    mufilt.tobytes(), msfilt.tobytes(), mn_tables()]
         offs = []
         cur = (hdr_size + 15) // 16 * 16
         for k, s in enumerate(sections):
@@ -502,7 +552,7 @@ class Bank:
         blob = bytearray(total)
         hdr = struct.pack(HDR_FMT, MAGIC, VERSION, len(self.pids), len(self.mu_pids), len(self.ms_pids),
                           len(self.mc_pids), len(dfas), n_class, *offs[:8], total, offs[8], offs[9], offs[10], offs[11], offs[12],
-                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], offs[14], offs[15], offs[16], 0)
+                          len(mmtab), mm_states, len(glist), len(self.mn_pids), offs[13], offs[14], offs[15], offs[16], offs[17])
         blob[:hdr_size] = hdr
         for o, s in zip(offs, sections):
             blob[o:o + len(s)] = s

@@ -2331,7 +2331,8 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
       (size_t)h.off_mn + sizeof(sdx_mn_proto) * h.n_mn > nbytes || (h.off_mn & 15u) ||
       (size_t)h.off_json + sizeof(sdx_json_rec) * ((size_t)h.n_mu + h.n_ms + h.n_mc + h.n_mn) > nbytes ||
       (size_t)h.off_mufilt + sizeof(sdx_mu_filt) * h.n_mu > nbytes || (h.off_mufilt & 127u) ||
-      (size_t)h.off_msfilt + sizeof(sdx_ms_filt) * h.n_ms > nbytes || (h.off_msfilt & 127u))
+      (size_t)h.off_msfilt + sizeof(sdx_ms_filt) * h.n_ms > nbytes || (h.off_msfilt & 127u) ||
+      (size_t)h.off_mntab + SDX_MNTAB_BYTES > nbytes || (h.off_mntab & 15u))
     return fail(SDX_EBANK, "bank blob: processing-order section out of range");
   HIPCHK(hipSetDevice(device));
   void* d = nullptr;

@@ -262,8 +262,8 @@ class Engine:
         lens = np.fromiter((len(b) for b in bs), np.int64, len(bs))
         offsets = np.zeros(len(bs) + 1, np.int64)
         np.cumsum(lens, out=offsets[1:])
-        data = np.frombuffer(b"".join(bs), np.uint8)
-        return {"hex": t.from_numpy(data.copy() if len(data) else np.zeros(1, np.uint8)).to(self.dev),
+        data = np.concatenate([np.frombuffer(b"".join(bs), np.uint8), np.zeros(16, np.uint8)])  # 8-byte read slack
+        return {"hex": t.from_numpy(data).to(self.dev),
                 "offsets": t.from_numpy(offsets).to(self.dev), "n": len(bs), "lengths": lens}
 
     def launch_mn(self, bd, out, elig: int = 0, method: int = -1, sel=None) -> None:

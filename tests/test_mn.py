@@ -215,3 +215,38 @@ def test_gpu_mixed_stream_with_mn():
     assert [_flat(g) for g in got[1::2]] == [_flat(g) for g in alone_mn]
     assert [_flat(g) if not isinstance(g, Exception) else type(g) for g in got[0::2]] == \
         [_flat(g) if not isinstance(g, Exception) else type(g) for g in alone_base]
+
+
+def test_checksum_tables_match_the_bit_serial_oracle():
+    """bank.mn_tables (k_mn's LDS tables) reproduce lfsr_digest16 / _calc_crc16 / the LaCrosse CRC-8."""
+    import numpy as np
+    from pysignalduino_amd import bank as B
+    t = B.mn_tables()
+    c1021 = np.frombuffer(t[0:512], np.uint16)
+    c8005 = np.frombuffer(t[512:1024], np.uint16)
+    c31 = np.frombuffer(t[1024:1280], np.uint8)
+    l8 = np.frombuffer(t[1280:1792], np.uint16).reshape(16, 16)
+    l21 = np.frombuffer(t[1792:3136], np.uint16).reshape(42, 16)
+    rng = np.random.default_rng(5)
+    for _ in range(300):
+        d = [int(x) for x in rng.integers(0, 256, size=21)]
+        s = "".join("%02X" % x for x in d)
+        for T, nb, key in ((l21, 21, 0xBA95), (l8, 8, 0xABF9)):
+            acc = 0
+            for k in range(nb):
+                acc ^= int(T[2 * k][d[k] >> 4]) ^ int(T[2 * k + 1][d[k] & 15])
+            assert acc == M.lfsr16(nb, 0x8810, key, s[:2 * nb])
+        for T, poly, nb in ((c1021, 0x1021, 15), (c8005, 0x8005, 10)):
+            c = 0
+            for k in range(nb):
+                c = ((c << 8) & 0xFFFF) ^ int(T[((c >> 8) ^ d[k]) & 0xFF])
+            assert c == M.crc16(s[:2 * nb], poly)
+        c = 0
+        for k in range(4):
+            c = int(c31[c ^ d[k]])
+        ref = 0
+        for k in range(4):
+            ref ^= d[k]
+            for _ in range(8):
+                ref = ((ref << 1) ^ 0x31) & 0xFF if ref & 0x80 else (ref << 1) & 0xFF
+        assert c == ref

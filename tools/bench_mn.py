@@ -71,7 +71,7 @@ def main():
         data = np.frombuffer(b"".join(bs), np.uint8).copy()
         np.savez(cache, data=data, offsets=offsets)
     n = len(offsets) - 1
-    bd = {"hex": torch.from_numpy(data).cuda(), "offsets": torch.from_numpy(offsets).cuda(), "n": n}
+    bd = {"hex": torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda(), "offsets": torch.from_numpy(offsets).cuda(), "n": n}
     elig = (1 << len(bk.mn_pids)) - 1
     out = eng.alloc_out(n, 20 * n + 4096, int(4 * offsets[-1]) + 160 * n + 65536)
     stream = torch.cuda.current_stream()
