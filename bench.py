@@ -78,8 +78,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SDX_DIST_BACKEND=gloo rehearses the N > 1 code path on fewer GPUs than ranks (ranks share
+    # devices round-robin); the driver's runs use RCCL ("nccl") with one GPU per rank
+    backend = os.environ.get("SDX_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -114,11 +122,10 @@ def main():
                 eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, outs[k])
             if record:
                 ev[k][1].record(stream)
-        if world > 1:  # RCCL all-gather of the decoded dmsg buffers (config 5), pysignalduino_amd/dist.py
-            for k, bd in (("MU", bmu), ("MS", bms), ("MC", bmc)):
-                o = outs[k]
-                cur = o["cursor"].cpu()
-                sdist.allgather_results(o["desc"], o["rec"], o["heap"], bd["n"], int(cur[0]), int(cur[1]))
+        if world > 1:  # RCCL all-gather of the decoded dmsg buffers (config 5), pysignalduino_amd/dist.py:
+            # one exchange of the counts, one all-gather of the packed MU/MS/MC buffers
+            sdist.allgather_streams([(outs[k]["desc"], outs[k]["rec"], outs[k]["heap"], bd["n"], outs[k]["cursor"])
+                                     for k, bd in (("MU", bmu), ("MS", bms), ("MC", bmc))])
 
     for _ in range(args.warmup):
         step()

@@ -8,7 +8,7 @@ buffers stay in HBM; the same code runs on ``gloo`` with CPU tensors (tests/test
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import List, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -22,6 +22,66 @@ def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
     q, r = divmod(n, world)
     lo = rank * q + min(rank, r)
     return lo, lo + q + (1 if rank < r else 0)
+
+
+def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """all_gather into one contiguous tensor (one collective; list form where the backend lacks it)."""
+    try:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    except (RuntimeError, NotImplementedError, AttributeError):
+        dist.all_gather(list(out.chunk(dist.get_world_size(group))), inp, group=group)
+
+
+def allgather_streams(parts: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, int, torch.Tensor]],
+                      group=None) -> List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+    """Gather the result buffers of several demodulation launches (e.g. MU, MS, MC) in ONE exchange.
+
+    ``parts``: per launch (desc u8, rec u8, heap u8, n_msgs, cursor) with ``cursor`` the launch's
+    device cursor (cursor[0] = records, cursor[1] = heap bytes): the counts stay on the device.
+    Steps: one all-gather of every rank's counts (the only host synchronisation), then every rank
+    packs its sections into one buffer -- re-basing its own rec_begin / payload_off / msg by the
+    counts of the lower ranks while copying -- and ONE all-gather moves all of it; the receivers
+    only drop the per-rank padding.  Returns per launch (desc, rec, heap) of the whole job in
+    global message order (the contract of :func:`allgather_results`).
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    K = len(parts)
+    dev = parts[0][0].device
+    counts = torch.stack([torch.stack([torch.tensor(n, dtype=torch.int64, device=dev), cur[0].to(torch.int64),
+                                       cur[1].to(torch.int64)]) for _, _, _, n, cur in parts])  # [K, 3]
+    allc = torch.empty(world * K * 3, dtype=torch.int64, device=dev)
+    _all_gather_flat(allc, counts.reshape(-1), group)
+    S = allc.view(world, K, 3).cpu()
+    nb = S * torch.tensor([DESC_BYTES, REC_BYTES, 1], dtype=torch.int64)        # section bytes
+    cap = ((nb.max(dim=0).values + 15) // 16 * 16).clamp(min=16)                # [K, 3]
+    sec_off = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.int64), cap.reshape(-1)]), 0)
+    total = int(sec_off[-1])
+    base = S[:rank].sum(dim=0) if rank else torch.zeros(K, 3, dtype=torch.int64)  # (msgs, recs, heap) below
+    send = torch.zeros(total, dtype=torch.uint8, device=dev)
+    for k, (desc, rec, heap, _, _) in enumerate(parts):
+        nm, nr, nh = (int(x) for x in S[rank, k])
+        o_d, o_r, o_h = (int(sec_off[3 * k + j]) for j in range(3))
+        if nm:
+            send[o_d: o_d + nm * DESC_BYTES] = desc[: nm * DESC_BYTES]
+            send[o_d: o_d + nm * DESC_BYTES].view(torch.int32).view(nm, 2)[:, 0] += int(base[k, 1])
+        if nr:
+            send[o_r: o_r + nr * REC_BYTES] = rec[: nr * REC_BYTES]
+            rv = send[o_r: o_r + nr * REC_BYTES].view(torch.int32).view(nr, 4)
+            rv[:, 0] += int(base[k, 2])
+            rv[:, 3] += int(base[k, 0])
+        if nh:
+            send[o_h: o_h + nh] = heap[:nh]
+    recv = torch.empty(world * total, dtype=torch.uint8, device=dev)
+    _all_gather_flat(recv, send, group)
+    out = []
+    for k in range(K):
+        secs = []
+        for j in range(3):
+            o = int(sec_off[3 * k + j])
+            secs.append(torch.cat([recv[r * total + o: r * total + o + int(nb[r, k, j])] for r in range(world)]))
+        out.append(tuple(secs))
+    return out
 
 
 def allgather_results(desc: torch.Tensor, rec: torch.Tensor, heap: torch.Tensor, n_msgs: int, n_rec: int,

@@ -78,7 +78,19 @@ def _worker(rank, world, port, msgs, pids, q):
     th = torch.from_numpy(h.copy()) if len(h) else torch.zeros(1, dtype=torch.uint8)
     gd, gr, gh = sdist.allgather_results(td, tr, th, hi - lo, len(r), len(h))
     got = decode(gd.numpy().view(runtime.DESC_DT), gr.numpy().view(runtime.RES_DT), gh.numpy(), pids)
-    q.put((rank, got))
+    # the multi-launch form (one count exchange + one data collective), twice: launches of different
+    # sizes, device-side counts
+    cur = torch.tensor([len(r), len(h), 0, 0], dtype=torch.int32)
+    half = (hi - lo) // 2
+    d2, r2, h2 = encode(_oracle_results(msgs[lo:lo + half]), pids)
+    cur2 = torch.tensor([len(r2), len(h2), 0, 0], dtype=torch.int32)
+    t2 = (torch.from_numpy(d2.view(np.uint8).copy()),
+          torch.from_numpy(r2.view(np.uint8).copy()) if len(r2) else torch.zeros(1, dtype=torch.uint8),
+          torch.from_numpy(h2.copy()) if len(h2) else torch.zeros(1, dtype=torch.uint8))
+    (a, b, c), (a2, b2, c2) = sdist.allgather_streams([(td, tr, th, hi - lo, cur), (*t2, half, cur2)])
+    got_multi = decode(a.numpy().view(runtime.DESC_DT), b.numpy().view(runtime.RES_DT), c.numpy(), pids)
+    got_half = decode(a2.numpy().view(runtime.DESC_DT), b2.numpy().view(runtime.RES_DT), c2.numpy(), pids)
+    q.put((rank, got, got_multi, got_half))
     dist.destroy_process_group()
 
 
@@ -107,5 +119,11 @@ def test_gloo_world2_allgather_matches_unsharded():
     outs = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    for rank, got in outs:
+    halves = []
+    for r in range(2):
+        lo, hi = sdist.shard_bounds(len(msgs), r, 2)
+        halves += full[lo: lo + (hi - lo) // 2]
+    for rank, got, got_multi, got_half in outs:
         assert got == full, f"rank {rank} gathered stream differs"
+        assert got_multi == full, f"rank {rank}: allgather_streams differs"
+        assert got_half == halves, f"rank {rank}: second launch of allgather_streams differs"
