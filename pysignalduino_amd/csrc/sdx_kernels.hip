@@ -54,8 +54,6 @@ __device__ unsigned long long g_prof[32];
 
 namespace sdx {
 
-constexpr int REC_CAP = 160;     // MC: staged results per wave
-constexpr int HEAP_CAP = 4096;   // MC: staged payload bytes per wave
 constexpr int POOL_REC = 640;    // MU/MS: staged results per tile (shared by the 4 waves)
 constexpr int POOL_HEAP = 16384; // MU/MS: staged payload bytes per tile
 constexpr int POOL_REC_MS = 256;   // short MS tiles: ~1 result per message; smaller LDS -> more tiles/CU
@@ -1818,11 +1816,21 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
 // =============================================================================================
 // MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
 // =============================================================================================
-constexpr int MC_MAXW = 8;  // <= 512 bits = 128 hex characters per frame (device contract)
+constexpr int MC_MAXW = 8;   // <= 512 bits = 128 hex characters per frame (device contract)
+constexpr int MC_SHORTW = 4; // k_mc<4>: frames of <= 64 hex characters (the long variant takes the rest)
+constexpr int MC_REC_CAP = 152, MC_HEAP_CAP = 3584;  // per wave: k_mc<4> fits 4 workgroups per CU
 
+// a frame's bit string, word w at base[w * 256] (words beyond nw read as 0).  dm: the Funkbus
+// mc2dmc(lh/hl) view of the same words, bit k = (b[k] == b[k+1]) -- derived on the fly
 struct LaneBits {
-  uint64_t* base;  // word w at base[w * 256]
-  SDX_DEV uint64_t word(int w) const { return w < MC_MAXW ? base[w * 256] : 0ull; }
+  const uint64_t* base;
+  int nw;
+  bool dm;
+  SDX_DEV uint64_t raw(int w) const { return w < nw ? base[w * 256] : 0ull; }
+  SDX_DEV uint64_t word(int w) const {
+    const uint64_t x = raw(w);
+    return dm ? (w < nw ? ~(x ^ ((x << 1) | (raw(w + 1) >> 63))) : 0ull) : x;
+  }
   SDX_DEV int get(int i) const { return (int)((word(i >> 6) >> (63 - (i & 63))) & 1ull); }
   // P <= 32 bits starting at i (MSB-first), zero beyond the array
   SDX_DEV uint32_t win(int i, int P) const {
@@ -1838,12 +1846,12 @@ struct LaneBits {
   }
 };
 
+template <int MW>
 struct McLds {
-  uint64_t bn[MC_MAXW * 256];   // bits, polarity as given
-  uint64_t bi[MC_MAXW * 256];   // bits, polarity inverted
-  uint64_t dm[MC_MAXW * 256];   // Funkbus differential-manchester scratch
-  StageRec rec[4][REC_CAP];
-  uint8_t heap[4][HEAP_CAP];
+  uint64_t bn[MW * 256];   // bits, polarity as given
+  uint64_t bi[MW * 256];   // bits, polarity inverted
+  StageRec rec[4][MC_REC_CAP];
+  uint8_t heap[4][MC_HEAP_CAP];
   int nrec[4], nheap[4], ovf[4];
 };
 
@@ -2102,16 +2110,24 @@ SDX_DEV int hexval(uint8_t c) {
   return -1;
 }
 
+// MW = 4: frames of <= 64 hex characters, longer ones are left to the MW = 8 launch (LONG = true),
+// which takes only those (sdx_demod_mc launches both; a wave without long frames exits at once)
+template <int MW, bool LONG>
 __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
-  __shared__ McLds L;
+  __shared__ McLds<MW> L;
   const BankView bv = bank_view(bank);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int ntot = b.sel_dev ? b.n_sel : b.n;
   const int gi = blockIdx.x * 256 + tid;
-  const bool valid = gi < ntot;
+  bool valid = gi < ntot;
   const int msg = valid ? (b.sel_dev ? b.sel_dev[gi] : gi) : 0;
+  if (valid) {  // this launch's share: short frames (MW = 4) or long ones
+    const int hl0 = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - b.offsets_dev[msg]);
+    valid = LONG ? hl0 > MC_SHORTW * 16 : hl0 <= MC_SHORTW * 16;
+  }
+  if (LONG && !__ballot(valid)) return;  // whole wave without long frames (nothing staged yet)
   if (lane == 0) { L.nrec[wave] = 0; L.nheap[wave] = 0; L.ovf[wave] = 0; }
-  LaneBits BN{&L.bn[tid]}, BI{&L.bi[tid]}, DM{&L.dm[tid]};
+  const LaneBits BN{&L.bn[tid], MW, false}, BI{&L.bi[tid], MW, false};
   // hex -> bits for both polarities (helpers.py:168-188: leading zero nibbles are dropped)
   int nN = 0, nI = 0;
   bool hex_ok = false;
@@ -2122,9 +2138,9 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     clock = b.clock_dev[msg];
     mcbit = b.mcbitnum_dev[msg];
     flags = b.flags_dev[msg];
-    hex_ok = hl > 0 && hl <= MC_MAXW * 16;
+    hex_ok = hl > 0 && hl <= MW * 16;
     bool startedN = false, startedI = false;
-    for (int w = 0; w < MC_MAXW; ++w) { L.bn[w * 256 + tid] = 0; L.bi[w * 256 + tid] = 0; }
+    for (int w = 0; w < MW; ++w) { L.bn[w * 256 + tid] = 0; L.bi[w * 256 + tid] = 0; }
     for (int i = 0; i < hl && hex_ok; ++i) {
       const uint8_t c = b.hex_dev[off + i];
       const int v = hexval(c);
@@ -2160,12 +2176,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     const int nb = inv ? nI : nN;
     if (go && !hex_ok) { raise = SDX_RAISE_TYPE; go = false; }  // len(None) -> TypeError
     if (go) {
-      if (cld(&r->method) == SDX_MC_FUNKBUS) {
-        for (int w = 0; w < MC_MAXW; ++w) {  // mc2dmc(lh/hl): bit k = (b[k] == b[k+1])
-          const uint64_t x = B.word(w), nx = B.word(w + 1);
-          L.dm[w * 256 + tid] = ~(x ^ ((x << 1) | (nx >> 63)));
-        }
-      }
+      const LaneBits DM{B.base, MW, true};  // mc2dmc(lh/hl) view for Funkbus
       o = mc_method(r, B, nb, DM);
       if (o.rc == -1) { raise = SDX_RAISE_TYPE; o.rc = 0; }
       if (o.rc == -2) { raise = SDX_RAISE_VALUE; o.rc = 0; }
@@ -2182,7 +2193,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     const uint64_t hm = ballot(has);
     const int nnew = popc64(hm);
     const int hb = L.nheap[wave], rb = L.nrec[wave];
-    const bool fits = hb + wtot <= HEAP_CAP && rb + nnew <= REC_CAP;
+    const bool fits = hb + wtot <= MC_HEAP_CAP && rb + nnew <= MC_REC_CAP;
     if (has && fits) {
       uint8_t* dst = &L.heap[wave][hb + incl - plen];
       for (int i = 0; i < cld(&r->pre_len); ++i) dst[i] = bv.str[cld(&r->pre_off) + i];
@@ -2402,7 +2413,8 @@ int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out*
   if (ntot <= 0) return SDX_OK;
   hipStream_t st = (hipStream_t)hip_stream;
   const int grid = (ntot + 255) / 256;
-  hipLaunchKernelGGL(sdx::k_mc, dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  hipLaunchKernelGGL((sdx::k_mc<sdx::MC_SHORTW, false>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  hipLaunchKernelGGL((sdx::k_mc<sdx::MC_MAXW, true>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
   HIPCHK(hipGetLastError());
   return SDX_OK;
 }

@@ -183,3 +183,55 @@ def test_large_corpus_vs_c_oracle(kind, n, seed):
             if not same:
                 bad.append((int(i), x, y))
     assert not bad, f"{len(bad)} record mismatches; first: {bad[:2]}"
+
+
+@pytest.mark.gpu
+def test_mc_long_frames_vs_oracle():
+    """Frames of 1..128 hex characters: the short (<= 64) and long (65..128) k_mc launches together
+    equal the oracle's fixed chain, frame by frame (L drawn inside the protocols' length gates)."""
+    import numpy as np
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    ob = O.OracleBank()
+    rng = np.random.default_rng(77)
+    mc_ids = ob.ids_with("clockrange")
+    msgs, exp = [], []
+    for i in range(3000):
+        n = int(rng.integers(1, 129)) if i % 2 else int(rng.integers(60, 129))
+        hx = "".join("0123456789ABCDEFabcdef"[int(v)] for v in rng.integers(0, 22 if i % 7 == 0 else 16, size=n))
+        pid = mc_ids[int(rng.integers(0, len(mc_ids)))]  # a clock and L inside one protocol's gates
+        lo, hi = (float(x) for x in ob.prop(pid, "clockrange")[:2])
+        clock = int(rng.integers(int(lo), int(hi) + 2))
+        lmin = int(ob.prop(pid, "length_min", 1) or 1)
+        lmax = int(ob.prop(pid, "length_max", 4 * n) or 4 * n)
+        L = int(rng.integers(lmin, max(lmin, lmax) + 1))
+        mt = "Mc" if i % 5 == 0 else "MC"
+        msgs.append({"raw_hex": hx, "clock": clock, "mcbitnum": L, "messagetype": mt, "version": None})
+    # bench-corpus frames, every other one padded past 64 hex characters with random digits
+    from pysignalduino_amd import bank as B, synth
+    mb = synth.mc_corpus(B.load_protocols(), 4000, seed=12)
+    for i in range(mb.n):
+        hx = mb.hex(i)
+        if i % 2 == 0:
+            lo_n = 65 - len(hx) if len(hx) < 65 else 1
+            hx += "".join("0123456789ABCDEF"[int(v)] for v in rng.integers(0, 16, size=int(rng.integers(lo_n, 129 - len(hx)))))
+        msgs.append({"raw_hex": hx, "clock": int(mb.clock[i]), "mcbitnum": int(mb.mcbitnum[i]),
+                     "messagetype": "Mc" if mb.mtype[i] else "MC", "version": None})
+    for m in msgs:
+        try:
+            exp.append({"results": [[r["protocol_id"], r["payload"]] for r in
+                                    O.demod_mc_fixed(ob, m["raw_hex"], m["clock"], m["mcbitnum"], m["messagetype"], None)]})
+        except Exception as e:  # noqa: BLE001
+            exp.append({"raise": type(e).__name__})
+    got = SDProtocols(mc_mode="fixed").demodulate_mc_batch(msgs)
+    bad, nres, nlong = [], 0, 0
+    for m, g, e in zip(msgs, got, exp):
+        gg = {"raise": type(g).__name__} if isinstance(g, BaseException) else \
+            {"results": [[r["protocol_id"], r["payload"]] for r in g]}
+        nres += len(gg.get("results", []))
+        nlong += len(m["raw_hex"]) > 64
+        if gg != e:
+            bad.append((m, e, gg))
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:2]}"
+    # long frames (the MW = 8 launch) rarely decode -- the decoders check the bit length -- but
+    # every one of them is compared (statuses, raises, empty lists)
+    assert nres > 500 and nlong > 3000, (nres, nlong)
