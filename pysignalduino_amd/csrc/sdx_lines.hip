@@ -999,26 +999,17 @@ __global__ __launch_bounds__(PT) void k_parse_lines(sdx_lines in, sdx_lines_out 
     Str P{L + a + 1, b - a - 2};
     const uint8_t t1 = hdr ? up(L[a + 2]) : 0;
     // A payload whose first byte after the header has the high bit set is (the firmware's) Mred=1
-    // form: extract_payload's checks and the decompression into the slot region run first, then
-    // every lane runs the fast path on its payload (raw or decompressed) together.  Other lines
-    // reach extract_payload's checks only when the fast path declines (its success implies them:
-    // every payload byte was checked to be ASCII and not a newline); one that turns out to be
-    // compressed after all is finished by k_parse_rare.
+    // form: it is left to k_parse_comp (extract_payload's checks, decompression into the slot, the
+    // parser), which runs the compressed lines of a batch on full waves.  Other lines reach
+    // extract_payload's checks only when the fast path declines (its success implies them: every
+    // payload byte was checked to be ASCII and not a newline); one that turns out to be compressed
+    // after all goes to k_parse_comp as well.
     const bool likely = hdr && (t1 == 'S' || t1 == 'U' || t1 == 'O' || t1 == 'N') && (L[a + 4] & 0x80);
-    bool framed = hdr, comp = false, decided = !hdr;
-    if (likely) {
-      framed = frame_check(L, a, b, comp);
-      decided = !framed;
-      if (framed && comp) {  // decompress_payload into the slot region, parsed there
-        Writer8 w(out.slot_dev + 3 * lo, 3 * len);
-        const bool ok = decompress(P, w) && !w.ovf;
-        P = Str{out.slot_dev + 3 * lo, w.n};
-        plen = ok ? w.n : -1;
-        if (!ok) {
-          r.status = SDX_LS_UNSUPPORTED;
-          decided = true;
-        }
-      }
+    const bool comp = false;  // compressed lines are finished by k_parse_comp
+    bool decided = !hdr;
+    if (likely) {  // Mred=1 form: decompressed and parsed by k_parse_comp with all lanes busy
+      r.status = ST_RARE;
+      decided = true;
     }
     if (!decided) {
       const uint8_t ty = P.n > 1 ? P.p[1] : 0;
@@ -1064,12 +1055,9 @@ __global__ __launch_bounds__(PT) void k_parse_lines(sdx_lines in, sdx_lines_out 
   }
 }
 
-// the lines k_parse_lines left to it (ST_RARE): the whole extract_payload / decompress_payload /
-// parser sequence on global memory, general parser only
-__global__ __launch_bounds__(64) void k_parse_rare(sdx_lines in, sdx_lines_out out) {
-  __shared__ uint32_t pv[10 * 64];
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= in.n || out.status_dev[i] != ST_RARE) return;
+// one compressed line (ST_RARE): extract_payload's checks, decompress_payload into the line's slot,
+// then the fast path on the decompressed payload with the general parser behind it
+LD void parse_compressed(const sdx_lines& in, const sdx_lines_out& out, int i, uint32_t* pvt) {
   const int64_t lo = in.offsets_dev[i];
   const int len = (int)(in.offsets_dev[i + 1] - lo);
   const uint8_t* L = in.bytes_dev + lo;
@@ -1078,19 +1066,63 @@ __global__ __launch_bounds__(64) void k_parse_rare(sdx_lines in, sdx_lines_out o
   while (b > a && py_space(L[b - 1])) --b;
   LineRes r;
   int plen = -1;
-  Writer8 w(out.slot_dev + 3 * lo, 3 * len);
-  if (!(decompress(Str{L + a + 1, b - a - 2}, w) && !w.ovf)) {
-    r.status = SDX_LS_UNSUPPORTED;
-  } else {
-    plen = w.n;
-    const Str P{out.slot_dev + 3 * lo, w.n};
-    parse_payload(P, r, out, i, pv + threadIdx.x);
-    if (r.status == SDX_LS_OK) finish_fields(P, r, out, i);
+  int64_t doff = 3 * lo;
+  bool comp = false;
+  if (!frame_check(L, a, b, comp)) {
+    r.status = SDX_LS_NOFRAME;
+  } else {  // comp holds: the first payload byte, or another one, has the high bit set
+    Writer8 w(out.slot_dev + 3 * lo, 3 * len);
+    if (!(decompress(Str{L + a + 1, b - a - 2}, w) && !w.ovf)) {
+      r.status = SDX_LS_UNSUPPORTED;
+    } else {
+      plen = w.n;
+      const Str P{out.slot_dev + 3 * lo, w.n};
+      const uint8_t ty = P.n > 1 ? P.p[1] : 0;
+      if (!((ty == 'U' || ty == 'S' || ty == 'C') && fast_payload(P.p, P.n, r, out, i))) parse_payload(P, r, out, i, pvt);
+      if (r.status == SDX_LS_OK) {
+        finish_fields(P, r, out, i);
+        doff = 3 * lo + r.dS;
+      }
+    }
   }
-  out.doff_dev[i] = 3 * lo + (r.status == SDX_LS_OK ? r.dS : 0);
+  out.doff_dev[i] = doff;
   out.plen_dev[i] = plen;
   out.kind_dev[i] = r.kind;
   out.status_dev[i] = r.status;
+}
+
+// the lines k_parse_lines left to it (ST_RARE): each wave scans COMP_CHUNK lines, queues the
+// compressed ones in LDS and parses them 64 at a time (lane = line), so the decompression work of
+// the ~20 % compressed lines of a mixed stream runs on full waves
+constexpr int COMP_CHUNK = 192;  // lines scanned per wave (~40 compressed at the bench mix): measured best of 128-2048
+__global__ __launch_bounds__(256) void k_parse_comp(sdx_lines in, sdx_lines_out out) {
+  __shared__ uint32_t pv[4][10 * 64];
+  __shared__ int q[4][128];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* pvt = pv[wave] + lane;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + wave) * COMP_CHUNK;
+  int qn = 0;
+  for (int c = 0; c < COMP_CHUNK; c += 64) {
+    const int64_t i = base + c + lane;
+    const bool rare = i < in.n && out.status_dev[i] == ST_RARE;
+    const uint64_t m = __ballot(rare);
+    if (rare) q[wave][qn + __popcll(m & ((1ull << lane) - 1))] = (int)i;
+    qn += __popcll(m);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (qn >= 64) {
+      const int li = q[wave][lane];
+      const int rest = lane < qn - 64 ? q[wave][64 + lane] : 0;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < qn - 64) q[wave][lane] = rest;
+      qn -= 64;
+      parse_compressed(in, out, li, pvt);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (lane < qn) parse_compressed(in, out, q[wave][lane], pvt);
 }
 
 // ---- selection lists (sdx_select_lines): class of a parsed line, -1 = not demodulated
@@ -1238,8 +1270,8 @@ extern "C" int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out,
     return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: bytes_dev and slot_dev must be 8-byte aligned");
   const int grid = (lines->n + sdxl::PT - 1) / sdxl::PT;
   hipLaunchKernelGGL(sdxl::k_parse_lines, dim3(grid), dim3(sdxl::PT), 0, (hipStream_t)hip_stream, *lines, *out);
-  hipLaunchKernelGGL(sdxl::k_parse_rare, dim3((lines->n + 63) / 64), dim3(64), 0, (hipStream_t)hip_stream, *lines,
-                     *out);
+  hipLaunchKernelGGL(sdxl::k_parse_comp, dim3((lines->n + 4 * sdxl::COMP_CHUNK - 1) / (4 * sdxl::COMP_CHUNK)),
+                     dim3(256), 0, (hipStream_t)hip_stream, *lines, *out);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("sdx_parse_lines: ") + hipGetErrorString(e));
   return SDX_OK;

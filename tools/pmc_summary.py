@@ -12,7 +12,7 @@ def short(name: str) -> str:
                      ("k_pulses<0, 64,", "k_pulses<MU,long>"), ("k_pulses<1, 64,", "k_pulses<MS,long>"),
                      ("k_pulsesILi0ELi4E", "k_pulses<MU>"), ("k_pulsesILi1ELi4E", "k_pulses<MS>"),
                      ("k_mc<8", "k_mc<long>"), ("k_mcILi8", "k_mc<long>"), ("k_mc", "k_mc"), ("k_parse_lines", "k_parse_lines"), ("k_sel_count", "k_sel_count"),
-                     ("k_sel_write", "k_sel_write"), ("k_mn(", "k_mn"), ("k_parse_rare", "k_parse_rare")):
+                     ("k_sel_write", "k_sel_write"), ("k_mn(", "k_mn"), ("k_parse_rare", "k_parse_rare"), ("k_parse_comp", "k_parse_comp")):
         if key in name:
             return tag
     return name[:40]
