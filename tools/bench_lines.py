@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mix", default="1,1,1", help="MU,MS,MC proportions")
     ap.add_argument("--compress-frac", type=float, default=0.3)
+    ap.add_argument("--json", action="store_true",
+                    help="also time sdx_serialize_json (the MQTT texts of every line's first result) per step")
     args = ap.parse_args()
     mix = tuple(float(x) for x in args.mix.split(","))
     import torch
@@ -95,7 +97,11 @@ def main():
     outs = {"MU": eng.alloc_out(n, 8 * n + 4096, 160 * n + 65536), "MS": eng.alloc_out(n, 2 * n + 4096, 48 * n + 65536),
             "MC": eng.alloc_out(n, 2 * n + 4096, 48 * n + 65536)}
     stream = torch.cuda.current_stream()
-    names = ["parse+select", "MU", "MS", "MC"]
+    names = ["parse+select", "MU", "MS", "MC"] + (["json"] if args.json else [])
+    jouts = {k: eng.alloc_json(n, 700 * n + 65536 if k == "MU" else 300 * n + 65536) for k in ("MU", "MS", "MC")} \
+        if args.json else {}
+    lo = {"meta": lb.meta, "pat_val": lb.pat_val, "cp_slot": lb.cp_slot}
+    kinds = {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS, "MC": runtime.KIND_MC}
     ev = {k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in names}
     ev_parse = torch.cuda.Event(enable_timing=True)
     kt = {k: [] for k in names + ["parse"]}
@@ -130,6 +136,14 @@ def main():
                     eng.launch_pulses(kind, pb, outs[k], sel=sels[long_], long_variant=True)
             if record:
                 ev[k][1].record(stream)
+        if args.json:  # one text per line with results (controller.py:254-257), device-built
+            if record:
+                ev["json"][0].record(stream)
+            for k, jo in jouts.items():
+                jo["cursor"].zero_()
+                eng.launch_json(kinds[k], outs[k], lo, n, jo, first_only=True)
+            if record:
+                ev["json"][1].record(stream)
         return cnt
 
     for _ in range(args.warmup):
@@ -164,6 +178,10 @@ def main():
         tj = json.load(open(tpath))
         if tj.get("_config", {}).get("lines") == n and tj.get("k_parse_lines", {}).get("traffic_bytes"):
             traffic = float(tj["k_parse_lines"]["traffic_bytes"])
+    if args.json:
+        jbytes = sum(int(jo["cursor"][0].item()) for jo in jouts.values())
+        if any(int(jo["cursor"][1].item()) for jo in jouts.values()):
+            raise SystemExit("JSON capacity overflow in the bench configuration")
     res = {
         "metric": "raw firmware lines/sec parsed + demodulated (wire-line front end, SURVEY §8(f) 1)",
         "value": value, "unit": "lines/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -174,6 +192,9 @@ def main():
                                "MU/MS/MC ('fixed') demodulation",
                    "lines": n, "line_bytes": int(offsets[-1]), "classes": [int(c) for c in cnt]},
         "per_kernel_ms": {k: 1e3 * v for k, v in km.items()},
+        **({"json": {"bytes_per_step": jbytes, "GB_per_s_written": jbytes / km["json"] / 1e9,
+                     "note": "k_json x3 (MU/MS/MC launches), first result per line; included in ms_per_step"}}
+           if args.json else {}),
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": "k_parse_lines",
                      "alg_bytes_per_launch": alg},
