@@ -33,12 +33,17 @@ def per_launch(root: str, counter: str):
 
 def main(root: str, out: str) -> None:
     fetch, write = per_launch(root, "FETCH_SIZE"), per_launch(root, "WRITE_SIZE")
+    sq = {c: per_launch(root, c) for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+                                          "SQ_WAVES")}
     res = {}
     for k in sorted(set(fetch) | set(write)):
         f_kib, w_kib = fetch.get(k), write.get(k)
         tb = None if f_kib is None or w_kib is None else 2.0 * f_kib * 1024 + w_kib * 1024
         res[k] = {"fetch_size_kib": f_kib, "write_size_kib": w_kib, "traffic_bytes": tb,
                   "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM section)"}
+        for c, d in sq.items():  # per-launch instruction counts (the issue-side view of the kernel)
+            if k in d:
+                res[k][c.lower()] = d[k]
     res["_config"] = json.loads(os.environ.get("PMC_CONFIG", "null")) or \
         {"command": "python3 bench.py --steps 3 --warmup 1 --no-cpu", "msgs_per_gpu": 1000000}
     os.makedirs(os.path.dirname(out), exist_ok=True)
