@@ -1451,11 +1451,11 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     n = L.nlen[mi];
     lane_ok = n > 0;  // empty D -> [] (message_unsynced.py:22-25 / message_synced.py:23-25)
   }
-  uint64_t P0 = 0, P1 = 0;
+  PairRef PR{0, 0};
   if constexpr (NW <= 4) {
     if (mvalid) {
-      P0 = L.pairs[mi][0];
-      P1 = L.pairs[mi][1];
+      PR.P0 = L.pairs[mi][0];
+      PR.P1 = L.pairs[mi][1];
     }
   }
   const uint64_t* bmine = &L.bm[(mvalid ? mi : 0) * T::MSTRIDE];
@@ -1479,7 +1479,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   // pattern_exists: lane variant on a SpecV (compact MU filter record or full patspec), long
   // variant on the full patspec
   auto PEXV = [&](const SpecV& sv, const sdx_patspec* sp, int minpos, bool need_pos) -> PexRes {
-    if constexpr (NW <= 4) return pexists_lane<NW>(sv, kq, ids, npat, bmine, minpos, bv.rank, P0, P1, need_pos);
+    if constexpr (NW <= 4) return pexists_lane<NW>(sv, kq, ids, npat, bmine, minpos, bv.rank, PR, need_pos);
     else return pattern_exists(sp, kq, ids, npat, bmine, T::WS, nw, minpos);
   };
   // ---- protocol loop: waves take protocols one at a time, in the bank's processing order
@@ -1727,27 +1727,18 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     }
     PROF_ADD(12, t_dec);
   }
-  // modulematch tables for the finish phase: loaded into registers now, so that the global
-  // load latency overlaps the end barrier; stored over the (then dead) decode queues after it
-  static_assert(SDX_MMTAB_LDS <= 2 * 16 * 64 * LANE_WAVES, "prefetch covers the LDS table cap");
-  uint4 mm_pf[2];
-  const int m16 = LANE_MU ? (int)bv.hdr->mmtab_bytes >> 4 : 0;
-  if constexpr (LANE_MU) {
-    const uint4* msrc = reinterpret_cast<const uint4*>(bv.mmtab);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (tid + k * (int)blockDim.x < m16) mm_pf[k] = msrc[tid + k * blockDim.x];
-  }
   PROF_T(t_bar);
   __syncthreads();
   PROF_ADD(14, t_bar);
   if constexpr (LANE_MU) {  // finish every match of the tile: lane = match (message_unsynced.py:197-290)
     PROF_T(t_fin);
-    {
+    {  // modulematch tables over the (now dead) decode queues. Loaded after the barrier on
+       // purpose: values held in registers across it were parked in scratch by the compiler
+       // (8.5 KB per tile written to and re-read from memory)
+      const int m16 = (int)bv.hdr->mmtab_bytes >> 4;
+      const uint4* msrc = reinterpret_cast<const uint4*>(bv.mmtab);
       uint4* mdst = reinterpret_cast<uint4*>(L.u.mmtab);
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (tid + k * (int)blockDim.x < m16) mdst[tid + k * blockDim.x] = mm_pf[k];
+      for (int i = tid; i < m16; i += blockDim.x) mdst[i] = msrc[i];
       __syncthreads();
     }
     const int nm = L.nmatch < MATCH_CAP ? L.nmatch : MATCH_CAP;

@@ -140,9 +140,12 @@ SDX_DEV M<NW> m_occ(const uint64_t* bm, uint64_t tgt, int tlen) {
 // pattern_exists (pattern_utils.py:34-136) for one lane; fast path = one candidate per value
 // ---------------------------------------------------------------------------------------------
 // pair-presence bit of ids (a, b): set iff "ab" occurs in the message (TileLds::pairs)
-SDX_DEV bool pair_bit(uint64_t P0, uint64_t P1, int a, int b) {
+struct PairRef {  // held in registers (reading the LDS row at each use measured 1.7 % slower)
+  uint64_t P0, P1;
+};
+SDX_DEV bool pair_bit(const PairRef& P, int a, int b) {
   const int q = 10 * a + b;
-  return ((q < 64 ? P0 >> q : P1 >> (q - 64)) & 1ull) != 0;
+  return ((q < 64 ? P.P0 >> q : P.P1 >> (q - 64)) & 1ull) != 0;
 }
 
 // one search list as the lane filter reads it (wave-uniform, scalar registers): from the full
@@ -208,7 +211,7 @@ SDX_DEV int first_cand(uint32_t m, const int* kq, int klo, const uint16_t* rt) {
 
 template <int NW>
 SDX_DEV PexRes pexists_lane(const SpecV& sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
-                            int minpos, const uint16_t* ranks, uint64_t P0, uint64_t P1, bool need_pos) {
+                            int minpos, const uint16_t* ranks, const PairRef& PR, bool need_pos) {
   PexRes res{false, -1, 0};
 #ifdef SDX_X_NOCAND
   return PexRes{true, minpos, 0};
@@ -246,7 +249,7 @@ SDX_DEV PexRes pexists_lane(const SpecV& sp, const int* kq, uint64_t ids, int np
     const bool cheap = minpos == 0 && !need_pos;  // pair presence decides exactly
     auto valid = [&](int a, int b, int* pos) -> bool {
       const int ida = (int)((ids >> (4 * a)) & 15), idb = (int)((ids >> (4 * b)) & 15);
-      if (!pair_bit(P0, P1, ida, idb)) return false;  // "ab" occurs nowhere
+      if (!pair_bit(PR, ida, idb)) return false;  // "ab" occurs nowhere
       if (cheap) {
         *pos = 0;
         return true;
@@ -254,44 +257,76 @@ SDX_DEV PexRes pexists_lane(const SpecV& sp, const int* kq, uint64_t ids, int np
       *pos = m_first(m_occ<NW>(bm, (uint64_t)ida | ((uint64_t)idb << 4), 2), minpos);
       return *pos >= 0;
     };
+    // the position of the last valid pair tested is kept: in the common case of one candidate
+    // per value the pair is tested once (no re-test for b* or for the position)
     uint32_t va = 0;
+    int b_last = -1, pos_last = -1;
     for (uint32_t ma = okm[0]; ma; ma &= ma - 1) {
       const int a = __ffs(ma) - 1;
       for (uint32_t mb = okm[1] & ~(1u << a); mb; mb &= mb - 1) {
         int p;
         if (valid(a, __ffs(mb) - 1, &p)) {
           va |= 1u << a;
+          b_last = __ffs(mb) - 1;
+          pos_last = p;
           break;
         }
       }
     }
     if (!va) return res;
-    const int a = first_cand(va, kq, sp.klo[0], ranks + sp.rk_off[0]);
-    uint32_t vb = 0;
-    int pos_of_first = 0;
-    for (uint32_t mb = okm[1] & ~(1u << a); mb; mb &= mb - 1) {
-      int p;
-      if (valid(a, __ffs(mb) - 1, &p)) vb |= 1u << (__ffs(mb) - 1);
+    int a, b, pos_of_first;
+    const uint32_t others_of = okm[1];
+    if (!(va & (va - 1))) {
+      a = __ffs(va) - 1;
+      const uint32_t others = others_of & ~(1u << a);
+      if (!(others & (others - 1))) {  // a single partner: the pair found above
+        b = b_last;
+        pos_of_first = pos_last;
+      } else {
+        b = -1;
+      }
+    } else {
+      a = first_cand(va, kq, sp.klo[0], ranks + sp.rk_off[0]);
+      b = -1;
     }
-    const int b = first_cand(vb, kq, sp.klo[1], ranks + sp.rk_off[1]);
-    valid(a, b, &pos_of_first);
+    if (b < 0) {
+      uint32_t vb = 0;
+      int nvb = 0;
+      for (uint32_t mb = others_of & ~(1u << a); mb; mb &= mb - 1) {
+        int p;
+        if (valid(a, __ffs(mb) - 1, &p)) {
+          vb |= 1u << (__ffs(mb) - 1);
+          pos_last = p;
+          ++nvb;
+        }
+      }
+      b = first_cand(vb, kq, sp.klo[1], ranks + sp.rk_off[1]);
+      if (nvb == 1) pos_of_first = pos_last;
+      else if (need_pos) valid(a, b, &pos_of_first);
+      else pos_of_first = 0;  // only found / tgt are read when the position is not needed
+    }
     const int ida = (int)((ids >> (4 * a)) & 15), idb = (int)((ids >> (4 * b)) & 15);
     res.found = true;
     res.tgt = (uint64_t)ida | ((uint64_t)idb << 4);
-    res.pos = pos_of_first;  // 0 when pair presence decided (minpos == 0, position not needed)
+    res.pos = pos_of_first;  // meaningful only with need_pos
     return res;
   }
   if (nu == 1 && slen == 1) {
     uint32_t va = 0;
+    int pos_last = -1;
     for (uint32_t ma = okm[0]; ma; ma &= ma - 1) {
       const int a = __ffs(ma) - 1, ida = (int)((ids >> (4 * a)) & 15);
-      if (m_first(m_occ<NW>(bm, (uint64_t)ida, 1), minpos) >= 0) va |= 1u << a;
+      const int p = m_first(m_occ<NW>(bm, (uint64_t)ida, 1), minpos);
+      if (p >= 0) {
+        va |= 1u << a;
+        pos_last = p;
+      }
     }
     if (!va) return res;
     const int a = first_cand(va, kq, sp.klo[0], ranks + sp.rk_off[0]);
     res.found = true;
     res.tgt = (ids >> (4 * a)) & 15;
-    res.pos = m_first(m_occ<NW>(bm, res.tgt, 1), minpos);
+    res.pos = (va & (va - 1)) ? m_first(m_occ<NW>(bm, res.tgt, 1), minpos) : pos_last;
     return res;
   }
   // general shape: the sorted candidate lists (packed nibbles), then the product loop
@@ -340,7 +375,7 @@ SDX_DEV PexRes pexists_lane(const SpecV& sp, const int* kq, uint64_t ids, int np
       // searched from position 0, a necessary condition otherwise
       bool ok = true;
       for (int i = 0; i + 1 < slen; ++i)
-        ok = ok && pair_bit(P0, P1, (int)((tgt >> (4 * i)) & 15), (int)((tgt >> (4 * i + 4)) & 15));
+        ok = ok && pair_bit(PR, (int)((tgt >> (4 * i)) & 15), (int)((tgt >> (4 * i + 4)) & 15));
       int p = -1;
       if (ok) p = (slen == 2 && minpos == 0 && !need_pos) ? 0 : m_first(m_occ<NW>(bm, tgt, slen), minpos);
       if (p >= 0) {
