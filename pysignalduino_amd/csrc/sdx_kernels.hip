@@ -87,6 +87,10 @@ struct MsItem {
   uint16_t p;             // protocol index
   uint8_t mi, fmask;      // tile message, found-key mask
 };
+// Per tile (bench corpus: 1.6 survivors per message, ~104 per tile); more -> tile overflow ->
+// exact re-run on the long variant.  No decode inside the protocol loop: the loop's state is
+// not live across a decode, so nothing is spilled to scratch
+constexpr int MS_SURV_CAP = 1024;
 
 // MU (NW <= 4): one finditer match, finished after the protocol loop with lane = match
 struct MuMatch {
@@ -147,7 +151,9 @@ struct TileLds {
     MuItem q[LM == 1 ? LANE_WAVES : 1][LM == 1 ? QCAP : 1];
     uint8_t mmtab[LM == 1 ? SDX_MMTAB_LDS : 16];
   } u;
-  MsItem msq[LM == 2 ? LANE_WAVES : 1][LM == 2 ? QCAP : 1];  // MS decode queues
+  // MS survivors of the whole tile, decoded after the protocol loop with lane = survivor
+  MsItem slist[LM == 2 ? MS_SURV_CAP : 1];
+  int nsurv;
 #ifdef SDX_PROF
   unsigned int prof[LM != 0 ? LANE_WAVES : 4][24];  // s_memtime deltas per wave (< 2^32 per kernel)
 #endif
@@ -1306,6 +1312,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     L.nmatch = 0;
     L.pool_ctr = 0;
     L.ovf = 0;
+    L.nsurv = 0;
   }
   if constexpr (LANE_MU) {  // MU decode descriptors + modulematch tables -> LDS (16-B pieces)
     const int ndesc = (int)bv.hdr->n_mu < SDX_MUDESC_LDS ? (int)bv.hdr->n_mu : SDX_MUDESC_LDS;
@@ -1489,10 +1496,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   const uint16_t* order = bv.order + (KIND == SDX_KIND_MU ? 0 : (int)bv.hdr->n_mu);
   double last_clock = __builtin_nan("");  // NaN != anything: the first protocol normalises
   MuItem* Q = nullptr;
-  MsItem* QS = nullptr;
   int q_head = 0, q_tail = 0;
   if constexpr (LANE_MU) Q = L.u.q[wave];
-  if constexpr (LANE_MS) QS = L.msq[wave];
   auto drain = [&](int head, int cnt) {
     wave_sync();
     if constexpr (KIND == SDX_KIND_MU && NW <= 4) {
@@ -1512,16 +1517,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           decode_mu_lane<NW>(L, wave, bv, bv.mu + qp, d, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx,
                              ((uint64_t)it.st_hi << 32) | it.st_lo, it.u0, it.u1, it.u2, it.fmask);
         }
-      }
-    }
-    if constexpr (LANE_MS) {
-      if (lane < cnt) {
-        const MsItem it = QS[(head + lane) & (QCAP - 1)];
-        const int qm = it.mi, qp = it.p;
-        const uint32_t rk = L.raise_key[qm];
-        if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp)
-          decode_ms_lane<NW>(L, bv, bv.ms + qp, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.start,
-                             ((uint64_t)it.k0_hi << 32) | it.k0_lo, it.k1, it.k2, it.k3, it.fmask);
       }
     }
     wave_sync();
@@ -1685,10 +1680,14 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         if (r.found) { kt3 = r.tgt; fmask |= 8; }
       }
       alive = alive && fmask != 0;
-      if constexpr (LANE_MS) {  // queue the survivors; drain 64 at a time, lane = (message, protocol)
+      if constexpr (LANE_MS) {  // append the survivors to the tile list (decoded after the loop)
         const uint64_t pass = ballot(alive);
         if (pass) {
-          if (alive) {
+          int base = 0;
+          if (lane == 0) base = atomicAdd(&L.nsurv, popc64(pass));
+          base = __builtin_amdgcn_readfirstlane(base);
+          const int slot = base + lanes_below(pass);
+          if (alive && slot < MS_SURV_CAP) {
             MsItem it;
             it.k0_lo = (uint32_t)kt0;
             it.k0_hi = (uint32_t)(kt0 >> 32);
@@ -1699,13 +1698,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
             it.p = (uint16_t)p;
             it.mi = (uint8_t)mi;
             it.fmask = (uint8_t)fmask;
-            QS[(q_tail + lanes_below(pass)) & (QCAP - 1)] = it;
+            L.slist[slot] = it;
           }
-          q_tail += popc64(pass);
-          if (q_tail - q_head >= WAVE) {
-            drain(q_head, WAVE);
-            q_head += WAVE;
-          }
+          if (base + popc64(pass) > MS_SURV_CAP && lane == 0) L.ovf = 1;  // tile re-run (long variant)
         }
       } else {
         uint64_t surv = ballot(alive);
@@ -1718,7 +1713,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       }
     }
   }
-  if constexpr (LANE_MU || LANE_MS) {
+  if constexpr (LANE_MU) {
     PROF_T(t_dec);
     while (q_head < q_tail) {
       const int c = (q_tail - q_head < WAVE) ? q_tail - q_head : WAVE;
@@ -1730,6 +1725,22 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   PROF_T(t_bar);
   __syncthreads();
   PROF_ADD(14, t_bar);
+  if constexpr (LANE_MS) {  // decode every survivor of the tile: lane = (message, protocol)
+    PROF_T(t_dec);
+    const int ns = L.nsurv < MS_SURV_CAP ? L.nsurv : MS_SURV_CAP;
+    if (!L.ovf) {
+      for (int i = tid; i < ns; i += blockDim.x) {
+        const MsItem it = L.slist[i];
+        const int qm = it.mi, qp = it.p;
+        const uint32_t rk = L.raise_key[qm];
+        if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp)
+          decode_ms_lane<NW>(L, bv, bv.ms + qp, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.start,
+                             ((uint64_t)it.k0_hi << 32) | it.k0_lo, it.k1, it.k2, it.k3, it.fmask);
+      }
+    }
+    __syncthreads();  // the flush scratch aliases the bitmaps the decode reads
+    PROF_ADD(12, t_dec);
+  }
   if constexpr (LANE_MU) {  // finish every match of the tile: lane = match (message_unsynced.py:197-290)
     PROF_T(t_fin);
     {  // modulematch tables over the (now dead) decode queues. Loaded after the barrier on

@@ -142,6 +142,36 @@ def test_size_independent_properties(proto):
     assert per_msg(d3, r3, h3) == a[10000:]
 
 
+def test_ms_tile_overflow_reruns(proto, obank):
+    """A tile whose MS survivors exceed the tile list (MS_SURV_CAP = 1024) is marked
+    SDX_ST_OVF_TILE by the short kernel and re-run exactly on the long variant.  The message
+    below survives the sync/one/zero lookups of 21 MS protocols (searched with the oracle), so
+    64 copies in one tile need 1344 slots."""
+    from pysignalduino_amd import runtime, synth
+    from pysignalduino_amd.packing import PulsePacker
+    heavy = {"P0": "1200", "P1": "400", "P2": "-2400", "P3": "-400", "P4": "-7200", "P5": "-3200",
+             "P6": "-1200", "P7": "-3600", "CP": "1", "SP": "0", "R": "10",
+             "data": "5471115027363400667351410245004006624247207240055141125723665270103635536264520237234703"
+                     "1535357666035460372151345551047053162221571240443230735373311622430214516551552051466321"
+                     "262560504771330060154657"}
+    pb = synth.ms_corpus(proto.get_protocol_list(), 64, seed=5)
+    msgs = [heavy] * 64 + [pb.to_msg_dict(i) for i in range(pb.n)] + [heavy] * 70
+    pk = PulsePacker("MS")
+    for m in msgs:
+        pk.add(m)
+    eng = proto._ensure()
+    bd = eng.to_device_pulses(pk.batch())
+    out = eng.alloc_out(len(msgs), 64 * len(msgs), 256 * len(msgs))
+    eng.launch_pulses(runtime.KIND_MS, bd, out)
+    desc, _, _ = eng.fetch(out)
+    assert (desc["status"][:64] == runtime.ST_OVF_TILE).all()   # the first tile overflowed ...
+    assert (desc["status"][64:128] == runtime.ST_OK).all()      # ... the synthetic tile did not
+    got = proto.demodulate_batch(msgs, "MS")                    # ... and the re-run is exact
+    bad = [(i, _oracle(obank, m, "MS"), _flat(g)) for i, (m, g) in enumerate(zip(msgs, got))
+           if _flat(g) != _oracle(obank, m, "MS")]
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:1]}"
+
+
 @pytest.mark.parametrize("kind,n,seed", [("MU", 50000, 9101), ("MS", 100000, 9102), ("MC", 100000, 9103)])
 def test_large_corpus_vs_c_oracle(kind, n, seed):
     """Record-level, bit-exact: the device path (runtime.Engine through the C-ABI) against the
