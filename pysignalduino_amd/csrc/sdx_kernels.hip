@@ -1362,6 +1362,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     const int mi = wave + k * NWAVE;
     if (mi >= nvalid) break;
     const int n = __shfl(pf_n, k);
+    const int nwu = (n + 63) >> 6;  // words holding pulses (wave-uniform); the rest are empty
     bool nondigit = false;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
@@ -1369,10 +1370,13 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const uint8_t c = (uint8_t)pf_c[k][w];
       nondigit |= pos < n && !((c >= '0' && c <= '9') || c == 0xFE);
       uint64_t mine = 0;
+      if (KIND != SDX_KIND_MS || w < nwu) {  // short MS messages (sync + bits, mostly < 128 pulses)
+        // skip the ballots of empty words (MU: the uniform branch measured 1.8 % slower)
 #pragma unroll
-      for (int id = 0; id < 10; ++id) {
-        const uint64_t bb = ballot(c == (uint8_t)('0' + id));
-        if (lane == id) mine = bb;
+        for (int id = 0; id < 10; ++id) {
+          const uint64_t bb = ballot(c == (uint8_t)('0' + id));
+          if (lane == id) mine = bb;
+        }
       }
       if (lane < 10) L.bm[mi * T::MSTRIDE + lane * T::WS + w] = mine;
     }
@@ -1388,7 +1392,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           const uint64_t* A = &L.bm[mi * T::MSTRIDE + (q / 10) * T::WS];
           const uint64_t* B = &L.bm[mi * T::MSTRIDE + (q % 10) * T::WS];
 #pragma unroll
-          for (int w = 0; w < NW; ++w) acc |= A[w] & ((B[w] >> 1) | (w + 1 < NW ? B[w + 1] << 63 : 0ull));
+          for (int w = 0; w < NW; ++w)
+            if (KIND != SDX_KIND_MS || w < nwu) acc |= A[w] & ((B[w] >> 1) | (w + 1 < NW ? B[w + 1] << 63 : 0ull));
         }
         pr[h] = ballot(acc != 0);
       }
