@@ -80,7 +80,8 @@ typedef struct {
 
 /* MC batch */
 typedef struct {
-  const uint8_t* hex_dev;      /* hex characters (D=) of all frames concatenated */
+  const uint8_t* hex_dev;      /* hex characters (D=) of all frames concatenated; readable 8 bytes
+                                * past every frame's end (k_mc stages frames with aligned 8-byte loads) */
   const int64_t* offsets_dev;  /* [n+1] */
   const int32_t* clock_dev;    /* [n] C= */
   const int32_t* mcbitnum_dev; /* [n] L= */

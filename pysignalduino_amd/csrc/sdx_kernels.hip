@@ -2117,6 +2117,77 @@ SDX_DEV int hexval(uint8_t c) {
   return -1;
 }
 
+// a[w] <<= S bits across the 4-word bitstring (MSB-first words, 0 <= S < 256), no dynamic
+// register indexing
+SDX_DEV void shl_words4(uint64_t* a, int S) {
+  const int q = S >> 6, r = S & 63;
+  uint64_t o[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    uint64_t hi = 0, lo = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hi |= a[k] & (0ull - (uint64_t)(k == w + q));
+      lo |= a[k] & (0ull - (uint64_t)(k == w + q + 1));
+    }
+    o[w] = r ? ((hi << r) | (lo >> (64 - r))) : hi;
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) a[w] = o[w];
+}
+
+// hex -> MSB-first bits of a frame of 1..64 characters, both polarities, into the LDS words
+// dn[w * 256] / di[w * 256] (helpers.py:168-188, manchester.py:36; leading zero nibbles dropped as
+// bin(int(h, 16)) does, the last nibble always kept).  The characters come in with nine aligned
+// 8-byte loads issued together (hex_dev is readable 8 bytes past every frame's end) and are
+// decoded in registers; the LDS words are written once.
+SDX_DEV void mc_stage_short(const uint8_t* src, int hl, uint64_t* dn, uint64_t* di, int* nN, int* nI, bool* ok) {
+  const int s = (int)((uintptr_t)src & 7);
+  const uint64_t* wp = reinterpret_cast<const uint64_t*>(src - s);
+  uint64_t raw[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) raw[k] = (8 * k < s + hl) ? wp[k] : 0ull;
+  uint64_t wn[4] = {0, 0, 0, 0}, wi[4] = {0, 0, 0, 0};
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t x = s ? ((raw[k] >> (8 * s)) | (raw[k + 1] << (64 - 8 * s))) : raw[k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = 8 * k + j;
+      const uint32_t c = (uint32_t)(x >> (8 * j)) & 0xFFu;
+      const bool in = i < hl;
+      const bool dig = c - '0' < 10u, up = c - 'A' < 6u, lo = c - 'a' < 6u;
+      bad |= in && !(dig || up || lo);
+      const uint32_t v = dig ? c - '0' : (c & 7u) + 9u;  // 'A'/'a' -> 10 ... 'F'/'f' -> 15
+      const uint32_t vi = (dig || up) ? 15u - v : v;      // str.translate: uppercase only
+      const int sh = 60 - 4 * (i & 15);
+      wn[i >> 4] |= (uint64_t)(in ? v & 15u : 0u) << sh;
+      wi[i >> 4] |= (uint64_t)(in ? vi & 15u : 0u) << sh;
+    }
+  }
+  *ok = !bad;
+  // leading zero nibbles (at most hl - 1 of them)
+  auto lead = [&](const uint64_t* a) -> int {
+    int f = 256;
+#pragma unroll
+    for (int w = 3; w >= 0; --w)
+      if (a[w]) f = 64 * w + __clzll((long long)a[w]);
+    const int lz = f >> 2;
+    return lz < hl - 1 ? lz : hl - 1;
+  };
+  const int lzn = lead(wn), lzi = lead(wi);
+  shl_words4(wn, 4 * lzn);
+  shl_words4(wi, 4 * lzi);
+  *nN = 4 * (hl - lzn);
+  *nI = 4 * (hl - lzi);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    dn[w * 256] = wn[w];
+    di[w * 256] = wi[w];
+  }
+}
+
 // MW = 4: frames of <= 64 hex characters, longer ones are left to the MW = 8 launch (LONG = true),
 // which takes only those (sdx_demod_mc launches both; a wave without long frames exits at once)
 template <int MW, bool LONG>
@@ -2146,6 +2217,13 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     mcbit = b.mcbitnum_dev[msg];
     flags = b.flags_dev[msg];
     hex_ok = hl > 0 && hl <= MW * 16;
+    if constexpr (!LONG) {
+      if (hex_ok) mc_stage_short(b.hex_dev + off, hl, &L.bn[tid], &L.bi[tid], &nN, &nI, &hex_ok);
+    }
+  }
+  if (LONG && valid) {  // frames of 65..128 characters: character by character
+    const int64_t off = b.offsets_dev[msg];
+    const int hl = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
     bool startedN = false, startedI = false;
     for (int w = 0; w < MW; ++w) { L.bn[w * 256 + tid] = 0; L.bi[w * 256 + tid] = 0; }
     for (int i = 0; i < hl && hex_ok; ++i) {
@@ -2168,7 +2246,11 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
       }
     }
   }
+#ifndef SDX_X_MCHEXONLY
   const int nmc = (int)bv.hdr->n_mc;
+#else
+  const int nmc = 0;  // timing experiment: hex staging + flush only
+#endif
   int raise = 0;
   for (int p = 0; p < nmc; ++p) {
     const sdx_mc_proto* r = uniform_ptr(bv.mc + p);

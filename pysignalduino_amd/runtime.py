@@ -209,7 +209,8 @@ class Engine:
         d = self.dev
         flags = (mb.mtype.astype(np.uint8) & 1) | ((mb.v32.astype(np.uint8) & 1) << 1)
         return {
-            "hex": t.from_numpy(np.ascontiguousarray(mb.hexdata) if len(mb.hexdata) else np.zeros(1, np.uint8)).to(d),
+            # 16 bytes of slack: k_mc stages frames with aligned 8-byte loads (include/sdx.h)
+            "hex": t.from_numpy(np.concatenate([np.asarray(mb.hexdata, np.uint8), np.zeros(16, np.uint8)])).to(d),
             "offsets": t.from_numpy(np.ascontiguousarray(mb.offsets, dtype=np.int64)).to(d),
             "clock": t.from_numpy(np.ascontiguousarray(mb.clock, dtype=np.int32)).to(d),
             "mcbitnum": t.from_numpy(np.ascontiguousarray(mb.mcbitnum, dtype=np.int32)).to(d),
