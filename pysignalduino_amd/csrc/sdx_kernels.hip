@@ -1858,7 +1858,7 @@ struct McLds {
   uint64_t bn[MW * 256];   // bits, polarity as given
   uint64_t bi[MW * 256];   // bits, polarity inverted
   StageRec rec[4][MC_REC_CAP];
-  uint8_t heap[4][MC_HEAP_CAP];
+  alignas(16) uint8_t heap[4][MC_HEAP_CAP];
   int nrec[4], nheap[4], ovf[4];
 };
 
@@ -2251,7 +2251,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
 #else
   const int nmc = 0;  // timing experiment: hex staging + flush only
 #endif
-  int raise = 0;
+  int raise = 0, mycnt = 0;
   for (int p = 0; p < nmc; ++p) {
     const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
     bool go = valid && !raise;
@@ -2272,6 +2272,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     }
     // stage results of the wave in lane (= frame) order for this protocol
     const bool has = o.rc == 1;
+    if (!ballot(has)) continue;  // no result in this wave: nothing to stage (wave-uniform)
     const int plen = has ? cld(&r->pre_len) + o.len : 0;
     int incl = plen;  // inclusive scan over lanes
     for (int d = 1; d < WAVE; d <<= 1) {
@@ -2293,8 +2294,9 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
       sr.proto = (uint16_t)p;
       sr.bitlen = 0;
       sr.msg = (uint16_t)lane;
-      sr.rank = 0;
+      sr.rank = (uint16_t)mycnt;  // this frame's records so far (protocol order)
       L.rec[wave][rb + lanes_below(hm)] = sr;
+      ++mycnt;
     }
     wave_sync();
     if (lane == 0) {
@@ -2303,11 +2305,11 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     }
     wave_sync();
   }
-  // flush this wave's frames (records are in protocol-major order: count per lane)
-  const int nr = L.nrec[wave], nh = L.nheap[wave];
+  // flush this wave's frames: records are staged in protocol-major order, each carrying its rank
+  // among its frame's records; the wave writes them 64 at a time to (frame, protocol) order
+  const int nr = L.nrec[wave];
+  const int nh = (L.nheap[wave] + 15) & ~15;  // 16-B pieces: every reservation keeps hbase aligned
   const bool bad = L.ovf[wave] != 0;
-  int mycnt = 0;
-  for (int i = 0; i < nr; ++i) mycnt += (L.rec[wave][i].msg == lane) ? 1 : 0;
   if (raise) mycnt = 0;
   int incl = mycnt;
   for (int d = 1; d < WAVE; d <<= 1) {
@@ -2327,22 +2329,30 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   hbase = (uint32_t)__shfl((int)hbase, 0);
   st = __shfl(st, 0);
   if (st == 0) {
-    // each lane writes its own records in protocol order
-    int q = incl - mycnt;
-    if (mycnt)
-      for (int i = 0; i < nr; ++i) {
-        const StageRec sr = L.rec[wave][i];
-        if (sr.msg != lane) continue;
+    const int excl = incl - mycnt;
+    for (int i0 = 0; i0 < nr; i0 += WAVE) {  // wave-uniform trip count (the shuffles below)
+      const int i = i0 + lane;
+      StageRec sr{};
+      if (i < nr) sr = L.rec[wave][i];
+      const int fl = i < nr ? (int)sr.msg : 0;
+      const int fbase = __shfl(excl, fl), fmsg = __shfl(msg, fl), fraise = __shfl(raise, fl);
+      if (i < nr && !fraise) {
         sdx_result o;
         o.payload_off = hbase + sr.off;
         o.payload_len = sr.len;
         o.proto = sr.proto;
         o.bit_length = 0;
-        o.msg = (uint32_t)msg;
-        out.rec_dev[rbase + q] = o;
-        ++q;
+        o.msg = (uint32_t)fmsg;
+        out.rec_dev[rbase + fbase + sr.rank] = o;
       }
-    for (int i = lane; i < nh; i += WAVE) out.heap_dev[hbase + i] = L.heap[wave][i];
+    }
+    uint4* hd = reinterpret_cast<uint4*>(out.heap_dev + hbase);
+    const uint4* hs = reinterpret_cast<const uint4*>(L.heap[wave]);
+    if ((((uintptr_t)hd) & 15u) == 0) {
+      for (int i = lane; i < (nh >> 4); i += WAVE) hd[i] = hs[i];
+    } else {
+      for (int i = lane; i < nh; i += WAVE) out.heap_dev[hbase + i] = L.heap[wave][i];
+    }
   }
   if (valid) {
     sdx_desc d;
