@@ -1764,7 +1764,11 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     static_assert(sizeof(L.u) >= SDX_MMTAB_LDS + MATCH_CAP * 2 + NBIN * 4, "sort scratch fits the union");
     uint16_t* perm = reinterpret_cast<uint16_t*>(L.u.mmtab + SDX_MMTAB_LDS);
     uint32_t* bin = reinterpret_cast<uint32_t*>(perm + MATCH_CAP);
+#ifndef SDX_X_NOSORT
     const bool sorted = (int)bv.hdr->n_mu <= NBIN;
+#else
+    const bool sorted = false;  // timing experiment
+#endif
     if (sorted) {
       for (int i = tid; i < NBIN; i += blockDim.x) bin[i] = 0;
       __syncthreads();
@@ -1798,6 +1802,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const MuMatch mm = L.mlist[sorted ? perm[i] : i];
       const int qm = mm.mi, qp = mm.p;
       const uint32_t rk = L.raise_key[qm];
+#ifdef SDX_X_NOFINISH
+      if (rk != 0x12345u) continue;  // timing experiment
+#endif
       if (rk != 0xFFFFFFFFu && (rk >> 8) < (uint32_t)qp) continue;  // an earlier protocol raised
       sdx_mu_desc d;
       if (qp < SDX_MUDESC_LDS) d = L.desc[qp];
