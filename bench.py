@@ -120,22 +120,28 @@ def main():
         "MS": eng.alloc_out(ms.n, 4 * ms.n + 4096, 64 * ms.n + 65536),
         "MC": eng.alloc_out(mc.n, 4 * mc.n + 4096, 96 * mc.n + 65536),
     }
+    # the three launches' cursors are rows of one tensor: one fill per step resets them all
+    cursors = torch.zeros((3, 4), dtype=torch.int32, device=dev)
+    for i, k in enumerate(("MU", "MS", "MC")):
+        outs[k]["cursor"] = cursors[i]
     stream = torch.cuda.current_stream(dev)
-    ev = {k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in outs}
+    # one event pair per kernel and timed step: the steps run back to back and are read after the
+    # closing synchronize (no host round trip between steps)
+    ev = [{k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in outs}
+          for _ in range(args.steps)]
     ktimes = {k: [] for k in outs}
 
-    def step(record=False):
-        for k in outs:
-            outs[k]["cursor"].zero_()
+    def step(si=None):
+        cursors.zero_()
         for k, bd in (("MU", bmu), ("MS", bms), ("MC", bmc)):
-            if record:
-                ev[k][0].record(stream)
+            if si is not None:
+                ev[si][k][0].record(stream)
             if k == "MC":
                 eng.launch_mc(bd, outs[k])
             else:
                 eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, outs[k])
-            if record:
-                ev[k][1].record(stream)
+            if si is not None:
+                ev[si][k][1].record(stream)
         if world > 1:  # RCCL all-gather of the decoded dmsg buffers (config 5), pysignalduino_amd/dist.py:
             # one exchange of the counts, one all-gather of the packed MU/MS/MC buffers
             sdist.allgather_streams([(outs[k]["desc"], outs[k]["rec"], outs[k]["heap"], bd["n"], outs[k]["cursor"])
@@ -153,15 +159,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
-        torch.cuda.synchronize()
-        for k in outs:
-            ktimes[k].append(ev[k][0].elapsed_time(ev[k][1]) * 1e-3)
+    for si in range(args.steps):
+        step(si)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    for si in range(args.steps):
+        for k in outs:
+            ktimes[k].append(ev[si][k][0].elapsed_time(ev[si][k][1]) * 1e-3)
     tt = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
