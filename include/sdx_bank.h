@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 15u
+#define SDX_BANK_VERSION 16u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -166,7 +166,9 @@ typedef struct {
  * pair (message_unsynced.py:146-290), staged in LDS once per tile (the first SDX_MUDESC_LDS).
  * mm_on: 0 no modulematch; 1 LDS tables: st = mmtab[(mm_base + st) * 16 + digit] per hex digit,
  * then st = mmtab[17 * S + mm_post + st] for the postamble, accept on flags mmtab[16 * S + mm_base
- * + st] (ACC_NOW and DEAD are absorbing); 2 byte walk through the blob's t256 table. */
+ * + st] (ACC_NOW and DEAD are absorbing); 2 byte walk through the blob's t256 table; 3 the table
+ * walk's outcome depends on the digit count only (bank.py _mm_length_interval, exact for <= 64
+ * digits): accept iff res[0] <= digits <= res[1], no walk (the non-fast paths walk t256 as for 2). */
 #define SDX_MUDESC_LDS 144
 #define SDX_MMTAB_LDS 10240
 typedef struct {
@@ -175,7 +177,7 @@ typedef struct {
   uint8_t width, len_s, recon, dispatch_bin, remove_zero, postdemo, pad_bits, mm_on;
   uint16_t lmin, lmax;                  /* chunk-count limits, 65535 = none */
   uint16_t mm_base, mm_post;
-  uint8_t pre_state, res[3];
+  uint8_t pre_state, res[3];           /* mm_on 3: res[0..1] = accepted digit counts [lo, hi] */
 } sdx_mu_desc;                          /* 40 bytes */
 
 /* modulematch DFA (search semantics of re.search over the payload).

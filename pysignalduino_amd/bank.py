@@ -28,7 +28,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 15
+MAGIC, VERSION = 0x4B4E4253, 16
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("klo", "<i4", (MAXUNIQ,)), ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)),
@@ -112,6 +112,7 @@ MU_DESC = np.dtype([("pre", "u1", (16,)), ("post", "u1", (2,)), ("pre_len", "u1"
                     ("pre_state", "u1"), ("res", "u1", (3,))])
 MUDESC_LDS = 160      # SDX_MUDESC_LDS: descriptors held in LDS (the rest are read from the blob)
 MMTAB_LDS = 10240     # SDX_MMTAB_LDS: bytes of modulematch tables held in LDS
+MM_FAST_DIGITS = 64   # hex digits of a payload on the device's fast path (64 * NW / 4, NW = 4)
 
 POSTDEMO = {"postDemo_EM": 1, "postDemo_Revolt": 2, "postDemo_FS20": 3, "postDemo_FHT80": 4,
             "postDemo_FHT80TF": 5, "postDemo_WS2000": 6, "postDemo_WS7035": 7, "postDemo_WS7053": 8,
@@ -611,6 +612,31 @@ class Bank:
             x["flags"] = (int(rec["never"]) << 1) | ((0 if ok else 1) << 3)
         return f
 
+    @staticmethod
+    def _mm_length_interval(hex16, flags, post_map, pre_state, nmax: int = MM_FAST_DIGITS):
+        """[lo, hi] if the LDS-table walk's outcome (message_unsynced.py:277-280) depends on the
+        number of hex digits only, for every digit string of 0..nmax digits, and the accepted
+        counts form one interval (lo > hi: none accepted); else None.  Exact: the set of states
+        reachable after n digits is enumerated and every one of them must give the same outcome."""
+        def accept(st):
+            f = int(flags[int(post_map[st])])
+            return bool(f & regex_dfa.ACC_NOW) or (not f & regex_dfa.DEAD and bool(f & regex_dfa.ACC_END))
+
+        cur = {pre_state}
+        acc = []
+        for _ in range(nmax + 1):
+            outs = {accept(st) for st in cur}
+            if len(outs) != 1:
+                return None
+            acc.append(outs.pop())
+            cur = {int(hex16[st][v]) for st in cur for v in range(16)}
+        ns = [n for n, a in enumerate(acc) if a]
+        if not ns:
+            return (1, 0)
+        if ns != list(range(ns[0], ns[-1] + 1)):
+            return None
+        return (ns[0], ns[-1])
+
     def _mu_desc(self, mu, dfas, cls_of):
         """MU decode descriptors + the LDS modulematch tables.
 
@@ -681,7 +707,13 @@ class Bank:
             x["mm_on"] = 1
             x["mm_base"] = base_of[k]
             x["mm_post"] = len(post_rows)
-            post_rows.extend(walk(dfas[k], st, post) for st in range(nst))
+            post_map = [walk(dfas[k], st, post) for st in range(nst)]
+            post_rows.extend(post_map)
+            hex16 = np.asarray(trans, dtype=np.int64)[:, [cls_of[c] for c in hexc]]
+            iv = self._mm_length_interval(hex16, flags, post_map, int(rec["mm_pre_state"]))
+            if iv is not None:  # the outcome depends on the digit count only: no walk on the device
+                x["mm_on"] = 3
+                x["res"][0], x["res"][1] = iv
         hexs = np.concatenate(hex_rows).reshape(-1) if hex_rows else np.zeros(0, np.uint8)
         fls = np.concatenate(flag_rows) if flag_rows else np.zeros(0, np.uint8)
         tab = np.concatenate([hexs, fls, np.asarray(post_rows, dtype=np.uint8)])

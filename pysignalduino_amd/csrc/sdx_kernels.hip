@@ -687,7 +687,9 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   __builtin_memcpy(&pre1, d.pre + 8, 8);
   const uint64_t post16 = (uint64_t)d.post[0] | ((uint64_t)d.post[1] << 8);
   auto post_c = [&](int i) -> uint8_t { return post_g ? post_g[i] : (uint8_t)(post16 >> (8 * i)); };
-  if (d.mm_on == 1 && fast) {  // re.search(modulematch, payload) (:277-280) on the LDS hex tables
+  if (d.mm_on == 3 && fast && dlen <= 64) {  // re.search(modulematch, payload) (:277-280): a digit-count
+    if (dlen < (int)d.res[0] || dlen > (int)d.res[1]) return;  // interval (bank.py _mm_length_interval)
+  } else if ((d.mm_on == 1 || d.mm_on == 3) && fast) {  // re.search(modulematch, payload) (:277-280) on the LDS hex tables
     const uint8_t* hx = L.u.mmtab + 16 * (int)d.mm_base;
     int st = d.pre_state;
     uint64_t cur = 0;

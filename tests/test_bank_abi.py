@@ -119,27 +119,34 @@ def test_mu_desc_modulematch_tables(bk):
     rng = random.Random(11)
     P = bk.protocols
     checked = 0
+    n_interval = 0
     for r, pid in enumerate(bk.mu_pids):
         d = bk.mu_desc[r]
-        if int(d["mm_on"]) != 1:
+        mm_on = int(d["mm_on"])
+        if mm_on not in (1, 3):
             continue
+        n_interval += mm_on == 3
         p = P[pid]
         pre, post = f"{p.get('preamble', '')}", f"{p.get('postamble', '')}"
         for _ in range(60):
-            n = rng.randint(0, 24)
+            n = rng.randint(0, 24) if rng.random() < 0.8 else rng.randint(0, bankmod.MM_FAST_DIGITS)
             digits = "".join(rng.choice("0123456789ABCDEF") for _ in range(n))
             if rng.random() < 0.3:  # bias towards the pattern's own literal digits
                 lit = "".join(c for c in p["modulematch"] if c in "0123456789ABCDEF")
                 digits = (lit + digits)[:max(n, len(lit))]
+            # the LDS table walk (mm_on 1, and still valid for 3)
             st = int(d["pre_state"])
             for c in digits:
                 st = int(tab[16 * (int(d["mm_base"]) + st) + int(c, 16)])
             st = int(tab[17 * S + int(d["mm_post"]) + st])
             f = int(tab[16 * S + int(d["mm_base"]) + st])
             dev = bool(f & 1) or (not (f & 4) and bool(f & 2))
-            assert dev == bool(re.search(p["modulematch"], pre + digits + post)), (pid, digits)
+            exp = bool(re.search(p["modulematch"], pre + digits + post))
+            assert dev == exp, (pid, digits)
+            if mm_on == 3:  # the digit-count interval the device uses instead of the walk
+                assert (int(d["res"][0]) <= len(digits) <= int(d["res"][1])) == exp, (pid, digits)
             checked += 1
-    assert checked > 1000
+    assert checked > 1000 and n_interval > 0
 
 
 def test_blob_header(bk):
