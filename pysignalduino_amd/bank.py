@@ -357,6 +357,8 @@ class Bank:
             one = p.get("one")
             width = len(one) if one else 0
             rec["width"] = width
+            if width not in (0, 1, 2, 4):  # the device's chunk grid (residue masks, stride extraction)
+                raise NotImplementedError(f"MS {pid}: unit width {width} not in (1, 2, 4)")
             never = False
             for k, key in enumerate(("sync", "one", "zero", "float")):
                 spec = p.get(key)

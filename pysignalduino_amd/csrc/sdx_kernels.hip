@@ -1092,8 +1092,12 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
   const uint8_t KSYM[4] = {3, 1, 0, 2};  // 3: the sync symbol '' (no bit)
   const int span = start < n ? n - start : 0;
   const int nfull = span / Wd, part = span - nfull * Wd;
-  // chunk-indexed masks (bit t = chunk at start + t*Wd): symbol '1', 'F', sync-skip, unit, tail
-  M<NW> C1 = m_zero<NW>(), CF = m_zero<NW>(), CS = m_zero<NW>(), CU = m_zero<NW>(), CT = m_zero<NW>();
+  // The chunk loop (:174-189) reads chunk t at position start + t*Wd.  Everything is kept in the
+  // position domain (bit p = a key occurrence starting at p), where "chunk t is a unit" is bit
+  // start + t*Wd: the break is found there directly, and only the symbol-'1' mask (and, when
+  // present, 'F' / sync-in-data) is compacted to chunk order -- one stride extraction instead of
+  // one per key.  Wd is 1, 2 or 4 (m_stride_extract, residue_word).
+  M<NW> R1 = m_zero<NW>(), RF = m_zero<NW>(), RS = m_zero<NW>(), RU = m_zero<NW>(), RT = m_zero<NW>();
   // pattern_lookup (:122-135): distinct strings, value = the last writer's symbol
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
@@ -1102,17 +1106,18 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
 #pragma unroll
     for (int j = kk + 1; j < 4; ++j) later |= ((fmask >> j) & 1) && klen[j] == klen[kk] && kt[j] == kt[kk];
     if (later) continue;
-    const M<NW> C = m_stride_extract(m_occ<NW>(bm, kt[kk], Wd), start, Wd, nfull);
-    CU = m_or(CU, C);
-    if (KSYM[kk] == 1) C1 = m_or(C1, C);
-    if (KSYM[kk] == 2) CF = m_or(CF, C);
-    if (KSYM[kk] == 3) CS = m_or(CS, C);
+    const M<NW> O = m_occ<NW>(bm, kt[kk], Wd);
+    RU = m_or(RU, O);
+    if (KSYM[kk] == 1) R1 = m_or(R1, O);
+    if (KSYM[kk] == 2) RF = m_or(RF, O);
+    if (KSYM[kk] == 3) RS = m_or(RS, O);
   }
   // end_pattern_lookup (:124-127, reset after the sync :158): one/zero/float pstr[:-1], first
   // writer wins; a full chunk that is no unit continues with chunk[:-1]'s symbol (:183-187)
   const bool recon = cld(&rec->recon) != 0 && Wd > 1;
   const uint64_t emsk = (Wd - 1 >= 16) ? ~0ull : ((1ull << (4 * (Wd - 1))) - 1);
   if (recon) {
+    const M<NW> notU = m_not(RU);
 #pragma unroll
     for (int kk = 1; kk < 4; ++kk) {
       if (!((fmask >> kk) & 1) || klen[kk] != Wd) continue;
@@ -1121,15 +1126,21 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
 #pragma unroll
       for (int j = 1; j < kk; ++j) earlier |= ((fmask >> j) & 1) && klen[j] == Wd && (kt[j] & emsk) == key;
       if (earlier) continue;
-      const M<NW> C = m_and(m_stride_extract(m_occ<NW>(bm, key, Wd - 1), start, Wd, nfull), m_not(CU));
-      CT = m_or(CT, C);
-      if (KSYM[kk] == 1) C1 = m_or(C1, C);
-      if (KSYM[kk] == 2) CF = m_or(CF, C);
+      const M<NW> X = m_and(m_occ<NW>(bm, key, Wd - 1), notU);
+      RT = m_or(RT, X);
+      if (KSYM[kk] == 1) R1 = m_or(R1, X);
+      if (KSYM[kk] == 2) RF = m_or(RF, X);
     }
   }
+  // chunk grid: positions start + t*Wd, t < nfull
+  const int wsh = __ffs(Wd) - 1;
+  const uint64_t res = residue_word(Wd, start & (Wd - 1));
+  M<NW> G = m_and(m_range_lo<NW>(start + nfull * Wd), m_not(m_range_lo<NW>(start)));
+#pragma unroll
+  for (int i = 0; i < NW; ++i) G.w[i] &= res;
   // the first chunk that is neither ends the loop (:188-189)
-  int k = m_first(m_and(m_not(m_or(CU, CT)), m_range_lo<NW>(nfull)), 0);
-  if (k < 0) k = nfull;
+  const int pb = m_first(m_and(G, m_not(m_or(RU, RT))), 0);
+  const int k = pb < 0 ? nfull : (pb - start) >> wsh;
   // a partial last chunk: a unit of its length (last writer), else (recon) the chunk as a tail key
   int extra = -1;
   if (k == nfull && part > 0) {
@@ -1145,16 +1156,17 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
     }
   }
   // bits = chunks [0, k) without the sync-symbol ones, then the partial chunk's bit
-  const M<NW> R = m_range_lo<NW>(k);
-  M<NW> P1, PF;
+  const M<NW> Gk = m_and(G, m_range_lo<NW>(start + k * Wd));
+  M<NW> P1, PF = m_zero<NW>();
   int nb;
-  if (!m_any(m_and(CS, R))) {
-    P1 = m_and(C1, R);
-    PF = m_and(CF, R);
+  if (!m_any(m_and(RS, Gk))) {
+    P1 = m_stride_extract(R1, start, Wd, k);
+    if (m_any(m_and(RF, Gk))) PF = m_stride_extract(RF, start, Wd, k);
     nb = k;
   } else {  // a sync-string chunk inside the data (rare): compact serially
+    const M<NW> C1 = m_stride_extract(R1, start, Wd, k), CF = m_stride_extract(RF, start, Wd, k),
+                CS = m_stride_extract(RS, start, Wd, k);
     P1 = m_zero<NW>();
-    PF = m_zero<NW>();
     nb = 0;
     for (int t = 0; t < k; ++t) {
       if (m_test(CS, t)) continue;
@@ -1734,7 +1746,11 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   PROF_ADD(14, t_bar);
   if constexpr (LANE_MS) {  // decode every survivor of the tile: lane = (message, protocol)
     PROF_T(t_dec);
+#ifndef SDX_X_NODECODE
     const int ns = L.nsurv < MS_SURV_CAP ? L.nsurv : MS_SURV_CAP;
+#else
+    const int ns = 0;  // timing experiment
+#endif
     if (!L.ovf) {
       for (int i = tid; i < ns; i += blockDim.x) {
         const MsItem it = L.slist[i];
