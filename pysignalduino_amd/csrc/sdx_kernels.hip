@@ -283,7 +283,7 @@ SDX_DEV void finish_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, con
   // padding (:257-259), after postDemod
   const int pad = cld(&rec->pad_bits);
   int nbp = nb;
-  while (nbp % pad) ++nbp;
+  nbp = (nbp + pad - 1) / pad * pad;  // append '0' until len % pad == 0 (pad >= 1, bank.py)
   for (int i = nb + lane_id(); i < nbp; i += WAVE) buf[i] = 0;
   wave_sync();
   const bool isf = any_float(buf, nbp);
@@ -557,6 +557,19 @@ struct ByteWriter {
   }
 };
 
+// append `len` bytes of a string in global memory: 8 independent byte loads per step, so one
+// memory latency per 8 bytes instead of one per byte
+SDX_DEV void put_str(ByteWriter& w, const uint8_t* s, int len) {
+  for (int i = 0; i < len; i += 8) {
+    const int c = len - i < 8 ? len - i : 8;
+    uint64_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < c) x |= (uint64_t)s[i + j] << (8 * j);
+    w.put(x, c);
+  }
+}
+
 // 8 hex digits (nibble i of x = digit i) -> 8 ASCII bytes '0'-'9','A'-'F' (byte i); only the low
 // `cnt` bytes are kept
 SDX_DEV uint64_t hex8(uint64_t x, int cnt) {
@@ -626,7 +639,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   PROF_T(t_fmt);
   const int pad = d.pad_bits;
   int nbp = nb;
-  while (nbp % pad) ++nbp;
+  nbp = (nbp + pad - 1) / pad * pad;  // append '0' until len % pad == 0 (pad >= 1, bank.py)
   const int nd = (nbp + 3) >> 2;
   if (!usearr && 4 * nd > 64 * NW) {  // does not fit the packed words: use the byte array
     for (int b = 0; b < nb; ++b) pout[b] = m_test(PF, b) ? 2 : (m_test(P1, b) ? 1 : 0);
@@ -730,7 +743,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   }
   ByteWriter w(reinterpret_cast<uint64_t*>(L.heap + off));
   if (pre_g) {
-    for (int i = 0; i < pre_len; ++i) w.put(pre_g[i], 1);
+    put_str(w, pre_g, pre_len);
   } else {
     auto lowb = [](uint64_t x, int c) { return c >= 8 ? x : x & ((1ull << (8 * c)) - 1); };
     if (pre_len) w.put(lowb(pre0, pre_len), pre_len < 8 ? pre_len : 8);
@@ -748,7 +761,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
     for (int i = 0; i < dlen; ++i) w.put(dchar(i), 1);
   }
   if (post_g) {
-    for (int i = 0; i < post_len; ++i) w.put(post_g[i], 1);
+    put_str(w, post_g, post_len);
   } else if (post_len) {
     w.put(post_len == 1 ? (post16 & 0xFFull) : post16, post_len);
   }
@@ -1000,14 +1013,18 @@ template <int NW, class T>
 SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, int p, int mi, const M<NW>& P1,
                             const M<NW>& PF, int nb) {
   constexpr int NB = 64 * NW + 64;
-  if (nb == 0) return;  // (:191-192)
-  if (cld(&rec->lir_min) != -1 && nb < cld(&rec->lir_min)) return;  // length_in_range (:194-196)
-  if (nb > cld(&rec->lir_max)) return;
-  int nbits = nb;  // padding (:198-200): appended '0' bits (P1/PF hold zeros beyond nb)
-  const int pad = cld(&rec->pad_bits);
-  while (nbits % pad) ++nbits;
-  const bool anyf = m_any(PF);
+  // every record field up front: independent loads in flight together (rec varies per lane, so
+  // these are vector loads; issued after each early exit they would form a chain of latencies)
+  const int lir_min = cld(&rec->lir_min), lir_max = cld(&rec->lir_max), pad = cld(&rec->pad_bits);
   const int pd = cld(&rec->postdemo);
+  const int pre_len = cld(&rec->pre_len), post_len = cld(&rec->post_len);
+  const int pre_off = cld(&rec->pre_off), post_off = cld(&rec->post_off);
+  if (nb == 0) return;  // (:191-192)
+  if (lir_min != -1 && nb < lir_min) return;  // length_in_range (:194-196)
+  if (nb > lir_max) return;
+  int nbits = nb;  // padding (:198-200): appended '0' bits (P1/PF hold zeros beyond nb)
+  nbits = (nbits + pad - 1) / pad * pad;  // pad >= 1 (bank.py)
+  const bool anyf = m_any(PF);
   uint8_t pout[NB];
   bool usearr = false;
   if (pd != SDX_PD_NONE) {  // (:203-219)
@@ -1041,9 +1058,8 @@ SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
 #pragma unroll
     for (int i = 0; i < NW; ++i) H.w[i] = nibrev(H.w[i]);
   }
-  const int pre_len = cld(&rec->pre_len), post_len = cld(&rec->post_len);
-  const uint8_t* pre = bv.str + cld(&rec->pre_off);
-  const uint8_t* post = bv.str + cld(&rec->post_off);
+  const uint8_t* pre = bv.str + pre_off;
+  const uint8_t* post = bv.str + post_off;
   const int total = pre_len + nd + post_len;
   const int span = (total + 7) & ~7;
   const unsigned long long o = atomicAdd(&L.pool_ctr, ((unsigned long long)span << 32) | 1ull);
@@ -1053,7 +1069,7 @@ SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
     return;
   }
   ByteWriter w(reinterpret_cast<uint64_t*>(L.heap + off));
-  for (int i = 0; i < pre_len; ++i) w.put(pre[i], 1);
+  put_str(w, pre, pre_len);
   if (!usearr) {
     for (int t = 0; t < nd; t += 8) {
       const int b = 4 * t, wi = b >> 6, sh = b & 63;
@@ -1070,7 +1086,7 @@ SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
       w.put((uint64_t)(v < 10 ? '0' + v : 'A' + v - 10), 1);
     }
   }
-  for (int i = 0; i < post_len; ++i) w.put(post[i], 1);
+  put_str(w, post, post_len);
   w.flush();
   StageRec r;
   r.off = (uint32_t)off;
@@ -2311,7 +2327,15 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     const bool fits = hb + wtot <= MC_HEAP_CAP && rb + nnew <= MC_REC_CAP;
     if (has && fits) {
       uint8_t* dst = &L.heap[wave][hb + incl - plen];
-      for (int i = 0; i < cld(&r->pre_len); ++i) dst[i] = bv.str[cld(&r->pre_off) + i];
+      const int pl = cld(&r->pre_len), po = cld(&r->pre_off);
+      for (int i = 0; i < pl; i += 8) {  // 8 independent loads per step
+        uint8_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[j] = (i + j < pl) ? bv.str[po + i + j] : (uint8_t)0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (i + j < pl) dst[i + j] = c[j];
+      }
       mc_write(r, o, B, nb, dst + cld(&r->pre_len));
       StageRec sr;
       sr.off = (uint32_t)(hb + incl - plen);
