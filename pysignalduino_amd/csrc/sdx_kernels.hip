@@ -91,6 +91,14 @@ struct MsItem {
 // exact re-run on the long variant.  No decode inside the protocol loop: the loop's state is
 // not live across a decode, so nothing is spilled to scratch
 constexpr int MS_SURV_CAP = 1024;
+constexpr int MS_DESC_LDS = 96;  // MS decode descriptors staged in LDS (the bank has 66 MS ids)
+// the fields the MS lane decode reads per survivor (ms_desc builds one from a record)
+struct MsDesc {
+  int32_t lir_min, lir_max, pad, pre_off, post_off;
+  uint16_t pre_len, post_len;
+  uint8_t width, klen[4], recon, postdemo, res;
+};  // 32 bytes
+static_assert(sizeof(MsDesc) == 32, "MsDesc layout");
 
 // MU (NW <= 4): one finditer match, finished after the protocol loop with lane = match
 struct MuMatch {
@@ -154,6 +162,7 @@ struct TileLds {
   // MS survivors of the whole tile, decoded after the protocol loop with lane = survivor
   MsItem slist[LM == 2 ? MS_SURV_CAP : 1];
   int nsurv;
+  MsDesc msdesc[LM == 2 ? MS_DESC_LDS : 1];
 #ifdef SDX_PROF
   unsigned int prof[LM != 0 ? LANE_WAVES : 4][24];  // s_memtime deltas per wave (< 2^32 per kernel)
 #endif
@@ -1007,18 +1016,37 @@ SDX_DEV void decode_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, con
 // ---------------------------------------------------------------------------------------------
 // MS, lane = (message, protocol) survivor (message_synced.py:160-241) on register bitmasks
 // ---------------------------------------------------------------------------------------------
+// the fields the MS lane decode reads per survivor, staged in LDS once per tile (the first
+// MS_DESC_LDS protocols): the survivors of a tile mix protocols, so reading them from the record
+// would be per-lane vector loads from L2 on every decode
+SDX_DEV MsDesc ms_desc(const sdx_ms_proto* rec) {
+  MsDesc d;
+  d.lir_min = cld(&rec->lir_min);
+  d.lir_max = cld(&rec->lir_max);
+  d.pad = cld(&rec->pad_bits);
+  d.pre_off = cld(&rec->pre_off);
+  d.post_off = cld(&rec->post_off);
+  d.pre_len = (uint16_t)cld(&rec->pre_len);
+  d.post_len = (uint16_t)cld(&rec->post_len);
+  d.width = (uint8_t)cld(&rec->width);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d.klen[k] = (uint8_t)cld(&rec->key[k].len);
+  d.recon = (uint8_t)(cld(&rec->recon) != 0);
+  d.postdemo = (uint8_t)cld(&rec->postdemo);
+  d.res = 0;
+  return d;
+}
+
 // finish one MS result from its packed bits (P1 = '1', PF = 'F', nb bits): length_in_range,
 // padding BEFORE postDemod, postDemod without try, hex (None -> skipped), payload
 template <int NW, class T>
-SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, int p, int mi, const M<NW>& P1,
+SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, int mi, const M<NW>& P1,
                             const M<NW>& PF, int nb) {
   constexpr int NB = 64 * NW + 64;
-  // every record field up front: independent loads in flight together (rec varies per lane, so
-  // these are vector loads; issued after each early exit they would form a chain of latencies)
-  const int lir_min = cld(&rec->lir_min), lir_max = cld(&rec->lir_max), pad = cld(&rec->pad_bits);
-  const int pd = cld(&rec->postdemo);
-  const int pre_len = cld(&rec->pre_len), post_len = cld(&rec->post_len);
-  const int pre_off = cld(&rec->pre_off), post_off = cld(&rec->post_off);
+  const int lir_min = D.lir_min, lir_max = D.lir_max, pad = D.pad;
+  const int pd = D.postdemo;
+  const int pre_len = D.pre_len, post_len = D.post_len;
+  const int pre_off = D.pre_off, post_off = D.post_off;
   if (nb == 0) return;  // (:191-192)
   if (lir_min != -1 && nb < lir_min) return;  // length_in_range (:194-196)
   if (nb > lir_max) return;
@@ -1100,11 +1128,12 @@ SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
 }
 
 template <int NW, class T>
-SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, int p, int mi, const uint64_t* bm,
+SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, int mi, const uint64_t* bm,
                             int n, int start, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3, int fmask) {
-  const int Wd = cld(&rec->width);
+  const int Wd = D.width;
   const uint64_t kt[4] = {k0, k1, k2, k3};
-  const int klen[4] = {cld(&rec->key[0].len), cld(&rec->key[1].len), cld(&rec->key[2].len), cld(&rec->key[3].len)};
+  const int klen[4] = {D.klen[0], D.klen[1], D.klen[2], D.klen[3]};
+  const bool recon = D.recon != 0 && Wd > 1;
   const uint8_t KSYM[4] = {3, 1, 0, 2};  // 3: the sync symbol '' (no bit)
   const int span = start < n ? n - start : 0;
   const int nfull = span / Wd, part = span - nfull * Wd;
@@ -1130,7 +1159,6 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
   }
   // end_pattern_lookup (:124-127, reset after the sync :158): one/zero/float pstr[:-1], first
   // writer wins; a full chunk that is no unit continues with chunk[:-1]'s symbol (:183-187)
-  const bool recon = cld(&rec->recon) != 0 && Wd > 1;
   const uint64_t emsk = (Wd - 1 >= 16) ? ~0ull : ((1ull << (4 * (Wd - 1))) - 1);
   if (recon) {
     const M<NW> notU = m_not(RU);
@@ -1196,7 +1224,7 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const sdx_ms_proto* rec, i
     if (extra == 2) m_set(PF, nb);
     ++nb;
   }
-  finish_ms_lane<NW>(L, bv, rec, p, mi, P1, PF, nb);
+  finish_ms_lane<NW>(L, bv, D, p, mi, P1, PF, nb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1351,6 +1379,10 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     uint4* dst = reinterpret_cast<uint4*>(L.desc);
     for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
     if (tid == 0) L.mm_states = (int)bv.hdr->mm_states;
+  }
+  if constexpr (LANE_MS) {
+    const int nd = (int)bv.hdr->n_ms < MS_DESC_LDS ? (int)bv.hdr->n_ms : MS_DESC_LDS;
+    for (int i = tid; i < nd; i += blockDim.x) L.msdesc[i] = ms_desc(bv.ms + i);
   }
 #ifdef SDX_PROF
   if (lane < 24) L.prof[wave][lane] = 0;
@@ -1773,7 +1805,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         const int qm = it.mi, qp = it.p;
         const uint32_t rk = L.raise_key[qm];
         if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp)
-          decode_ms_lane<NW>(L, bv, bv.ms + qp, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.start,
+          decode_ms_lane<NW>(L, bv, qp < MS_DESC_LDS ? L.msdesc[qp] : ms_desc(bv.ms + qp), qp, qm,
+                             &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.start,
                              ((uint64_t)it.k0_hi << 32) | it.k0_lo, it.k1, it.k2, it.k3, it.fmask);
       }
     }
