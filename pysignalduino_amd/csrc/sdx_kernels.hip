@@ -1920,9 +1920,23 @@ struct LaneBits {
     if (o) hi |= word(w + 1) >> (64 - o);
     return (uint32_t)(hi >> (64 - P));
   }
+  // first i >= from with bits [i, i+P) == pat and i + P <= n (P <= 32): 64 start positions per
+  // step, matched bit-parallel on two words (two LDS reads per 64 positions, not per position)
   SDX_DEV int find(uint32_t pat, int P, int from, int n) const {
-    for (int i = from < 0 ? 0 : from; i + P <= n; ++i)
-      if (win(i, P) == pat) return i;
+    if (from < 0) from = 0;
+    for (int w = from >> 6; 64 * w + P <= n; ++w) {
+      const uint64_t a = word(w), b = word(w + 1);
+      uint64_t m = ~0ull;  // bit 63 - j: start 64w + j still matches
+      for (int t = 0; t < P; ++t) {
+        const uint64_t xt = t ? ((a << t) | (b >> (64 - t))) : a;  // bit 63 - j = string bit 64w + j + t
+        m &= ((pat >> (P - 1 - t)) & 1u) ? xt : ~xt;
+      }
+      const int lo = from - 64 * w;  // j >= lo
+      if (lo > 0) m &= ~0ull >> lo;
+      const int hi = n - P - 64 * w;  // j <= hi
+      if (hi < 63) m &= ~0ull << (63 - hi);
+      if (m) return 64 * w + __clzll((long long)m);
+    }
     return -1;
   }
 };
@@ -1943,8 +1957,7 @@ SDX_DEV int lane_hex(const LaneBits& B, int a, int e, uint8_t* dst) {
   const int nd = (nb + 3) >> 2;
   for (int d = 0; d < nd; ++d) {
     const int de = e - 4 * (nd - 1 - d), da = (de - 4 > a) ? de - 4 : a;
-    int v = 0;
-    for (int i = da; i < de; ++i) v = (v << 1) | B.get(i);
+    const int v = (int)B.win(da, de - da);  // int(bits[da:de], 2)
     if (dst) dst[d] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
   }
   return nd;
