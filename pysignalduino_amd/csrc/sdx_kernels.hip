@@ -1966,9 +1966,13 @@ SDX_DEV int lane_hex(const LaneBits& B, int a, int e, uint8_t* dst) {
 SDX_DEV bool hex_equal(const LaneBits& B, int a1, int e1, int a2, int e2) {
   if (((e1 - a1 + 3) >> 2) != ((e2 - a2 + 3) >> 2)) return false;
   const int m = (e1 - a1 > e2 - a2) ? e1 - a1 : e2 - a2;
-  for (int t = 0; t < m; ++t) {
-    const int x = (e1 - 1 - t >= a1) ? B.get(e1 - 1 - t) : 0;
-    const int y = (e2 - 1 - t >= a2) ? B.get(e2 - 1 - t) : 0;
+  // right-aligned, 32 bits per step; bits left of a1 / a2 count as 0
+  for (int t = 0; t < m; t += 32) {
+    const int k = m - t < 32 ? m - t : 32;
+    const int s1 = e1 - t - k, s2 = e2 - t - k;
+    const int v1 = e1 - t - (s1 > a1 ? s1 : a1), v2 = e2 - t - (s2 > a2 ? s2 : a2);
+    const uint32_t x = v1 > 0 ? B.win(e1 - t - v1, v1) : 0u;
+    const uint32_t y = v2 > 0 ? B.win(e2 - t - v2, v2) : 0u;
     if (x != y) return false;
   }
   return true;
