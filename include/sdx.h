@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 3
+#define SDX_ABI_VERSION 4
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -239,6 +239,57 @@ typedef struct {
 } sdx_json_out;
 
 int sdx_serialize_json(const sdx_bank* bank, const sdx_json_in* in, const sdx_json_out* out, void* hip_stream);
+
+/* ---- unit-level entry ------------------------------------------------------------------------
+ * The reference's helper methods that its own unit tests call on SDProtocols, evaluated on n
+ * independent inputs in one launch (lane = item), with the device code the demodulation kernels
+ * run.  Replaces, per op:
+ *   SDX_UNIT_POSTDEMO   SDProtocols.postDemo_EM/_Revolt/_FS20/_FHT80/_FHT80TF/_WS2000/_WS7035/
+ *                       _WS7053/_lengtnPrefix(name, bit_msg_array)   postdemodulation.py:27-730
+ *                       in: the bits as bytes 0/1; arg: enum sdx_postdemo (sdx_bank.h).
+ *                       proto 0: (1, payload bits as bytes 0/1); proto 1: (0, None);
+ *                       RAISED ValueError: int('', 2).
+ *   SDX_UNIT_HEX2BIN    SDProtocols.hex_to_bin_str(hex_string)      helpers.py:168-188, and with
+ *                       arg = 1 _convert_mc_hex_to_bits's polarity translate first
+ *                       (manchester.py:18-47).  in: the string's bytes; proto 0: payload '0'/'1';
+ *                       proto 1: None.
+ *   SDX_UNIT_BIN2HEX    SDProtocols.bin_str_2_hex_str(num)          helpers.py:28-64.
+ *                       proto 0: payload (hex); proto 1: None.
+ *   SDX_UNIT_MC2DMC     SDProtocols.mc2dmc(bit_data)                helpers.py:6-26 (ASCII input).
+ *   SDX_UNIT_PEXISTS    pattern_utils.pattern_exists(search, patterns, raw_data)  pattern_utils.py:34-136.
+ *                       in: [npat][npat id lengths][id bytes][raw_data]; val: the search values
+ *                       then the pattern values (fp64, dict order); arg: number of search values
+ *                       (<= SDX_UNIT_PX_SEARCH; npat <= SDX_UNIT_PX_PAT).  proto 0: the target
+ *                       string; proto 1: -1.
+ *   SDX_UNIT_MC_METHOD  SDProtocols.mcBit2Funkbus/Sainlogic/AS/Hideki/Maverick/OSV1/OSV2o3/OSPIR/
+ *                       TFA/Grothe/SomfyRTS, mcRaw, mcraw(name, bit_data, protocol_id, mcbitnum)
+ *                       manchester.py:207-795, helpers.py:90-122.  in: bit_data ('0'/'1',
+ *                       <= SDX_UNIT_MC_BITS); arg: mcbitnum; mcrec_dev[i]: the sdx_mc_proto of
+ *                       (protocol_id, method) (pysignalduino_amd/bank.py mc_record).  proto 0:
+ *                       (1, payload), bit_length = payload kind (2: a Python list repr); proto k > 0:
+ *                       (-1, text k) of the McWhy codes (csrc/sdx_mc.h), bit_length = its argument;
+ *                       RAISED TypeError / ValueError where the reference raises.
+ * Item i: desc[i] = {rec_begin i, n_rec 1 (0 when RAISED), status, raise_kind}, rec[i] = {payload at
+ * heap[out_off[i]..], payload_len, proto (above), bit_length, msg i}; rec_cap >= n. */
+enum sdx_unit_op { SDX_UNIT_POSTDEMO = 1, SDX_UNIT_HEX2BIN = 2, SDX_UNIT_BIN2HEX = 3, SDX_UNIT_MC2DMC = 4,
+                   SDX_UNIT_PEXISTS = 5, SDX_UNIT_MC_METHOD = 6 };
+#define SDX_UNIT_MC_BITS 512
+#define SDX_UNIT_PX_SEARCH 32
+#define SDX_UNIT_PX_PAT 16
+
+typedef struct {
+  int32_t op;                  /* enum sdx_unit_op */
+  int32_t n;                   /* items */
+  const uint8_t* in_dev;       /* item i's input: in[in_off[i], in_off[i+1]) */
+  const int64_t* in_off_dev;   /* [n+1] */
+  const int32_t* arg_dev;      /* [n] per-item argument (see above); NULL = 0 */
+  const double* val_dev;       /* SDX_UNIT_PEXISTS: values of item i from val[val_off[i]] */
+  const int64_t* val_off_dev;  /* SDX_UNIT_PEXISTS: [n+1] */
+  const void* mcrec_dev;       /* SDX_UNIT_MC_METHOD: [n] sdx_mc_proto */
+  const int64_t* out_off_dev;  /* [n+1] item i writes its payload to heap[out_off[i], out_off[i+1]) */
+} sdx_unit_batch;
+
+int sdx_units(const sdx_unit_batch* batch, const sdx_out* out, void* hip_stream);
 
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */
 #define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */

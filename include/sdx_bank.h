@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #define SDX_BANK_MAGIC 0x4B4E4253u /* "SBNK" */
-#define SDX_BANK_VERSION 16u
+#define SDX_BANK_VERSION 17u
 #define SDX_MAXSEARCH 16 /* longest start/sync/one/zero/float list (start of id 111 = 14) */
 #define SDX_MAXUNIQ 4    /* distinct values inside one search list (bank max: 4) */
 #define SDX_MAXPAT 10    /* P0..P9: pattern ids are single digits (device contract) */
@@ -112,15 +112,20 @@ enum sdx_mc_method {
   SDX_MC_GROTHE, SDX_MC_SOMFY
 };
 
-/* MC protocol = every id with 'clockrange' (manchester.py:49-144) */
+#define SDX_PID_NOT_INT ((int32_t)0x80000000)
+
+/* MC protocol = every id with 'clockrange' (manchester.py:49-144); the unit entry (sdx_units) takes
+ * one such record per call, built by the host for any protocol id */
 typedef struct {
   double cr_lo, cr_hi;                  /* clockrange[0], clockrange[1] */
   int32_t proto_index;
   int32_t method;                       /* enum sdx_mc_method */
   int32_t lmin, lmax;                   /* parsed length_min / length_max */
   int32_t pre_off, pre_len;
-  int32_t pid_num;                      /* int(pid) when integral (Funkbus id test) else -1 */
-  uint8_t has_lmin, has_lmax, lmax_is_str, invert, has_cr, res[3];
+  int32_t pid_num;                      /* int(pid) (Funkbus id test); SDX_PID_NOT_INT when int() raises */
+  uint8_t has_lmin, has_lmax, lmax_is_str, invert, has_cr;
+  uint8_t lir_noexist;                  /* length_in_range: protocol_exists(str(pid)) is False */
+  uint8_t res[2];
 } sdx_mc_proto;
 
 /* MN protocol = every id with 'modulation' (signalduino/parser/mn.py:80) */

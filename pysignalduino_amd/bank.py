@@ -28,7 +28,7 @@ from . import regex_dfa
 DEFAULT_BANK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sd_bank.json")
 
 MAXSEARCH, MAXUNIQ = 16, 4
-MAGIC, VERSION = 0x4B4E4253, 16
+MAGIC, VERSION = 0x4B4E4253, 17
 INT_NONE = 2147483647  # "no length_max" sentinel
 
 PATSPEC = np.dtype([("klo", "<i4", (MAXUNIQ,)), ("khi", "<i4", (MAXUNIQ,)), ("rk_off", "<u4", (MAXUNIQ,)),
@@ -47,7 +47,7 @@ MS_REC = np.dtype([("pclock", "<f8"), ("key", PATSPEC, (4,)), ("proto_index", "<
 MC_REC = np.dtype([("cr_lo", "<f8"), ("cr_hi", "<f8"), ("proto_index", "<i4"), ("method", "<i4"), ("lmin", "<i4"),
                    ("lmax", "<i4"), ("pre_off", "<i4"), ("pre_len", "<i4"), ("pid_num", "<i4"),
                    ("has_lmin", "u1"), ("has_lmax", "u1"), ("lmax_is_str", "u1"), ("invert", "u1"),
-                   ("has_cr", "u1"), ("res", "u1", (3,))], align=True)
+                   ("has_cr", "u1"), ("lir_noexist", "u1"), ("res", "u1", (2,))], align=True)
 DFA_REC = np.dtype([("nstates", "<i4"), ("start", "<i4"), ("trans_off", "<i4"), ("flags_off", "<i4"),
                     ("t256_off", "<i4"), ("res", "<i4", (3,))])
 MN_REC = np.dtype([("proto_index", "<i4"), ("lir_min", "<i4"), ("lir_max", "<i4"), ("dfa", "<i4"), ("method", "<i4"),
@@ -164,6 +164,55 @@ def _int_exact(v, what) -> int:
     if isinstance(v, str) and not v.strip().lstrip("+-").isdigit():
         raise NotImplementedError(f"{what}: non-integer string {v!r}")
     return int(v)
+
+
+def mc_record(P: Dict[str, dict], pid, method: str, rec=None):
+    """The sdx_mc_proto of one (protocol id, MC method) pair, with the property lookups the
+    reference's methods make (manchester.py:207-795, helpers.py:90-166): ``P.get(pid, {})`` with
+    whatever object ``pid`` is (an int id finds no properties, as check_property does),
+    length_in_range's ``protocol_exists(str(pid))``, and ``int(pid)`` for the Funkbus id test.
+    Used for the bank's clockrange protocols and for the unit entry's per-call records."""
+    if rec is None:
+        rec = np.zeros((), MC_REC)
+    try:
+        p = P.get(pid, {})
+    except TypeError:
+        raise NotImplementedError(f"MC protocol id {pid!r}: unhashable") from None
+    if not isinstance(p, dict):
+        raise NotImplementedError(f"MC protocol id {pid!r}: properties are not a dict")
+    rec["method"] = MC_METHODS[method]
+    cr = p.get("clockrange")
+    if isinstance(cr, list) and len(cr) >= 2:
+        rec["has_cr"] = 1
+        rec["cr_lo"], rec["cr_hi"] = float(cr[0]), float(cr[1])
+    if "length_min" in p:
+        rec["has_lmin"] = 1
+        rec["lmin"] = _int32(_int_exact(p["length_min"], f"MC {pid} length_min"))
+    if "length_max" in p and p["length_max"] is not None:
+        rec["has_lmax"] = 1
+        rec["lmax"] = _int32(_int_exact(p["length_max"], f"MC {pid} length_max"))
+        rec["lmax_is_str"] = 1 if isinstance(p["length_max"], str) else 0
+    rec["invert"] = 1 if p.get("polarity", "") == "invert" else 0
+    rec["lir_noexist"] = 0 if str(pid) in P else 1
+    if isinstance(pid, str):
+        try:
+            rec["pid_num"] = _int32(int(pid))
+        except ValueError:
+            rec["pid_num"] = PID_NOT_INT
+    elif isinstance(pid, int) and not isinstance(pid, bool):
+        rec["pid_num"] = _int32(pid)
+    else:   # the Funkbus test compares the object itself with 119
+        rec["pid_num"] = 119 if pid == 119 else -1
+    return rec
+
+
+def _int32(v: int) -> int:
+    if not -(1 << 31) < v < (1 << 31):
+        raise NotImplementedError(f"value {v} outside int32")
+    return v
+
+
+PID_NOT_INT = -(1 << 31)   # SDX_PID_NOT_INT
 
 
 K_LIMIT = 1 << 28  # |k| bound of every interval (the device's k sentinel lies beyond it)
@@ -402,24 +451,10 @@ class Bank:
             cr = p["clockrange"]
             if not (isinstance(cr, list) and len(cr) >= 2):
                 raise NotImplementedError(f"MC {pid}: clockrange {cr!r}")
-            rec["has_cr"] = 1
-            rec["cr_lo"], rec["cr_hi"] = float(cr[0]), float(cr[1])
             meth = str(p.get("method", "")).split(".")[-1]
             if meth not in MC_METHODS:
                 raise NotImplementedError(f"MC {pid}: method {meth!r} not on the device")
-            rec["method"] = MC_METHODS[meth]
-            if "length_min" in p:
-                rec["has_lmin"] = 1
-                rec["lmin"] = _int_exact(p["length_min"], f"MC {pid} length_min")
-            if "length_max" in p and p["length_max"] is not None:
-                rec["has_lmax"] = 1
-                rec["lmax"] = _int_exact(p["length_max"], f"MC {pid} length_max")
-                rec["lmax_is_str"] = 1 if isinstance(p["length_max"], str) else 0
-            rec["invert"] = 1 if p.get("polarity", "") == "invert" else 0
-            try:
-                rec["pid_num"] = int(pid)
-            except ValueError:
-                rec["pid_num"] = -1
+            mc_record(P, pid, meth, rec)
             pre = f"{p.get('preamble', '')}"
             self.mc_preamble.append(pre)
             rec["pre_off"], rec["pre_len"] = self._str(pre)

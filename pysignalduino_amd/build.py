@@ -10,7 +10,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", "sdx_kernels.hip"),   # demodulation kernels + bank + C-ABI
         os.path.join(HERE, "csrc", "sdx_lines.hip"),     # wire-line front end (sdx_parse_lines/select)
         os.path.join(HERE, "csrc", "sdx_mn.hip"),        # MN (FSK) engine (sdx_demod_mn)
-        os.path.join(HERE, "csrc", "sdx_json.hip")]      # publish-ready JSON (sdx_serialize_json)
+        os.path.join(HERE, "csrc", "sdx_json.hip"),      # publish-ready JSON (sdx_serialize_json)
+        os.path.join(HERE, "csrc", "sdx_units.hip")]     # unit-level helpers (sdx_units)
 OUT = os.path.join(HERE, "_lib", "libsdx.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
@@ -19,11 +20,24 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     deps = [*SRCS, os.path.join(HERE, "csrc", "sdx_device.h"), os.path.join(HERE, "csrc", "sdx_lane.h"),
+            os.path.join(HERE, "csrc", "sdx_mc.h"),
             os.path.join(os.path.dirname(HERE), "include", "sdx.h"),
             os.path.join(os.path.dirname(HERE), "include", "sdx_bank.h")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = [HIPCC, *FLAGS, *SRCS, "-o", OUT + ".tmp"]
+    # one object per translation unit, compiled in parallel, then one link
+    objdir = os.path.join(os.path.dirname(OUT), "obj")
+    os.makedirs(objdir, exist_ok=True)
+    objs = [os.path.join(objdir, os.path.basename(src) + ".o") for src in SRCS]
+    cmds = [[HIPCC, *FLAGS[:-1], "-c", src, "-o", obj] for src, obj in zip(SRCS, objs)]
+    if verbose:
+        for c in cmds:
+            print(" ".join(c))
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as ex:
+        for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
+            f.result()
+    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", *objs, "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -17,6 +17,7 @@
 // MC engine (k_mc): lane = frame, the 12 clockrange protocols are a uniform loop.
 #include "sdx_device.h"
 #include "sdx_lane.h"
+#include "sdx_mc.h"
 
 #include <atomic>
 #include <cstdio>
@@ -1897,49 +1898,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
 // =============================================================================================
 // MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
 // =============================================================================================
-constexpr int MC_MAXW = 8;   // <= 512 bits = 128 hex characters per frame (device contract)
-constexpr int MC_SHORTW = 4; // k_mc<4>: frames of <= 64 hex characters (the long variant takes the rest)
 constexpr int MC_REC_CAP = 152, MC_HEAP_CAP = 3584;  // per wave: k_mc<4> fits 4 workgroups per CU
-
-// a frame's bit string, word w at base[w * 256] (words beyond nw read as 0).  dm: the Funkbus
-// mc2dmc(lh/hl) view of the same words, bit k = (b[k] == b[k+1]) -- derived on the fly
-struct LaneBits {
-  const uint64_t* base;
-  int nw;
-  bool dm;
-  SDX_DEV uint64_t raw(int w) const { return w < nw ? base[w * 256] : 0ull; }
-  SDX_DEV uint64_t word(int w) const {
-    const uint64_t x = raw(w);
-    return dm ? (w < nw ? ~(x ^ ((x << 1) | (raw(w + 1) >> 63))) : 0ull) : x;
-  }
-  SDX_DEV int get(int i) const { return (int)((word(i >> 6) >> (63 - (i & 63))) & 1ull); }
-  // P <= 32 bits starting at i (MSB-first), zero beyond the array
-  SDX_DEV uint32_t win(int i, int P) const {
-    const int w = i >> 6, o = i & 63;
-    uint64_t hi = word(w) << o;
-    if (o) hi |= word(w + 1) >> (64 - o);
-    return (uint32_t)(hi >> (64 - P));
-  }
-  // first i >= from with bits [i, i+P) == pat and i + P <= n (P <= 32): 64 start positions per
-  // step, matched bit-parallel on two words (two LDS reads per 64 positions, not per position)
-  SDX_DEV int find(uint32_t pat, int P, int from, int n) const {
-    if (from < 0) from = 0;
-    for (int w = from >> 6; 64 * w + P <= n; ++w) {
-      const uint64_t a = word(w), b = word(w + 1);
-      uint64_t m = ~0ull;  // bit 63 - j: start 64w + j still matches
-      for (int t = 0; t < P; ++t) {
-        const uint64_t xt = t ? ((a << t) | (b >> (64 - t))) : a;  // bit 63 - j = string bit 64w + j + t
-        m &= ((pat >> (P - 1 - t)) & 1u) ? xt : ~xt;
-      }
-      const int lo = from - 64 * w;  // j >= lo
-      if (lo > 0) m &= ~0ull >> lo;
-      const int hi = n - P - 64 * w;  // j <= hi
-      if (hi < 63) m &= ~0ull << (63 - hi);
-      if (m) return 64 * w + __clzll((long long)m);
-    }
-    return -1;
-  }
-};
 
 template <int MW>
 struct McLds {
@@ -1949,257 +1908,6 @@ struct McLds {
   alignas(16) uint8_t heap[4][MC_HEAP_CAP];
   int nrec[4], nheap[4], ovf[4];
 };
-
-// bin_str_2_hex_str of bits [a, e) of LaneBits -> dst; returns the length
-SDX_DEV int lane_hex(const LaneBits& B, int a, int e, uint8_t* dst) {
-  const int nb = e - a;
-  if (nb <= 0) return 0;
-  const int nd = (nb + 3) >> 2;
-  for (int d = 0; d < nd; ++d) {
-    const int de = e - 4 * (nd - 1 - d), da = (de - 4 > a) ? de - 4 : a;
-    const int v = (int)B.win(da, de - da);  // int(bits[da:de], 2)
-    if (dst) dst[d] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
-  }
-  return nd;
-}
-
-SDX_DEV bool hex_equal(const LaneBits& B, int a1, int e1, int a2, int e2) {
-  if (((e1 - a1 + 3) >> 2) != ((e2 - a2 + 3) >> 2)) return false;
-  const int m = (e1 - a1 > e2 - a2) ? e1 - a1 : e2 - a2;
-  // right-aligned, 32 bits per step; bits left of a1 / a2 count as 0
-  for (int t = 0; t < m; t += 32) {
-    const int k = m - t < 32 ? m - t : 32;
-    const int s1 = e1 - t - k, s2 = e2 - t - k;
-    const int v1 = e1 - t - (s1 > a1 ? s1 : a1), v2 = e2 - t - (s2 > a2 ? s2 : a2);
-    const uint32_t x = v1 > 0 ? B.win(e1 - t - v1, v1) : 0u;
-    const uint32_t y = v2 > 0 ? B.win(e2 - t - v2, v2) : 0u;
-    if (x != y) return false;
-  }
-  return true;
-}
-
-// length_in_range (helpers.py:124-166) for a clockrange protocol
-SDX_DEV bool mc_lir(const sdx_mc_proto* r, int n) {
-  const int lo = cld(&r->has_lmin) ? cld(&r->lmin) : -1;
-  if (lo != -1 && n < lo) return false;
-  if (cld(&r->has_lmax) && n > cld(&r->lmax)) return false;
-  return true;
-}
-
-// TFA message iterator (manchester.py:615-719): yields windows [pos, end)
-struct TfaIter {
-  int pos, end, n, loops;
-  bool first_done;
-  SDX_DEV bool next(const LaneBits& B, int* a, int* e) {
-    if (!(end < n)) return false;
-    int me = B.find(0x1FFDu /*1111111111101*/, 13, pos, n);
-    if (me < pos) me = n;
-    *a = pos;
-    *e = me;
-    end = me;
-    const int nx = B.find(0xDu /*1101*/, 4, me, n);
-    if (nx != -1) pos = nx + 4;
-    else end = n;
-    ++loops;
-    return true;
-  }
-};
-
-// result of one (frame, protocol): rc and how to print it
-struct McOut {
-  int rc;        // 1 ok, 0 no result, -1 raise TypeError, -2 raise ValueError
-  int kind;      // 0 hex window, 1 funkbus bytes, 2 tfa list
-  int a, e;      // hex window
-  uint64_t fb;   // funkbus 6 bytes (big-endian)
-  int len;       // payload length without the preamble
-};
-
-SDX_DEV McOut mc_method(const sdx_mc_proto* r, const LaneBits& B, int n, const LaneBits& D) {
-  McOut o{0, 0, 0, 0, 0, 0};
-  switch (cld(&r->method)) {
-    case SDX_MC_FUNKBUS: {  // manchester.py:207-300
-      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : -1;
-      if (n < lmin) return o;
-      if (cld(&r->has_lmax) && n > cld(&r->lmax)) return o;
-      const int dn = n > 0 ? n - 1 : 0;  // mc2dmc of the lh/hl expansion
-      int base, slen;
-      if (cld(&r->pid_num) == 119) {
-        const int pos = D.find(0xCu /*01100*/, 5, 0, dn);
-        if (!(pos >= 0 && pos < 5)) return o;
-        base = pos;
-        slen = 3 + dn - pos;
-        if (slen < 48) return o;
-      } else {
-        base = 0;
-        slen = 1 + dn;
-      }
-      const uint32_t pre = (cld(&r->pid_num) == 119) ? 1u /*001*/ : 0u;
-      const int plen = (cld(&r->pid_num) == 119) ? 3 : 1;
-      auto sbit = [&](int t) -> int { return t < plen ? (int)((pre >> (plen - 1 - t)) & 1) : D.get(base + t - plen); };
-      uint64_t bytes = 0;
-      int xr = 0, chk = 0, par = 0;
-      for (int i = 0; i < 6; ++i) {
-        const int a = 8 * i, e = (8 * i + 8 < slen) ? 8 * i + 8 : slen;
-        if (e <= a) { o.rc = -2; return o; }  // int('', 2)
-        int d = 0;
-        for (int t = a; t < e; ++t) d = (d << 1) | sbit(t);
-        bytes = (bytes << 8) | (uint64_t)d;
-        if (i < 5) xr ^= d;
-        else {
-          chk = d & 0x0F;
-          xr ^= d & 0xE0;
-          d &= 0xF0;
-        }
-        par ^= __popc(d) & 1;
-      }
-      if (par == 1) return o;
-      const int nib = ((xr & 0xF0) >> 4) ^ (xr & 0x0F);
-      int res = 0;
-      if (nib & 8) res ^= 0xC;
-      if (nib & 4) res ^= 0x2;
-      if (nib & 2) res ^= 0x8;
-      if (nib & 1) res ^= 0x3;
-      if (res != chk) return o;
-      o.rc = 1; o.kind = 1; o.fb = bytes; o.len = 12;
-      return o;
-    }
-    case SDX_MC_SAINLOGIC: {  // manchester.py:302-354
-      const int lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 0;
-      if (n > lmax) return o;
-      int pad = 0, m = n;
-      if (n < 128) {
-        const int st = B.find(0x14u /*010100*/, 6, 0, n);
-        if (st < 0 || st > 10) return o;
-        pad = st < 10 ? 10 - st : 0;
-        m = (n + pad < 128) ? n + pad : 128;
-      }
-      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : 0;
-      if (m < lmin) return o;
-      // bits = '1'*pad + B[0 : m-pad]; encode as window with a virtual prefix
-      o.rc = 1; o.kind = 3; o.a = pad; o.e = m; o.len = (m + 3) >> 2;
-      return o;
-    }
-    case SDX_MC_AS: {  // manchester.py:356-416
-      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : -1, lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 9999;
-      const int st = B.find(0xCu /*1100*/, 4, 16, n);
-      if (st >= 0) {
-        int en = B.find(0xCu, 4, st + 16, n);
-        if (en == -1) en = n;
-        const int ml = en - st;
-        if (ml < lmin || ml > lmax) return o;
-        o.rc = 1; o.a = st; o.e = n; o.len = (n - st + 3) >> 2;
-        return o;
-      }
-      if (n < lmin || n > lmax) return o;
-      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
-      return o;
-    }
-    case SDX_MC_PLAIN: {  // manchester.py:418-586
-      const int lmin = cld(&r->has_lmin) ? cld(&r->lmin) : -1, lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 9999;
-      if (n < lmin || n > lmax) return o;
-      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
-      return o;
-    }
-    case SDX_MC_RAW: {  // manchester.py:588-613
-      const int lmax = cld(&r->has_lmax) ? cld(&r->lmax) : 0;
-      if (n > lmax) return o;
-      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
-      return o;
-    }
-    case SDX_MC_HMCRAW: {  // helpers.py:90-122: un-converted str length_max -> int > str TypeError
-      if (cld(&r->has_lmax)) {
-        if (cld(&r->lmax_is_str)) { o.rc = -1; return o; }
-        if (n > cld(&r->lmax)) return o;
-      }
-      o.rc = 1; o.a = 0; o.e = n; o.len = (n + 3) >> 2;
-      return o;
-    }
-    case SDX_MC_TFA: {  // manchester.py:615-719
-      const int p0 = B.find(0xFFDu /*111111111101*/, 12, 0, n);
-      if (p0 == -1) return o;
-      TfaIter it{p0 + 12, -1, n, 1, false};
-      int a, e, ndup = 0, len = 2;
-      // messages = accepted windows; a duplicate is emitted when exactly one equal one precedes it
-      TfaIter outer = it;
-      int j = 0;
-      while (outer.next(B, &a, &e)) {
-        if (mc_lir(r, e - a)) {
-          int eq = 0;
-          TfaIter inner = it;
-          int a2, e2, k = 0;
-          while (k < j && inner.next(B, &a2, &e2)) {
-            if (mc_lir(r, e2 - a2) && hex_equal(B, a, e, a2, e2)) ++eq;
-            ++k;
-          }
-          if (eq == 1) {
-            len += (ndup ? 2 : 0) + 2 + ((e - a + 3) >> 2);
-            ++ndup;
-          }
-        }
-        ++j;
-      }
-      if (outer.loops == 10) return o;  // 'loop error'
-      if (ndup == 0) return o;
-      o.rc = 1; o.kind = 2; o.len = len; o.a = p0 + 12;
-      return o;
-    }
-    case SDX_MC_GROTHE: {  // manchester.py:721-754
-      if (n != 32) return o;
-      o.rc = 1; o.a = 0; o.e = n; o.len = 8;
-      return o;
-    }
-    case SDX_MC_SOMFY: {  // manchester.py:756-795
-      int a = 0, e = n;
-      if (n == 57) { a = 1; e = 57; }
-      if (e - a != 56) return o;
-      o.rc = 1; o.a = a; o.e = e; o.len = 14;
-      return o;
-    }
-  }
-  return o;
-}
-
-SDX_DEV void mc_write(const sdx_mc_proto* r, const McOut& o, const LaneBits& B, int n, uint8_t* dst) {
-  if (o.kind == 0) {
-    lane_hex(B, o.a, o.e, dst);
-  } else if (o.kind == 1) {
-    for (int i = 0; i < 12; ++i) {
-      const int v = (int)((o.fb >> (4 * (11 - i))) & 15);
-      dst[i] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
-    }
-  } else if (o.kind == 3) {  // Sainlogic: '1'*pad + bits, truncated to e (<=128) characters
-    const int pad = o.a, m = o.e, nd = (m + 3) >> 2;
-    for (int d = 0; d < nd; ++d) {
-      const int de = m - 4 * (nd - 1 - d), da = (de - 4 > 0) ? de - 4 : 0;
-      int v = 0;
-      for (int i = da; i < de; ++i) v = (v << 1) | (i < pad ? 1 : B.get(i - pad));
-      dst[d] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
-    }
-  } else {  // TFA: Python list repr "['A', 'B']"
-    TfaIter it{o.a, -1, n, 1, false}, outer = it;
-    int a, e, j = 0, q = 0, nd = 0;
-    dst[q++] = '[';
-    while (outer.next(B, &a, &e)) {
-      if (mc_lir(r, e - a)) {
-        int eq = 0, a2, e2, k = 0;
-        TfaIter inner = it;
-        while (k < j && inner.next(B, &a2, &e2)) {
-          if (mc_lir(r, e2 - a2) && hex_equal(B, a, e, a2, e2)) ++eq;
-          ++k;
-        }
-        if (eq == 1) {
-          if (nd) { dst[q++] = ','; dst[q++] = ' '; }
-          dst[q++] = '\'';
-          q += lane_hex(B, a, e, dst + q);
-          dst[q++] = '\'';
-          ++nd;
-        }
-      }
-      ++j;
-    }
-    dst[q++] = ']';
-  }
-}
 
 SDX_DEV int hexval(uint8_t c) {
   if (c >= '0' && c <= '9') return c - '0';
@@ -2350,14 +2058,14 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     if (go && mcbit < (cld(&r->has_lmin) ? cld(&r->lmin) : -1)) go = false;
     if (go && mcbit > (cld(&r->has_lmax) ? cld(&r->lmax) : 9999)) go = false;
     if (go && cld(&r->has_cr) && !((double)clock > cld(&r->cr_lo) && (double)clock < cld(&r->cr_hi))) go = false;
-    McOut o{0, 0, 0, 0, 0, 0};
+    McOut o{0, 0, 0, 0, 0, 0, 0, 0};
     const bool inv = (cld(&r->invert) != 0) ^ ((flags & 3) != 0);  // (:91-96)
     const LaneBits& B = inv ? BI : BN;
     const int nb = inv ? nI : nN;
     if (go && !hex_ok) { raise = SDX_RAISE_TYPE; go = false; }  // len(None) -> TypeError
     if (go) {
       const LaneBits DM{B.base, MW, true};  // mc2dmc(lh/hl) view for Funkbus
-      o = mc_method(r, B, nb, DM);
+      o = mc_method(r, cld(&r->method), B, nb, nb, DM);
       if (o.rc == -1) { raise = SDX_RAISE_TYPE; o.rc = 0; }
       if (o.rc == -2) { raise = SDX_RAISE_VALUE; o.rc = 0; }
     }
@@ -2386,7 +2094,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
         for (int j = 0; j < 8; ++j)
           if (i + j < pl) dst[i + j] = c[j];
       }
-      mc_write(r, o, B, nb, dst + cld(&r->pre_len));
+      mc_write(r, o, B, nb, nb, dst + cld(&r->pre_len));
       StageRec sr;
       sr.off = (uint32_t)(hb + incl - plen);
       sr.len = (uint16_t)plen;

@@ -35,7 +35,7 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
-            "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json"]
+            "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units"]
 
 
 class SdxPulseBatch(Structure):
@@ -65,6 +65,11 @@ class SdxJsonIn(Structure):
 class SdxJsonOut(Structure):
     _fields_ = [("json_dev", c_void_p), ("off_dev", c_void_p), ("len_dev", c_void_p), ("cursor_dev", c_void_p),
                 ("json_cap", c_uint32), ("res", c_uint32)]
+
+
+class SdxUnitBatch(Structure):
+    _fields_ = [("op", c_int32), ("n", c_int32), ("in_dev", c_void_p), ("in_off_dev", c_void_p), ("arg_dev", c_void_p),
+                ("val_dev", c_void_p), ("val_off_dev", c_void_p), ("mcrec_dev", c_void_p), ("out_off_dev", c_void_p)]
 
 
 class SdxOut(Structure):
@@ -128,7 +133,9 @@ def load_library(path: Optional[str] = None):
     lib.sdx_parse_lines.restype = c_int
     lib.sdx_select_lines.argtypes = [POINTER(SdxLinesOut), c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.sdx_select_lines.restype = c_int
-    if lib.sdx_abi_version() != 3:
+    lib.sdx_units.argtypes = [POINTER(SdxUnitBatch), POINTER(SdxOut), c_void_p]
+    lib.sdx_units.restype = c_int
+    if lib.sdx_abi_version() != 4:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -383,4 +390,79 @@ class Engine:
         nheap = min(int(cur[1]), out["heap_cap"])
         rec = out["rec"][: nrec * RES_DT.itemsize].cpu().numpy().view(RES_DT).copy()
         heap = out["heap"][:nheap].cpu().numpy().copy()
+        return desc, rec, heap
+
+
+# ---- unit-level entry (sdx_units) ----------------------------------------------------------------
+UNIT_POSTDEMO, UNIT_HEX2BIN, UNIT_BIN2HEX, UNIT_MC2DMC, UNIT_PEXISTS, UNIT_MC_METHOD = 1, 2, 3, 4, 5, 6
+UNIT_MC_BITS, UNIT_PX_SEARCH, UNIT_PX_PAT = 512, 32, 16
+
+_UNIT_RUNNERS: Dict[int, "UnitRunner"] = {}
+
+
+class UnitRunner:
+    """sdx_units launches on one device (no bank needed: every input travels with the call)."""
+
+    def __init__(self, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("pysignalduino_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
+        self.torch = torch
+        self.lib = load_library()
+        self.dev = torch.device("cuda", device)
+
+    @staticmethod
+    def get(device: int = 0) -> "UnitRunner":
+        r = _UNIT_RUNNERS.get(device)
+        if r is None:
+            r = _UNIT_RUNNERS[device] = UnitRunner(device)
+        return r
+
+    def run(self, op: int, ins, caps, args=None, vals=None, mcrecs=None):
+        """Run one op over the byte strings ``ins`` (``caps[i]``: payload capacity of item i).
+        ``vals``: per-item float64 arrays (UNIT_PEXISTS); ``mcrecs``: numpy MC_REC array (UNIT_MC_METHOD).
+        Returns (desc, rec, heap) as host numpy arrays, one desc/rec per item."""
+        t, d = self.torch, self.dev
+        n = len(ins)
+        if n == 0:
+            return np.zeros(0, DESC_DT), np.zeros(0, RES_DT), np.zeros(0, np.uint8)
+        lens = np.fromiter((len(b) for b in ins), np.int64, n)
+        in_off = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=in_off[1:])
+        data = np.frombuffer(b"".join(ins) + b"\0" * 8, np.uint8)
+        out_off = np.zeros(n + 1, np.int64)
+        np.cumsum(np.asarray(caps, np.int64), out=out_off[1:])
+        keep = []
+
+        def dev(a):
+            a = np.ascontiguousarray(a)
+            if not a.flags.writeable:
+                a = a.copy()
+            x = t.from_numpy(a).to(d)
+            keep.append(x)
+            return _ptr(x)
+
+        val_p = val_off_p = mc_p = None
+        if vals is not None:
+            vl = np.fromiter((len(v) for v in vals), np.int64, n)
+            val_off = np.zeros(n + 1, np.int64)
+            np.cumsum(vl, out=val_off[1:])
+            flat = np.concatenate([np.asarray(v, np.float64) for v in vals] + [np.zeros(1)])
+            val_p, val_off_p = dev(flat), dev(val_off)
+        if mcrecs is not None:
+            mc_p = dev(np.frombuffer(np.ascontiguousarray(mcrecs).tobytes(), np.uint8))
+        heap_cap = int(out_off[-1])
+        out = {"desc": t.zeros(n * DESC_DT.itemsize, dtype=t.uint8, device=d),
+               "rec": t.zeros(n * RES_DT.itemsize, dtype=t.uint8, device=d),
+               "heap": t.zeros(max(heap_cap, 1), dtype=t.uint8, device=d),
+               "cursor": t.zeros(4, dtype=t.int32, device=d)}
+        b = SdxUnitBatch(op, n, dev(data), dev(in_off), None if args is None else dev(np.asarray(args, np.int32)),
+                         val_p, val_off_p, mc_p, dev(out_off))
+        o = SdxOut(_ptr(out["desc"]), _ptr(out["rec"]), _ptr(out["heap"]), _ptr(out["cursor"]), n, max(heap_cap, 1))
+        _check(self.lib, self.lib.sdx_units(ctypes.byref(b), ctypes.byref(o),
+                                            c_void_p(t.cuda.current_stream(d).cuda_stream)))
+        t.cuda.current_stream(d).synchronize()
+        desc = out["desc"].cpu().numpy().view(DESC_DT).copy()
+        rec = out["rec"].cpu().numpy().view(RES_DT).copy()
+        heap = out["heap"].cpu().numpy()
         return desc, rec, heap

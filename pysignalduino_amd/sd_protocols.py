@@ -34,6 +34,7 @@ import numpy as np
 from . import bank as bankmod
 from . import packing
 from . import runtime
+from .units import UnitsMixin
 
 _SENTINEL = object()
 _HEX_RE = re.compile(r"[0-9a-fA-F]*")
@@ -81,7 +82,7 @@ class _Observed(dict):
         self._bump()
 
 
-class SDProtocols:
+class SDProtocols(UnitsMixin):
     """GPU-backed drop-in for ``sd_protocols.SDProtocols`` (demodulation path)."""
 
     def __init__(self, protocols_path: Optional[str] = None, device: int = 0, mc_mode: str = "strict"):
@@ -382,8 +383,11 @@ class SDProtocols:
 
         mc_mode='strict' (default): exactly the reference's observable behaviour.  Without a
         ``protocol_id`` (how MCParser calls it, parser/mc.py:78) the result is [].  With one, the
-        reference's gates run (manchester.py:70-89) and every MC protocol then raises TypeError
-        (``int > list`` at :83-84) -- nothing is ever decoded, so no device work is involved.
+        reference's gates run with the same Python operations (manchester.py:70-120): [] when a
+        length gate fails, TypeError for every clockrange protocol (``int > list`` at :83-84) and
+        for every method call (one positional argument too many at :120; mcRaw's shifted
+        arguments run on the device), ValueError for a protocol without a method (a one-element
+        list unpacked into three names, sd_protocols.py:94).
         mc_mode='fixed': the intended chain (clockrange[0] < C < clockrange[1], method called
         without the extra ``self``) on the GPU for every clockrange protocol (or the given id).
         """
@@ -393,22 +397,12 @@ class SDProtocols:
         if not protocol_id or not self.protocol_exists(protocol_id):
             self._logging(f"MC Demodulation failed: Protocol ID {protocol_id} not found or missing.", 3)
             return []
-        clock = msg_data.get("clock", 0)
-        mcbitnum = msg_data.get("bit_length", 0)
-        # manchester.py:70-89, evaluated with the same Python operations (same exceptions)
-        length_min = int(self.check_property(protocol_id, "length_min", -1))
-        if mcbitnum < length_min:
-            return []
-        length_max = int(self.check_property(protocol_id, "length_max", 9999))
-        if mcbitnum > length_max:
-            return []
-        clockrange = self.get_property(protocol_id, "clockrange")
-        if clockrange and len(clockrange) >= 2:
-            clock_min, clock_max = clockrange, clockrange
-            if not (clock > clock_min and clock < clock_max):
-                return []
-        raise NotImplementedError("strict-mode MC for a protocol without clockrange (reference reaches its "
-                                  "method-call bug); use mc_mode='fixed'")
+        rcode, dmsg, metadata = self._mc_data_strict(
+            f"Protocol {protocol_id}", protocol_id, msg_data.get("clock", 0), msg_data.get("data", ""),
+            msg_data.get("bit_length", 0), msg_type, version)
+        if rcode == 1:
+            return [{"protocol_id": str(protocol_id), "payload": dmsg, "meta": metadata}]
+        return []
 
     def demodulate_mc_batch(self, messages: Sequence[Dict[str, Any]], msg_type: str = "MC",
                             version: Optional[str] = None, raise_errors: bool = False):

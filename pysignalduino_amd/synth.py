@@ -588,3 +588,281 @@ def mn_payload(h: str, y: bool = False, r: Optional[int] = None, a: Optional[int
     if a is not None:
         s += "A=%d;" % a
     return s.encode("ascii")
+
+
+# ---------------------------------------------------------------------------------------------
+# Planted accept paths: bit vectors that each postDemodulation function accepts
+# (sd_protocols/postdemodulation.py:27-730), MU/MS messages of the bank's postDemo users carrying
+# them, and MC frames that the TFA / Grothe / Funkbus / ... methods accept
+# (manchester.py:207-795).  Generator-side helpers only: they construct inputs whose checksums,
+# parities and lengths are valid, so the parity tests reach the accept branches.
+# ---------------------------------------------------------------------------------------------
+def _byte_bits(v: int, n: int = 8) -> List[int]:
+    return [(v >> (n - 1 - i)) & 1 for i in range(n)]
+
+
+def _par9(v: int) -> List[int]:
+    b = _byte_bits(v)
+    return b + [sum(b) & 1]            # even parity over the 9-bit group
+
+
+def postdemo_bits(rng: np.random.Generator, method: str, lead: Optional[int] = None) -> List[int]:
+    """One bit list that ``method`` accepts.  ``lead``: leading zeros before the data start (the
+    functions that look for the first '1' or for a preamble), drawn when None."""
+    ri = lambda lo, hi: int(rng.integers(lo, hi + 1))  # noqa: E731
+    rb = lambda k: [int(x) for x in rng.integers(0, 2, size=k)]  # noqa: E731
+    z = ri(0, 6) if lead is None else lead
+    if method == "postDemo_EM":                      # :27-88 preamble 0000000001 + 9 x (8 + 1) + xor
+        out = [0] * (z + 9) + [1]
+        crc = 0
+        for _ in range(9):
+            v = ri(0, 255)
+            crc ^= v
+            out += _byte_bits(v) + [1]
+        return out + _byte_bits(crc)
+    if method == "postDemo_Revolt":                  # :90-137 11 bytes + their sum
+        data = [ri(0, 255) for _ in range(11)]
+        out = []
+        for v in data:
+            out += _byte_bits(v)
+        return out + _byte_bits(sum(data) & 0xFF) + rb(ri(0, 20))
+    if method in ("postDemo_FS20", "postDemo_FHT80", "postDemo_FHT80TF"):   # :139-423
+        if method == "postDemo_FS20":
+            nd, base = (4 if rng.random() < 0.5 else 5), 6
+        elif method == "postDemo_FHT80":
+            nd, base = 5, 12
+        else:
+            nd, base = 4, 12
+        data = [ri(0, 255) for _ in range(nd)]
+        if method == "postDemo_FHT80TF":
+            data[3] &= ~0x20 & 0xFF                  # bit 26 of the 40 data bits must be 0
+        out = [0] * z + [1]
+        for v in data:
+            out += _par9(v)
+        out += _par9((base + sum(data)) & 0xFF)
+        if method != "postDemo_FHT80TF" and rng.random() < 0.3:
+            out.append(ri(0, 1))                     # 46 / 55: the last bit is popped
+        return out
+    if method == "postDemo_WS2000":                  # :425-578 5-bit groups '1' + nibble (LSB first)
+        typ = ri(0, 7)
+        k = [35, 50, 35, 50, 70, 40, 40, 85][typ] // 5
+        z = min(z, 9)
+        if typ == 1 and rng.random() < 0.3:          # the 45/46-bit Thermo/Hygro form: XOR of all 9
+            nib = [typ] + [ri(0, 15) for _ in range(7)]
+            x = 0
+            for v in nib:
+                x ^= v
+            nib.append(x)
+        else:
+            nib = [typ] + [ri(0, 15) for _ in range(k - 3)]
+            x = 0
+            for v in nib:
+                x ^= v
+            nib.append(x)                            # XOR over the first k-1 nibbles = 0
+            nib.append((5 + sum(nib)) & 0x0F)        # the sum nibble
+        out = [0] * z
+        for v in nib:
+            out += [1] + [(v >> i) & 1 for i in range(4)]
+        if rng.random() < 0.3:
+            out.append(ri(0, 1))
+        return out
+    if method == "postDemo_WS7035":                  # :580-640 ident, parity 15..27, nibble sum
+        b = [1, 0, 1, 0, 0, 0, 0, 0] + rb(32)
+        if sum(b[15:28]) & 1:
+            b[20] ^= 1
+        s = sum(int("".join(map(str, b[i:i + 4])), 2) for i in range(0, 40, 4))
+        return b + _byte_bits(s % 16, 4)
+    if method == "postDemo_WS7053":                  # :642-706 ident anywhere, parity 15..27
+        pre = [0] * min(z, 2)
+        b = [1, 0, 1, 0, 0, 0, 0, 0] + rb(ri(24, 26))
+        full = pre + b
+        msg = full[len(pre):] + ([0] if pre else [])
+        if sum(msg[15:28]) & 1:
+            b[20] ^= 1
+        return pre + b
+    if method == "postDemo_lengtnPrefix":            # :708-730
+        return rb(ri(0, 60))
+    raise KeyError(method)
+
+
+POSTDEMO_USERS = {"80": "postDemo_EM", "45": "postDemo_Revolt", "74": "postDemo_FS20", "74.1": "postDemo_FS20",
+                  "73": "postDemo_FHT80", "70": "postDemo_FHT80TF", "60": "postDemo_WS2000",
+                  "66": "postDemo_WS7035", "67": "postDemo_WS7053", "39": "postDemo_lengtnPrefix"}
+
+
+def _lead_for(pid: str, method: str, rng) -> int:
+    """Leading zeros that put a planted frame inside the protocol's length_min..length_max."""
+    want = {"80": (5, 15), "74": (4, 12), "74.1": (4, 12), "73": (4, 12), "70": (4, 11), "60": (3, 9)}
+    lo, hi = want.get(pid, (0, 0))
+    return int(rng.integers(lo, hi + 1))
+
+
+def _planted_bits(rng, pid: str, P: Dict[str, dict]) -> List[int]:
+    method = POSTDEMO_USERS[pid]
+    p = P[pid]
+    lmin, lmax = int(p.get("length_min", 0)), int(p.get("length_max", 999))
+    for _ in range(200):
+        b = postdemo_bits(rng, method, _lead_for(pid, method, rng))
+        if method == "postDemo_WS2000" and len(b) > lmax:
+            continue
+        if method == "postDemo_lengtnPrefix":
+            b = [int(x) for x in rng.integers(0, 2, size=int(rng.integers(lmin, lmax + 1)))]
+        if method == "postDemo_Revolt":
+            b = b[:lmax]
+        if lmin <= len(b) <= lmax:
+            return b
+    return b
+
+
+def planted_pulse_messages(P: Dict[str, dict], kind: str, n: int, seed: int = 50,
+                           corrupt_frac: float = 0.25) -> List[Dict[str, str]]:
+    """n MU or MS messages of the postDemo users (ids 80, 45, 74, 74.1, 73,
+    70, 60, 66, 67, 39) whose frames carry ``postdemo_bits`` payloads, some with one bit flipped.
+    MU: separator pulse + frame repeated (2-3 times, <= 256 pulses); MS: sync + one frame."""
+    rng = np.random.default_rng(seed)
+    pids = [pid for pid in POSTDEMO_USERS if ("sync" in P[pid]) == (kind == "MS") and pid in P]
+    out = []
+    for _ in range(n):
+        pid = pids[int(rng.integers(0, len(pids)))]
+        p = P[pid]
+        bits = _planted_bits(rng, pid, P)
+        if rng.random() < corrupt_frac and bits:
+            j = int(rng.integers(0, len(bits)))
+            bits[j] ^= 1
+        head = [float(x) for x in (p.get("sync") if kind == "MS" else p.get("start") or [])]
+        one, zero = [float(x) for x in p["one"]], [float(x) for x in p["zero"]]
+        vals: List[float] = []
+        for v in head + one + zero:
+            if v not in vals:
+                vals.append(v)
+        sep = None
+        if kind == "MU" and not head:
+            sep = float(p["pause"][0]) if p.get("pause") else -100.0
+            if sep not in vals:
+                vals.append(sep)
+        frame = [vals.index(v) for v in head]
+        for b in bits:
+            frame += [vals.index(v) for v in (one if b else zero)]
+        if kind == "MU":
+            reps = int(rng.integers(2, 4))
+            unit = ([vals.index(sep)] if sep is not None else []) + frame
+            seq = (unit * reps)[:256]
+        else:
+            seq = frame + frame[: int(rng.integers(0, 6))]
+        clock = float(p["clockabs"]) * float(rng.uniform(0.97, 1.03))
+        ids = [int(x) for x in rng.permutation(10)[: len(vals)]]
+        pv = [int(round(v * clock * float(rng.uniform(0.97, 1.03)))) for v in vals]
+        d: Dict[str, str] = {kind: ""}
+        for slot in sorted(range(len(vals)), key=lambda s: ids[s]):
+            d["P%d" % ids[slot]] = str(pv[slot])
+        d["D"] = "".join(str(ids[s]) for s in seq)
+        if kind == "MS":
+            cp = min(range(len(vals)), key=lambda s: abs(abs(vals[s]) - 1.0))
+            sp = max(range(len(head)), key=lambda s: abs(head[s])) if head else 0
+            d["CP"] = str(ids[cp])
+            d["SP"] = str(ids[vals.index(head[sp])]) if head else str(ids[0])
+        else:
+            d["CP"] = str(ids[min(range(len(vals)), key=lambda s: abs(abs(vals[s]) - 1.0))])
+        if rng.random() < 0.9:
+            d["R"] = str(int(rng.integers(0, 256)))
+        d["data"] = d["D"]
+        out.append(d)
+    return out
+
+
+def _bits_to_hex(bits: List[int]) -> str:
+    s = "".join(map(str, bits))
+    s = "0" * (-len(s) % 4) + s
+    return "".join(_HEXD[int(s[i:i + 4], 2)] for i in range(0, len(s), 4))
+
+
+def _inv_hex(h: str) -> str:
+    return h.translate(str.maketrans("0123456789ABCDEF", "FEDCBA9876543210"))
+
+
+def mc_method_bits(rng: np.random.Generator, pid: str, P: Dict[str, dict]) -> List[int]:
+    """A bit string the MC method of protocol ``pid`` accepts (manchester.py:207-795)."""
+    ri = lambda lo, hi: int(rng.integers(lo, hi + 1))  # noqa: E731
+    rb = lambda k: [int(x) for x in rng.integers(0, 2, size=k)]  # noqa: E731
+    p = P[pid]
+    meth = p["method"].split(".")[-1]
+    lmin, lmax = int(p.get("length_min", 8)), int(p.get("length_max", 64))
+    if meth == "mcBit2Funkbus":                      # :207-300 mc2dmc + 6 bytes parity/checksum
+        data = [0x2C] + [ri(0, 255) for _ in range(4)]
+        b5 = ri(0, 7) << 5
+        xr = 0
+        for v in data:
+            xr ^= v
+        xr ^= b5
+        nib = ((xr & 0xF0) >> 4) ^ (xr & 0x0F)
+        chk = 0
+        if nib & 8:
+            chk ^= 0xC
+        if nib & 4:
+            chk ^= 0x2
+        if nib & 2:
+            chk ^= 0x8
+        if nib & 1:
+            chk ^= 0x3
+        par = sum(bin(v).count("1") for v in data) + bin(b5).count("1")
+        b5 |= (par & 1) << 4
+        s = []
+        for v in data + [b5 | chk]:
+            s += _byte_bits(v)
+        d = s[3:] + rb(ri(1, 4))                     # s = '001' + d: d starts with '01100'
+        bits = [1]                                   # b[k+1] == b[k] <=> d[k] == 1
+        for x in d:
+            bits.append(bits[-1] if x else 1 - bits[-1])
+        return bits
+    if meth == "mcBit2TFA":                          # :615-719 sync + repeated 52-bit windows
+        while True:
+            w = rb(lmin)
+            if "1111111111101" not in "".join(map(str, w)) and "1101" not in "".join(map(str, w[-3:] + [1])):
+                break
+        reps = ri(2, 4)
+        out = [1] * 10 + [0, 1] + w
+        for _ in range(reps - 1):
+            out += [1] * 11 + [0, 1] + w
+        return out + rb(ri(0, 6))
+    if meth == "mcBit2Grothe":                       # :721-754 exactly 32 bits
+        return [1] + rb(31)
+    if meth == "mcBit2SomfyRTS":                     # :756-795 56 or 57
+        return [1] + rb(55 if rng.random() < 0.5 else 56)
+    if meth == "mcBit2Sainlogic":                    # :302-354 sync 010100 at <= 10, 128 bits
+        st = ri(0, 10)
+        b = [1] + rb(st - 1) if st else []
+        b = (b + [0, 1, 0, 1, 0, 0] + rb(128))[: 128 - (10 - st)]
+        return b
+    if meth == "mcBit2AS":                           # :356-416 '1100' at >= 16
+        head = [1] + [0, 1] * 8
+        body = [1, 1, 0, 0] + [1, 0] * ((ri(lmin, lmax) - 4) // 2)
+        return head[:16] + body
+    n = ri(lmin, lmax)                               # length-gated hex methods, mcraw
+    return [1] + rb(n - 1)
+
+
+def mc_planted_frames(P: Dict[str, dict], n: int, seed: int = 51, corrupt_frac: float = 0.2):
+    """n MC frames (hex, clock, L, messagetype, version) that the fixed chain
+    decodes for the 12 clockrange ids: hex from ``mc_method_bits`` with the polarity the chain
+    will undo, L and clock inside the protocol's gates; some with one hex digit changed."""
+    rng = np.random.default_rng(seed)
+    mc_ids = [pid for pid, p in P.items() if "clockrange" in p]
+    out = []
+    for _ in range(n):
+        pid = mc_ids[int(rng.integers(0, len(mc_ids)))]
+        p = P[pid]
+        bits = mc_method_bits(rng, pid, P)
+        h = _bits_to_hex(bits)
+        mtype = "Mc" if rng.random() < 0.5 else "MC"
+        ver = "V 3.2.1" if rng.random() < 0.1 else None
+        inv = (p.get("polarity", "") == "invert") ^ (mtype == "Mc" or (ver is not None and ver[:6] == "V 3.2."))
+        if inv:
+            h = _inv_hex(h)
+        if rng.random() < corrupt_frac:
+            j = int(rng.integers(0, len(h)))
+            h = h[:j] + _HEXD[(int(h[j], 16) + int(rng.integers(1, 16))) % 16] + h[j + 1:]
+        lo, hi = p["clockrange"]
+        clock = int(rng.integers(int(lo) + 1, int(hi)))
+        L = int(rng.integers(int(p.get("length_min", 8)), int(p.get("length_max", 64)) + 1))
+        out.append((h, clock, L, mtype, ver))
+    return out

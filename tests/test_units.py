@@ -1,0 +1,330 @@
+"""Accept paths and the unit-level API (§8(b)).
+
+Expected outputs come from the reference itself (tests/golden/make_accept_golden.py and
+make_golden.py, run in the development container).  The CPU tests pin the oracle on the planted
+corpora; the GPU tests run the drop-in SDProtocols -- demodulate_batch, demodulate_mc(_batch), and
+the helper methods bound to sdx_units -- and compare bit-exact, including the exception classes
+and the (-1, text) failure tuples of the reference's methods."""
+import collections
+
+import numpy as np
+import pytest
+
+from oracle import sd_oracle as O
+
+POSTDEMO = ["postDemo_EM", "postDemo_Revolt", "postDemo_FS20", "postDemo_FHT80", "postDemo_FHT80TF",
+            "postDemo_WS2000", "postDemo_WS7035", "postDemo_WS7053", "postDemo_lengtnPrefix"]
+
+
+def _flat(res):
+    if isinstance(res, BaseException):
+        return {"raise": type(res).__name__}
+    return {"results": [[r["protocol_id"], r["payload"], r["meta"]["bit_length"], r["meta"]["rssi"],
+                         r["meta"]["clock"]] for r in res]}
+
+
+def _jsonish(v):
+    if isinstance(v, tuple):
+        return [_jsonish(x) for x in v]
+    if isinstance(v, list):
+        return [_jsonish(x) for x in v]
+    if isinstance(v, dict):
+        return {k: _jsonish(x) for k, x in v.items()}
+    return v
+
+
+def _outcome(r):
+    if isinstance(r, BaseException):
+        return ["raise", type(r).__name__]
+    return ["ok", _jsonish(r)]
+
+
+# ----------------------------------------------------------------------------------------- CPU
+@pytest.fixture(scope="module")
+def obank():
+    return O.OracleBank()
+
+
+def test_oracle_planted_mu_ms(obank, golden):
+    g = golden("accept_golden.json.gz")
+    for kind in ("MU", "MS"):
+        bad = []
+        for c in g[kind.lower()]:
+            try:
+                got = _flat(O.demod(obank, dict(c["msg"]), kind))
+            except Exception as e:
+                got = {"raise": type(e).__name__}
+            if got != c["exp"]:
+                bad.append((c["msg"], c["exp"], got))
+        assert not bad, f"{kind}: {len(bad)} mismatches, first {bad[:2]}"
+
+
+def test_oracle_planted_mc(obank, golden):
+    bad = []
+    for f in golden("accept_golden.json.gz")["mc"]:
+        try:
+            got = {"results": [[r["protocol_id"], r["payload"]] for r in
+                               O.demod_mc_fixed(obank, f["hex"], f["clock"], f["L"], f["mtype"], f["version"])]}
+        except Exception as e:
+            got = {"raise": type(e).__name__}
+        if got != f["fixed"]:
+            bad.append((f, got))
+    assert not bad, f"{len(bad)} mismatches, first {bad[:2]}"
+
+
+def test_oracle_planted_postdemo(golden):
+    bad = []
+    for meth, bits, kind, val in golden("accept_golden.json.gz")["postdemo"]:
+        try:
+            got = ["ok", _jsonish(O.POSTDEMO[meth](list(bits)))]
+        except Exception as e:
+            got = ["raise", type(e).__name__]
+        if got != [kind, val]:
+            bad.append((meth, bits, kind, val, got))
+    assert not bad, f"{len(bad)} mismatches, first {bad[:2]}"
+
+
+def test_planted_corpora_reach_every_accept_path(golden):
+    """The reference accepts >= 100 planted frames per postDemo function / MC method and per
+    postDemo user id (what the GPU tests below then compare)."""
+    g = golden("accept_golden.json.gz")
+    acc = collections.Counter(m for m, _, kind, val in g["postdemo"] if kind == "ok" and val[0] == 1)
+    assert all(acc[m] >= 100 for m in POSTDEMO), acc
+    accm = collections.Counter(m for m, *_, r in g["mc_methods"] if r[0] == "ok" and r[1][0] == 1)
+    assert all(accm[m] >= 100 for m in ["mcBit2Funkbus", "mcBit2Sainlogic", "mcBit2AS", "mcBit2Hideki",
+                                         "mcBit2Maverick", "mcBit2OSV1", "mcBit2OSV2o3", "mcBit2OSPIR",
+                                         "mcBit2TFA", "mcBit2Grothe", "mcBit2SomfyRTS", "mcRaw", "mcraw"]), accm
+    ids = collections.Counter(r[0] for c in g["mu"] + g["ms"] for r in c["exp"].get("results", []))
+    assert all(ids[p] >= 100 for p in ["80", "45", "74", "74.1", "73", "70", "60", "66", "67", "39"]), ids
+    mc = collections.Counter(r[0] for f in g["mc"] for r in f["fixed"].get("results", []))
+    assert all(mc[p] >= 100 for p in ["58", "96", "119", "10", "11", "12", "18", "43", "47", "129"]), mc
+
+
+# ----------------------------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def proto():
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    return SDProtocols()
+
+
+@pytest.mark.gpu
+def test_gpu_planted_mu_ms(proto, golden):
+    g = golden("accept_golden.json.gz")
+    for kind in ("MU", "MS"):
+        cases = g[kind.lower()]
+        got = proto.demodulate_batch([c["msg"] for c in cases], kind)
+        bad = [(c["msg"], c["exp"], _flat(x)) for c, x in zip(cases, got) if _flat(x) != c["exp"]]
+        assert not bad, f"{kind}: {len(bad)}/{len(cases)} mismatches; first {bad[:2]}"
+        acc = collections.Counter(r["protocol_id"] for x in got if not isinstance(x, BaseException) for r in x)
+        users = ["80", "45", "74", "74.1", "73", "70", "60", "66", "67", "39"] if kind == "MU" else ["74.1"]
+        assert all(acc[p] >= 100 for p in users), acc
+
+
+@pytest.mark.gpu
+def test_gpu_planted_mc_fixed(golden):
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    p = SDProtocols(mc_mode="fixed")
+    frames = golden("accept_golden.json.gz")["mc"]
+    msgs = [{"raw_hex": f["hex"], "clock": f["clock"], "mcbitnum": f["L"], "messagetype": f["mtype"],
+             "version": f["version"]} for f in frames]
+    got = p.demodulate_mc_batch(msgs)
+    bad = []
+    acc = collections.Counter()
+    for f, x in zip(frames, got):
+        gg = {"raise": type(x).__name__} if isinstance(x, BaseException) else \
+            {"results": [[r["protocol_id"], r["payload"]] for r in x]}
+        if gg != f["fixed"]:
+            bad.append((f, gg))
+        acc.update(r[0] for r in gg.get("results", []))
+    assert not bad, f"{len(bad)} mismatches; first {bad[:2]}"
+    assert all(acc[q] >= 100 for q in ["58", "96", "119"]), acc
+
+
+@pytest.mark.gpu
+def test_gpu_mc_strict_every_protocol(proto, golden):
+    g = golden("accept_golden.json.gz")["mc_strict"]
+    bad = []
+    for f in g["frames"]:
+        for pid, exp in zip(g["pids"], f["per_pid"]):
+            msg = {"protocol_id": pid, "data": f["hex"], "clock": f["clock"], "bit_length": f["L"]}
+            try:
+                r = proto.demodulate_mc(msg, f["mtype"], version=f["version"])
+                got = ["ok", [[x["protocol_id"], x["payload"], x["meta"]] for x in r]]
+            except Exception as e:
+                got = ["raise", type(e).__name__]
+            if got != exp:
+                bad.append((pid, f["hex"], exp, got))
+    assert not bad, f"{len(bad)} mismatches; first {bad[:3]}"
+
+
+@pytest.mark.gpu
+def test_gpu_units_postdemo(proto, golden):
+    cases = [(m, b, k, v) for m, b, k, v in golden("accept_golden.json.gz")["postdemo"]]
+    cases += [(m, b, k, [rc, ret]) for m, b, k, rc, ret in golden("units_golden.json.gz")["postdemo"]]
+    bad, acc = [], collections.Counter()
+    for meth in POSTDEMO:
+        sub = [c for c in cases if c[0] == meth]
+        got = proto.postdemo_batch(meth, [list(c[1]) for c in sub])
+        for (m, b, kind, val), x in zip(sub, got):
+            o = _outcome(x)
+            exp = [kind, val] if kind == "ok" else ["raise", val if isinstance(val, str) else val[0]]
+            if o != exp:
+                bad.append((m, b, exp, o))
+            elif kind == "ok" and val[0] == 1:
+                acc[m] += 1
+    assert not bad, f"{len(bad)} mismatches; first {bad[:3]}"
+    assert all(acc[m] >= 100 for m in POSTDEMO), acc
+    # the single-call methods are the same launch
+    assert proto.postDemo_lengtnPrefix("x", [1, 0, 1]) == (1, [0, 0, 0, 0, 0, 0, 1, 1, 1, 0, 1])
+    with pytest.raises(ValueError):
+        proto.postDemo_WS2000("x", [0] * 58 + [1])
+
+
+@pytest.mark.gpu
+def test_gpu_units_mc_methods(proto, golden):
+    cases = list(golden("accept_golden.json.gz")["mc_methods"])
+    P = proto.get_protocol_list()
+    for pid, s, kind, rc, res in golden("units_golden.json.gz")["mc_methods"]:
+        meth = P[pid]["method"].split(".")[-1]
+        cases.append([meth, "n", s, pid, len(s), ["ok", [rc, res]] if kind == "ok" else ["raise", rc]])
+    bad, acc = [], collections.Counter()
+    by = collections.defaultdict(list)
+    for c in cases:
+        by[c[0]].append(c)
+    for meth, sub in by.items():
+        got = proto.mc_method_batch(meth, [(name, bits, pid, mb) for _, name, bits, pid, mb, _ in sub])
+        for c, x in zip(sub, got):
+            exp = c[5]
+            o = _outcome(x)
+            if o != exp:
+                bad.append((c, o))
+            elif exp[0] == "ok" and exp[1][0] == 1:
+                acc[meth] += 1
+    assert not bad, f"{len(bad)} mismatches; first {bad[:3]}"
+    assert all(acc[m] >= 100 for m in by), acc
+    # the reference's own unit-test calls (tests/test_manchester_protocols.py)
+    assert proto.mcBit2Funkbus("some_name", "1001110101001111001111110111010101010101101000000000", "119", 52) == \
+        (1, "2C175F30008F")
+    assert proto.mcBit2Funkbus("x", "100111010100111100111111011101010101010110110000000", "119", 51) == \
+        (-1, "parity error")
+    assert proto.mcBit2Funkbus("x", "1001110101001111101111110111010101010101101000000000", "119", 52) == \
+        (-1, "checksum error")
+
+
+@pytest.mark.gpu
+def test_gpu_units_custom_protocols(golden):
+    """mcraw / _demodulate_mc_data on protocols edited in place (test_helpers.py:80-126,
+    test_manchester_protocols.py:50-101)."""
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    cust = golden("accept_golden.json.gz")["custom"]
+    p2 = SDProtocols()
+    p2._protocols[9989] = {"length_max": 24, "name": "Test Protocol"}
+    p3 = SDProtocols()
+    p3._protocols["119"] = {"length_min": 50, "name": "TestLength"}
+    p4 = SDProtocols()
+    p4._protocols["0"]["method"] = "manchester.mcRaw"
+    p4._protocols["0"]["length_min"] = 1
+    p4._protocols["0"]["length_max"] = 999
+    p4._protocols["0"]["preamble"] = "u0#"
+    p4._protocols["12"]["method"] = "manchester.mcRaw"
+    for tag, arg, pid, mb, exp in cust:
+        if tag == "mcraw":
+            got = _outcome(_try(p2.mcraw, "some_name", arg, pid, mb))
+        else:
+            if tag == "dmc2":
+                p3._protocols["119"]["length_min"] = 10
+                p3._protocols["119"]["length_max"] = 40
+                p3._protocols["119"]["method"] = "manchester.mcRaw"
+            if tag == "dmc3":
+                p3._protocols["119"]["length_max"] = 400
+            pp = p4 if tag in ("dmc4", "dmc5") else p3
+            got = _outcome(_try(pp._demodulate_mc_data, "TestLen" if pp is p3 else "n", pid, 500, arg, mb, "MC", None))
+        assert got == exp, (tag, arg, exp, got)
+    assert p2.mcraw("x", None, 9989, 24) == (-1, "no bitData provided")
+    assert p2.mcraw("x", "0101", None, 4) == (-1, "no protocolId provided")
+
+
+def _try(fn, *a):
+    try:
+        return fn(*a)
+    except Exception as e:
+        return e
+
+
+@pytest.mark.gpu
+def test_gpu_units_helpers(proto, golden):
+    from pysignalduino_amd import pattern_utils as PU
+    u, a = golden("units_golden.json.gz"), golden("accept_golden.json.gz")
+    pe = u["pattern_exists"] + a["pattern_exists"]
+    got = PU.pattern_exists_batch([(s, t, d) for s, t, d, _ in pe])
+    bad = [(s, t, d, e, g) for (s, t, d, e), g in zip(pe, got) if g != e]
+    assert not bad, f"pattern_exists: {len(bad)} mismatches; first {bad[:3]}"
+    assert PU.pattern_exists([1, -1], {"0": 1.0, "1": -1.0}, "0101") == "01"
+    assert PU.calculate_tolerance(20) == pytest.approx(3.6)
+    hx = u["hex_to_bin_str"]
+    assert proto.hex_to_bin_batch([s for s, _ in hx]) == [e for _, e in hx]
+    inv = a["hex_to_bin_inv"]
+    for flag in (False, True):
+        sub = [(s, e) for s, f, e in inv if f == flag]
+        got = proto.hex_to_bin_batch([s for s, _ in sub], invert=flag)
+        assert [[1, g] for g in got] == [e for _, e in sub]
+    assert proto._convert_mc_hex_to_bits("n", "0F", True, 2) == (1, "11110000")  # "F0"
+    bh = u["bin_str_2_hex_str"] + a["bin2hex"]
+    assert proto.bin_str_2_hex_batch([s for s, _ in bh]) == [e for _, e in bh]
+    assert proto.bin_str_2_hex_str(None) is None and proto.bin_str_2_hex_str(5) is None
+    md = u["mc2dmc"] + a["mc2dmc"]
+    assert proto.mc2dmc_batch([s for s, _ in md]) == [e for _, e in md]
+    assert proto.mc2dmc(None) == (-1, "no bitData provided")
+    assert proto.dec_2_bin_ppari(32) == "001000001" and proto.dec_2_bin_ppari(204) == "110011000"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n,seed", [("MU", 40000, 9201), ("MS", 20000, 9202), ("MC", 60000, 9203)])
+def test_gpu_planted_large_vs_c_oracle(kind, n, seed):
+    """Record-level, bit-exact on large planted corpora (every postDemo user, every MC method's
+    accept branch): the device path against the plain-C oracle, with >= 1000 accepted results per
+    postDemo user id / TFA, Grothe and Funkbus frame set."""
+    import os
+    from oracle import c_oracle as CO
+    from pysignalduino_amd import bank as B, packing, runtime, synth
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    cb = CO.CBank()
+    if kind == "MC":
+        frames = synth.mc_planted_frames(bk.protocols, n, seed=seed)
+        d_desc, d_rec, d_heap = eng.run(runtime.KIND_MC, eng.to_device_mc(packing.mc_batch_from_frames(frames)))
+        packed = CO.pack_mc(frames)
+        cls_pids = bk.mc_pids
+    else:
+        msgs = synth.planted_pulse_messages(bk.protocols, kind, n, seed=seed)
+        packer = packing.PulsePacker(kind)
+        for m in msgs:
+            packer.add(m)
+        d_desc, d_rec, d_heap = eng.run(runtime.KIND_MU if kind == "MU" else runtime.KIND_MS,
+                                        eng.to_device_pulses(packer.batch()))
+        packed = CO.pack_pulses(msgs)
+        cls_pids = bk.mu_pids if kind == "MU" else bk.ms_pids
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    st, rk, rb, nr, rec, heap = CO.run(kind, packed, threads)
+    dh, ch = d_heap.tobytes(), heap.tobytes()
+    assert np.array_equal(d_desc["status"] == runtime.ST_RAISED, st == 1)
+    assert np.array_equal(np.where(st == 1, d_desc["raise_kind"], 0), np.where(st == 1, rk, 0))
+    ok = st == 0
+    assert np.array_equal(d_desc["n_rec"][ok], nr[ok])
+    bad, acc = [], collections.Counter()
+    for i in np.nonzero(ok & (nr > 0))[0]:
+        a = d_rec[int(d_desc["rec_begin"][i]):int(d_desc["rec_begin"][i]) + int(nr[i])]
+        b = rec[int(rb[i]):int(rb[i]) + int(nr[i])]
+        for x, y in zip(a, b):
+            pid = cls_pids[int(x["proto"])]
+            same = (pid == cb.pids[int(y["proto"])] and
+                    dh[int(x["payload_off"]):int(x["payload_off"]) + int(x["payload_len"])] ==
+                    ch[int(y["off"]):int(y["off"]) + int(y["len"])] and
+                    (kind == "MC" or int(x["bit_length"]) == int(y["bitlen"])))
+            acc[pid] += 1
+            if not same:
+                bad.append((int(i), x, y))
+    assert not bad, f"{len(bad)} record mismatches; first: {bad[:2]}"
+    want = {"MU": ["80", "45", "74", "73", "70", "60", "66", "67", "39"], "MS": ["74.1"],
+            "MC": ["58", "96", "119"]}[kind]
+    assert all(acc[p] >= 1000 for p in want), acc
