@@ -34,14 +34,18 @@ def parse():
     ap.add_argument("--msgs", type=int, default=1_000_000, help="messages per rank (1/3 MU, 1/3 MS, 1/3 MC)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--kind", default="mixed", choices=("mixed", "MU", "MS", "MC"),
+                    help="mixed = config 5's per-GPU shard (1/3 each); MU/MS/MC = configs 2/3/4 (--msgs of one type)")
+    ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
+                    help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
 
 
-def cpu_baseline(mu, ms, mc, budget_s: float):
+def cpu_baseline(mu, ms, mc, budget_s: float, kinds=("MU", "MS", "MC")):
     """The plain-C oracle (oracle/sd_oracle_c.c, a restatement of the reference path: kind 'port')
-    timed on this host over a bounded 1:1:1 MU/MS/MC sample of the SAME corpora the GPU
-    demodulates: once on one core, once on all cores this process may use.  Each message is
-    fully demodulated against the whole bank, with results written, as on the GPU."""
+    timed on this host over a bounded sample of the SAME corpora the GPU demodulates (1:1:1
+    MU/MS/MC for the mixed workload): once on one core, once on all cores this process may use.
+    Each message is fully demodulated against the whole bank, with results written, as on the GPU."""
     from oracle import c_oracle as CO
     CO.build()
     bank = CO.CBank()
@@ -49,26 +53,29 @@ def cpu_baseline(mu, ms, mc, budget_s: float):
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():  # the box's CPU share (16 per GPU)
         cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     cores = max(1, min(cores, 64))
+    src = {"MU": mu, "MS": ms, "MC": mc}
+    nmax = min(src[k].n for k in kinds)
 
     def timed(k, threads):
         idx = np.arange(k)
-        packs = [("MU", CO.pack_batch(mu.subset(idx))), ("MS", CO.pack_batch(ms.subset(idx))),
-                 ("MC", CO.mc_batch(mc.subset(idx)))]
+        packs = [(t, CO.mc_batch(src[t].subset(idx)) if t == "MC" else CO.pack_batch(src[t].subset(idx)))
+                 for t in kinds]
         t0 = time.perf_counter()
         for kind, pk in packs:
             CO.run(kind, pk, threads)
-        return 3 * k / (time.perf_counter() - t0)
+        return len(kinds) * k / (time.perf_counter() - t0)
 
     # size the samples from a short probe so the whole leg stays within ~budget_s seconds
-    probe = timed(min(300, mu.n, ms.n, mc.n), 1)
-    k1 = int(max(300, min(mu.n, ms.n, mc.n, probe * budget_s * 0.35 / 3)))
+    probe = timed(min(300, nmax), 1)
+    k1 = int(max(300, min(nmax, probe * budget_s * 0.35 / len(kinds))))
     v1 = timed(k1, 1)
-    kn = int(max(300, min(mu.n, ms.n, mc.n, v1 * cores * budget_s * 0.5 / 3)))
+    kn = int(max(300, min(nmax, v1 * cores * budget_s * 0.5 / len(kinds))))
     vn = timed(kn, cores)
+    mix = "/".join(kinds)
     return {"value": vn, "unit": "msgs/s", "cores": cores, "kind": "port", "value_1core": v1,
-            "sample": f"oracle/sd_oracle_c.c (plain C, gcc -O2): {3 * kn} messages (1:1:1 MU/MS/MC, the "
-                      f"first {kn} of each bench corpus) on {cores} threads; 1-core rate on {3 * k1} messages; "
-                      f"{platform.processor() or platform.machine()}"}
+            "sample": f"oracle/sd_oracle_c.c (plain C, gcc -O2): {len(kinds) * kn} messages ({mix}, the "
+                      f"first {kn} of each bench corpus) on {cores} threads; 1-core rate on {len(kinds) * k1} "
+                      f"messages; {platform.processor() or platform.machine()}"}
 
 
 def issue_view(pmc, t_kernel):
@@ -83,6 +90,25 @@ def issue_view(pmc, t_kernel):
     return {"valu_insts": v, "salu_insts": sa, "valu_frac": v / t_kernel / valu_peak,
             "salu_frac": sa / t_kernel / salu_peak,
             "wait_frac": (pmc["sq_wait_any"] / pmc["sq_wave_cycles"]) if pmc.get("sq_wave_cycles") else None}
+
+
+def alg_bytes(kind, bd, rec_np):
+    """SURVEY §8(d) algorithmic bytes of one launch: per MU/MS message n_pulses + 8*4 B pattern
+    values + 8 B ids/order + 8 B header (304 B at 256 pulses); per MC frame ceil(L/4) hex + 8 B
+    header; outputs sum(16 B record + payload); the bank once per GPU (<= 16 KB)."""
+    n = bd["n"]
+    if kind == "MC":
+        inp = int(bd["lengths"].sum()) + 8 * n
+    else:
+        inp = int(bd["lengths"].sum()) + 48 * n
+    out = 16 * len(rec_np) + int(rec_np["payload_len"].astype(np.int64).sum())
+    return inp + out + 16384
+
+
+def latest_pmc():
+    import glob
+    c = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_traffic.json")))
+    return c[-1] if c else None
 
 
 def main():
@@ -107,117 +133,154 @@ def main():
 
     from pysignalduino_amd import bank as bankmod, runtime, synth
     from pysignalduino_amd import dist as sdist
+    from pysignalduino_amd.runtime import RES_DT
     bk = bankmod.Bank()
     P = bk.protocols
     eng = runtime.Engine(bk, local)
-    n3 = args.msgs // 3
-    mu = synth.mu_corpus(P, n3, seed=42 + 1000 * rank)
-    ms = synth.ms_corpus(P, n3, seed=43 + 1000 * rank)
-    mc = synth.mc_corpus(P, args.msgs - 2 * n3, seed=44 + 1000 * rank)
-    bmu, bms, bmc = eng.to_device_pulses(mu), eng.to_device_pulses(ms), eng.to_device_mc(mc)
-    outs = {
-        "MU": eng.alloc_out(mu.n, 8 * mu.n + 4096, 200 * mu.n + 65536),
-        "MS": eng.alloc_out(ms.n, 4 * ms.n + 4096, 64 * ms.n + 65536),
-        "MC": eng.alloc_out(mc.n, 4 * mc.n + 4096, 96 * mc.n + 65536),
-    }
-    # the three launches' cursors are rows of one tensor: one fill per step resets them all
-    cursors = torch.zeros((3, 4), dtype=torch.int32, device=dev)
-    for i, k in enumerate(("MU", "MS", "MC")):
-        outs[k]["cursor"] = cursors[i]
+    kinds = ("MU", "MS", "MC") if args.kind == "mixed" else (args.kind,)
+    per = {k: (args.msgs // 3 if k != "MC" else args.msgs - 2 * (args.msgs // 3)) if args.kind == "mixed" else args.msgs
+           for k in kinds}
+    seeds = {"MU": 42, "MS": 43, "MC": 44}
+    corp, bds = {}, {}
+    for k in kinds:
+        sd = seeds[k] + 1000 * rank
+        if k == "MU":
+            corp[k] = synth.mu_corpus(P, per[k], seed=sd, noise_frac=0.0 if args.corpus == "dense" else 0.15)
+        elif k == "MS":
+            corp[k] = synth.ms_corpus(P, per[k], seed=sd, noise_frac=0.0 if args.corpus == "dense" else 0.1)
+        else:
+            corp[k] = synth.mc_corpus(P, per[k], seed=sd)
+        bds[k] = eng.to_device_mc(corp[k]) if k == "MC" else eng.to_device_pulses(corp[k])
+    caps = {"MU": (12, 320), "MS": (4, 64), "MC": (4, 96)}
+    nslot = 2 if world > 1 else 1   # double-buffered outputs: step k+1 computes while step k is exchanged
+    outs = []
+    cursors = torch.zeros((nslot, len(kinds), 4), dtype=torch.int32, device=dev)
+    for s_ in range(nslot):
+        o = {}
+        for i, k in enumerate(kinds):
+            n = corp[k].n
+            o[k] = eng.alloc_out(n, caps[k][0] * n + 4096, caps[k][1] * n + 65536)
+            o[k]["cursor"] = cursors[s_, i]   # one fill per step resets a slot's cursors
+        outs.append(o)
     stream = torch.cuda.current_stream(dev)
-    # one event pair per kernel and timed step: the steps run back to back and are read after the
-    # closing synchronize (no host round trip between steps)
-    ev = [{k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in outs}
+    exch = sdist.Exchange() if world > 1 else None
+    done = [None] * nslot
+    # one event pair per kernel and timed step: read after the closing synchronize
+    ev = [{k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in kinds}
           for _ in range(args.steps)]
-    ktimes = {k: [] for k in outs}
 
-    def step(si=None):
-        cursors.zero_()
-        for k, bd in (("MU", bmu), ("MS", bms), ("MC", bmc)):
+    def step(j, si=None):
+        s_ = j % nslot
+        if done[s_] is not None:            # the exchange that read this slot has finished
+            stream.wait_event(done[s_])
+            done[s_] = None
+        cursors[s_].zero_()
+        for k in kinds:
             if si is not None:
                 ev[si][k][0].record(stream)
             if k == "MC":
-                eng.launch_mc(bd, outs[k])
+                eng.launch_mc(bds[k], outs[s_][k])
             else:
-                eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, outs[k])
+                eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[s_][k])
             if si is not None:
                 ev[si][k][1].record(stream)
-        if world > 1:  # RCCL all-gather of the decoded dmsg buffers (config 5), pysignalduino_amd/dist.py:
-            # one exchange of the counts, one all-gather of the packed MU/MS/MC buffers
-            sdist.allgather_streams([(outs[k]["desc"], outs[k]["rec"], outs[k]["heap"], bd["n"], outs[k]["cursor"])
-                                     for k, bd in (("MU", bmu), ("MS", bms), ("MC", bmc))])
+        if exch is not None:  # RCCL all-gather of the decoded dmsg buffers (config 5), overlapped
+            d = exch.submit([(outs[s_][k]["desc"], outs[s_][k]["rec"], outs[s_][k]["heap"], bds[k]["n"],
+                              outs[s_][k]["cursor"]) for k in kinds], stream)
+            done[(j - 1) % nslot] = d
 
+    def drain():
+        if exch is not None:
+            d = exch.flush()
+            if d is not None:
+                stream.wait_event(d)
+        torch.cuda.synchronize()
+
+    j = 0
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    # overflow check (capacities sized so that the timed steps never re-run)
-    for k, o in outs.items():
-        cur = o["cursor"].cpu().numpy()
+        step(j)
+        j += 1
+    drain()
+    ovf = {}
+    for k in kinds:   # capacities are sized so that the timed steps never re-run
+        cur = outs[(j - 1) % nslot][k]["cursor"].cpu().numpy()
         if cur[2] != 0:
-            raise SystemExit(f"{k}: result capacity overflow in bench configuration ({cur})")
+            ovf[k] = int(cur[2])
+    if ovf and args.corpus != "dense":
+        raise SystemExit(f"result capacity overflow in bench configuration ({ovf})")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for si in range(args.steps):
-        step(si)
-    torch.cuda.synchronize()
+        step(j, si)
+        j += 1
+    drain()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    for si in range(args.steps):
-        for k in outs:
-            ktimes[k].append(ev[si][k][0].elapsed_time(ev[si][k][1]) * 1e-3)
+    ktimes = {k: [ev[si][k][0].elapsed_time(ev[si][k][1]) * 1e-3 for si in range(args.steps)] for k in kinds}
     tt = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
-    total_msgs = args.msgs * world * args.steps
+    total_msgs = sum(per.values()) * world * args.steps
     value = total_msgs / dt
 
-    # roofline of the dominant kernel (MU): algorithmic bytes / measured kernel time
+    # roofline of the dominant kernel: SURVEY §8(d) algorithmic bytes / its HIP-event time
     kt = {k: float(np.mean(v)) for k, v in ktimes.items()}
-    # HBM traffic of the same kernel/launch from the committed PMC passes (tools/pmc.sh ->
-    # tools/pmc_traffic.py); null when absent or recorded for another launch size
+    dom = max(kt, key=kt.get)
+    o = outs[(j - 1) % nslot][dom]
+    cur = o["cursor"].cpu().numpy().astype(np.int64)
+    rec_np = o["rec"][: int(cur[0]) * RES_DT.itemsize].cpu().numpy().view(RES_DT)
+    alg = alg_bytes(dom, bds[dom], rec_np)
+    n = bds[dom]["n"]
+    layout = (int(bds[dom]["lengths"].sum()) + n * ((8 + 4 + 4 + 1) if dom == "MC" else
+                                                    (8 + 1 + 10 + 80 + (2 if dom == "MS" else 0)))
+              + n * runtime.DESC_DT.itemsize + int(cur[0]) * RES_DT.itemsize + int(cur[1]) + len(bk.blob))
+    achieved = alg / kt[dom]
     traffic = issue = None
-    tpath = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
-    if os.path.exists(tpath):
+    tag = f"k_pulses<{dom}>" if dom != "MC" else "k_mc"
+    tpath = latest_pmc()
+    if tpath and args.corpus == "bench":
         with open(tpath) as fh:
             tj = json.load(fh)
-    dom = max(kt, key=kt.get)
-    bd = {"MU": bmu, "MS": bms, "MC": bmc}[dom]
-    o = outs[dom]
-    cur = o["cursor"].cpu().numpy().astype(np.int64)
-    n = bd["n"]
-    if dom == "MC":
-        in_bytes = int(bd["lengths"].sum()) + n * (8 + 4 + 4 + 1)
-    else:
-        in_bytes = int(bd["lengths"].sum()) + n * (8 + 1 + 10 + 80 + (2 if dom == "MS" else 0))
-    out_bytes = n * runtime.DESC_DT.itemsize + int(cur[0]) * runtime.RES_DT.itemsize + int(cur[1])
-    alg = in_bytes + out_bytes + len(bk.blob)
-    achieved = alg / kt[dom]
-    if os.path.exists(tpath):
-        tag = f"k_pulses<{dom}>" if dom != "MC" else "k_mc"
-        if tj.get("_config", {}).get("msgs_per_gpu") == args.msgs and tj.get(tag, {}).get("traffic_bytes"):
+        cfg = tj.get("_config", {})
+        if cfg.get("msgs_per_gpu") == args.msgs and cfg.get("kind", "mixed") == args.kind and \
+                tj.get(tag, {}).get("traffic_bytes"):
             traffic = float(tj[tag]["traffic_bytes"])
             issue = issue_view(tj[tag], kt[dom])
+    wl = {"mixed": "mixed MU/MS/MC stream, 1/3 each per rank: MU 256-pulse messages x 129-id MU bank, MS sync+bits x "
+                   "66-id MS bank (clock x U(0.6,1.4)), MC frames x 12 clockrange ids ('fixed' chain)",
+          "MU": "config 2: 256-pulse MU messages x 129-id MU bank",
+          "MS": "config 3: MS sync+bits messages x 66-id MS bank, clock x U(0.6,1.4) sweep of the +-30 % gate",
+          "MC": "config 4: MC frames x 12 clockrange ids ('fixed' chain, mc2dmc + postdemodulation methods)"}[args.kind]
+    if world > 1:
+        wl += "; N>1 adds the RCCL all-gather of dmsg buffers (config 5), overlapped with the next step"
     res = {
         "metric": "RF messages/sec demodulated (MU+MS+MC, full protocol bank)",
         "value": value, "unit": "msgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8+f64", "data": "synthetic (seeded generators, pysignalduino_amd/synth.py)",
-        "config": {"workload": "mixed MU/MS/MC stream, 1/3 each per rank: MU 256-pulse messages x 129-id MU bank, "
-                               "MS sync+bits x 66-id MS bank (clock x U(0.6,1.4)), MC frames x 12 clockrange ids "
-                               "('fixed' chain); N>1 adds the RCCL all-gather of dmsg buffers (config 5)",
-                   "msgs_per_gpu": args.msgs, "parallelism": f"dp{world}"},
+        "vs_baseline": None, "dtype": "u8+f64",
+        "data": "synthetic (seeded generators, pysignalduino_amd/synth.py" +
+                (", noise-free dense corpus)" if args.corpus == "dense" else ")"),
+        "config": {"workload": wl, "kind": args.kind, "corpus": args.corpus, "msgs_per_gpu": sum(per.values()),
+                   "parallelism": f"dp{world}"},
         "per_kernel_ms": {k: 1e3 * v for k, v in kt.items()},
-        "per_type_msgs_per_s": {"MU": mu.n / kt["MU"], "MS": ms.n / kt["MS"], "MC": mc.n / kt["MC"]},
+        "per_type_msgs_per_s": {k: per[k] / kt[k] for k in kinds},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": f"k_pulses<{dom}>" if dom != "MC" else "k_mc",
-                     "alg_bytes_per_launch": alg, "issue": issue},
+                     "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": tag,
+                     "alg_bytes_per_launch": alg, "layout_bytes_per_launch": layout,
+                     "results_per_launch": int(cur[0]), "issue": issue},
     }
+    if ovf:   # dense corpus: messages whose results did not fit the on-chip staging (the product re-runs them)
+        res["overflow"] = {}
+        for k in ovf:
+            d = outs[(j - 1) % nslot][k]["desc"][: corp[k].n * runtime.DESC_DT.itemsize].cpu().numpy().view(runtime.DESC_DT)
+            res["overflow"][k] = {"flags": ovf[k], "tile_msgs": int((d["status"] == runtime.ST_OVF_TILE).sum()),
+                                  "out_msgs": int((d["status"] == runtime.ST_OVF_OUT).sum())}
     if rank == 0 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(mu, ms, mc, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(corp.get("MU"), corp.get("MS"), corp.get("MC"), args.cpu_seconds, kinds)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -291,6 +291,22 @@ typedef struct {
 
 int sdx_units(const sdx_unit_batch* batch, const sdx_out* out, void* hip_stream);
 
+/* ---- multi-GPU exchange (BASELINE config 5) --------------------------------------
+ * The packing step of the all-gather of decoded dmsg buffers (pysignalduino_amd/dist.py): one
+ * launch copies K (<= 8) demodulation launches' descriptors, records and heap into the caller's
+ * send buffer, re-basing them to the whole job (rec_begin += base_rec; payload_off += base_heap,
+ * msg += base_msg).  Section offsets and heap_dev must be 16-byte aligned. */
+typedef struct {
+  const uint8_t* desc_dev;     /* sdx_desc[n_msgs] */
+  const uint8_t* rec_dev;      /* sdx_result[n_rec] */
+  const uint8_t* heap_dev;     /* n_heap payload bytes */
+  uint32_t n_msgs, n_rec, n_heap;
+  uint32_t base_msg, base_rec, base_heap;  /* the lower ranks' messages / records / heap bytes */
+  uint64_t off_desc, off_rec, off_heap;    /* section offsets in send_dev */
+} sdx_xchg_part;
+
+int sdx_exchange_pack(const sdx_xchg_part* parts, int k, uint8_t* send_dev, void* hip_stream);
+
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */
 #define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */
 #define SDX_MC_HEX_MAX 128  /* sdx_demod_mc */

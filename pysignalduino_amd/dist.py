@@ -1,15 +1,28 @@
 """Multi-GPU: contiguous message shards per rank + all-gather of the decoded dmsg buffers.
 
-Messages are independent: each rank demodulates its contiguous shard
-with no communication, then ONE exchange step gathers every rank's result buffers
-(descriptors, result records, payload heap) so that every rank holds the whole stream's
-results in global message order.  With the ``nccl`` backend (RCCL over xGMI on ROCm) the
-buffers stay in HBM; the same code runs on ``gloo`` with CPU tensors (tests/test_dist.py).
+Messages are independent: each rank demodulates its contiguous shard with no
+communication during compute.  The one exchange step gathers every rank's result buffers
+(descriptors, result records, payload heap) so that every rank holds the whole stream's results
+in global message order (BASELINE config 5).  With the ``nccl`` backend (RCCL over xGMI on ROCm)
+the buffers stay in HBM and the exchange runs on its own HIP stream, overlapped with the next
+step's kernels (:class:`Exchange`); the same protocol runs on ``gloo`` with CPU tensors
+(tests/test_dist.py).
+
+Per exchange:
+  1. one all-gather of every rank's counts (messages, records, heap bytes per launch), read from
+     the launches' device cursors on the exchange stream;
+  2. the host reads those counts one step later -- while the GPU runs the next step -- and sizes
+     the sections (max over ranks, 16-byte aligned);
+  3. ``sdx_exchange_pack`` (csrc/sdx_exchange.hip) copies the rank's K launches into one send buffer,
+     re-basing rec_begin / payload_off / msg by the counts of the lower ranks;
+  4. ONE all-gather moves the packed buffers; receivers only drop the per-rank padding.
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+import ctypes
+from typing import List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -25,40 +38,25 @@ def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
-    """all_gather into one contiguous tensor (one collective; list form where the backend lacks it)."""
-    try:
+    """all_gather into one contiguous tensor.  The collective is chosen once from the backend:
+    RCCL's all_gather_into_tensor, the list form on gloo -- every rank issues the same one."""
+    if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, inp, group=group)
-    except (RuntimeError, NotImplementedError, AttributeError):
+    else:
         dist.all_gather(list(out.chunk(dist.get_world_size(group))), inp, group=group)
 
 
-def allgather_streams(parts: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, int, torch.Tensor]],
-                      group=None) -> List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
-    """Gather the result buffers of several demodulation launches (e.g. MU, MS, MC) in ONE exchange.
+def _layout(S: np.ndarray, rank: int):
+    """S[world, K, 3] = (messages, records, heap bytes) -> section sizes, offsets, bases."""
+    nb = S * np.array([DESC_BYTES, REC_BYTES, 1], np.int64)                    # bytes per section
+    cap = np.maximum((nb.max(axis=0) + 15) // 16 * 16, 16)                      # [K, 3]
+    sec_off = np.concatenate([[0], np.cumsum(cap.reshape(-1))]).astype(np.int64)
+    base = S[:rank].sum(axis=0) if rank else np.zeros(S.shape[1:], np.int64)  # lower ranks' counts
+    return nb, sec_off, int(sec_off[-1]), base
 
-    ``parts``: per launch (desc u8, rec u8, heap u8, n_msgs, cursor) with ``cursor`` the launch's
-    device cursor (cursor[0] = records, cursor[1] = heap bytes): the counts stay on the device.
-    Steps: one all-gather of every rank's counts (the only host synchronisation), then every rank
-    packs its sections into one buffer -- re-basing its own rec_begin / payload_off / msg by the
-    counts of the lower ranks while copying -- and ONE all-gather moves all of it; the receivers
-    only drop the per-rank padding.  Returns per launch (desc, rec, heap) of the whole job in
-    global message order (the contract of :func:`allgather_results`).
-    """
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    K = len(parts)
-    dev = parts[0][0].device
-    counts = torch.stack([torch.stack([torch.tensor(n, dtype=torch.int64, device=dev), cur[0].to(torch.int64),
-                                       cur[1].to(torch.int64)]) for _, _, _, n, cur in parts])  # [K, 3]
-    allc = torch.empty(world * K * 3, dtype=torch.int64, device=dev)
-    _all_gather_flat(allc, counts.reshape(-1), group)
-    S = allc.view(world, K, 3).cpu()
-    nb = S * torch.tensor([DESC_BYTES, REC_BYTES, 1], dtype=torch.int64)        # section bytes
-    cap = ((nb.max(dim=0).values + 15) // 16 * 16).clamp(min=16)                # [K, 3]
-    sec_off = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.int64), cap.reshape(-1)]), 0)
-    total = int(sec_off[-1])
-    base = S[:rank].sum(dim=0) if rank else torch.zeros(K, 3, dtype=torch.int64)  # (msgs, recs, heap) below
-    send = torch.zeros(total, dtype=torch.uint8, device=dev)
+
+def _pack_torch(parts, S, rank, sec_off, base, send):
+    """The packing step with torch ops (CPU tensors, gloo)."""
     for k, (desc, rec, heap, _, _) in enumerate(parts):
         nm, nr, nh = (int(x) for x in S[rank, k])
         o_d, o_r, o_h = (int(sec_off[3 * k + j]) for j in range(3))
@@ -72,57 +70,147 @@ def allgather_streams(parts: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Te
             rv[:, 3] += int(base[k, 0])
         if nh:
             send[o_h: o_h + nh] = heap[:nh]
-    recv = torch.empty(world * total, dtype=torch.uint8, device=dev)
-    _all_gather_flat(recv, send, group)
-    out = []
-    for k in range(K):
-        secs = []
-        for j in range(3):
-            o = int(sec_off[3 * k + j])
-            secs.append(torch.cat([recv[r * total + o: r * total + o + int(nb[r, k, j])] for r in range(world)]))
-        out.append(tuple(secs))
-    return out
+
+
+def _pack_device(parts, S, rank, sec_off, base, send, stream):
+    """The packing step on the GPU: one sdx_exchange_pack launch for all K launches."""
+    from . import runtime
+    lib = runtime.load_library()
+    K = len(parts)
+    arr = (runtime.SdxXchgPart * K)()
+    for k, (desc, rec, heap, _, _) in enumerate(parts):
+        nm, nr, nh = (int(x) for x in S[rank, k])
+        arr[k] = runtime.SdxXchgPart(desc.data_ptr(), rec.data_ptr(), heap.data_ptr(), nm, nr, nh,
+                                     int(base[k, 0]), int(base[k, 1]), int(base[k, 2]),
+                                     int(sec_off[3 * k]), int(sec_off[3 * k + 1]), int(sec_off[3 * k + 2]))
+    runtime._check(lib, lib.sdx_exchange_pack(arr, K, ctypes.c_void_p(send.data_ptr()),
+                                              ctypes.c_void_p(stream.cuda_stream)))
+
+
+class _Pending:
+    __slots__ = ("parts", "counts_host", "event", "S")
+
+    def __init__(self, parts, counts_host, event):
+        self.parts, self.counts_host, self.event, self.S = parts, counts_host, event, None
+
+
+class Exchange:
+    """All-gather of the decoded dmsg buffers of K launches per step, pipelined.
+
+    ``submit(parts, stream)`` is called after the step's kernels are enqueued on ``stream``
+    (``parts``: per launch (desc u8, rec u8, heap u8, n_msgs, cursor), cursor[0] = records,
+    cursor[1] = heap bytes, left on the device).  It enqueues the count all-gather of this step on
+    the exchange stream and completes the PREVIOUS step's exchange (pack + data all-gather),
+    whose counts arrived while this step's kernels were running.  It returns the event after
+    which the previous step's buffers may be overwritten (double-buffer the outputs).  ``flush()``
+    completes the last step.  ``gathered()`` gives the last completed step's results as per
+    launch (desc, rec, heap) of the whole job in global message order.
+
+    On gloo / CPU tensors every call completes synchronously (same protocol, torch-op packing)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.pending: Optional[_Pending] = None
+        self.stream = None
+        self._bufs = {}
+        self.last = None   # (recv, S, nb, sec_off, total) of the last completed exchange
+
+    def _buf(self, name, n, dev):
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n or b.device != dev:
+            b = self._bufs[name] = torch.empty(max(n, 16), dtype=torch.uint8, device=dev)
+        return b[:n]
+
+    def _counts(self, parts):
+        dev = parts[0][0].device
+        return torch.stack([torch.stack([torch.tensor(n, dtype=torch.int64, device=dev), cur[0].to(torch.int64),
+                                         cur[1].to(torch.int64)]) for _, _, _, n, cur in parts]).reshape(-1)
+
+    def submit(self, parts, stream=None):
+        parts = list(parts)
+        K = len(parts)
+        dev = parts[0][0].device
+        overlap = dev.type == "cuda" and dist.get_backend(self.group) == "nccl"
+        if not overlap:
+            allc = torch.empty(self.world * K * 3, dtype=torch.int64, device=dev)
+            _all_gather_flat(allc, self._counts(parts), self.group)
+            self._complete(_Pending(parts, allc.cpu(), None))
+            return None
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(dev)
+        stream = stream or torch.cuda.current_stream(dev)
+        ready = torch.cuda.Event()
+        ready.record(stream)
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ready)
+            allc = torch.empty(self.world * K * 3, dtype=torch.int64, device=dev)
+            _all_gather_flat(allc, self._counts(parts), self.group)
+            host = torch.empty(allc.numel(), dtype=torch.int64, pin_memory=True)
+            host.copy_(allc, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        prev, self.pending = self.pending, _Pending(parts, host, ev)
+        return self._complete(prev) if prev is not None else None
+
+    def flush(self):
+        prev, self.pending = self.pending, None
+        return self._complete(prev) if prev is not None else None
+
+    def _complete(self, p: _Pending):
+        K = len(p.parts)
+        if p.event is not None:
+            p.event.synchronize()            # the counts (the GPU has moved on to the next step)
+        S = p.counts_host.numpy().reshape(self.world, K, 3).astype(np.int64)
+        nb, sec_off, total, base = _layout(S, self.rank)
+        dev = p.parts[0][0].device
+        if p.event is None:
+            send = torch.zeros(total, dtype=torch.uint8, device=dev)
+            _pack_torch(p.parts, S, self.rank, sec_off, base, send)
+            recv = torch.empty(self.world * total, dtype=torch.uint8, device=dev)
+            _all_gather_flat(recv, send, self.group)
+            self.last = (recv, S, nb, sec_off, total)
+            return None
+        with torch.cuda.stream(self.stream):
+            send = self._buf("send", total, dev)
+            _pack_device(p.parts, S, self.rank, sec_off, base, send, self.stream)
+            recv = self._buf("recv", self.world * total, dev)
+            _all_gather_flat(recv, send, self.group)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+        self.last = (recv, S, nb, sec_off, total)
+        return done
+
+    def gathered(self) -> List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+        """Per launch (desc, rec, heap) of the last completed exchange, whole job, global order."""
+        recv, S, nb, sec_off, total = self.last
+        if self.stream is not None:
+            self.stream.synchronize()
+        out = []
+        for k in range(S.shape[1]):
+            secs = []
+            for j in range(3):
+                o = int(sec_off[3 * k + j])
+                secs.append(torch.cat([recv[r * total + o: r * total + o + int(nb[r, k, j])]
+                                       for r in range(self.world)]))
+            out.append(tuple(secs))
+        return out
+
+
+def allgather_streams(parts: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, int, torch.Tensor]],
+                      group=None) -> List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+    """One exchange of several launches (e.g. MU, MS, MC), completed at once: per launch (desc,
+    rec, heap) of the whole job in global message order, with rec_begin / payload_off / msg
+    re-based to the concatenation."""
+    ex = Exchange(group)
+    ex.submit(parts)
+    ex.flush()
+    return ex.gathered()
 
 
 def allgather_results(desc: torch.Tensor, rec: torch.Tensor, heap: torch.Tensor, n_msgs: int, n_rec: int,
                       n_heap: int, group=None):
-    """Gather every rank's (desc[n_msgs], rec[n_rec], heap[n_heap]) byte buffers.
-
-    Returns (desc, rec, heap) uint8 tensors of the whole job in global message order, with
-    rec_begin / payload_off / msg re-based to the concatenation.
-    """
-    world = dist.get_world_size(group)
-    dev = desc.device
-    sizes = torch.tensor([n_msgs, n_rec, n_heap], dtype=torch.int64, device=dev)
-    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-    dist.all_gather(all_sizes, sizes, group=group)
-    S = torch.stack(all_sizes).cpu()
-    mx = S.max(dim=0).values.clamp(min=1)
-
-    def gather(buf: torch.Tensor, nbytes: int, cap: int):
-        padded = torch.zeros(cap, dtype=torch.uint8, device=dev)
-        if nbytes:
-            padded[:nbytes] = buf[:nbytes]
-        parts = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
-        dist.all_gather(parts, padded, group=group)
-        return parts
-
-    dparts = gather(desc, n_msgs * DESC_BYTES, int(mx[0]) * DESC_BYTES)
-    rparts = gather(rec, n_rec * REC_BYTES, int(mx[1]) * REC_BYTES)
-    hparts = gather(heap, n_heap, int(mx[2]))
-    out_d, out_r, out_h = [], [], []
-    m_base = r_base = h_base = 0
-    for k in range(world):
-        nm, nr, nh = (int(x) for x in S[k])
-        d = dparts[k][: nm * DESC_BYTES].clone().view(torch.int32).view(nm, 2)
-        d[:, 0] += r_base
-        r = rparts[k][: nr * REC_BYTES].clone().view(torch.int32).view(nr, 4)
-        r[:, 0] += h_base
-        r[:, 3] += m_base
-        out_d.append(d.reshape(-1).view(torch.uint8))
-        out_r.append(r.reshape(-1).view(torch.uint8))
-        out_h.append(hparts[k][:nh])
-        m_base += nm
-        r_base += nr
-        h_base += nh
-    return torch.cat(out_d), torch.cat(out_r), torch.cat(out_h)
+    """One launch's (desc[n_msgs], rec[n_rec], heap[n_heap]) of every rank (host-known counts)."""
+    cur = torch.tensor([n_rec, n_heap, 0, 0], dtype=torch.int32, device=desc.device)
+    return allgather_streams([(desc, rec, heap, n_msgs, cur)], group)[0]

@@ -35,7 +35,8 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
-            "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units"]
+            "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
+            "sdx_exchange_pack"]
 
 
 class SdxPulseBatch(Structure):
@@ -70,6 +71,13 @@ class SdxJsonOut(Structure):
 class SdxUnitBatch(Structure):
     _fields_ = [("op", c_int32), ("n", c_int32), ("in_dev", c_void_p), ("in_off_dev", c_void_p), ("arg_dev", c_void_p),
                 ("val_dev", c_void_p), ("val_off_dev", c_void_p), ("mcrec_dev", c_void_p), ("out_off_dev", c_void_p)]
+
+
+class SdxXchgPart(Structure):
+    _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("n_msgs", c_uint32),
+                ("n_rec", c_uint32), ("n_heap", c_uint32), ("base_msg", c_uint32), ("base_rec", c_uint32),
+                ("base_heap", c_uint32), ("off_desc", ctypes.c_uint64), ("off_rec", ctypes.c_uint64),
+                ("off_heap", ctypes.c_uint64)]
 
 
 class SdxOut(Structure):
@@ -135,6 +143,8 @@ def load_library(path: Optional[str] = None):
     lib.sdx_select_lines.restype = c_int
     lib.sdx_units.argtypes = [POINTER(SdxUnitBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_units.restype = c_int
+    lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, c_void_p]
+    lib.sdx_exchange_pack.restype = c_int
     if lib.sdx_abi_version() != 4:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)

@@ -310,7 +310,8 @@ class SDProtocols(UnitsMixin):
         """Demodulate many messages in one GPU pass.
 
         Returns one result list per message.  A message on which the reference raises
-        yields the exception instance (or re-raises it when ``raise_errors``).
+        yields the exception instance (or re-raises it when ``raise_errors``); so does a message
+        outside the device contract (``packing.ContractError``), without failing the others.
         """
         if msg_type == "MC":
             return [self._catch(self.demodulate_mc, m, "MC", raise_errors=raise_errors) for m in messages] \
@@ -321,11 +322,13 @@ class SDProtocols(UnitsMixin):
         pack_err: Dict[int, BaseException] = {}
         for i, m in enumerate(messages):
             try:
+                d = m.get("data", "")
+                if isinstance(d, str) and len(d) > runtime.LONG_MAX:
+                    raise packing.ContractError(f"messages longer than {runtime.LONG_MAX} pulses are outside "
+                                                "the device contract")
                 packer.add(m)
-            except packing.ContractError:
-                raise
-            except Exception as e:  # the reference raises on this message (same class)
-                if raise_errors:
+            except Exception as e:  # the reference raises on this message (same class), or the
+                if raise_errors:    # message is outside the device contract (ContractError): per slot
                     raise
                 pack_err[i] = e
                 packer.add({"data": ""})
@@ -408,13 +411,22 @@ class SDProtocols(UnitsMixin):
                             version: Optional[str] = None, raise_errors: bool = False):
         """'fixed' MC chain on the GPU; accepts MCParser dicts (raw_hex/clock/mcbitnum/messagetype)
         or demodulate_mc dicts (data/clock/bit_length)."""
-        frames = []
-        for m in messages:
-            hx = m.get("raw_hex", m.get("data", m.get("D", "")))
-            clk = m.get("clock", m.get("C", 0))
-            L = m.get("mcbitnum", m.get("bit_length", m.get("L", 0)))
-            mt = m.get("messagetype", msg_type if msg_type in ("MC", "Mc") else "MC")
-            frames.append((hx, int(clk), int(L), mt, m.get("version", version)))
+        frames, slot_err = [], {}
+        for i, m in enumerate(messages):
+            try:
+                hx = m.get("raw_hex", m.get("data", m.get("D", "")))
+                clk = m.get("clock", m.get("C", 0))
+                L = m.get("mcbitnum", m.get("bit_length", m.get("L", 0)))
+                mt = m.get("messagetype", msg_type if msg_type in ("MC", "Mc") else "MC")
+                if not isinstance(hx, str) or len(hx) > runtime.MC_HEX_MAX:
+                    raise packing.ContractError(f"MC frames must be str of at most {runtime.MC_HEX_MAX} hex "
+                                                "characters for the device path")
+                frames.append((hx, int(clk), int(L), mt, m.get("version", version)))
+            except Exception as e:
+                if raise_errors:
+                    raise
+                slot_err[i] = e
+                frames.append(("", 0, 0, "MC", None))
         mb = packing.mc_batch_from_frames(frames)
         eng = self._ensure()
         desc, rec, heap = eng.run(runtime.KIND_MC, eng.to_device_mc(mb))
@@ -423,6 +435,9 @@ class SDProtocols(UnitsMixin):
         hb = heap.tobytes()
         out: List[Any] = []
         for i in range(len(desc)):
+            if i in slot_err:
+                out.append(slot_err[i])
+                continue
             d = desc[i]
             if d["status"] == runtime.ST_RAISED:
                 exc = runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)("reference raises on this MC frame")

@@ -90,7 +90,15 @@ def _worker(rank, world, port, msgs, pids, q):
     (a, b, c), (a2, b2, c2) = sdist.allgather_streams([(td, tr, th, hi - lo, cur), (*t2, half, cur2)])
     got_multi = decode(a.numpy().view(runtime.DESC_DT), b.numpy().view(runtime.RES_DT), c.numpy(), pids)
     got_half = decode(a2.numpy().view(runtime.DESC_DT), b2.numpy().view(runtime.RES_DT), c2.numpy(), pids)
-    q.put((rank, got, got_multi, got_half))
+    # the pipelined form the bench runs: submit per step, the results of each completed step
+    ex = sdist.Exchange()
+    steps = []
+    for parts in ([(td, tr, th, hi - lo, cur)], [(*t2, half, cur2), (td, tr, th, hi - lo, cur)]):
+        ex.submit(parts)
+        steps.append([decode(a.numpy().view(runtime.DESC_DT), b.numpy().view(runtime.RES_DT), c.numpy(), pids)
+                      for a, b, c in ex.gathered()])
+    ex.flush()
+    q.put((rank, got, got_multi, got_half, steps))
     dist.destroy_process_group()
 
 
@@ -123,7 +131,35 @@ def test_gloo_world2_allgather_matches_unsharded():
     for r in range(2):
         lo, hi = sdist.shard_bounds(len(msgs), r, 2)
         halves += full[lo: lo + (hi - lo) // 2]
-    for rank, got, got_multi, got_half in outs:
+    for rank, got, got_multi, got_half, steps in outs:
         assert got == full, f"rank {rank} gathered stream differs"
         assert got_multi == full, f"rank {rank}: allgather_streams differs"
         assert got_half == halves, f"rank {rank}: second launch of allgather_streams differs"
+        assert steps == [[full], [halves, full]], f"rank {rank}: Exchange steps differ"
+
+
+@pytest.mark.gpu
+def test_exchange_pack_kernel_matches_torch_pack():
+    """sdx_exchange_pack (HIP) == the torch-op packing, for a rank with lower ranks below it
+    (re-based rec_begin / payload_off / msg, 16-byte heap copies plus tails), K = 3 launches."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    parts = []
+    for k in range(3):
+        nm, nr, nh = int(rng.integers(1, 5000)), int(rng.integers(0, 20000)), int(rng.integers(0, 300000))
+        desc = torch.from_numpy(rng.integers(0, 255, size=nm * 8 + 64, dtype=np.uint8)).to(dev)
+        rec = torch.from_numpy(rng.integers(0, 255, size=nr * 16 + 64, dtype=np.uint8)).to(dev)
+        heap = torch.from_numpy(rng.integers(0, 255, size=nh + 64, dtype=np.uint8)).to(dev)
+        cur = torch.tensor([nr, nh, 0, 0], dtype=torch.int32, device=dev)
+        parts.append((desc, rec, heap, nm, cur))
+    S = np.zeros((3, 3, 3), np.int64)
+    for r in range(3):
+        for k, (_, _, _, nm, cur) in enumerate(parts):
+            S[r, k] = (nm, int(cur[0]), int(cur[1])) if r == 2 else rng.integers(0, 100000, size=3)
+    nb, sec_off, total, base = sdist._layout(S, 2)
+    a = torch.zeros(total, dtype=torch.uint8, device=dev)
+    b = torch.zeros(total, dtype=torch.uint8, device=dev)
+    sdist._pack_torch(parts, S, 2, sec_off, base, a)
+    sdist._pack_device(parts, S, 2, sec_off, base, b, torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

@@ -328,3 +328,28 @@ def test_gpu_planted_large_vs_c_oracle(kind, n, seed):
     want = {"MU": ["80", "45", "74", "73", "70", "60", "66", "67", "39"], "MS": ["74.1"],
             "MC": ["58", "96", "119"]}[kind]
     assert all(acc[p] >= 1000 for p in want), acc
+
+
+@pytest.mark.gpu
+def test_gpu_zero_padded_pattern_keys_and_per_message_contract(proto, golden):
+    """P01 / P001 keys name pattern "1" as in the reference; a message outside the device contract
+    (a pattern id >= 10, > 4096 pulses, an MC frame > 128 hex characters) yields ContractError in
+    its own slot while the rest of the batch decodes."""
+    from pysignalduino_amd.packing import ContractError
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    cases = golden("accept_golden.json.gz")["mu_p0x"]
+    got = proto.demodulate_batch([c["msg"] for c in cases], "MU")
+    assert [_flat(x) for x in got] == [c["exp"] for c in cases]
+    msgs = [dict(c["msg"]) for c in cases[:20]]
+    msgs[3] = dict(msgs[3], P10="500")
+    msgs[7] = dict(msgs[7], data="0" * 5000, D="0" * 5000)
+    got = proto.demodulate_batch(msgs, "MU")
+    assert isinstance(got[3], ContractError) and isinstance(got[7], ContractError)
+    assert [_flat(x) for i, x in enumerate(got) if i not in (3, 7)] == \
+        [c["exp"] for i, c in enumerate(cases[:20]) if i not in (3, 7)]
+    pf = SDProtocols(mc_mode="fixed")
+    frames = [{"raw_hex": f["hex"], "clock": f["clock"], "mcbitnum": f["L"], "messagetype": f["mtype"],
+               "version": f["version"]} for f in golden("accept_golden.json.gz")["mc"][:10]]
+    frames[4] = dict(frames[4], raw_hex="A" * 200)
+    got = pf.demodulate_mc_batch(frames)
+    assert isinstance(got[4], ContractError) and all(not isinstance(x, ContractError) for i, x in enumerate(got) if i != 4)
