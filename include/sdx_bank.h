@@ -81,7 +81,12 @@ typedef struct {
   uint64_t start_upk;    /* uidx_pk of the start list (<= 16 positions) */
   uint32_t flags;        /* bit0 has_start, bit1 never, bit2 active, bit3 full */
   sdx_fspec spec[4];     /* start, one, zero, float */
-  uint32_t res[3];
+  /* integer normalisation of round(P / clockabs, 1) (message_unsynced.py:64) for integral P:
+   * k = round-half-even(10*|P| / clk_c) with floor(x / clk_c) == (x * clk_m) >> clk_sh for every
+   * x < 2^30 (Granlund-Montgomery); exact ties (2r == clk_c) and non-integral P take the fp64 path */
+  uint32_t clk_c;        /* |clockabs| when it is an integer in [1, 2^20) */
+  uint32_t clk_m;        /* ceil(2^clk_sh / clk_c) */
+  uint32_t clk_sh;       /* bits 0-7: shift (30 + ceil(log2 clk_c)); bit 8: valid; bit 9: clockabs < 0 */
 } sdx_mu_filt;           /* 128 bytes */
 
 /* the MS lane filter's view of one protocol (as sdx_mu_filt; spec = sync, one, zero, float) */

@@ -99,7 +99,7 @@ def mn_tables() -> bytes:
 
 FSPEC = np.dtype([("lohi", "<u4", (3,)), ("rk01", "<u4"), ("rk2_len_nu", "<u4"), ("upk", "<u4")])
 MU_FILT = np.dtype([("clock", "<f8"), ("start_upk", "<u8"), ("flags", "<u4"), ("spec", FSPEC, (4,)),
-                    ("res", "<u4", (3,))])
+                    ("clk_c", "<u4"), ("clk_m", "<u4"), ("clk_sh", "<u4")])
 MS_FILT = np.dtype([("pclock", "<f8"), ("sync_upk", "<u8"), ("flags", "<u4"), ("width", "<i4"), ("lmin_sync", "<i4"),
                     ("spec", FSPEC, (4,)), ("res", "<u4")])
 HDR_FMT = "<" + "I" * 31  # sdx_bank_hdr: 31 uint32
@@ -213,6 +213,21 @@ def _int32(v: int) -> int:
 
 
 PID_NOT_INT = -(1 << 31)   # SDX_PID_NOT_INT
+
+
+def clock_divider(clock: float):
+    """(c, m, sh | flags) of sdx_mu_filt: the integer normalisation k = round(10*|P| / c) the MU
+    filter uses for integral pattern values.  floor(x / c) == (x * m) >> sh for all 0 <= x < 2^30
+    with m = ceil(2^(30+L) / c), L = ceil(log2 c) (Granlund-Montgomery, N = 30: m*c - 2^(30+L) <
+    c <= 2^L); valid only for an integral clock with 1 <= |clock| < 2^20."""
+    if not (math.isfinite(clock) and clock == math.floor(clock) and 1 <= abs(clock) < (1 << 20)):
+        return 0, 0, 0
+    c = int(abs(clock))
+    L = (c - 1).bit_length()
+    sh = 30 + L
+    m = -(-(1 << sh) // c)
+    assert m < (1 << 32) and m * c - (1 << sh) < (1 << L)
+    return c, m, sh | (1 << 8) | ((1 << 9) if clock < 0 else 0)
 
 
 K_LIMIT = 1 << 28  # |k| bound of every interval (the device's k sentinel lies beyond it)
@@ -632,6 +647,7 @@ class Bank:
         for r in range(len(mu)):
             rec, x = mu[r], f[r]
             x["clock"] = rec["clock"]
+            x["clk_c"], x["clk_m"], x["clk_sh"] = clock_divider(float(rec["clock"]))
             ok = cls._fspecs([rec[k] for k in ("start", "one", "zero", "flt")], x, "start_upk")
             x["flags"] = (int(rec["has_start"]) | (int(rec["never"]) << 1) | (int(rec["active"]) << 2) |
                           ((0 if ok else 1) << 3))

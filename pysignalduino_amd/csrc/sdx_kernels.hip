@@ -1397,6 +1397,41 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   // length, then every message's characters are loaded into registers -- so the global-load
   // latencies of the wave's messages overlap instead of adding up message after message
   constexpr int MPW = NW <= 4 ? (TM + NWAVE - 1) / NWAVE : 1;
+  // short variants: the tile's pattern tables, one thread per (message, pattern) with consecutive
+  // addresses, into the result pool's heap (unused until the finish phase): every wave then reads
+  // its lanes' patterns from LDS instead of each of the NWAVE waves loading them strided from HBM.
+  //   MU: x = 10|P| (integral P, |P| < 2^26) for the integer normalisation, flags (bit0 sign, bit1 fp64 path)
+  //   MS: k of round(P / abs(P[CP]), 1) (message_synced.py:64-72) and the clock abs(P[CP])
+  static_assert(T::PHEAP >= TM * SDX_MAXPAT * 6 + TM * 16, "pattern staging fits the pool heap");
+  uint32_t* st_x = reinterpret_cast<uint32_t*>(L.heap);                    // [TM][10]
+  uint8_t* st_f = L.heap + TM * SDX_MAXPAT * 4;                            // [TM][10]
+  uint8_t* st_id = st_f + TM * SDX_MAXPAT;                                 // [TM][10]
+  double* st_clk = reinterpret_cast<double*>(st_id + TM * SDX_MAXPAT);     // [TM] (MS)
+  uint8_t* st_np = reinterpret_cast<uint8_t*>(st_clk + TM);                // [TM]
+  if constexpr (NW <= 4) {
+    for (int i = tid; i < TM * SDX_MAXPAT; i += blockDim.x) {
+      const int m = i / SDX_MAXPAT, k = i - m * SDX_MAXPAT;
+      if (m >= nvalid) break;
+      const int msg = msg_of[m];
+      int np = b.npat_dev[msg];
+      np = np > SDX_MAXPAT ? SDX_MAXPAT : np;
+      if (k == 0) st_np[m] = (uint8_t)np;
+      if (k >= np) continue;
+      const double v = b.pat_val_dev[msg * SDX_MAXPAT + k];
+      st_id[i] = (uint8_t)((b.pat_id_dev[msg * SDX_MAXPAT + k] - '0') & 15);
+      if constexpr (KIND == SDX_KIND_MU) {
+        const double av = fabs(v);
+        const bool fast = av < 67108864.0 && av == floor(av);  // 2^26; NaN fails
+        st_x[i] = fast ? (uint32_t)av * 10u : 0u;
+        st_f[i] = (uint8_t)((signbit(v) ? 1 : 0) | (fast ? 0 : 2));
+      } else {
+        const int cp = b.cp_slot_dev[msg];
+        const double clk = (cp >= 0 && cp < np) ? fabs(b.pat_val_dev[msg * SDX_MAXPAT + cp]) : 0.0;
+        if (k == 0) st_clk[m] = clk;
+        st_x[i] = (uint32_t)(clk != 0.0 ? py_round1_k(v / clk) : SDX_K_NONE);
+      }
+    }
+  }
   int64_t pf_off = 0;
   int pf_n = 0;
   uint32_t pf_c[MPW][NW <= 4 ? NW : 1];
@@ -1512,15 +1547,40 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     kq[k] = SDX_K_NONE;
   }
   bool lane_ok = false;
+  // MU (lane variant): the integer form of every pattern value for the per-clock normalisation,
+  // x = 10 * |P| when P is integral and |P| < 2^26 (bit k of slowm otherwise: fp64 path), sign in negm
+  uint32_t xk[SDX_MAXPAT];
+  uint32_t negm = 0, slowm = 0;
+#pragma unroll
+  for (int k = 0; k < SDX_MAXPAT; ++k) xk[k] = 0;
   if (mvalid) {
     const int msg = msg_of[mi];
-    npat = b.npat_dev[msg];
-    if (npat > SDX_MAXPAT) npat = SDX_MAXPAT;
+    if constexpr (NW <= 4) {  // the staged pattern tables
+      npat = st_np[mi];
 #pragma unroll
-    for (int k = 0; k < SDX_MAXPAT; ++k) {
-      if (k < npat) {
-        ids |= (uint64_t)((b.pat_id_dev[msg * SDX_MAXPAT + k] - '0') & 15) << (4 * k);
-        val[k] = b.pat_val_dev[msg * SDX_MAXPAT + k];
+      for (int k = 0; k < SDX_MAXPAT; ++k) {
+        if (k < npat) {
+          const int i = mi * SDX_MAXPAT + k;
+          ids |= (uint64_t)st_id[i] << (4 * k);
+          if constexpr (LANE_MU) {
+            xk[k] = st_x[i];
+            const uint32_t f = st_f[i];
+            negm |= (f & 1u) << k;
+            slowm |= ((f >> 1) & 1u) << k;
+          } else {
+            kq[k] = (int)st_x[i];  // MS: k staged (normalised once, by the message's own clock)
+          }
+        }
+      }
+    } else {
+      npat = b.npat_dev[msg];
+      if (npat > SDX_MAXPAT) npat = SDX_MAXPAT;
+#pragma unroll
+      for (int k = 0; k < SDX_MAXPAT; ++k) {
+        if (k < npat) {
+          ids |= (uint64_t)((b.pat_id_dev[msg * SDX_MAXPAT + k] - '0') & 15) << (4 * k);
+          val[k] = b.pat_val_dev[msg * SDX_MAXPAT + k];
+        }
       }
     }
     n = L.nlen[mi];
@@ -1541,14 +1601,23 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     const int msg = msg_of[mi];
     const int cp = b.cp_slot_dev[msg];
     lane_ok = lane_ok && L.digit_ok[mi] && b.ms_ok_dev[msg] && cp >= 0 && cp < npat;
+    if constexpr (NW <= 4) {  // clock and k were staged (st_clk / st_x)
+      clock = st_clk[mi];
+      lane_ok = lane_ok && clock != 0.0;
+      if (!lane_ok) {
 #pragma unroll
-    for (int k = 0; k < SDX_MAXPAT; ++k)
-      if (k == cp) clock = fabs(val[k]);
-    lane_ok = lane_ok && clock != 0.0;
-    if (lane_ok) {
+        for (int k = 0; k < SDX_MAXPAT; ++k) kq[k] = SDX_K_NONE;
+      }
+    } else {
 #pragma unroll
       for (int k = 0; k < SDX_MAXPAT; ++k)
-        if (k < npat) kq[k] = py_round1_k(val[k] / clock);
+        if (k == cp) clock = fabs(val[k]);
+      lane_ok = lane_ok && clock != 0.0;
+      if (lane_ok) {
+#pragma unroll
+        for (int k = 0; k < SDX_MAXPAT; ++k)
+          if (k < npat) kq[k] = py_round1_k(val[k] / clock);
+      }
     }
   }
   // pattern_exists: lane variant on a SpecV (compact MU filter record or full patspec), long
@@ -1626,9 +1695,36 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const double pclk = cld(&fr->clock);
       if (pclk != last_clock) {  // wave-uniform: consecutive protocols often share a clock
         last_clock = pclk;
+        if constexpr (LANE_MU) {
+          // round(P / clock, 1) == k / 10 (message_unsynced.py:64): for integral P and an integral
+          // clock, k = round-half-even(10|P| / |clock|) with the signs applied -- exact, because
+          // fl(P / clock) differs from the rational by < 2^-23 while a non-tie is >= 1 / (2 |clock|)
+          // from a rounding boundary.  Exact ties and the rest use py_round1_k on fl(P / clock).
+          const uint32_t csh = cld(&fr->clk_sh);
+          const uint32_t cc = cld(&fr->clk_c), cm = cld(&fr->clk_m), sh = csh & 0xFFu;
+          const bool ivalid = (csh & 0x100u) != 0, cneg = (csh & 0x200u) != 0;
 #pragma unroll
-        for (int k = 0; k < SDX_MAXPAT; ++k)
-          if (k < npat) kq[k] = py_round1_k(val[k] / pclk);
+          for (int k = 0; k < SDX_MAXPAT; ++k) {
+            if (k < npat) {
+              bool slow = !ivalid || ((slowm >> k) & 1u);
+              int kk = 0;
+              if (!slow) {
+                const uint32_t x = xk[k];
+                const uint32_t q = (uint32_t)(((uint64_t)x * cm) >> sh);
+                const int d2 = 2 * (int)(x - q * cc) - (int)cc;
+                slow = d2 == 0;  // exact rational tie: fp64 decides
+                kk = (int)q + (d2 > 0 ? 1 : 0);
+                if ((((negm >> k) & 1u) != 0) != cneg) kk = -kk;
+              }
+              if (slow) kk = py_round1_k(b.pat_val_dev[msg_of[mi] * SDX_MAXPAT + k] / pclk);
+              kq[k] = kk;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < SDX_MAXPAT; ++k)
+            if (k < npat) kq[k] = py_round1_k(val[k] / pclk);
+        }
       }
       PROF_ADD(1, t_norm);
       auto SV = [&](int key, const sdx_patspec* sp) -> SpecV {
