@@ -159,7 +159,8 @@ def main():
         o = {}
         for i, k in enumerate(kinds):
             n = corp[k].n
-            o[k] = eng.alloc_out(n, caps[k][0] * n + 4096, caps[k][1] * n + 65536)
+            o[k] = eng.alloc_out(n, caps[k][0] * n + 4096, caps[k][1] * n + 65536,
+                                 eng.pulses_work_bytes(n) if k != "MC" else 0)
             o[k]["cursor"] = cursors[s_, i]   # one fill per step resets a slot's cursors
         outs.append(o)
     stream = torch.cuda.current_stream(dev)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 4
+#define SDX_ABI_VERSION 5
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -113,8 +113,16 @@ typedef struct {
   sdx_desc* desc_dev;          /* [n] */
   sdx_result* rec_dev;         /* [rec_cap] */
   uint8_t* heap_dev;           /* [heap_cap] */
-  uint32_t* cursor_dev;        /* [4] zeroed by the caller before the first launch: rec, heap, ovf */
+  uint32_t* cursor_dev;        /* [4] zeroed by the caller before the first launch: rec, heap, ovf,
+                                * workspace bytes taken */
   uint32_t rec_cap, heap_cap;
+  uint8_t* work_dev;           /* optional device workspace (MU/MS short variant, NULL = none), 256-B
+                                * aligned: the message grouping of sdx_demod_pulses (batches of
+                                * >= SDX_GROUP_MIN messages) and after it the spill regions of heavy
+                                * tiles; size it with sdx_pulses_work_bytes().  Without it messages run
+                                * in batch order and a tile whose results overflow LDS is re-run
+                                * (ST_OVF_TILE) */
+  uint64_t work_cap;           /* bytes at work_dev */
 } sdx_out;
 
 typedef struct sdx_bank sdx_bank;
@@ -130,9 +138,15 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
 int sdx_bank_destroy(sdx_bank* bank);
 const void* sdx_bank_device_ptr(const sdx_bank* bank);
 
-/* MU/MS demodulation of a batch: one launch, results appended to out */
+/* MU/MS demodulation of a batch: results appended to out.  With out->work_dev the messages are first
+ * grouped (a per-message key + device radix sort, sdx_group.hip): same results, fewer instructions */
+#define SDX_GROUP_MIN 4096
 int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
                      void* hip_stream);
+/* workspace bytes for sdx_demod_pulses over n messages: the grouping (n >= SDX_GROUP_MIN) plus room
+ * for `spill_tiles` heavy tiles (112 KB each; a tile of 64 messages spills when its results exceed
+ * 512 records / 10 KB of payload / 768 matches in LDS) */
+size_t sdx_pulses_work_bytes(int n, int spill_tiles);
 /* same, for messages of 257..4096 pulses (4 messages per workgroup tile) */
 int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
                           void* hip_stream);

@@ -12,7 +12,8 @@ SRCS = [os.path.join(HERE, "csrc", "sdx_kernels.hip"),   # demodulation kernels 
         os.path.join(HERE, "csrc", "sdx_mn.hip"),        # MN (FSK) engine (sdx_demod_mn)
         os.path.join(HERE, "csrc", "sdx_json.hip"),      # publish-ready JSON (sdx_serialize_json)
         os.path.join(HERE, "csrc", "sdx_units.hip"),     # unit-level helpers (sdx_units)
-        os.path.join(HERE, "csrc", "sdx_exchange.hip")]  # multi-GPU exchange packing (sdx_exchange_pack)
+        os.path.join(HERE, "csrc", "sdx_exchange.hip"),  # multi-GPU exchange packing (sdx_exchange_pack)
+        os.path.join(HERE, "csrc", "sdx_group.hip")]     # MU/MS message grouping (k_sig + radix sort)
 OUT = os.path.join(HERE, "_lib", "libsdx.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]

@@ -1,0 +1,276 @@
+// sdx_group.hip -- message grouping for k_pulses (MU / MS): a per-message key and a device radix
+// sort that orders the batch by it.
+//
+// k_pulses runs its filter with lane = message and one protocol per wave (scalar bank records).
+// The expensive part of pattern_exists (pattern_utils.py:86-136: combinations, substring searches)
+// runs for a wave when ANY of its 64 messages has candidates for every value of the protocol's
+// keys (the cheap first step, :53-80); on a random message order about a third of the lanes of
+// such a wave do.  Sorting the messages by WHICH protocols they pass that cheap step puts messages
+// with the same candidate protocols into one tile (the bench corpus runs 2.3x fewer
+// wave-iterations of the expensive part, at 2.3x the lane occupancy).  The key only orders the
+// work: every message still runs against the whole bank and results are placed by message index,
+// so the output is identical (tests/test_gpu_parity.py runs both orders).  GPU tiles finish in any
+// order anyway: consumers read results through the descriptors (sdx_desc.rec_begin / n_rec).
+#include "sdx_device.h"
+#include "sdx_lane.h"
+
+namespace sdx {
+
+// lanes below this one in `mask`
+SDX_DEV int lanes_below_mask(uint64_t mask) {
+  const int l = lane_id();
+  return popc64(l ? (mask & ((1ull << l) - 1)) : 0ull);
+}
+// the lanes of the wave (among `active`) whose 8-bit value equals this lane's
+SDX_DEV uint64_t peers8(uint32_t v, bool active) {
+  uint64_t peers = ballot(active);
+#pragma unroll
+  for (int bit = 0; bit < 8; ++bit) {
+    const uint64_t bb = ballot(active && ((v >> bit) & 1u));
+    peers &= ((v >> bit) & 1u) ? bb : ~bb;
+  }
+  return peers;
+}
+
+// ---------------------------------------------------------------------------------------------
+// the key: bit 31 - r = the message passes the candidate-interval test of the first search list of
+// protocol r (bank order, r < 32) -- start, else one, for MU after round(P / clockabs, 1)
+// (message_unsynced.py:64); the clockabs gate and sync for MS (message_synced.py:64-88, 128).
+// Lane = message; the protocol loop is uniform (scalar record loads).  (Measured on the bench
+// corpus: the first list groups better than all of a protocol's lists, and bank order better than
+// the clock-grouped processing order.)
+// ---------------------------------------------------------------------------------------------
+constexpr int SIG_PROTOS = 32;
+template <int KIND>
+__global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_pulse_batch b, uint32_t* __restrict__ key,
+                                             uint32_t* __restrict__ msg_out) {
+  const BankView bv = bank_view(bank);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const bool valid = i < ntot;
+  const int msg = valid ? (b.sel_dev ? b.sel_dev[i] : i) : 0;
+  int npat = valid ? b.npat_dev[msg] : 0;
+  npat = npat > SDX_MAXPAT ? SDX_MAXPAT : npat;
+  double val[SDX_MAXPAT];
+#pragma unroll
+  for (int k = 0; k < SDX_MAXPAT; ++k) val[k] = k < npat ? b.pat_val_dev[msg * SDX_MAXPAT + k] : 0.0;
+  int kq[SDX_MAXPAT];
+  uint32_t sig = 0;
+  // the candidate test of one search list: every unique value has a slot in [klo, khi]
+  auto keys_ok = [&](const SpecV& sv) -> bool {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < SDX_MAXUNIQ; ++u) {
+      if (u < sv.nu) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < SDX_MAXPAT; ++j) any |= k_in(kq[j], sv.klo[u], sv.khi[u]);
+        ok = ok && any;
+      }
+    }
+    return ok;
+  };
+  if constexpr (KIND == SDX_KIND_MU) {
+    // round(P / clockabs, 1) * 10 in fp32: the key only orders the work, so a value that lands on
+    // the other side of an interval border than the exact fp64 test would costs nothing but grouping
+    float x10[SDX_MAXPAT];
+#pragma unroll
+    for (int k = 0; k < SDX_MAXPAT; ++k) x10[k] = (float)(val[k] * 10.0);
+    const int nr = (int)bv.hdr->n_mu < SIG_PROTOS ? (int)bv.hdr->n_mu : SIG_PROTOS;
+    double last = __builtin_nan("");
+    for (int r = 0; r < nr; ++r) {
+      const sdx_mu_filt* fr = uniform_ptr(bv.mufilt + r);
+      const sdx_mu_proto* rec = uniform_ptr(bv.mu + r);
+      const uint32_t ff = cld(&fr->flags);
+      bool ok = !(ff & 2u) && (ff & 4u);  // active, not never
+      if (ok) {
+        const double pclk = cld(&fr->clock);
+        if (pclk != last) {
+          last = pclk;
+          const float inv = 1.0f / (float)pclk;
+#pragma unroll
+          for (int k = 0; k < SDX_MAXPAT; ++k) {
+            const float q = x10[k] * inv;
+            kq[k] = (k < npat && fabsf(q) < 1.0e8f) ? (int)rintf(q) : SDX_K_NONE;
+          }
+        }
+        // the protocol's first search list: start if it has one, else one (the list whose test
+        // decides most often whether k_pulses runs the expensive search for the pair)
+        const bool full = (ff & 8u) != 0;
+        const int k = (ff & 1u) ? 0 : 1;
+        const SpecV sv = full ? spec_full(k == 0 ? &rec->start : &rec->one)
+                              : spec_compact(&fr->spec[k], k == 0 ? cld(&fr->start_upk) : (uint64_t)cld(&fr->spec[k].upk));
+        if (sv.slen) ok = ok && keys_ok(sv);
+      }
+      sig |= (uint32_t)ok << (31 - r);
+    }
+  } else {
+    const int cp = valid ? b.cp_slot_dev[msg] : -1;
+    double clock = 0.0;
+#pragma unroll
+    for (int k = 0; k < SDX_MAXPAT; ++k)
+      if (k == cp) clock = fabs(val[k]);
+    const bool gate = valid && b.ms_ok_dev[msg] && cp >= 0 && cp < npat && clock != 0.0;
+    const float inv = clock != 0.0 ? (float)(10.0 / clock) : 0.0f;  // fp32 is enough for a grouping key
+#pragma unroll
+    for (int k = 0; k < SDX_MAXPAT; ++k) {
+      const float q = (float)val[k] * inv;
+      kq[k] = (gate && k < npat && fabsf(q) < 1.0e8f) ? (int)rintf(q) : SDX_K_NONE;
+    }
+    const int nr = (int)bv.hdr->n_ms < SIG_PROTOS ? (int)bv.hdr->n_ms : SIG_PROTOS;
+    for (int r = 0; r < nr; ++r) {
+      const sdx_ms_filt* fr = uniform_ptr(bv.msfilt + r);
+      const sdx_ms_proto* rec = uniform_ptr(bv.ms + r);
+      const uint32_t ff = cld(&fr->flags);
+      bool ok = gate && !(ff & 2u);
+      const double pclk = cld(&fr->pclock);
+      if (ok && pclk > 0.0) ok = !(fabs(pclk - clock) > clock * 0.3);
+      if (ok) {  // the sync list (searched first, message_synced.py:128-143)
+        const bool full = (ff & 8u) != 0;
+        const SpecV sv = full ? spec_full(&rec->key[0]) : spec_compact(&fr->spec[0], cld(&fr->sync_upk));
+        if (sv.slen) ok = ok && keys_ok(sv);
+      }
+      sig |= (uint32_t)ok << (31 - r);
+    }
+  }
+  if (valid) {
+    key[i] = sig;
+    msg_out[i] = (uint32_t)msg;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// stable LSD radix sort of (key, message) pairs: 4 passes of 8 bits over partitions of RS_PART
+// elements; per pass the partitions' digit counts (k_rs_hist), their prefix over the partitions (a
+// wave per digit, k_rs_scan_rows) and the scatter (k_rs_scatter, which also scans the 256 digit
+// totals).  No inter-workgroup waiting: a decoupled look-back sort is latency-bound at these sizes.
+// ---------------------------------------------------------------------------------------------
+constexpr int RS_T = 512, RS_ROUNDS = 4, RS_PART = RS_T * RS_ROUNDS;
+
+// hist[digit * np + part] = elements of the partition with that digit in pass d
+__global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ key, int n, int np, int d,
+                                                  uint32_t* __restrict__ hist) {
+  __shared__ uint32_t c[256];
+  const int tid = threadIdx.x, p = blockIdx.x;
+  if (tid < 256) c[tid] = 0;
+  __syncthreads();
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int e = p * RS_PART + r * RS_T + tid;
+    const bool valid = e < n;
+    const uint32_t dig = valid ? (key[e] >> (8 * d)) & 255u : 0u;
+    const uint64_t peers = peers8(dig, valid);
+    if (valid && lane_id() == ffs64(peers)) atomicAdd(&c[dig], (uint32_t)popc64(peers));
+  }
+  __syncthreads();
+  if (tid < 256) hist[(size_t)tid * np + p] = c[tid];
+}
+
+// each digit's row: exclusive prefix over the partitions (one wave per row); tot[digit] = total
+__global__ __launch_bounds__(256) void k_rs_scan_rows(uint32_t* __restrict__ hist, int np, uint32_t* __restrict__ tot) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint32_t* h = hist + (size_t)row * np;
+  uint32_t run = 0;
+  for (int b0 = 0; b0 < np; b0 += 64) {
+    const int x = b0 + lane;
+    const uint32_t v = x < np ? h[x] : 0u;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (x < np) h[x] = run + incl - v;
+    run += __shfl(incl, 63);
+  }
+  if (lane == 0) tot[row] = run;
+}
+
+// pass d: every partition scatters its elements, in order (stable), to
+// (digit base = prefix of the digit totals) + (row offset of the partition) + (rank inside it)
+__global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     int n, int np, int d, const uint32_t* __restrict__ hist,
+                                                     const uint32_t* __restrict__ tot, uint32_t* __restrict__ kout,
+                                                     uint32_t* __restrict__ vout) {
+  __shared__ uint32_t run[256];
+  __shared__ uint32_t wc[RS_T / 64][256];
+  const int tid = threadIdx.x, p = blockIdx.x, wave = tid >> 6;
+  const uint32_t t = tid < 256 ? tot[tid] : 0u;
+  if (tid < 256) run[tid] = t;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the digit totals
+    const uint32_t y = (tid < 256 && tid >= o) ? run[tid - o] : 0u;
+    __syncthreads();
+    if (tid < 256) run[tid] += y;
+    __syncthreads();
+  }
+  if (tid < 256) run[tid] = run[tid] - t + hist[(size_t)tid * np + p];
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int e = p * RS_PART + r * RS_T + tid;
+    const bool valid = e < n;
+    const uint32_t k = valid ? kin[e] : 0u;
+    const uint32_t v = valid ? vin[e] : 0u;
+    const uint32_t dig = (k >> (8 * d)) & 255u;
+    for (int x = tid; x < RS_T / 64 * 256; x += RS_T) (&wc[0][0])[x] = 0;
+    __syncthreads();
+    const uint64_t peers = peers8(dig, valid);
+    if (valid && lane_id() == ffs64(peers)) wc[wave][dig] = (uint32_t)popc64(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = run[dig] + (uint32_t)lanes_below_mask(peers);
+      for (int w = 0; w < wave; ++w) pos += wc[w][dig];
+      kout[pos] = k;
+      vout[pos] = v;
+    }
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t add = 0;
+#pragma unroll
+      for (int w = 0; w < RS_T / 64; ++w) add += wc[w][tid];
+      run[tid] += add;
+    }
+    __syncthreads();
+  }
+}
+
+constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// workspace of the grouping: keys and message indices (two copies each) + the sort's counts
+size_t group_bytes(int n) {
+  if (n <= 0) return 0;
+  const size_t np = (size_t)(n + RS_PART - 1) / RS_PART;
+  return 4 * align256(4 * (size_t)n) + align256(4 * 256 * np) + align256(4 * 256);
+}
+
+// The grouped order of a batch's messages into `work`; returns the device list of message indices
+// (the sel_dev of the k_pulses launch), or nullptr.
+const int32_t* group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, uint8_t* work, size_t bytes,
+                              hipStream_t st) {
+  const int n = b.sel_dev ? b.n_sel : b.n;
+  const size_t need = group_bytes(n);
+  if (!need || bytes < need) return nullptr;
+  const int np = (n + RS_PART - 1) / RS_PART;
+  const size_t a = align256(4 * (size_t)n);
+  uint32_t* k0 = reinterpret_cast<uint32_t*>(work);
+  uint32_t* v0 = reinterpret_cast<uint32_t*>(work + a);
+  uint32_t* k1 = reinterpret_cast<uint32_t*>(work + 2 * a);
+  uint32_t* v1 = reinterpret_cast<uint32_t*>(work + 3 * a);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(work + 4 * a);
+  uint32_t* tot = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)np));
+  const int grid = (n + 255) / 256;
+  if (kind == SDX_KIND_MU)
+    hipLaunchKernelGGL((k_sig<SDX_KIND_MU>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0);
+  else
+    hipLaunchKernelGGL((k_sig<SDX_KIND_MS>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0);
+  for (int d = 0; d < 4; ++d) {  // (k0, v0) -> (k1, v1) -> (k0, v0) -> ...: the result is back in v0
+    const bool even = (d & 1) == 0;
+    uint32_t* kin = even ? k0 : k1;
+    hipLaunchKernelGGL(k_rs_hist, dim3(np), dim3(RS_T), 0, st, kin, n, np, d, hist);
+    hipLaunchKernelGGL(k_rs_scan_rows, dim3(256 / 4), dim3(256), 0, st, hist, np, tot);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(np), dim3(RS_T), 0, st, kin, even ? v0 : v1, n, np, d, hist, tot,
+                       even ? k1 : k0, even ? v1 : v0);
+  }
+  if (hipGetLastError() != hipSuccess) return nullptr;
+  return reinterpret_cast<const int32_t*>(v0);
+}
+
+}  // namespace sdx

@@ -26,6 +26,10 @@
 #include <string>
 #include <type_traits>
 
+#ifdef SDX_WGTIME
+// diagnostic build only (tools/wg_timeline.py): per-workgroup start / end stamps (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_wgt[2 * 65536];
+#endif
 #ifdef SDX_PROF
 __device__ unsigned long long g_prof[32];
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -77,7 +81,10 @@ struct MuItem {
   uint8_t mi, fmask;        // tile message, found-key mask
 };
 constexpr int QCAP = 128;  // per-wave ring: < 64 pending before a push of <= 64
-constexpr int LANE_WAVES = 8;  // lane-decode MU variant: 8 waves (512 threads) share one tile
+#ifndef SDX_LANE_WAVES
+#define SDX_LANE_WAVES 8
+#endif
+constexpr int LANE_WAVES = SDX_LANE_WAVES;  // short variants: 8 waves (512 threads) share one tile
 
 // MS (NW <= 4): a (message, protocol) pair that passed the sync/one/zero/float lookups, queued
 // for the lane decode
@@ -110,7 +117,20 @@ struct MuMatch {
   uint8_t flags;         // bit0 tail matched, bits1-2 tail symbol, bits3-5 found-key mask
   uint8_t j;             // match index within the (message, protocol) pair
 };
-constexpr int MATCH_CAP = 768;  // per tile (bench corpus: mean 290, max 513); more -> tile overflow -> exact re-run
+constexpr int MATCH_CAP = 768;  // per tile in LDS (bench corpus: mean 290, max 513); more -> the spill region
+
+// Heavy tiles (a grouped message order puts messages with many results together: up to ~2000
+// results and ~37 KB of payload per tile on the bench corpus) overflow the LDS pools into a
+// per-tile region of the caller's workspace (sdx_out.work_dev), allocated by the first result
+// that needs it: matches, staged records and payload bytes.  Only past these does a tile
+// overflow (ST_OVF_TILE -> exact re-run).
+constexpr uint32_t SPILL_M = 2048, SPILL_R = 2048, SPILL_H = 49152;
+constexpr uint32_t SPILL_OFF_R = SPILL_M * 16, SPILL_OFF_H = SPILL_OFF_R + SPILL_R * 16;
+constexpr uint32_t SPILL_BYTES = SPILL_OFF_H + SPILL_H;  // 112 KB
+constexpr uint32_t SPILL_NONE = 0xFFFFFFFFu, SPILL_PENDING = 0xFFFFFFFEu;
+constexpr uint32_t HEAP_SPILLED = 0x80000000u;  // StageRec.off: payload in the spill region
+constexpr uint8_t REC_HOLE = 0xFF;              // StageRec.msg: LDS slot left unused (result spilled)
+static_assert(sizeof(MuMatch) == 16, "MuMatch spill layout");
 
 // LM: 0 = wave-cooperative decode (the long variants), 1 = lane-decode MU (NW <= 4: decode
 // descriptors, modulematch tables, match list), 2 = lane-decode MS (NW <= 4).  The lane variants
@@ -150,6 +170,7 @@ struct TileLds {
   StageRec rec[PREC];
   alignas(16) uint8_t heap[PHEAP];
   unsigned long long pool_ctr;  // low 32: staged records, high 32: staged heap bytes (one LDS atomic)
+  uint32_t spill_base, sp_rec, sp_heap;  // the tile's spill region (SPILL_NONE: none yet) and its fill
   int ovf, next_p;
   int mm_states, nmatch;
   MuMatch mlist[LM == 1 ? MATCH_CAP : 1];
@@ -215,6 +236,60 @@ SDX_DEV void pool_commit(T& L, int slot, int wave, int msg_local, int proto, int
     L.rec[slot] = r;
   }
   wave_sync();
+}
+
+// the tile's spill region in the workspace (allocated once, by the first lane that needs it), or
+// SPILL_NONE when the workspace is absent or exhausted
+template <class T>
+SDX_DEV uint32_t spill_region(T& L, const sdx_out& out) {
+  uint32_t b = __hip_atomic_load(&L.spill_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (b >= SPILL_PENDING) {  // none yet: one leader lane per wave; the first leader allocates, the
+                             // others wait for its address (waves progress independently)
+    const int leader = ffs64(ballot(true));
+    if (lane_id() == leader) {
+      uint32_t cur = atomicCAS(&L.spill_base, SPILL_NONE, SPILL_PENDING);
+      if (cur == SPILL_NONE) {
+        cur = atomicAdd(&out.cursor_dev[3], SPILL_BYTES);
+        __hip_atomic_store(&L.spill_base, cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      while (cur == SPILL_PENDING) cur = __hip_atomic_load(&L.spill_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      b = cur;
+    }
+    b = (uint32_t)__shfl((int)b, leader);
+  }
+  if (!out.work_dev || (uint64_t)b + SPILL_BYTES > out.work_cap) return SPILL_NONE;
+  return b;
+}
+
+// one staged result (lane-level writers): record slot + `span` payload bytes (multiple of 8) in the
+// tile's LDS pool, else in its spill region; false (tile overflow) when neither has room
+struct PoolSlot {
+  StageRec* rec;
+  uint8_t* heap;
+  uint32_t off;  // StageRec.off
+};
+template <class T>
+SDX_DEV bool pool_take(T& L, const sdx_out& out, int span, PoolSlot* ps) {
+  const unsigned long long o = atomicAdd(&L.pool_ctr, ((unsigned long long)span << 32) | 1ull);
+  const int slot = (int)(uint32_t)o, off = (int)(o >> 32);
+  if (slot < T::PREC && off + span <= T::PHEAP) {
+    ps->rec = &L.rec[slot];
+    ps->heap = L.heap + off;
+    ps->off = (uint32_t)off;
+    return true;
+  }
+  if (slot < T::PREC) L.rec[slot].msg = REC_HOLE;  // skipped by the flush
+  const uint32_t base = spill_region(L, out);
+  const uint32_t rs = atomicAdd(&L.sp_rec, 1u), hs = atomicAdd(&L.sp_heap, (uint32_t)span);
+  if (base == SPILL_NONE || rs >= SPILL_R || hs + (uint32_t)span > SPILL_H) {
+    L.ovf = 1;
+    return false;
+  }
+  uint8_t* reg = out.work_dev + base;
+  ps->rec = reinterpret_cast<StageRec*>(reg + SPILL_OFF_R) + rs;
+  ps->heap = reg + SPILL_OFF_H + hs;
+  ps->off = HEAP_SPILLED | hs;
+  return true;
 }
 
 // copy a bank string to LDS (lanes in parallel)
@@ -616,7 +691,7 @@ SDX_DEV void sym_masks(const uint64_t* bm, uint64_t ut0, uint64_t ut1, uint64_t 
 }
 
 template <int NW, class T>
-SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
+SDX_DEV void finish_mu_lane(T& L, const sdx_out& out, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
                             int mi, int j,
                             int q, int k, int Lw, bool emf, uint8_t esym, const M<NW>& V1, const M<NW>& VF) {
   constexpr int NB = 64 * NW + 64;
@@ -745,13 +820,9 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   // payload (:271-274): preamble + digits + postamble into an 8-byte aligned pool slot
   const int total = pre_len + dlen + post_len;
   const int span = (total + 7) & ~7;
-  const unsigned long long o = atomicAdd(&L.pool_ctr, ((unsigned long long)span << 32) | 1ull);
-  const int slot = (int)(uint32_t)o, off = (int)(o >> 32);
-  if (slot >= T::PREC || off + span > T::PHEAP) {
-    L.ovf = 1;
-    return;
-  }
-  ByteWriter w(reinterpret_cast<uint64_t*>(L.heap + off));
+  PoolSlot ps;
+  if (!pool_take(L, out, span, &ps)) return;
+  ByteWriter w(reinterpret_cast<uint64_t*>(ps.heap));
   if (pre_g) {
     put_str(w, pre_g, pre_len);
   } else {
@@ -777,7 +848,7 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   }
   w.flush();
   StageRec r;
-  r.off = (uint32_t)off;
+  r.off = ps.off;
   r.len = (uint16_t)total;
   r.proto = (uint16_t)p;
   r.bitlen = (uint32_t)nbp;
@@ -785,13 +856,13 @@ SDX_DEV void finish_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
   r.wave = (uint8_t)wave;
   r.rank = (uint16_t)j;  // match index within this (message, protocol) pair: monotone
   PROF_CNTL(20);
-  L.rec[slot] = r;
+  *ps.rec = r;
   PROF_ADDD(8, t_wr);
 }
 
 // MU, lane = message: exact re.finditer emulation on register bitmasks (message_unsynced.py:146-290)
 template <int NW, class T>
-SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
+SDX_DEV void decode_mu_lane(T& L, const sdx_out& out, int wave, const BankView& bv, const sdx_mu_proto* rec, const sdx_mu_desc& d, int p,
                             int mi, const uint64_t* bm, int n, int idx, uint64_t st_tgt, uint64_t ut0, uint64_t ut1,
                             uint64_t ut2, int fmask) {
   PROF_T(t_setup);
@@ -859,9 +930,16 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
     if (nch > (int)d.lmax) continue;  // (:217-218); 65535 = none
     PROF_CNTL(22);
     const int slot = atomicAdd(&L.nmatch, 1);  // finished after the protocol loop, lane = match
-    if (slot >= MATCH_CAP) {
-      L.ovf = 1;
-      return;
+    MuMatch* dst;
+    if (slot < MATCH_CAP) {
+      dst = &L.mlist[slot];
+    } else {  // heavy tile: the spill region
+      const uint32_t base = spill_region(L, out);
+      if (base == SPILL_NONE || slot >= MATCH_CAP + (int)SPILL_M) {
+        L.ovf = 1;
+        return;
+      }
+      dst = reinterpret_cast<MuMatch*>(out.work_dev + base) + (slot - MATCH_CAP);
     }
     MuMatch mm;
     mm.q = (uint16_t)q;
@@ -874,7 +952,7 @@ SDX_DEV void decode_mu_lane(T& L, int wave, const BankView& bv, const sdx_mu_pro
     mm.flags = (uint8_t)((emf ? 1 : 0) | (esym << 1) | (fmask << 3));
     mm.j = (uint8_t)(nfin < 255 ? nfin : 255);
     ++nfin;
-    L.mlist[slot] = mm;
+    *dst = mm;
   }
 }
 
@@ -1041,7 +1119,7 @@ SDX_DEV MsDesc ms_desc(const sdx_ms_proto* rec) {
 // finish one MS result from its packed bits (P1 = '1', PF = 'F', nb bits): length_in_range,
 // padding BEFORE postDemod, postDemod without try, hex (None -> skipped), payload
 template <int NW, class T>
-SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, int mi, const M<NW>& P1,
+SDX_DEV void finish_ms_lane(T& L, const sdx_out& out, const BankView& bv, const MsDesc& D, int p, int mi, const M<NW>& P1,
                             const M<NW>& PF, int nb) {
   constexpr int NB = 64 * NW + 64;
   const int lir_min = D.lir_min, lir_max = D.lir_max, pad = D.pad;
@@ -1091,13 +1169,9 @@ SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, in
   const uint8_t* post = bv.str + post_off;
   const int total = pre_len + nd + post_len;
   const int span = (total + 7) & ~7;
-  const unsigned long long o = atomicAdd(&L.pool_ctr, ((unsigned long long)span << 32) | 1ull);
-  const int slot = (int)(uint32_t)o, off = (int)(o >> 32);
-  if (slot >= T::PREC || off + span > T::PHEAP) {
-    L.ovf = 1;
-    return;
-  }
-  ByteWriter w(reinterpret_cast<uint64_t*>(L.heap + off));
+  PoolSlot ps;
+  if (!pool_take(L, out, span, &ps)) return;
+  ByteWriter w(reinterpret_cast<uint64_t*>(ps.heap));
   put_str(w, pre, pre_len);
   if (!usearr) {
     for (int t = 0; t < nd; t += 8) {
@@ -1118,18 +1192,18 @@ SDX_DEV void finish_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, in
   put_str(w, post, post_len);
   w.flush();
   StageRec r;
-  r.off = (uint32_t)off;
+  r.off = ps.off;
   r.len = (uint16_t)total;
   r.proto = (uint16_t)p;
   r.bitlen = (uint32_t)nbits;
   r.msg = (uint8_t)mi;
   r.wave = 0;
   r.rank = 0;  // one result per (message, protocol)
-  L.rec[slot] = r;
+  *ps.rec = r;
 }
 
 template <int NW, class T>
-SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, int mi, const uint64_t* bm,
+SDX_DEV void decode_ms_lane(T& L, const sdx_out& out, const BankView& bv, const MsDesc& D, int p, int mi, const uint64_t* bm,
                             int n, int start, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3, int fmask) {
   const int Wd = D.width;
   const uint64_t kt[4] = {k0, k1, k2, k3};
@@ -1225,7 +1299,7 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, in
     if (extra == 2) m_set(PF, nb);
     ++nb;
   }
-  finish_ms_lane<NW>(L, bv, D, p, mi, P1, PF, nb);
+  finish_ms_lane<NW>(L, out, bv, D, p, mi, P1, PF, nb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1237,23 +1311,40 @@ SDX_DEV void decode_ms_lane(T& L, const BankView& bv, const MsDesc& D, int p, in
 // ---------------------------------------------------------------------------------------------
 template <int NW, int TM, int LM>
 SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
+  using T = TileLds<NW, TM, LM>;
   const int tid = threadIdx.x;
+  // staged records: the LDS pool [0, nr_l), then (lane writers of heavy tiles) the spill region
+  // [nr_l, nr); payload bytes likewise (StageRec.off with HEAP_SPILLED: spill region)
+  constexpr int RMAX = T::PREC + (LM != 0 ? (int)SPILL_R : 0);
   // flush scratch aliases the id bitmaps (dead once every wave has left the protocol loop)
-  static_assert(sizeof(L.bm) >= TM * 8 + TileLds<NW, TM, LM>::PREC * 2, "flush scratch does not fit the bitmaps");
+  static_assert(sizeof(L.bm) >= TM * 8 + RMAX * 2, "flush scratch does not fit the bitmaps");
   uint32_t* fill = reinterpret_cast<uint32_t*>(L.bm);       // bucket fill per message
   uint32_t* cntm = fill + TM;                               // staged records per message
-  uint16_t* bidx = reinterpret_cast<uint16_t*>(cntm + TM);  // pool records bucketed by message
+  uint16_t* bidx = reinterpret_cast<uint16_t*>(cntm + TM);  // record indices bucketed by message
   if (tid < TM) {
     fill[tid] = 0;
     cntm[tid] = 0;
   }
   __syncthreads();
-  const int nr = (int)(uint32_t)L.pool_ctr;
-  const int nh = (int)(L.pool_ctr >> 32);
+  const int nr_l = (int)(uint32_t)L.pool_ctr < T::PREC ? (int)(uint32_t)L.pool_ctr : T::PREC;
+  const int nh_raw = (int)(L.pool_ctr >> 32);
+  const int nh_l = nh_raw < T::PHEAP ? nh_raw : T::PHEAP;
+  const bool spill = LM != 0 && L.spill_base < SPILL_PENDING;
+  const int nr_s = spill ? ((int)L.sp_rec < (int)SPILL_R ? (int)L.sp_rec : (int)SPILL_R) : 0;
+  const int nh_s = spill ? ((int)L.sp_heap < (int)SPILL_H ? (int)L.sp_heap : (int)SPILL_H) : 0;
+  const int nr = nr_l + nr_s;
+  const uint8_t* sreg = spill ? out.work_dev + L.spill_base : nullptr;
+  auto rec_at = [&](int i) -> StageRec {
+    return i < nr_l ? L.rec[i] : reinterpret_cast<const StageRec*>(sreg + SPILL_OFF_R)[i - nr_l];
+  };
   const bool ovf = L.ovf != 0;
   if (!ovf)
-    for (int r = tid; r < nr; r += blockDim.x) atomicAdd(&cntm[L.rec[r].msg], 1u);
+    for (int r = tid; r < nr; r += blockDim.x) {
+      const int m = rec_at(r).msg;
+      if (m != REC_HOLE) atomicAdd(&cntm[m], 1u);
+    }
   __syncthreads();
+  const uint32_t nh_l16 = ((uint32_t)nh_l + 15u) & ~15u;
   if (tid == 0) {
     int bad = ovf ? 1 : 0;
     uint32_t nrec = 0;
@@ -1261,7 +1352,8 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       L.mbase[m] = nrec;
       if (L.raise_key[m] == 0xFFFFFFFFu && !bad) nrec += cntm[m];
     }
-    const uint32_t nheap = bad ? 0u : (((uint32_t)nh + 15u) & ~15u);  // 16-B pieces: full-width copy
+    // 16-B pieces: full-width copies
+    const uint32_t nheap = bad ? 0u : nh_l16 + (((uint32_t)nh_s + 15u) & ~15u);
     uint32_t rb = 0, hb = 0;
     if (!bad) {
       rb = atomicAdd(&out.cursor_dev[0], nrec);
@@ -1282,24 +1374,24 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
   const int bad = L.tile_bad;  // block-uniform
   if (!bad) {
     for (int r = tid; r < nr; r += blockDim.x) {
-      const int m = L.rec[r].msg;
-      if (L.raise_key[m] != 0xFFFFFFFFu) continue;
+      const int m = rec_at(r).msg;
+      if (m == REC_HOLE || L.raise_key[m] != 0xFFFFFFFFu) continue;
       const uint32_t b = atomicAdd(&fill[m], 1u);
       bidx[L.mbase[m] + b] = (uint16_t)r;
     }
     __syncthreads();
     const int nt = (int)L.tot_rec;
     for (int j = tid; j < nt; j += blockDim.x) {
-      const StageRec sr = L.rec[bidx[j]];
+      const StageRec sr = rec_at(bidx[j]);
       const uint32_t key = ((uint32_t)sr.proto << 16) | sr.rank;
       const uint32_t b0 = L.mbase[sr.msg], b1 = b0 + cntm[sr.msg];
       uint32_t rk = 0;
       for (uint32_t i = b0; i < b1; ++i) {
-        const StageRec& o = L.rec[bidx[i]];
+        const StageRec o = rec_at(bidx[i]);
         rk += (((uint32_t)o.proto << 16) | o.rank) < key ? 1u : 0u;
       }
       sdx_result o;
-      o.payload_off = L.heap_base + sr.off;
+      o.payload_off = L.heap_base + ((sr.off & HEAP_SPILLED) ? nh_l16 + (sr.off & ~HEAP_SPILLED) : sr.off);
       o.payload_len = sr.len;
       o.proto = sr.proto;
       o.bit_length = sr.bitlen;
@@ -1308,12 +1400,19 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
     }
     uint8_t* hd = out.heap_dev + L.heap_base;
     if ((((uintptr_t)hd) & 15u) == 0) {  // 16-B stores (every tile reserves a multiple of 16 B)
-      const int n16 = (nh + 15) >> 4;
+      const int n16 = (nh_l + 15) >> 4;
       const uint4* src = reinterpret_cast<const uint4*>(L.heap);
       uint4* dst = reinterpret_cast<uint4*>(hd);
       for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
+      const int s16 = (nh_s + 15) >> 4;
+      if (s16) {
+        const uint4* ssrc = reinterpret_cast<const uint4*>(sreg + SPILL_OFF_H);
+        uint4* sdst = reinterpret_cast<uint4*>(hd + nh_l16);
+        for (int i = tid; i < s16; i += blockDim.x) sdst[i] = ssrc[i];
+      }
     } else {
-      for (int i = tid; i < nh; i += blockDim.x) hd[i] = L.heap[i];
+      for (int i = tid; i < nh_l; i += blockDim.x) hd[i] = L.heap[i];
+      for (int i = tid; i < nh_s; i += blockDim.x) hd[nh_l16 + i] = sreg[SPILL_OFF_H + i];
     }
   }
   for (int m = tid; m < nvalid; m += blockDim.x) {
@@ -1345,11 +1444,11 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
 template <int KIND, int NW>
 constexpr int pulses_threads() { return NW <= 4 ? 64 * LANE_WAVES : 256; }
 template <int KIND, int NW>
-constexpr int pulses_min_blocks() { return NW <= 4 ? 2 : 1; }
+constexpr int pulses_min_blocks() { return NW <= 4 ? 16 / LANE_WAVES : 1; }
 
 template <int KIND, int NW, int TM>
 __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
-    (pulses_min_blocks<KIND, NW>() == 2 ? 4 : 1)))) void k_pulses(
+    (NW <= 4 ? 4 : 1)))) void k_pulses(
     const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
   constexpr bool LANE_MU = KIND == SDX_KIND_MU && NW <= 4;
   constexpr bool LANE_MS = KIND == SDX_KIND_MS && NW <= 4;
@@ -1360,6 +1459,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   const int ntot = b.sel_dev ? b.n_sel : b.n;
   const int tile0 = blockIdx.x * TM;
   const int nvalid = (ntot - tile0 < TM) ? ntot - tile0 : TM;
+#ifdef SDX_WGTIME
+  if (tid == 0 && blockIdx.x < 65536) g_wgt[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ int msg_of[TM];
   if (tid < TM) {
     msg_of[tid] = (tid < nvalid) ? (b.sel_dev ? b.sel_dev[tile0 + tid] : tile0 + tid) : 0;
@@ -1370,6 +1472,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     L.next_p = 0;
     L.nmatch = 0;
     L.pool_ctr = 0;
+    L.spill_base = SPILL_NONE;
+    L.sp_rec = 0;
+    L.sp_heap = 0;
     L.ovf = 0;
     L.nsurv = 0;
   }
@@ -1651,7 +1756,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           if (qp < SDX_MUDESC_LDS) d = L.desc[qp];
           else d = bv.mudesc[qp];
           PROF_CNTL(21);
-          decode_mu_lane<NW>(L, wave, bv, bv.mu + qp, d, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx,
+          decode_mu_lane<NW>(L, out, wave, bv, bv.mu + qp, d, qp, qm, &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.idx,
                              ((uint64_t)it.st_hi << 32) | it.st_lo, it.u0, it.u1, it.u2, it.fmask);
         }
       }
@@ -1902,7 +2007,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         const int qm = it.mi, qp = it.p;
         const uint32_t rk = L.raise_key[qm];
         if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp)
-          decode_ms_lane<NW>(L, bv, qp < MS_DESC_LDS ? L.msdesc[qp] : ms_desc(bv.ms + qp), qp, qm,
+          decode_ms_lane<NW>(L, out, bv, qp < MS_DESC_LDS ? L.msdesc[qp] : ms_desc(bv.ms + qp), qp, qm,
                              &L.bm[qm * T::MSTRIDE], L.nlen[qm], it.start,
                              ((uint64_t)it.k0_hi << 32) | it.k0_lo, it.k1, it.k2, it.k3, it.fmask);
       }
@@ -1921,7 +2026,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       for (int i = tid; i < m16; i += blockDim.x) mdst[i] = msrc[i];
       __syncthreads();
     }
-    const int nm = L.nmatch < MATCH_CAP ? L.nmatch : MATCH_CAP;
+    // matches past MATCH_CAP are in the spill region (a tile that overflowed is re-run: none then)
+    const int nm = L.ovf ? 0 : (L.nmatch < MATCH_CAP + (int)SPILL_M ? L.nmatch : MATCH_CAP + (int)SPILL_M);
+    const MuMatch* spilled = nm > MATCH_CAP ? reinterpret_cast<const MuMatch*>(out.work_dev + L.spill_base) : nullptr;
     // group the matches by protocol (counting sort into the free half of the queue region):
     // lanes of one wave then follow the same postDemod / modulematch / formatting path
     constexpr int NBIN = 256;
@@ -1929,7 +2036,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     uint16_t* perm = reinterpret_cast<uint16_t*>(L.u.mmtab + SDX_MMTAB_LDS);
     uint32_t* bin = reinterpret_cast<uint32_t*>(perm + MATCH_CAP);
 #ifndef SDX_X_NOSORT
-    const bool sorted = (int)bv.hdr->n_mu <= NBIN;
+    const bool sorted = (int)bv.hdr->n_mu <= NBIN && nm <= MATCH_CAP;
 #else
     const bool sorted = false;  // timing experiment
 #endif
@@ -1963,7 +2070,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       __syncthreads();
     }
     for (int i = tid; i < nm; i += blockDim.x) {
-      const MuMatch mm = L.mlist[sorted ? perm[i] : i];
+      const MuMatch mm = i < MATCH_CAP ? L.mlist[sorted ? perm[i] : i] : spilled[i - MATCH_CAP];
       const int qm = mm.mi, qp = mm.p;
       const uint32_t rk = L.raise_key[qm];
 #ifdef SDX_X_NOFINISH
@@ -1976,7 +2083,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const uint64_t* bmm = &L.bm[qm * T::MSTRIDE];
       M<NW> U, V1, VF;
       sym_masks<NW>(bmm, mm.u0, mm.u1, mm.u2, (mm.flags >> 3) & 7, d.width, &U, &V1, &VF);
-      finish_mu_lane<NW>(L, wave, bv, bv.mu + qp, d, qp, qm, mm.j, mm.q, mm.k, d.width, (mm.flags & 1) != 0,
+      finish_mu_lane<NW>(L, out, wave, bv, bv.mu + qp, d, qp, qm, mm.j, mm.q, mm.k, d.width, (mm.flags & 1) != 0,
                          (uint8_t)((mm.flags >> 1) & 3), V1, VF);
     }
     __syncthreads();
@@ -1986,6 +2093,10 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   flush_tile(L, msg_of, nvalid, out);
   PROF_ADD(13, t_fl);
   PROF_ADD(15, t_kernel);
+#ifdef SDX_WGTIME
+  __syncthreads();
+  if (tid == 0 && blockIdx.x < 65536) g_wgt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef SDX_PROF
   if (lane < 24) atomicAdd(&g_prof[lane], (unsigned long long)L.prof[wave][lane]);
 #endif
@@ -2285,6 +2396,9 @@ static int fail(int code, const std::string& msg) {
   return code;
 }
 namespace sdx {
+size_t group_bytes(int n);  // sdx_group.hip
+const int32_t* group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, uint8_t* work, size_t bytes,
+                              hipStream_t st);
 // for the other translation units (sdx_lines.hip, sdx_mn.hip): the error text of sdx_last_error()
 // and the bank handle's fields
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
@@ -2308,6 +2422,12 @@ int sdx_prof_read(unsigned long long* out32, int reset) {
     unsigned long long z[32] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z));
   }
+  return SDX_OK;
+}
+#endif
+#ifdef SDX_WGTIME
+int sdx_wgtime_read(unsigned long long* out, int n) {
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wgt), sizeof(unsigned long long) * 2 * (n < 65536 ? n : 65536)));
   return SDX_OK;
 }
 #endif
@@ -2377,18 +2497,37 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
   if (ntot <= 0) return SDX_OK;
   hipStream_t st = (hipStream_t)hip_stream;
-  // variant: short (<= 256 pulses, 64 messages per tile) -- the caller routes longer messages
-  // (<= 4096) through sel_dev to the long variant by passing kind | 0x100.
+  // short variant (<= 256 pulses, 64 messages per tile); the caller routes longer messages (<= 4096)
+  // through sel_dev to sdx_demod_pulses_long
+  sdx_pulse_batch b = *batch;
+  sdx_out o = *out;
+  static const bool nogroup = getenv("SDX_NOGROUP") != nullptr;  // A/B timing of the plain order
+  if (ntot >= SDX_GROUP_MIN && o.work_dev && !nogroup) {  // grouped message order (sdx_group.hip)
+    const size_t gb = sdx::group_bytes(ntot);
+    if (gb && o.work_cap >= gb) {
+      const int32_t* sel = sdx::group_messages(bank->dev, kind, b, o.work_dev, gb, st);
+      if (!sel) return fail(SDX_EHIP, "message grouping (k_sig / radix sort) failed");
+      b.sel_dev = sel;
+      b.n_sel = ntot;
+      o.work_dev += gb;
+      o.work_cap -= gb;
+    }
+  }
   constexpr int TM = 64;
   const int grid = (ntot + TM - 1) / TM;
   if (kind == SDX_KIND_MU)
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), dim3(sdx::pulses_threads<SDX_KIND_MU, 4>()),
-                       0, st, bank->dev, *batch, *out);
+                       0, st, bank->dev, b, o);
   else
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), dim3(sdx::pulses_threads<SDX_KIND_MS, 4>()),
-                       0, st, bank->dev, *batch, *out);
+                       0, st, bank->dev, b, o);
   HIPCHK(hipGetLastError());
   return SDX_OK;
+}
+
+size_t sdx_pulses_work_bytes(int n, int spill_tiles) {
+  const size_t g = n >= SDX_GROUP_MIN ? sdx::group_bytes(n) : 0;
+  return g + (size_t)(spill_tiles > 0 ? spill_tiles : 0) * sdx::SPILL_BYTES;
 }
 
 int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,

@@ -36,7 +36,7 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
             "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
-            "sdx_exchange_pack"]
+            "sdx_exchange_pack", "sdx_pulses_work_bytes"]
 
 
 class SdxPulseBatch(Structure):
@@ -82,7 +82,7 @@ class SdxXchgPart(Structure):
 
 class SdxOut(Structure):
     _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("cursor_dev", c_void_p),
-                ("rec_cap", c_uint32), ("heap_cap", c_uint32)]
+                ("rec_cap", c_uint32), ("heap_cap", c_uint32), ("work_dev", c_void_p), ("work_cap", ctypes.c_uint64)]
 
 
 class SdxLines(Structure):
@@ -131,6 +131,8 @@ def load_library(path: Optional[str] = None):
         f = getattr(lib, fn)
         f.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), POINTER(SdxOut), c_void_p]
         f.restype = c_int
+    lib.sdx_pulses_work_bytes.argtypes = [c_int, c_int]
+    lib.sdx_pulses_work_bytes.restype = c_size_t
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mc.restype = c_int
     lib.sdx_demod_mn.argtypes = [c_void_p, POINTER(SdxMnBatch), POINTER(SdxOut), c_void_p]
@@ -145,7 +147,7 @@ def load_library(path: Optional[str] = None):
     lib.sdx_units.restype = c_int
     lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, c_void_p]
     lib.sdx_exchange_pack.restype = c_int
-    if lib.sdx_abi_version() != 4:
+    if lib.sdx_abi_version() != 5:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -236,7 +238,13 @@ class Engine:
             "lengths": np.diff(mb.offsets),
         }
 
-    def alloc_out(self, n: int, rec_cap: int, heap_cap: int):
+    def pulses_work_bytes(self, n: int, spill_frac: float = 0.5) -> int:
+        """Workspace of an MU/MS launch over n messages: the message grouping plus spill room for
+        `spill_frac` of its 64-message tiles (a grouped order makes tiles of result-heavy messages)."""
+        tiles = (n + 63) // 64
+        return int(self.lib.sdx_pulses_work_bytes(int(n), int(max(16, spill_frac * tiles))))
+
+    def alloc_out(self, n: int, rec_cap: int, heap_cap: int, work_bytes: int = 0):
         t = self.torch
         d = self.dev
         return {
@@ -244,13 +252,15 @@ class Engine:
             "rec": t.empty(max(rec_cap, 1) * RES_DT.itemsize, dtype=t.uint8, device=d),
             "heap": t.empty(max(heap_cap, 1), dtype=t.uint8, device=d),
             "cursor": t.zeros(4, dtype=t.int32, device=d),
+            "work": t.empty(work_bytes, dtype=t.uint8, device=d) if work_bytes else None,
             "rec_cap": rec_cap, "heap_cap": heap_cap, "n": n,
         }
 
     @staticmethod
     def _out_struct(o) -> SdxOut:
+        w = o.get("work")
         return SdxOut(_ptr(o["desc"]), _ptr(o["rec"]), _ptr(o["heap"]), _ptr(o["cursor"]), o["rec_cap"],
-                      o["heap_cap"])
+                      o["heap_cap"], _ptr(w), 0 if w is None else int(w.numel()))
 
     def stream_ptr(self):
         return c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
@@ -309,8 +319,11 @@ class Engine:
 
     # -- full run with contract routing and overflow re-runs (all on the GPU) --------------------
     def run(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None,
-            sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1):
+            sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1, workspace: bool = True):
         """Demodulate a device batch; returns host numpy (desc, rec, heap).
+
+        ``workspace``: MU/MS launches get a device workspace (grouped message order, spill regions
+        for result-heavy tiles, sdx_demod_pulses); False runs the messages in batch order.
 
         ``sel_short`` / ``sel_long``: device int32 lists of the messages to run with the short /
         long variant (MC: ``sel_short`` only), as sdx_select_lines builds them; the other
@@ -339,7 +352,8 @@ class Engine:
         if kind == KIND_MN and not selected:   # parser mode: <= n_mn results of <= preamble + frame bytes
             rec_cap = max(rec_cap, 4 * n_work + 1024)
             heap_cap = max(heap_cap, int(4 * int(np.sum(bd["lengths"])) + 160 * n_work + 65536))
-        out = self.alloc_out(n, rec_cap, heap_cap)
+        out = self.alloc_out(n, rec_cap, heap_cap,
+                             self.pulses_work_bytes(n_work) if workspace and kind in (KIND_MU, KIND_MS) else 0)
         if kind == KIND_MN:
             self.launch_mn(bd, out, elig=mn_elig, method=mn_method, sel=sel_short)
         elif selected:
@@ -468,7 +482,7 @@ class UnitRunner:
                "cursor": t.zeros(4, dtype=t.int32, device=d)}
         b = SdxUnitBatch(op, n, dev(data), dev(in_off), None if args is None else dev(np.asarray(args, np.int32)),
                          val_p, val_off_p, mc_p, dev(out_off))
-        o = SdxOut(_ptr(out["desc"]), _ptr(out["rec"]), _ptr(out["heap"]), _ptr(out["cursor"]), n, max(heap_cap, 1))
+        o = SdxOut(_ptr(out["desc"]), _ptr(out["rec"]), _ptr(out["heap"]), _ptr(out["cursor"]), n, max(heap_cap, 1), None, 0)
         _check(self.lib, self.lib.sdx_units(ctypes.byref(b), ctypes.byref(o),
                                             c_void_p(t.cuda.current_stream(d).cuda_stream)))
         t.cuda.current_stream(d).synchronize()

@@ -194,8 +194,15 @@ def test_large_corpus_vs_c_oracle(kind, n, seed):
                                         eng.to_device_pulses(batch))
         packed = CO.pack_batch(batch)
         cls_pids = bk.mu_pids if kind == "MU" else bk.ms_pids
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    st, rk, rb, nr, rec, heap = CO.run(kind, packed, threads)
+    _compare_c_oracle(kind, d_desc, d_rec, d_heap, CO.run(kind, packed, max(1, min(16, len(os.sched_getaffinity(0))))),
+                      cls_pids, cb)
+
+
+def _compare_c_oracle(kind, d_desc, d_rec, d_heap, cres, cls_pids, cb):
+    """Device outputs == C oracle outputs, record by record (statuses, raise kinds, protocols,
+    payload bytes, bit lengths), read through the descriptors."""
+    from pysignalduino_amd import runtime
+    st, rk, rb, nr, rec, heap = cres
     dh, ch = d_heap.tobytes(), heap.tobytes()
     assert np.array_equal(d_desc["status"] == runtime.ST_RAISED, st == 1)
     assert np.array_equal(np.where(st == 1, d_desc["raise_kind"], 0), np.where(st == 1, rk, 0))
@@ -213,6 +220,37 @@ def test_large_corpus_vs_c_oracle(kind, n, seed):
             if not same:
                 bad.append((int(i), x, y))
     assert not bad, f"{len(bad)} record mismatches; first: {bad[:2]}"
+
+
+@pytest.mark.parametrize("kind,n,seed", [("MU", 30000, 9201), ("MS", 30000, 9202)])
+def test_grouped_order_and_spill_regions_vs_c_oracle(kind, n, seed):
+    """sdx_demod_pulses with a workspace: the grouped message order (sdx_group.hip) on a noise-free
+    corpus, whose result-heavy tiles spill past the LDS pools into the workspace -- every message
+    exact against the C oracle, no tile overflow, spill regions in use (MU); and the same batch
+    without a workspace (batch order, overflowing tiles re-run) gives the same results."""
+    import os
+    from oracle import c_oracle as CO
+    from pysignalduino_amd import bank as B, runtime, synth
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    cb = CO.CBank()
+    gen = synth.mu_corpus if kind == "MU" else synth.ms_corpus
+    batch = gen(bk.protocols, n, seed=seed, noise_frac=0.0)
+    k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
+    bd = eng.to_device_pulses(batch)
+    out = eng.alloc_out(n, 40 * n + 4096, 1024 * n + 65536, eng.pulses_work_bytes(n))
+    eng.launch_pulses(k, bd, out)
+    desc, rec, heap = eng.fetch(out)
+    cur = out["cursor"].cpu().numpy()
+    assert cur[2] == 0 and not np.isin(desc["status"], (runtime.ST_OVF_TILE, runtime.ST_OVF_OUT)).any()
+    if kind == "MU":
+        assert cur[3] > 0, "no tile used its spill region"
+    cls_pids = bk.mu_pids if kind == "MU" else bk.ms_pids
+    cres = CO.run(kind, CO.pack_batch(batch), max(1, min(16, len(os.sched_getaffinity(0)))))
+    _compare_c_oracle(kind, desc, rec, heap, cres, cls_pids, cb)
+    # batch order (no workspace): Engine.run re-runs what overflows; identical results
+    d2, r2, h2 = eng.run(k, bd, rec_cap=40 * n + 4096, heap_cap=1024 * n + 65536, workspace=False)
+    _compare_c_oracle(kind, d2, r2, h2, cres, cls_pids, cb)
 
 
 @pytest.mark.gpu

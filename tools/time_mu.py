@@ -19,7 +19,7 @@ def main():
     for kind, gen in (("MU", synth.mu_corpus), ("MS", synth.ms_corpus)):
         pb = gen(bk.protocols, n, seed=42)
         bd = eng.to_device_pulses(pb)
-        out = eng.alloc_out(pb.n, 8 * pb.n + 4096, 200 * pb.n + 65536)
+        out = eng.alloc_out(pb.n, 12 * pb.n + 4096, 320 * pb.n + 65536, eng.pulses_work_bytes(pb.n))
         k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
         eng.launch_pulses(k, bd, out)
         torch.cuda.synchronize()
@@ -32,8 +32,10 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
-        res.append(f"{kind} {min(ts):.3f} ms")
-    print(os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")), " | ".join(res), flush=True)
+        cur = out["cursor"].cpu().numpy()
+        res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) >> 20} MB)")
+    tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped")
+    print(tag, " | ".join(res), flush=True)
 
 
 if __name__ == "__main__":
