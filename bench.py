@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kind", default="mixed", choices=("mixed", "MU", "MS", "MC"),
                     help="mixed = config 5's per-GPU shard (1/3 each); MU/MS/MC = configs 2/3/4 (--msgs of one type)")
+    ap.add_argument("--no-group", action="store_true",
+                    help="run MU/MS in batch order (no sdx_group_pulses)")
     ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
                     help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
@@ -164,6 +166,29 @@ def main():
             o[k]["cursor"] = cursors[s_, i]   # one fill per step resets a slot's cursors
         outs.append(o)
     stream = torch.cuda.current_stream(dev)
+    # MU/MS message grouping (sdx_group_pulses) on a side stream, one step ahead: the grouping of
+    # step j+1 (latency-bound small kernels) runs while step j demodulates; order buffers are
+    # double-buffered by step parity.  Every step still groups once.
+    gkinds = [k for k in kinds if k != "MC"] if not args.no_group else []
+    side = torch.cuda.Stream(dev)
+    gbufs = {k: [eng.group_buffers(corp[k].n) for _ in range(2)] for k in gkinds}
+    gdone, used = {}, [None, None]
+    gev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps + 1)]
+
+    def launch_group(j, si=None):
+        par = j % 2
+        if used[par] is not None:           # step j-2's launches have read this parity's order
+            side.wait_event(used[par])
+        with torch.cuda.stream(side):
+            if si is not None:
+                gev[si][0].record(side)
+            for k in gkinds:
+                eng.group(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], bufs=gbufs[k][par])
+                e = torch.cuda.Event()
+                e.record(side)
+                gdone[(k, par)] = e
+            if si is not None:
+                gev[si][1].record(side)
     exch = sdist.Exchange() if world > 1 else None
     done = [None] * nslot
     # one event pair per kernel and timed step: read after the closing synchronize
@@ -176,21 +201,34 @@ def main():
             stream.wait_event(done[s_])
             done[s_] = None
         cursors[s_].zero_()
+        if gkinds:
+            if j == 0:
+                launch_group(0)
+            launch_group(j + 1, si)         # the next step's grouping, concurrent with this step
+        par = j % 2
         for k in kinds:
+            if k in gkinds:
+                stream.wait_event(gdone[(k, par)])
             if si is not None:
                 ev[si][k][0].record(stream)
             if k == "MC":
                 eng.launch_mc(bds[k], outs[s_][k])
             else:
-                eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[s_][k])
+                eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[s_][k],
+                                  sel=gbufs[k][par][0][:corp[k].n] if k in gkinds else None, group=False)
             if si is not None:
                 ev[si][k][1].record(stream)
+        if gkinds:
+            u = torch.cuda.Event()
+            u.record(stream)
+            used[par] = u
         if exch is not None:  # RCCL all-gather of the decoded dmsg buffers (config 5), overlapped
             d = exch.submit([(outs[s_][k]["desc"], outs[s_][k]["rec"], outs[s_][k]["heap"], bds[k]["n"],
                               outs[s_][k]["cursor"]) for k in kinds], stream)
             done[(j - 1) % nslot] = d
 
     def drain():
+        stream.wait_stream(side)
         if exch is not None:
             d = exch.flush()
             if d is not None:
@@ -221,6 +259,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     ktimes = {k: [ev[si][k][0].elapsed_time(ev[si][k][1]) * 1e-3 for si in range(args.steps)] for k in kinds}
+    gtime = float(np.mean([gev[si][0].elapsed_time(gev[si][1]) * 1e-3 for si in range(args.steps)])) if gkinds else 0.0
     tt = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -266,8 +305,9 @@ def main():
         "data": "synthetic (seeded generators, pysignalduino_amd/synth.py" +
                 (", noise-free dense corpus)" if args.corpus == "dense" else ")"),
         "config": {"workload": wl, "kind": args.kind, "corpus": args.corpus, "msgs_per_gpu": sum(per.values()),
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "grouped": bool(gkinds)},
         "per_kernel_ms": {k: 1e3 * v for k, v in kt.items()},
+        "group_ms": 1e3 * gtime,   # sdx_group_pulses of all kinds per step (side stream, one step ahead)
         "per_type_msgs_per_s": {k: per[k] / kt[k] for k in kinds},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": tag,

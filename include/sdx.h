@@ -117,11 +117,9 @@ typedef struct {
                                 * workspace bytes taken */
   uint32_t rec_cap, heap_cap;
   uint8_t* work_dev;           /* optional device workspace (MU/MS short variant, NULL = none), 256-B
-                                * aligned: the message grouping of sdx_demod_pulses (batches of
-                                * >= SDX_GROUP_MIN messages) and after it the spill regions of heavy
-                                * tiles; size it with sdx_pulses_work_bytes().  Without it messages run
-                                * in batch order and a tile whose results overflow LDS is re-run
-                                * (ST_OVF_TILE) */
+                                * aligned: spill regions of result-heavy tiles (112 KB each, see
+                                * sdx_pulses_work_bytes); without it a tile whose results overflow
+                                * LDS is re-run (ST_OVF_TILE) */
   uint64_t work_cap;           /* bytes at work_dev */
 } sdx_out;
 
@@ -138,15 +136,21 @@ int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out)
 int sdx_bank_destroy(sdx_bank* bank);
 const void* sdx_bank_device_ptr(const sdx_bank* bank);
 
-/* MU/MS demodulation of a batch: results appended to out.  With out->work_dev the messages are first
- * grouped (a per-message key + device radix sort, sdx_group.hip): same results, fewer instructions */
-#define SDX_GROUP_MIN 4096
+/* MU/MS demodulation of a batch (or of batch->sel_dev, in that order): results appended to out */
 int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
                      void* hip_stream);
-/* workspace bytes for sdx_demod_pulses over n messages: the grouping (n >= SDX_GROUP_MIN) plus room
- * for `spill_tiles` heavy tiles (112 KB each; a tile of 64 messages spills when its results exceed
- * 512 records / 10 KB of payload / 768 matches in LDS) */
-size_t sdx_pulses_work_bytes(int n, int spill_tiles);
+/* out->work_cap for `spill_tiles` result-heavy tiles (112 KB each; a tile of 64 messages spills when
+ * its results exceed 512 records / 10 KB of payload / 768 matches in LDS) */
+size_t sdx_pulses_work_bytes(int spill_tiles);
+/* Message grouping (sdx_group.hip): order_dev[0, n) = the batch's messages (or batch->sel_dev's) in
+ * the order of a per-message key -- which of the first 32 protocols (bank order) the message passes
+ * the candidate-interval test of -- by a device radix sort.  sdx_demod_pulses on that order (as
+ * sel_dev) gives the same results with fewer instructions (tiles of messages that survive the same
+ * protocols).  work_dev: sdx_group_work_bytes(n) bytes.  Worth it from a few thousand messages. */
+size_t sdx_group_work_bytes(int n);
+int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, int32_t* order_dev, void* work_dev,
+                     size_t work_cap, void* hip_stream);
+#define SDX_GROUP_MIN 4096  /* batches from this size are grouped by the host wrappers */
 /* same, for messages of 257..4096 pulses (4 messages per workgroup tile) */
 int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
                           void* hip_stream);

@@ -234,20 +234,21 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
 
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// workspace of the grouping: keys and message indices (two copies each) + the sort's counts
+// workspace of the grouping: keys and message indices (two copies; the sorted indices end in the
+// caller's order buffer) + the sort's counts
 size_t group_bytes(int n) {
   if (n <= 0) return 0;
   const size_t np = (size_t)(n + RS_PART - 1) / RS_PART;
   return 4 * align256(4 * (size_t)n) + align256(4 * 256 * np) + align256(4 * 256);
 }
 
-// The grouped order of a batch's messages into `work`; returns the device list of message indices
-// (the sel_dev of the k_pulses launch), or nullptr.
-const int32_t* group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, uint8_t* work, size_t bytes,
-                              hipStream_t st) {
+// The grouped order of a batch's messages (or of its sel_dev subset): order[0, n) = message indices
+// (the sel_dev of the k_pulses launch that follows).
+bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, int32_t* order, uint8_t* work,
+                    size_t bytes, hipStream_t st) {
   const int n = b.sel_dev ? b.n_sel : b.n;
   const size_t need = group_bytes(n);
-  if (!need || bytes < need) return nullptr;
+  if (!need || bytes < need) return false;
   const int np = (n + RS_PART - 1) / RS_PART;
   const size_t a = align256(4 * (size_t)n);
   uint32_t* k0 = reinterpret_cast<uint32_t*>(work);
@@ -261,16 +262,16 @@ const int32_t* group_messages(const void* bank_dev, int kind, const sdx_pulse_ba
     hipLaunchKernelGGL((k_sig<SDX_KIND_MU>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0);
   else
     hipLaunchKernelGGL((k_sig<SDX_KIND_MS>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0);
-  for (int d = 0; d < 4; ++d) {  // (k0, v0) -> (k1, v1) -> (k0, v0) -> ...: the result is back in v0
+  for (int d = 0; d < 4; ++d) {  // (k0, v0) -> (k1, v1) -> (k0, v0) -> (k1, order)
     const bool even = (d & 1) == 0;
     uint32_t* kin = even ? k0 : k1;
+    uint32_t* vout = d == 3 ? reinterpret_cast<uint32_t*>(order) : (even ? v1 : v0);
     hipLaunchKernelGGL(k_rs_hist, dim3(np), dim3(RS_T), 0, st, kin, n, np, d, hist);
     hipLaunchKernelGGL(k_rs_scan_rows, dim3(256 / 4), dim3(256), 0, st, hist, np, tot);
     hipLaunchKernelGGL(k_rs_scatter, dim3(np), dim3(RS_T), 0, st, kin, even ? v0 : v1, n, np, d, hist, tot,
-                       even ? k1 : k0, even ? v1 : v0);
+                       even ? k1 : k0, vout);
   }
-  if (hipGetLastError() != hipSuccess) return nullptr;
-  return reinterpret_cast<const int32_t*>(v0);
+  return hipGetLastError() == hipSuccess;
 }
 
 }  // namespace sdx

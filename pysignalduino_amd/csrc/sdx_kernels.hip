@@ -1747,11 +1747,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         const MuItem it = Q[(head + lane) & (QCAP - 1)];
         const int qm = it.mi, qp = it.p;
         const uint32_t rk = L.raise_key[qm];
-#ifndef SDX_X_NODECODE
         if (rk == 0xFFFFFFFFu || (rk >> 8) > (uint32_t)qp) {
-#else
-        if (rk == 0x12345u) {
-#endif
           sdx_mu_desc d;
           if (qp < SDX_MUDESC_LDS) d = L.desc[qp];
           else d = bv.mudesc[qp];
@@ -1788,9 +1784,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const sdx_mu_filt* fr = uniform_ptr(bv.mufilt + p);  // the filter's state: two 64-byte lines
       const uint32_t ff = cld(&fr->flags);
       if ((ff & 2u) || !(ff & 4u)) continue;  // never / not active
-#ifdef SDX_X_NOSTARTPROTO
-      if (ff & 1u) continue;
-#endif
       const bool full = (ff & 8u) != 0;
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
       int idx = 0;
@@ -1847,9 +1840,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           alive = r.found;
           idx = r.pos;
           st_tgt = r.tgt;
-#ifdef SDX_X_STARTONLY
-          alive = false;
-#endif
         }
       }
       PROF_ADD(2, t_st);
@@ -1996,11 +1986,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   PROF_ADD(14, t_bar);
   if constexpr (LANE_MS) {  // decode every survivor of the tile: lane = (message, protocol)
     PROF_T(t_dec);
-#ifndef SDX_X_NODECODE
     const int ns = L.nsurv < MS_SURV_CAP ? L.nsurv : MS_SURV_CAP;
-#else
-    const int ns = 0;  // timing experiment
-#endif
     if (!L.ovf) {
       for (int i = tid; i < ns; i += blockDim.x) {
         const MsItem it = L.slist[i];
@@ -2035,11 +2021,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     static_assert(sizeof(L.u) >= SDX_MMTAB_LDS + MATCH_CAP * 2 + NBIN * 4, "sort scratch fits the union");
     uint16_t* perm = reinterpret_cast<uint16_t*>(L.u.mmtab + SDX_MMTAB_LDS);
     uint32_t* bin = reinterpret_cast<uint32_t*>(perm + MATCH_CAP);
-#ifndef SDX_X_NOSORT
     const bool sorted = (int)bv.hdr->n_mu <= NBIN && nm <= MATCH_CAP;
-#else
-    const bool sorted = false;  // timing experiment
-#endif
     if (sorted) {
       for (int i = tid; i < NBIN; i += blockDim.x) bin[i] = 0;
       __syncthreads();
@@ -2073,9 +2055,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const MuMatch mm = i < MATCH_CAP ? L.mlist[sorted ? perm[i] : i] : spilled[i - MATCH_CAP];
       const int qm = mm.mi, qp = mm.p;
       const uint32_t rk = L.raise_key[qm];
-#ifdef SDX_X_NOFINISH
-      if (rk != 0x12345u) continue;  // timing experiment
-#endif
       if (rk != 0xFFFFFFFFu && (rk >> 8) < (uint32_t)qp) continue;  // an earlier protocol raised
       sdx_mu_desc d;
       if (qp < SDX_MUDESC_LDS) d = L.desc[qp];
@@ -2252,11 +2231,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
       }
     }
   }
-#ifndef SDX_X_MCHEXONLY
   const int nmc = (int)bv.hdr->n_mc;
-#else
-  const int nmc = 0;  // timing experiment: hex staging + flush only
-#endif
   int raise = 0, mycnt = 0;
   for (int p = 0; p < nmc; ++p) {
     const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
@@ -2397,8 +2372,8 @@ static int fail(int code, const std::string& msg) {
 }
 namespace sdx {
 size_t group_bytes(int n);  // sdx_group.hip
-const int32_t* group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, uint8_t* work, size_t bytes,
-                              hipStream_t st);
+bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, int32_t* order, uint8_t* work,
+                    size_t bytes, hipStream_t st);
 // for the other translation units (sdx_lines.hip, sdx_mn.hip): the error text of sdx_last_error()
 // and the bank handle's fields
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
@@ -2499,20 +2474,8 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   hipStream_t st = (hipStream_t)hip_stream;
   // short variant (<= 256 pulses, 64 messages per tile); the caller routes longer messages (<= 4096)
   // through sel_dev to sdx_demod_pulses_long
-  sdx_pulse_batch b = *batch;
-  sdx_out o = *out;
-  static const bool nogroup = getenv("SDX_NOGROUP") != nullptr;  // A/B timing of the plain order
-  if (ntot >= SDX_GROUP_MIN && o.work_dev && !nogroup) {  // grouped message order (sdx_group.hip)
-    const size_t gb = sdx::group_bytes(ntot);
-    if (gb && o.work_cap >= gb) {
-      const int32_t* sel = sdx::group_messages(bank->dev, kind, b, o.work_dev, gb, st);
-      if (!sel) return fail(SDX_EHIP, "message grouping (k_sig / radix sort) failed");
-      b.sel_dev = sel;
-      b.n_sel = ntot;
-      o.work_dev += gb;
-      o.work_cap -= gb;
-    }
-  }
+  const sdx_pulse_batch& b = *batch;
+  const sdx_out& o = *out;
   constexpr int TM = 64;
   const int grid = (ntot + TM - 1) / TM;
   if (kind == SDX_KIND_MU)
@@ -2525,9 +2488,21 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   return SDX_OK;
 }
 
-size_t sdx_pulses_work_bytes(int n, int spill_tiles) {
-  const size_t g = n >= SDX_GROUP_MIN ? sdx::group_bytes(n) : 0;
-  return g + (size_t)(spill_tiles > 0 ? spill_tiles : 0) * sdx::SPILL_BYTES;
+size_t sdx_pulses_work_bytes(int spill_tiles) { return (size_t)(spill_tiles > 0 ? spill_tiles : 0) * sdx::SPILL_BYTES; }
+
+size_t sdx_group_work_bytes(int n) { return sdx::group_bytes(n); }
+
+int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, int32_t* order_dev, void* work_dev,
+                     size_t work_cap, void* hip_stream) {
+  if (!bank || !batch || !order_dev || !work_dev) return fail(SDX_EINVAL, "null argument");
+  if (kind != SDX_KIND_MU && kind != SDX_KIND_MS) return fail(SDX_EINVAL, "kind must be MU or MS");
+  if (kind == SDX_KIND_MS && (!batch->cp_slot_dev || !batch->ms_ok_dev)) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+  const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
+  if (ntot <= 0) return SDX_OK;
+  if (work_cap < sdx::group_bytes(ntot)) return fail(SDX_EINVAL, "grouping workspace smaller than sdx_group_work_bytes(n)");
+  if (!sdx::group_messages(bank->dev, kind, *batch, order_dev, (uint8_t*)work_dev, work_cap, (hipStream_t)hip_stream))
+    return fail(SDX_EHIP, "message grouping (k_sig / radix sort) launch failed");
+  return SDX_OK;
 }
 
 int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,

@@ -193,9 +193,6 @@ SDX_DEV SpecV spec_compact(const sdx_fspec* fs, uint64_t upk) {
 // rank key of candidate slot j for one search value: (gap rank << 4) | j -- the stable sort key of
 // pattern_utils.py:61-63 (equal fp64 gaps share a rank; ties keep dict order j)
 SDX_DEV uint32_t rank_key(const uint16_t* rt, int kqj, int klo, int j) {
-#ifdef SDX_X_NORANK
-  return (uint32_t)j;  // timing experiment: no rank-table loads
-#endif
   return ((uint32_t)rt[kqj - klo] << 4) | (uint32_t)j;
 }
 // the candidate of mask m (non-empty) that comes first in the sorted candidate list: one rank load
@@ -213,26 +210,9 @@ SDX_DEV int first_cand(uint32_t m, const int* kq, int klo, const uint16_t* rt) {
 }
 
 template <int NW>
-SDX_DEV PexRes pexists_lane_impl(const SpecV& sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
-                                 int minpos, const uint16_t* ranks, const PairRef& PR, bool need_pos);
-template <int NW>
-SDX_DEV PexRes pexists_lane(const SpecV& sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
-                            int minpos, const uint16_t* ranks, const PairRef& PR, bool need_pos) {
-#ifdef SDX_X_FULLFAIL
-  PexRes r = pexists_lane_impl<NW>(sp, kq, ids, npat, bm, minpos, ranks, PR, need_pos);
-  if (r.tgt == 0xFFFFFFFFFFFFull) r.found = true; else r.found = false;  // timing experiment: never found
-  return r;
-#else
-  return pexists_lane_impl<NW>(sp, kq, ids, npat, bm, minpos, ranks, PR, need_pos);
-#endif
-}
-template <int NW>
-SDX_DEV PexRes pexists_lane_impl(const SpecV& sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm,
-                                 int minpos, const uint16_t* ranks, const PairRef& PR, bool need_pos) {
+SDX_DEV PexRes pexists_lane(const SpecV& sp, const int* kq, uint64_t ids, int npat, const uint64_t* bm, int minpos,
+                            const uint16_t* ranks, const PairRef& PR, bool need_pos) {
   PexRes res{false, -1, 0};
-#ifdef SDX_X_NOCAND
-  return PexRes{true, minpos, 0};
-#endif
   const int nu = sp.nu, slen = sp.slen;
   // candidate slots per unique search value (pattern_utils.py:53-61) as an exact integer interval
   // test on k (bank.py _k_interval); kq[j] == SDX_K_NONE for j >= npat
@@ -256,9 +236,6 @@ SDX_DEV PexRes pexists_lane_impl(const SpecV& sp, const int* kq, uint64_t ids, i
     }
   }
   if (nu == 0 || total > 10000) return res;  // pattern_utils.py:93-101
-#ifdef SDX_X_MASKFAIL
-  return res;  // timing experiment: candidate masks only, never found
-#endif
   const uint64_t upk = sp.upk;
   // The first hit in itertools.product order (lexicographic in the sorted candidate lists) is
   // found without sorting for the two common shapes: (a) a 2-pulse search of two distinct values

@@ -340,7 +340,8 @@ class SignalParser:
         texts: List[Any] = [None] * n
         for kind, rec_cap, heap_cap, json_cap, launches in jobs:
             for _attempt in range(4):
-                out = eng.alloc_out(n, rec_cap, heap_cap)
+                work = eng.pulses_work_bytes(n) if kind in (runtime.KIND_MU, runtime.KIND_MS) else 0
+                out = eng.alloc_out(n, rec_cap, heap_cap, work)  # MU/MS: grouped order + spill room
                 for bd, sel, long_v in launches:
                     if not sel.numel():
                         continue

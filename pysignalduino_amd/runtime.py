@@ -36,7 +36,8 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
             "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
-            "sdx_exchange_pack", "sdx_pulses_work_bytes"]
+            "sdx_exchange_pack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses"]
+GROUP_MIN = 4096   # SDX_GROUP_MIN
 
 
 class SdxPulseBatch(Structure):
@@ -131,8 +132,12 @@ def load_library(path: Optional[str] = None):
         f = getattr(lib, fn)
         f.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), POINTER(SdxOut), c_void_p]
         f.restype = c_int
-    lib.sdx_pulses_work_bytes.argtypes = [c_int, c_int]
+    lib.sdx_pulses_work_bytes.argtypes = [c_int]
     lib.sdx_pulses_work_bytes.restype = c_size_t
+    lib.sdx_group_work_bytes.argtypes = [c_int]
+    lib.sdx_group_work_bytes.restype = c_size_t
+    lib.sdx_group_pulses.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.sdx_group_pulses.restype = c_int
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mc.restype = c_int
     lib.sdx_demod_mn.argtypes = [c_void_p, POINTER(SdxMnBatch), POINTER(SdxOut), c_void_p]
@@ -239,10 +244,32 @@ class Engine:
         }
 
     def pulses_work_bytes(self, n: int, spill_frac: float = 0.5) -> int:
-        """Workspace of an MU/MS launch over n messages: the message grouping plus spill room for
-        `spill_frac` of its 64-message tiles (a grouped order makes tiles of result-heavy messages)."""
+        """Workspace of an MU/MS launch over n messages: spill room for `spill_frac` of its
+        64-message tiles (a grouped order makes tiles of result-heavy messages)."""
         tiles = (n + 63) // 64
-        return int(self.lib.sdx_pulses_work_bytes(int(n), int(max(16, spill_frac * tiles))))
+        return int(self.lib.sdx_pulses_work_bytes(int(max(16, spill_frac * tiles))))
+
+    def group_buffers(self, n: int):
+        """(order, work) device buffers for sdx_group_pulses over n messages."""
+        t = self.torch
+        return (t.empty(max(n, 1), dtype=t.int32, device=self.dev),
+                t.empty(max(int(self.lib.sdx_group_work_bytes(int(n))), 1), dtype=t.uint8, device=self.dev))
+
+    def group(self, kind: int, bd, sel=None, bufs=None):
+        """The grouped message order of a batch (or of `sel`) as a device int32 tensor: the sel of
+        the launch_pulses that follows (same results, fewer instructions; sdx_group.hip).  `bufs`:
+        group_buffers() to use; default: a per-engine cache (one stream at a time)."""
+        n = int(sel.numel()) if sel is not None else bd["n"]
+        if bufs is None:
+            c = getattr(self, "_gcache", None)
+            if c is None or c[0].numel() < n:
+                c = self._gcache = self.group_buffers(n)
+            bufs = c
+        order, work = bufs
+        b = self._pulse_batch(bd, sel)
+        _check(self.lib, self.lib.sdx_group_pulses(self.handle, kind, ctypes.byref(b), _ptr(order), _ptr(work),
+                                                   int(work.numel()), self.stream_ptr()))
+        return order[:n]
 
     def alloc_out(self, n: int, rec_cap: int, heap_cap: int, work_bytes: int = 0):
         t = self.torch
@@ -266,11 +293,19 @@ class Engine:
         return c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
 
     # -- launches -------------------------------------------------------------------------------
-    def launch_pulses(self, kind: int, bd, out, sel=None, long_variant: bool = False) -> None:
-        b = SdxPulseBatch(_ptr(bd["data"]), _ptr(bd["offsets"]), _ptr(bd["npat"]), _ptr(bd["pat_id"]),
-                          _ptr(bd["pat_val"]), _ptr(bd["cp_slot"]), _ptr(bd["ms_ok"]), _ptr(bd.get("len")),
-                          _ptr(sel), bd["n"],
-                          0 if sel is None else int(sel.numel()))
+    @staticmethod
+    def _pulse_batch(bd, sel) -> SdxPulseBatch:
+        return SdxPulseBatch(_ptr(bd["data"]), _ptr(bd["offsets"]), _ptr(bd["npat"]), _ptr(bd["pat_id"]),
+                             _ptr(bd["pat_val"]), _ptr(bd["cp_slot"]), _ptr(bd["ms_ok"]), _ptr(bd.get("len")),
+                             _ptr(sel), bd["n"], 0 if sel is None else int(sel.numel()))
+
+    def launch_pulses(self, kind: int, bd, out, sel=None, long_variant: bool = False, group: bool = True) -> None:
+        """MU/MS launch; the short variant runs batches of >= GROUP_MIN messages in the grouped
+        order (group()) unless `group` is False (`sel` then runs in its own order)."""
+        n = int(sel.numel()) if sel is not None else bd["n"]
+        if group and not long_variant and n >= GROUP_MIN:
+            sel = self.group(kind, bd, sel)
+        b = self._pulse_batch(bd, sel)
         o = self._out_struct(out)
         fn = self.lib.sdx_demod_pulses_long if long_variant else self.lib.sdx_demod_pulses
         _check(self.lib, fn(self.handle, kind, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
@@ -322,8 +357,9 @@ class Engine:
             sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1, workspace: bool = True):
         """Demodulate a device batch; returns host numpy (desc, rec, heap).
 
-        ``workspace``: MU/MS launches get a device workspace (grouped message order, spill regions
-        for result-heavy tiles, sdx_demod_pulses); False runs the messages in batch order.
+        ``workspace``: MU/MS launches run in the grouped message order with spill regions for
+        result-heavy tiles (sdx_group_pulses, sdx_demod_pulses); False runs the messages in batch
+        order without a workspace.
 
         ``sel_short`` / ``sel_long``: device int32 lists of the messages to run with the short /
         long variant (MC: ``sel_short`` only), as sdx_select_lines builds them; the other
@@ -359,7 +395,7 @@ class Engine:
         elif selected:
             if sel_short is not None and sel_short.numel():
                 (self.launch_mc(bd, out, sel=sel_short) if kind == KIND_MC else
-                 self.launch_pulses(kind, bd, out, sel=sel_short))
+                 self.launch_pulses(kind, bd, out, sel=sel_short, group=workspace))
             if sel_long is not None and sel_long.numel():
                 self.launch_pulses(kind, bd, out, sel=sel_long, long_variant=True)
         elif kind == KIND_MC:
@@ -367,10 +403,11 @@ class Engine:
         else:
             short = lengths <= SHORT_MAX
             if short.all():
-                self.launch_pulses(kind, bd, out)
+                self.launch_pulses(kind, bd, out, group=workspace)
             else:
                 if short.any():
-                    self.launch_pulses(kind, bd, out, sel=t.from_numpy(np.nonzero(short)[0].astype(np.int32)).to(self.dev))
+                    self.launch_pulses(kind, bd, out, sel=t.from_numpy(np.nonzero(short)[0].astype(np.int32)).to(self.dev),
+                                       group=workspace)
                 self.launch_pulses(kind, bd, out, sel=t.from_numpy(np.nonzero(~short)[0].astype(np.int32)).to(self.dev),
                                    long_variant=True)
         desc, rec, heap = self.fetch(out)

@@ -21,14 +21,14 @@ def main():
         bd = eng.to_device_pulses(pb)
         out = eng.alloc_out(pb.n, 12 * pb.n + 4096, 320 * pb.n + 65536, eng.pulses_work_bytes(pb.n))
         k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
-        eng.launch_pulses(k, bd, out)
+        eng.launch_pulses(k, bd, out, group=not os.environ.get("SDX_NOGROUP"))
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ts = []
         for _ in range(reps):
             out["cursor"].zero_()
             e0.record()
-            eng.launch_pulses(k, bd, out)
+            eng.launch_pulses(k, bd, out, group=not os.environ.get("SDX_NOGROUP"))
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
