@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 5
+#define SDX_ABI_VERSION 6
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -45,7 +45,9 @@ enum sdx_status {
 };
 /* sdx_desc.raise_kind (Python exception class the reference raises) */
 enum sdx_raise { SDX_RAISE_NONE = 0, SDX_RAISE_INDEX = 1, SDX_RAISE_ATTRIBUTE = 2, SDX_RAISE_VALUE = 3,
-                 SDX_RAISE_TYPE = 4, SDX_RAISE_ZERODIV = 5 };
+                 SDX_RAISE_TYPE = 4, SDX_RAISE_ZERODIV = 5,
+                 SDX_RAISE_CONTRACT = 6 /* not a reference outcome: the message exceeds a general-path limit
+                                         * (SDX_GEN_*); the host reports it as outside the device contract */ };
 
 typedef struct {
   uint32_t rec_begin; /* index of the first result record of this message */
@@ -160,6 +162,46 @@ int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out*
  * Frames must hold hex digits only ([0-9A-Fa-f]; the front end guarantees [0-9A-F]) and at most
  * SDX_MN_HEX_MAX of them.  sdx_result.proto = MN table index (parser mode) / the method (method mode). */
 int sdx_demod_mn(const sdx_bank* bank, const sdx_mn_batch* batch, const sdx_out* out, void* hip_stream);
+
+/* ---- general path (messages outside the short / long kernels' contract) ------------------------
+ * MU/MS messages the fixed-layout kernels do not take: pattern ids of more than one digit (the
+ * reference keys patterns by str(int(key[1:])) for any "P<digits>" key, message_unsynced.py:28-35,
+ * message_synced.py:50-57 -- "P10" is pattern "10", and pattern_exists concatenates such strings,
+ * pattern_utils.py:120-130), more than 10 patterns, and more than SDX_LONG_MAX pulses.  The
+ * reference's string semantics run as they are: candidate targets are character strings, MU's
+ * re.finditer over (?:start)((?:u1|u2|..){length_min,}(?:e1|..)?) is emulated with Python sre's
+ * backtracking order, chunks are sliced by characters.  Lane = message, serial over the bank in
+ * bank order; every result list is counted, reserved (one atomic pair per message) and written in
+ * a second pass.  out->work_dev must hold sdx_general_work_bytes(offsets[n], n) bytes (per message
+ * scratch for bit lists and payload text).  Limits (status SDX_ST_RAISED + SDX_RAISE_CONTRACT when
+ * exceeded): SDX_GEN_MAXPAT patterns of <= 15 digits, target strings of <= SDX_GEN_STRMAX
+ * characters, length_min <= SDX_GEN_REPMAX, 2^22 sre steps per repetition match, payloads of
+ * <= 65535 bytes. */
+#define SDX_GEN_MAXPAT 16
+#define SDX_GEN_IDSTR 16    /* bytes per pattern id: [0] = length (1..15), [1..15] its digits */
+#define SDX_GEN_STRMAX 64
+#define SDX_GEN_REPMAX 128
+typedef struct {
+  const uint8_t* data_dev;     /* pulse-id characters, all messages concatenated */
+  const int64_t* offsets_dev;  /* [n+1] message i = data[offsets[i], offsets[i+1]) */
+  const uint8_t* npat_dev;     /* [n] patterns (<= SDX_GEN_MAXPAT) */
+  const uint8_t* pat_ids_dev;  /* [n * SDX_GEN_MAXPAT * SDX_GEN_IDSTR] id string of pattern slot k, dict order */
+  const double* pat_val_dev;   /* [n * SDX_GEN_MAXPAT] float(P#) */
+  const int8_t* cp_slot_dev;   /* [n] MS: slot of str(int(CP)) (NULL for MU) */
+  const uint8_t* ms_ok_dev;    /* [n] MS: string gates passed and CP names a pattern (NULL for MU) */
+  const int32_t* sel_dev;      /* optional [n_sel] subset to run, NULL = all */
+  int32_t n, n_sel;
+} sdx_general_batch;
+
+uint64_t sdx_general_work_bytes(int64_t total_chars, int32_t n);
+int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_batch* batch, const sdx_out* out,
+                             void* hip_stream);
+/* MC frames of any length (the "fixed" chain of sdx_demod_mc without its SDX_MC_HEX_MAX limit): lane =
+ * frame, the frame's bits in out->work_dev (sdx_mc_general_work_bytes(frames run, max_hex) bytes),
+ * results counted, reserved and written in a second pass.  Payloads of <= 65535 bytes. */
+uint64_t sdx_mc_general_work_bytes(int32_t n, int32_t max_hex);
+int sdx_demod_mc_general(const sdx_bank* bank, const sdx_mc_batch* batch, int32_t max_hex, const sdx_out* out,
+                         void* hip_stream);
 
 /* ---- wire-line front end ------------------------------------------------------
  * Raw firmware lines, byte for byte as the transport receives them (the reference decodes them

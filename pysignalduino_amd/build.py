@@ -13,7 +13,8 @@ SRCS = [os.path.join(HERE, "csrc", "sdx_kernels.hip"),   # demodulation kernels 
         os.path.join(HERE, "csrc", "sdx_json.hip"),      # publish-ready JSON (sdx_serialize_json)
         os.path.join(HERE, "csrc", "sdx_units.hip"),     # unit-level helpers (sdx_units)
         os.path.join(HERE, "csrc", "sdx_exchange.hip"),  # multi-GPU exchange packing (sdx_exchange_pack)
-        os.path.join(HERE, "csrc", "sdx_group.hip")]     # MU/MS message grouping (k_sig + radix sort)
+        os.path.join(HERE, "csrc", "sdx_group.hip"),     # MU/MS message grouping (k_sig + radix sort)
+        os.path.join(HERE, "csrc", "sdx_general.hip")]   # general path: multi-digit ids, long messages/frames
 OUT = os.path.join(HERE, "_lib", "libsdx.so")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]

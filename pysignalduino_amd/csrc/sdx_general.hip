@@ -1,0 +1,699 @@
+// sdx_general.hip -- the general path: MU/MS messages and MC frames outside the fixed-layout
+// kernels' contract (include/sdx.h "general path"), hand-written HIP for gfx950.
+//
+// k_pulses keeps a message as per-id position bitmaps, which needs single-character pattern ids
+// (P0..P9) and <= 4096 pulses; k_mc keeps a frame's bits in LDS (<= 128 hex characters).  The
+// reference has neither limit: it keys patterns by str(int(key[1:])) ("P10" is the two-character
+// id "10", message_unsynced.py:28-35, message_synced.py:50-57), builds candidate targets by string
+// concatenation (pattern_utils.py:120-130), matches MU with re.finditer over alternations of those
+// strings (message_unsynced.py:146-200) and slices chunks by characters (:203-221; MS :172-189).
+// This file restates that string semantics directly, lane = message, serially over the bank in
+// bank order (the order results and raises take in the reference):
+//   * pattern_exists: candidates by the fp64 gap test, stable gap order, itertools.product order,
+//     no id reused, first target string that occurs (str `in`);
+//   * MU matching: Python sre's order for (?:S)((?:U1|U2|..){lmin,}(?:E1|..)?) -- leftmost start,
+//     alternatives in order, greedy repetition that backtracks only while fewer than lmin units
+//     matched (past lmin every continuation succeeds), then the first end key that matches;
+//   * chunks, postDemodulation, padding, hex / bin formatting, modulematch: as the lane kernels
+//     (sdx_device.h run_postdemo, dfa_accepts).
+// Results: the message's list is counted in a first pass, reserved with one atomic pair and written
+// in a second (deterministic) pass.  Messages this path takes are rare (the SIGNALduino firmware
+// emits P0..P7 and short lines); throughput is not its goal, exactness is.
+#include "sdx_mc.h"
+
+#include <string>
+
+namespace sdx {
+int set_error(int code, const std::string& msg);  // sdx_kernels.hip
+const void* bank_dev_ptr(const sdx_bank* b);
+}  // namespace sdx
+
+namespace sdxg {
+using namespace sdx;
+
+#define GD __device__ __attribute__((noinline))
+#define GI __device__ __forceinline__
+
+constexpr int GP = SDX_GEN_MAXPAT, GID = SDX_GEN_IDSTR, GS = SDX_GEN_STRMAX, GREP = SDX_GEN_REPMAX;
+constexpr long long GBUDGET = 1ll << 22;  // sre steps per repetition match (catastrophic backtracking)
+constexpr int GSLACK = 512;               // per-message scratch beyond n: padding, postDemo prefixes, texts
+
+struct Str {
+  int len;
+  uint8_t c[GS];
+};
+
+struct Msg {
+  const uint8_t* d;
+  int n;
+  int npat;
+  const uint8_t* ids;  // [GP][GID]
+  const double* val;   // [GP]
+  double nv[GP];       // round(P / clock, 1)
+};
+
+// result sink: pass 1 counts, pass 2 writes at the reserved bases
+struct Sink {
+  bool write;
+  int nrec;
+  uint32_t nheap;
+  sdx_result* rec;
+  uint8_t* heap;
+  uint32_t rbase, hbase, msg;
+};
+
+GI bool at(const uint8_t* d, int n, int p, const uint8_t* s, int len) {
+  if (p < 0 || p + len > n) return false;
+  for (int i = 0; i < len; ++i)
+    if (d[p + i] != s[i]) return false;
+  return true;
+}
+GI bool str_eq(const Str& a, const Str& b) {
+  if (a.len != b.len) return false;
+  for (int i = 0; i < a.len; ++i)
+    if (a.c[i] != b.c[i]) return false;
+  return true;
+}
+// str.find(s, from)
+GD int find_str(const uint8_t* d, int n, int from, const Str& s) {
+  if (s.len == 0) return from <= n ? from : -1;
+  const uint8_t c0 = s.c[0];
+  for (int p = from; p + s.len <= n; ++p)
+    if (d[p] == c0 && at(d, n, p, s.c, s.len)) return p;
+  return -1;
+}
+
+// pattern_exists(search, patterns, d[base:]) (pattern_utils.py:34-136): 1 found (*out = the target
+// string), 0 = -1, -1 = the target would exceed SDX_GEN_STRMAX characters (contract)
+GD int pex(const Msg& m, const sdx_patspec* sp, int base, Str* out) {
+  const int slen = sp->len, nu = sp->nuniq;
+  uint8_t cand[SDX_MAXUNIQ][GP];
+  int cnt[SDX_MAXUNIQ];
+  int total = 1;
+  for (int u = 0; u < nu; ++u) {
+    const double uv = sp->uval[u], tol = sp->utol[u];
+    double gap[GP];
+    int c = 0;
+    for (int k = 0; k < m.npat; ++k) {
+      const double g = fabs(m.nv[k] - uv);
+      if (g <= 0.001 || g <= tol) {  // (:70-72)
+        int j = c++;                 // stable sort by gap (:76-78): move past strictly larger gaps only
+        while (j > 0 && gap[j - 1] > g) {
+          gap[j] = gap[j - 1];
+          cand[u][j] = cand[u][j - 1];
+          --j;
+        }
+        gap[j] = g;
+        cand[u][j] = (uint8_t)k;
+      }
+    }
+    if (c == 0) return 0;  // (:73-75)
+    cnt[u] = c;
+    total *= c;
+    if (total > 10000) return 0;  // (:88-95): the product only grows
+  }
+  int digit[SDX_MAXUNIQ];
+  for (int u = 0; u < SDX_MAXUNIQ; ++u) digit[u] = 0;
+  for (int it = 0; it < total; ++it) {
+    uint32_t used = 0;
+    bool dup = false;
+    for (int u = 0; u < nu; ++u) {
+      const int k = cand[u][digit[u]];
+      if ((used >> k) & 1u) dup = true;
+      used |= 1u << k;
+    }
+    if (!dup) {  // (:111-113)
+      Str t;
+      t.len = 0;
+      for (int s = 0; s < slen; ++s) {
+        const int u = sp->uidx[s];
+        const int k = cand[u][digit[u]];
+        const int L = m.ids[k * GID];
+        if (t.len + L > GS) return -1;
+        for (int j = 0; j < L; ++j) t.c[t.len++] = m.ids[k * GID + 1 + j];
+      }
+      if (find_str(m.d, m.n, base, t) >= 0) {  // (:133-134)
+        *out = t;
+        return 1;
+      }
+    }
+    for (int u = nu - 1; u >= 0; --u) {  // itertools.product: the last list varies fastest
+      if (digit[u] + 1 < cnt[u]) {
+        digit[u]++;
+        break;
+      }
+      digit[u] = 0;
+    }
+  }
+  return 0;
+}
+
+// (?:U0|U1|..){lmin,} at q in Python sre order: alternatives in order, another iteration before
+// stopping; a dead end below lmin iterations backtracks to the latest choice with a further
+// alternative.  Returns the end of the repetition or -1; *over on the step budget / depth limit.
+GD int rep_match(const uint8_t* d, int n, int q, const Str* U, int nu, int lmin, bool* over) {
+  long long steps = 0;
+  if (lmin > GREP) {
+    *over = true;
+    return -1;
+  }
+  uint8_t ch[GREP];
+  int ps[GREP];
+  int depth = 0, p = q, a0 = 0;
+  while (true) {
+    if (++steps > GBUDGET) {
+      *over = true;
+      return -1;
+    }
+    int a = -1;
+    for (int j = a0; j < nu; ++j)
+      if (at(d, n, p, U[j].c, U[j].len)) {
+        a = j;
+        break;
+      }
+    if (a >= 0) {
+      if (depth < lmin) {
+        ch[depth] = (uint8_t)a;
+        ps[depth] = p;
+      }
+      ++depth;
+      p += U[a].len;
+      a0 = 0;
+      continue;
+    }
+    if (depth >= lmin) return p;  // stop here: the optional tail always matches
+    if (depth == 0) return -1;
+    --depth;
+    p = ps[depth];
+    a0 = ch[depth] + 1;
+  }
+}
+
+GI bool any_f(const uint8_t* b, int n) {
+  for (int i = 0; i < n; ++i)
+    if (b[i] == 2) return true;
+  return false;
+}
+
+// hex digits of bits b[0, nb) (helpers.py:28-64) into T; returns the count (after lstrip('0'))
+GD int hex_text(const uint8_t* b, int nb, int strip_zero, uint8_t* T) {
+  const int nd = (nb + 3) >> 2;
+  int q = 0;
+  bool lead = strip_zero != 0;
+  for (int d = 0; d < nd; ++d) {
+    const int e = nb - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+    int v = 0;
+    for (int i = a; i < e; ++i) v = (v << 1) | b[i];
+    if (lead && v == 0) continue;
+    lead = false;
+    T[q++] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+  }
+  return q;
+}
+
+GD int emit(Sink& sk, const BankView& bv, int p, int pre_off, int pre_len, const uint8_t* T, int dl, int post_off,
+            int post_len, int bitlen) {
+  const int total = pre_len + dl + post_len;
+  if (total > 65535) return SDX_RAISE_CONTRACT;  // sdx_result.payload_len
+  if (sk.write) {
+    uint8_t* dst = sk.heap + sk.hbase + sk.nheap;
+    for (int i = 0; i < pre_len; ++i) dst[i] = bv.str[pre_off + i];
+    for (int i = 0; i < dl; ++i) dst[pre_len + i] = T[i];
+    for (int i = 0; i < post_len; ++i) dst[pre_len + dl + i] = bv.str[post_off + i];
+    sdx_result r;
+    r.payload_off = sk.hbase + sk.nheap;
+    r.payload_len = (uint16_t)total;
+    r.proto = (uint16_t)p;
+    r.bit_length = (uint32_t)bitlen;
+    r.msg = sk.msg;
+    sk.rec[sk.rbase + sk.nrec] = r;
+  }
+  ++sk.nrec;
+  sk.nheap += (uint32_t)total;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// MU (message_unsynced.py:11-296)
+// ---------------------------------------------------------------------------------------------
+// one match's bits -> postDemodulation, padding, dmsg, modulematch, result (:226-290)
+GD int finish_mu_g(const BankView& bv, const sdx_mu_proto* rec, int p, uint8_t* B, uint8_t* B2, uint8_t* T, int nb,
+                   Sink& sk) {
+  uint8_t* buf = B;
+  if (rec->postdemo != SDX_PD_NONE && !any_f(buf, nb)) {  // 'F': int() ValueError caught -> unchanged
+    int no = 0;
+    const int rc = run_postdemo(rec->postdemo, buf, nb, B2, &no);
+    if (rc == 0) return 0;  // rcode < 1
+    if (rc == 1) {
+      buf = B2;
+      nb = no;
+    }  // rc == -1: ValueError inside the method, caught -> bits unchanged
+  }
+  const int pad = rec->pad_bits;
+  const int nbp = (nb + pad - 1) / pad * pad;  // (:257-259)
+  for (int i = nb; i < nbp; ++i) buf[i] = 0;
+  const bool isf = any_f(buf, nbp);
+  int dl;
+  if (rec->dispatch_bin) {  // (:264-265)
+    for (int i = 0; i < nbp; ++i) T[i] = buf[i] == 2 ? 'F' : (uint8_t)('0' + buf[i]);
+    dl = nbp;
+  } else if (isf) {  // bin_str_2_hex_str -> None (helpers.py:44-45)
+    if (rec->remove_zero) return SDX_RAISE_ATTRIBUTE;  // None.lstrip (:269)
+    T[0] = 'N'; T[1] = 'o'; T[2] = 'n'; T[3] = 'e';  // f"{None}"
+    dl = 4;
+  } else {
+    dl = hex_text(buf, nbp, rec->remove_zero, T);
+  }
+  if (rec->mm_dfa >= 0) {  // re.search(modulematch, payload) (:277-280); the preamble is in the state
+    for (int i = 0; i < rec->post_len; ++i) T[dl + i] = bv.str[rec->post_off + i];
+    if (!dfa_accepts(bv, rec->mm_dfa, rec->mm_pre_state, T, dl + rec->post_len)) return 0;
+  }
+  return emit(sk, bv, p, rec->pre_off, rec->pre_len, T, dl, rec->post_off, rec->post_len, nbp);
+}
+
+GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* T, Sink& sk) {
+  if (m.n == 0) return 0;  // `if not raw_data` (:22-25)
+  double last = __builtin_nan("");
+  const int nmu = (int)bv.hdr->n_mu;
+  for (int p = 0; p < nmu; ++p) {
+    const sdx_mu_proto* rec = bv.mu + p;
+    if (!rec->active || rec->never) continue;  // (:47-48); never = the key loop always fails
+    if (!(rec->clock == last)) {
+      last = rec->clock;
+      for (int k = 0; k < m.npat; ++k) m.nv[k] = py_round1(m.val[k] / rec->clock);  // (:62-64)
+    }
+    int base = 0;
+    Str S;
+    S.len = 0;
+    if (rec->has_start) {  // (:70-88)
+      const int r = pex(m, &rec->start, 0, &S);
+      if (r < 0) return SDX_RAISE_CONTRACT;
+      if (r == 0) continue;
+      base = find_str(m.d, m.n, 0, S);
+    }
+    // pattern_lookup (distinct strings, last writer), end_pattern_lookup (pstr[:-1], first writer)
+    Str U[3], E[3];
+    uint8_t us[3], es[3];
+    int nu = 0, ne = 0;
+    bool fail = false;
+    const sdx_patspec* K[3] = {&rec->one, &rec->zero, &rec->flt};
+    const uint8_t SYM[3] = {1, 0, 2};
+    for (int k = 0; k < 3; ++k) {  // (:98-141)
+      if (K[k]->len == 0) continue;
+      Str t;
+      const int r = pex(m, K[k], base, &t);
+      if (r < 0) return SDX_RAISE_CONTRACT;
+      if (r == 0) {
+        if (k != 2) {
+          fail = true;
+          break;
+        }
+        continue;
+      }
+      int j = 0;
+      for (; j < nu; ++j)
+        if (str_eq(U[j], t)) break;
+      if (j == nu) U[nu++] = t;
+      us[j] = SYM[k];
+      if (t.len > 0) {
+        Str e = t;
+        e.len -= 1;
+        int i = 0;
+        for (; i < ne; ++i)
+          if (str_eq(E[i], e)) break;
+        if (i == ne) {
+          E[ne] = e;
+          es[ne] = SYM[k];
+          ++ne;
+        }
+      }
+    }
+    if (fail || nu == 0) continue;
+    if (!rec->recon) ne = 0;  // the regex tail and the chunk fallback both need reconstructBit
+    const uint8_t* w = m.d + base;
+    const int nw = m.n - base;
+    const int W = rec->width;
+    int pos = 0;
+    while (pos <= nw) {  // matcher.finditer(current_raw_data) (:195)
+      int gq = -1, ge = -1, s = pos;
+      for (; s <= nw; ++s) {
+        if (S.len && !at(w, nw, s, S.c, S.len)) continue;
+        bool over = false;
+        const int e = rep_match(w, nw, s + S.len, U, nu, rec->length_min, &over);
+        if (over) return SDX_RAISE_CONTRACT;
+        if (e >= 0) {
+          gq = s + S.len;
+          ge = e;
+          break;
+        }
+      }
+      if (gq < 0) break;
+      for (int j = 0; j < ne; ++j)  // (?:E0|E1|..)? : the first key that matches
+        if (at(w, nw, ge, E[j].c, E[j].len)) {
+          ge += E[j].len;
+          break;
+        }
+      pos = ge > s ? ge : s + 1;
+      if (W == 0) continue;  // (:204-205)
+      const int glen = ge - gq;
+      if (glen == 0) return SDX_RAISE_INDEX;  // chunks[-1] on [] (:212)
+      const int nch = (glen + W - 1) / W;
+      if (nch > rec->length_max) continue;  // (:217-218); INT32_MAX = no length_max
+      int nb = 0;
+      for (int c = 0; c < nch; ++c) {  // (:220-229)
+        const int x = gq + c * W, cl = (ge - x < W) ? ge - x : W;
+        int sy = -1;
+        for (int j = 0; j < nu && sy < 0; ++j)
+          if (U[j].len == cl && at(w, nw, x, U[j].c, cl)) sy = us[j];
+        for (int j = 0; j < ne && sy < 0; ++j)
+          if (E[j].len == cl && at(w, nw, x, E[j].c, cl)) sy = es[j];
+        if (sy >= 0) B[nb++] = (uint8_t)sy;
+      }
+      const int rr = finish_mu_g(bv, rec, p, B, B2, T, nb, sk);
+      if (rr) return rr;
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// MS (message_synced.py:10-243)
+// ---------------------------------------------------------------------------------------------
+GD int finish_ms_g(const BankView& bv, const sdx_ms_proto* rec, int p, uint8_t* B, uint8_t* B2, uint8_t* T, int nb,
+                   Sink& sk) {
+  uint8_t* buf = B;
+  if (nb == 0) return 0;                                           // (:191-192)
+  if (rec->lir_min != -1 && nb < rec->lir_min) return 0;           // length_in_range (:194-196)
+  if (nb > rec->lir_max) return 0;
+  const int pad = rec->pad_bits;                                   // padding before postDemod (:198-200)
+  const int nbp = (nb + pad - 1) / pad * pad;
+  for (int i = nb; i < nbp; ++i) buf[i] = 0;
+  nb = nbp;
+  if (rec->postdemo != SDX_PD_NONE) {                             // no try: 'F' raises ValueError (:209)
+    if (any_f(buf, nb)) return SDX_RAISE_VALUE;
+    int no = 0;
+    const int rc = run_postdemo(rec->postdemo, buf, nb, B2, &no);
+    if (rc == -1) return SDX_RAISE_VALUE;
+    if (rc == 0) return 0;
+    if (no > 0) {  // `if ret_bits`
+      buf = B2;
+      nb = no;
+    }
+  }
+  if (any_f(buf, nb)) return 0;  // bin_str_2_hex_str -> None -> skipped (:224-226)
+  const int dl = hex_text(buf, nb, 0, T);
+  return emit(sk, bv, p, rec->pre_off, rec->pre_len, T, dl, rec->post_off, rec->post_len, nb);
+}
+
+GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8_t* B2, uint8_t* T, Sink& sk) {
+  if (!ok || cp < 0 || cp >= m.npat) return 0;  // the string gates and `str(CP) in patterns` (:21-57)
+  const double clock = fabs(m.val[cp]);
+  if (clock == 0.0) return 0;  // (:60-62)
+  for (int k = 0; k < m.npat; ++k) m.nv[k] = py_round1(m.val[k] / clock);  // (:64-72)
+  const int nms = (int)bv.hdr->n_ms;
+  const uint8_t KS[4] = {3, 1, 0, 2};  // sync '', one '1', zero '0', float 'F'
+  for (int p = 0; p < nms; ++p) {
+    const sdx_ms_proto* rec = bv.ms + p;
+    if (rec->never) continue;
+    if (rec->pclock > 0.0 && fabs(rec->pclock - clock) > clock * 0.3) continue;  // (:81-86)
+    const int W = rec->width;
+    Str K[4], E[3];
+    uint8_t ks[4], es[3];
+    int nk = 0, ne = 0, mstart = 0;
+    bool fail = false;
+    for (int k = 0; k < 4; ++k) {  // (:109-160)
+      const sdx_patspec* sp = &rec->key[k];
+      if (sp->len == 0) continue;
+      Str t;
+      const int r = pex(m, sp, 0, &t);
+      if (r < 0) return SDX_RAISE_CONTRACT;
+      if (r == 0) {
+        if (k != 3) {
+          fail = true;
+          break;
+        }
+        continue;
+      }
+      int j = 0;
+      for (; j < nk; ++j)
+        if (str_eq(K[j], t)) break;
+      if (j == nk) K[nk++] = t;
+      ks[j] = KS[k];
+      if (t.len > 0) {
+        Str e = t;
+        e.len -= 1;
+        int i = 0;
+        for (; i < ne; ++i)
+          if (str_eq(E[i], e)) break;
+        if (i == ne) {
+          E[ne] = e;
+          es[ne] = KS[k];
+          ++ne;
+        }
+      }
+      if (k == 0) {  // (:145-158)
+        mstart = find_str(m.d, m.n, 0, t) + t.len;
+        const double bl = W > 0 ? (double)(m.n - mstart) / (double)W : 0.0;
+        if ((double)rec->lmin_sync > bl) {
+          fail = true;
+          break;
+        }
+        ne = 0;  // end_pattern_lookup = {}
+      }
+    }
+    if (fail || nk == 0 || W <= 0) continue;
+    int nb = 0;
+    for (int i = mstart; i < m.n; i += W) {  // (:172-189)
+      const int cl = (m.n - i < W) ? m.n - i : W;
+      int sy = -1;
+      for (int j = 0; j < nk && sy < 0; ++j)
+        if (K[j].len == cl && at(m.d, m.n, i, K[j].c, cl)) sy = ks[j];
+      if (sy >= 0) {
+        if (sy != 3) B[nb++] = (uint8_t)sy;
+        continue;
+      }
+      if (!rec->recon) break;
+      const int tl = cl == W ? cl - 1 : cl;  // chunk[:-1] if full else chunk
+      for (int j = 0; j < ne && sy < 0; ++j)
+        if (E[j].len == tl && at(m.d, m.n, i, E[j].c, tl)) sy = es[j];
+      if (sy < 0) break;
+      B[nb++] = (uint8_t)sy;
+    }
+    const int rr = finish_ms_g(bv, rec, p, B, B2, T, nb, sk);
+    if (rr) return rr;
+  }
+  return 0;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, sdx_general_batch b, sdx_out out) {
+  const BankView bv = bank_view(bank);
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= ntot) return;
+  const int msg = b.sel_dev ? b.sel_dev[i] : i;
+  const int64_t off = b.offsets_dev[msg];
+  Msg m;
+  m.d = b.data_dev + off;
+  m.n = (int)(b.offsets_dev[msg + 1] - off);
+  m.npat = b.npat_dev[msg] < GP ? b.npat_dev[msg] : GP;
+  m.ids = b.pat_ids_dev + (size_t)msg * GP * GID;
+  m.val = b.pat_val_dev + (size_t)msg * GP;
+  // per-message scratch: bits, postDemod output, payload text (include/sdx.h sdx_general_work_bytes)
+  uint8_t* B = out.work_dev + 3 * off + (int64_t)3 * GSLACK * msg;
+  uint8_t* B2 = B + m.n + GSLACK;
+  uint8_t* T = B2 + m.n + GSLACK;
+  const int cp = KIND == SDX_KIND_MS ? (int)b.cp_slot_dev[msg] : -1;
+  const bool ok = KIND == SDX_KIND_MS ? b.ms_ok_dev[msg] != 0 : true;
+  Sink sk{false, 0, 0u, out.rec_dev, out.heap_dev, 0u, 0u, (uint32_t)msg};
+  int raise = KIND == SDX_KIND_MU ? mu_message(bv, m, B, B2, T, sk) : ms_message(bv, m, cp, ok, B, B2, T, sk);
+  sdx_desc d;
+  d.rec_begin = 0;
+  d.n_rec = 0;
+  d.raise_kind = (uint8_t)raise;
+  d.status = raise ? SDX_ST_RAISED : SDX_ST_OK;
+  if (!raise && sk.nrec) {
+    const uint32_t nh = (sk.nheap + 15u) & ~15u;
+    const uint32_t rb = atomicAdd(&out.cursor_dev[0], (uint32_t)sk.nrec);
+    const uint32_t hb = atomicAdd(&out.cursor_dev[1], nh);
+    if (sk.nrec > 65535 || rb + sk.nrec > out.rec_cap || hb + nh > out.heap_cap) {
+      d.status = SDX_ST_OVF_OUT;
+      atomicOr(&out.cursor_dev[2], 1u);
+    } else {
+      Sink sw{true, 0, 0u, out.rec_dev, out.heap_dev, rb, hb, (uint32_t)msg};
+      raise = KIND == SDX_KIND_MU ? mu_message(bv, m, B, B2, T, sw) : ms_message(bv, m, cp, ok, B, B2, T, sw);
+      d.rec_begin = rb;
+      d.n_rec = (uint16_t)sw.nrec;
+    }
+  }
+  out.desc_dev[msg] = d;
+}
+
+// ---------------------------------------------------------------------------------------------
+// MC frames of any length: the "fixed" chain of k_mc (manchester.py:49-144) with the frame's bits
+// in global memory (LaneBits layout: word w of lane t at base[w * 256 + t])
+// ---------------------------------------------------------------------------------------------
+GD int mc_frame(const BankView& bv, const LaneBits& BN, const LaneBits& BI, int nN, int nI, bool hex_ok, int clock,
+                int mcbit, int flags, int mw, Sink& sk) {
+  const int nmc = (int)bv.hdr->n_mc;
+  for (int p = 0; p < nmc; ++p) {
+    const sdx_mc_proto* r = bv.mc + p;
+    // gates of _demodulate_mc_data (manchester.py:70-89; clockrange fixed to [0] / [1])
+    if (mcbit < (r->has_lmin ? r->lmin : -1)) continue;
+    if (mcbit > (r->has_lmax ? r->lmax : 9999)) continue;
+    if (r->has_cr && !((double)clock > r->cr_lo && (double)clock < r->cr_hi)) continue;
+    if (!hex_ok) return SDX_RAISE_TYPE;  // len(None) -> TypeError
+    const bool inv = (r->invert != 0) ^ ((flags & 3) != 0);  // (:91-96)
+    const LaneBits& B = inv ? BI : BN;
+    const int nb = inv ? nI : nN;
+    const LaneBits DM{B.base, mw, true};
+    const McOut o = mc_method(r, r->method, B, nb, nb, DM);
+    if (o.rc == -1) return SDX_RAISE_TYPE;
+    if (o.rc == -2) return SDX_RAISE_VALUE;
+    if (o.rc != 1) continue;
+    const int total = r->pre_len + o.len;
+    if (total > 65535) return SDX_RAISE_CONTRACT;
+    if (sk.write) {
+      uint8_t* dst = sk.heap + sk.hbase + sk.nheap;
+      for (int i = 0; i < r->pre_len; ++i) dst[i] = bv.str[r->pre_off + i];
+      mc_write(r, o, B, nb, nb, dst + r->pre_len);
+      sdx_result x;
+      x.payload_off = sk.hbase + sk.nheap;
+      x.payload_len = (uint16_t)total;
+      x.proto = (uint16_t)p;
+      x.bit_length = 0;
+      x.msg = sk.msg;
+      sk.rec[sk.rbase + sk.nrec] = x;
+    }
+    ++sk.nrec;
+    sk.nheap += (uint32_t)total;
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void k_mc_general(const void* __restrict__ bank, sdx_mc_batch b, int mw, sdx_out out) {
+  const BankView bv = bank_view(bank);
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int tid = threadIdx.x, gi = blockIdx.x * 256 + tid;
+  if (gi >= ntot) return;
+  const int msg = b.sel_dev ? b.sel_dev[gi] : gi;
+  uint64_t* bn = reinterpret_cast<uint64_t*>(out.work_dev) + (size_t)blockIdx.x * 512 * mw + tid;
+  uint64_t* bi = bn + (size_t)256 * mw;
+  const int64_t off = b.offsets_dev[msg];
+  const int hl = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
+  // hex -> bits of both polarities (helpers.py:168-188: leading zero nibbles dropped; the
+  // _convert_mc_hex_to_bits translate inverts uppercase digits only, manchester.py:33-36)
+  bool hex_ok = hl > 0 && hl <= mw * 16;
+  int nN = 0, nI = 0;
+  bool startedN = false, startedI = false;
+  uint64_t wn = 0, wi = 0;
+  for (int i = 0; i < hl && hex_ok; ++i) {
+    const uint8_t c = b.hex_dev[off + i];
+    int v = -1;
+    if (c >= '0' && c <= '9') v = c - '0';
+    else if (c >= 'A' && c <= 'F') v = c - 'A' + 10;
+    else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
+    if (v < 0) {
+      hex_ok = false;
+      break;
+    }
+    const bool upper = !(c >= 'a' && c <= 'f');
+    const int vi = upper ? 15 - v : v;
+    if (v || startedN || i == hl - 1) {
+      startedN = true;
+      wn |= (uint64_t)v << (60 - (nN & 63));
+      nN += 4;
+      if ((nN & 63) == 0) { bn[(size_t)((nN >> 6) - 1) * 256] = wn; wn = 0; }
+    }
+    if (vi || startedI || i == hl - 1) {
+      startedI = true;
+      wi |= (uint64_t)vi << (60 - (nI & 63));
+      nI += 4;
+      if ((nI & 63) == 0) { bi[(size_t)((nI >> 6) - 1) * 256] = wi; wi = 0; }
+    }
+  }
+  if (!hex_ok) {  // no method runs on these bits (TypeError before any decode)
+    nN = nI = 0;
+    wn = wi = 0;
+  }
+  for (int w = nN >> 6; w < mw; ++w) { bn[(size_t)w * 256] = (w == (nN >> 6)) ? wn : 0ull; }
+  for (int w = nI >> 6; w < mw; ++w) { bi[(size_t)w * 256] = (w == (nI >> 6)) ? wi : 0ull; }
+  const LaneBits BN{bn, mw, false}, BI{bi, mw, false};
+  const int clock = b.clock_dev[msg], mcbit = b.mcbitnum_dev[msg], flags = b.flags_dev[msg];
+  Sink sk{false, 0, 0u, out.rec_dev, out.heap_dev, 0u, 0u, (uint32_t)msg};
+  int raise = mc_frame(bv, BN, BI, nN, nI, hex_ok, clock, mcbit, flags, mw, sk);
+  sdx_desc d;
+  d.rec_begin = 0;
+  d.n_rec = 0;
+  d.raise_kind = (uint8_t)raise;
+  d.status = raise ? SDX_ST_RAISED : SDX_ST_OK;
+  if (!raise && sk.nrec) {
+    const uint32_t nh = (sk.nheap + 15u) & ~15u;
+    const uint32_t rb = atomicAdd(&out.cursor_dev[0], (uint32_t)sk.nrec);
+    const uint32_t hb = atomicAdd(&out.cursor_dev[1], nh);
+    if (rb + sk.nrec > out.rec_cap || hb + nh > out.heap_cap) {
+      d.status = SDX_ST_OVF_OUT;
+      atomicOr(&out.cursor_dev[2], 1u);
+    } else {
+      Sink sw{true, 0, 0u, out.rec_dev, out.heap_dev, rb, hb, (uint32_t)msg};
+      mc_frame(bv, BN, BI, nN, nI, hex_ok, clock, mcbit, flags, mw, sw);
+      d.rec_begin = rb;
+      d.n_rec = (uint16_t)sw.nrec;
+    }
+  }
+  out.desc_dev[msg] = d;
+}
+
+}  // namespace sdxg
+
+extern "C" {
+
+uint64_t sdx_general_work_bytes(int64_t total_chars, int32_t n) {
+  return (uint64_t)(3 * (total_chars > 0 ? total_chars : 0) + (int64_t)3 * sdxg::GSLACK * (n > 0 ? n : 0) + 256);
+}
+
+int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_batch* batch, const sdx_out* out,
+                             void* hip_stream) {
+  if (!bank || !batch || !out) return sdx::set_error(SDX_EINVAL, "null argument");
+  if (kind != SDX_KIND_MU && kind != SDX_KIND_MS) return sdx::set_error(SDX_EINVAL, "kind must be MU or MS");
+  if (kind == SDX_KIND_MS && (!batch->cp_slot_dev || !batch->ms_ok_dev))
+    return sdx::set_error(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+  const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
+  if (ntot <= 0) return SDX_OK;
+  if (!batch->data_dev || !batch->offsets_dev || !batch->npat_dev || !batch->pat_ids_dev || !batch->pat_val_dev ||
+      !out->work_dev)
+    return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: missing buffer (work_dev: sdx_general_work_bytes)");
+  const int grid = (ntot + 63) / 64;
+  hipStream_t st = (hipStream_t)hip_stream;
+  const void* bd = sdx::bank_dev_ptr(bank);
+  if (kind == SDX_KIND_MU)
+    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MU>), dim3(grid), dim3(64), 0, st, bd, *batch, *out);
+  else
+    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MS>), dim3(grid), dim3(64), 0, st, bd, *batch, *out);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("k_general: ") + hipGetErrorString(e));
+  return SDX_OK;
+}
+
+uint64_t sdx_mc_general_work_bytes(int32_t n, int32_t max_hex) {
+  const int64_t mw = ((int64_t)(max_hex > 0 ? max_hex : 1) + 15) / 16;
+  const int64_t blocks = ((int64_t)(n > 0 ? n : 0) + 255) / 256;
+  return (uint64_t)(blocks * 512 * mw * 8);
+}
+
+int sdx_demod_mc_general(const sdx_bank* bank, const sdx_mc_batch* batch, int32_t max_hex, const sdx_out* out,
+                         void* hip_stream) {
+  if (!bank || !batch || !out) return sdx::set_error(SDX_EINVAL, "null argument");
+  const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
+  if (ntot <= 0) return SDX_OK;
+  if (max_hex <= 0 || !out->work_dev || out->work_cap < sdx_mc_general_work_bytes(ntot, max_hex))
+    return sdx::set_error(SDX_EINVAL, "sdx_demod_mc_general: work_dev smaller than sdx_mc_general_work_bytes");
+  const int mw = (max_hex + 15) / 16;
+  hipLaunchKernelGGL(sdxg::k_mc_general, dim3((ntot + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream,
+                     sdx::bank_dev_ptr(bank), *batch, mw, *out);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("k_mc_general: ") + hipGetErrorString(e));
+  return SDX_OK;
+}
+
+}  // extern "C"

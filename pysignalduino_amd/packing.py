@@ -20,6 +20,15 @@ class ContractError(NotImplementedError):
     """An input the device path does not model (never silently approximated)."""
 
 
+class GeneralPathMessage(ContractError):
+    """Outside the fixed-layout kernels' contract (multi-digit pattern ids, more than LONG_MAX
+    pulses): the message runs on the general path (sdx_demod_pulses_general) instead."""
+
+
+GEN_MAXPAT = 16   # include/sdx.h SDX_GEN_MAXPAT
+GEN_IDSTR = 16    # SDX_GEN_IDSTR: [length][<= 15 digits]
+
+
 def _encode_data(data: str) -> bytes:
     """One byte per character; non-ASCII characters keep only their isdigit() property."""
     try:
@@ -40,7 +49,23 @@ def _patterns(msg: Dict[str, Any]) -> Tuple[List[str], List[float]]:
     ids = list(pats.keys())
     for i in ids:
         if len(i) != 1:
-            raise ContractError(f"pattern id P{i}: only single-digit pattern ids (P0..P9) are modelled on the device")
+            raise GeneralPathMessage(f"pattern id P{i}: the fixed-layout kernels take single-digit ids (P0..P9)")
+    return ids, [pats[i] for i in ids]
+
+
+def _patterns_general(msg: Dict[str, Any]) -> Tuple[List[str], List[float]]:
+    """The same dict, any ids (sdx_general_batch): at most GEN_MAXPAT ids of <= 15 digits."""
+    pats: Dict[str, float] = {}
+    for key, val in msg.items():
+        if key.startswith("P") and key[1:].isdigit():
+            try:
+                pats[str(int(key[1:]))] = float(val)
+            except ValueError:
+                pass
+    ids = list(pats.keys())
+    if len(ids) > GEN_MAXPAT or any(len(i) > GEN_IDSTR - 1 for i in ids):
+        raise ContractError(f"more than {GEN_MAXPAT} patterns or a pattern id of more than {GEN_IDSTR - 1} "
+                            "digits: outside the device contract")
     return ids, [pats[i] for i in ids]
 
 
@@ -79,7 +104,7 @@ class PulsePacker:
                     ms_ok = 0
         elif not data:
             data = ""
-        ids, vals = _patterns(msg) if (self.kind == "MU" and data) or (self.kind == "MS" and ms_ok) else ([], [])
+        ids, vals = self._pat(msg) if (self.kind == "MU" and data) or (self.kind == "MS" and ms_ok) else ([], [])
         if self.kind == "MS" and ms_ok:
             key = str(int(msg["CP"]))
             if key in ids:
@@ -97,6 +122,8 @@ class PulsePacker:
         self.ms_ok.append(ms_ok)
         self.clock_abs.append(clock_abs)
         self.rssi.append(msg.get("R"))
+
+    _pat = staticmethod(_patterns)
 
     def batch(self) -> PulseBatch:
         n = len(self.datas)
@@ -128,3 +155,28 @@ def mc_batch_from_frames(frames: Sequence[Tuple[str, int, int, str, Any]]) -> Mc
     mtype = np.array([1 if f[3] == "Mc" else 0 for f in frames], np.uint8)
     v32 = np.array([1 if (f[4] and str(f[4])[:6] == "V 3.2.") else 0 for f in frames], np.uint8)
     return McBatch(data, offsets, clock, L, mtype, v32)
+
+
+class GeneralPacker(PulsePacker):
+    """MU or MS messages for the general path (include/sdx.h sdx_general_batch): the same string
+    gates and conversions as PulsePacker, pattern ids of any length (<= 15 digits), <= 16 patterns,
+    any number of pulses."""
+
+    _pat = staticmethod(_patterns_general)
+
+    def arrays(self) -> Dict[str, np.ndarray]:
+        n = len(self.datas)
+        lens = np.array([len(d) for d in self.datas], dtype=np.int64)
+        offsets = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        ids = np.zeros((n, GEN_MAXPAT, GEN_IDSTR), np.uint8)
+        vals = np.zeros((n, GEN_MAXPAT), np.float64)
+        for i in range(n):
+            for k, (pid, v) in enumerate(zip(self.ids[i], self.vals[i])):
+                b = pid.encode("ascii")
+                ids[i, k, 0] = len(b)
+                ids[i, k, 1:1 + len(b)] = np.frombuffer(b, np.uint8)
+                vals[i, k] = v
+        return {"data": np.frombuffer(b"".join(self.datas), dtype=np.uint8).copy(), "offsets": offsets,
+                "npat": np.array(self.npat, np.uint8), "pat_ids": ids, "pat_val": vals,
+                "cp_slot": np.array(self.cp, np.int8), "ms_ok": np.array(self.ms_ok, np.uint8)}

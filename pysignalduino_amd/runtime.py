@@ -24,6 +24,7 @@ KIND_MU, KIND_MS, KIND_MC = 0, 1, 2
 KIND_MN = 3        # host-side tag for Engine.run (sdx_demod_mn)
 ST_OK, ST_RAISED, ST_OVF_TILE, ST_OVF_OUT = 0, 1, 2, 3
 RAISE_NAMES = {1: IndexError, 2: AttributeError, 3: ValueError, 4: TypeError, 5: ZeroDivisionError}
+RAISE_CONTRACT = 6  # SDX_RAISE_CONTRACT: a general-path limit (include/sdx.h), not a reference outcome
 SHORT_MAX = 256    # k_pulses<.., 4 words, 64 messages/tile>
 LONG_MAX = 4096    # k_pulses<.., 64 words, 4 messages/tile>
 MC_HEX_MAX = 128   # MC_MAXW * 16 hex characters
@@ -36,7 +37,8 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
             "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
-            "sdx_exchange_pack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses"]
+            "sdx_exchange_pack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
+            "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general"]
 GROUP_MIN = 4096   # SDX_GROUP_MIN
 
 
@@ -45,6 +47,12 @@ class SdxPulseBatch(Structure):
                 ("pat_id_dev", c_void_p), ("pat_val_dev", c_void_p), ("cp_slot_dev", c_void_p),
                 ("ms_ok_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p), ("n", c_int32),
                 ("n_sel", c_int32)]
+
+
+class SdxGeneralBatch(Structure):
+    _fields_ = [("data_dev", c_void_p), ("offsets_dev", c_void_p), ("npat_dev", c_void_p), ("pat_ids_dev", c_void_p),
+                ("pat_val_dev", c_void_p), ("cp_slot_dev", c_void_p), ("ms_ok_dev", c_void_p), ("sel_dev", c_void_p),
+                ("n", c_int32), ("n_sel", c_int32)]
 
 
 class SdxMcBatch(Structure):
@@ -138,6 +146,14 @@ def load_library(path: Optional[str] = None):
     lib.sdx_group_work_bytes.restype = c_size_t
     lib.sdx_group_pulses.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), c_void_p, c_void_p, c_size_t, c_void_p]
     lib.sdx_group_pulses.restype = c_int
+    lib.sdx_general_work_bytes.argtypes = [ctypes.c_int64, c_int32]
+    lib.sdx_general_work_bytes.restype = ctypes.c_uint64
+    lib.sdx_demod_pulses_general.argtypes = [c_void_p, c_int, POINTER(SdxGeneralBatch), POINTER(SdxOut), c_void_p]
+    lib.sdx_demod_pulses_general.restype = c_int
+    lib.sdx_mc_general_work_bytes.argtypes = [c_int32, c_int32]
+    lib.sdx_mc_general_work_bytes.restype = ctypes.c_uint64
+    lib.sdx_demod_mc_general.argtypes = [c_void_p, POINTER(SdxMcBatch), c_int32, POINTER(SdxOut), c_void_p]
+    lib.sdx_demod_mc_general.restype = c_int
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mc.restype = c_int
     lib.sdx_demod_mn.argtypes = [c_void_p, POINTER(SdxMnBatch), POINTER(SdxOut), c_void_p]
@@ -152,7 +168,7 @@ def load_library(path: Optional[str] = None):
     lib.sdx_units.restype = c_int
     lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, c_void_p]
     lib.sdx_exchange_pack.restype = c_int
-    if lib.sdx_abi_version() != 5:
+    if lib.sdx_abi_version() != 6:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -317,6 +333,50 @@ class Engine:
         o = self._out_struct(out)
         _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 
+    def launch_mc_general(self, bd, out, sel, max_hex: int) -> None:
+        """sdx_demod_mc_general over `sel` (frames of any length; its own bit workspace)."""
+        wb = int(self.lib.sdx_mc_general_work_bytes(int(sel.numel()), int(max_hex)))
+        work = self.torch.empty(max(wb, 1), dtype=self.torch.uint8, device=self.dev)
+        b = SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
+                       _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"], int(sel.numel()))
+        o = self._out_struct(out)
+        o.work_dev, o.work_cap = _ptr(work), wb
+        _check(self.lib, self.lib.sdx_demod_mc_general(self.handle, ctypes.byref(b), int(max_hex), ctypes.byref(o),
+                                                       self.stream_ptr()))
+        out["_mcg_work"] = work   # alive until the launch has run (the caller's fetch synchronises)
+
+    # -- general path (sdx_demod_pulses_general) --------------------------------------------------
+    def to_device_general(self, arrs) -> Dict[str, "object"]:
+        t, d = self.torch, self.dev
+        data = arrs["data"] if len(arrs["data"]) else np.zeros(1, np.uint8)
+        out = {k: t.from_numpy(np.ascontiguousarray(v)).to(d) for k, v in arrs.items() if k != "data"}
+        out["data"] = t.from_numpy(np.ascontiguousarray(data)).to(d)
+        out["n"] = int(len(arrs["npat"]))
+        out["total"] = int(arrs["offsets"][-1])
+        out["lengths"] = np.diff(arrs["offsets"])
+        return out
+
+    def run_general(self, kind: int, gd):
+        """MU/MS messages on the general path; returns host (desc, rec, heap) like run()."""
+        n = gd["n"]
+        rec_cap = 16 * n + 1024
+        heap_cap = int(2 * gd["total"] + 256 * n + 65536)
+        work = self.torch.empty(int(self.lib.sdx_general_work_bytes(gd["total"], n)), dtype=self.torch.uint8,
+                                device=self.dev)
+        for attempt in range(6):
+            out = self.alloc_out(n, rec_cap, heap_cap)
+            o = self._out_struct(out)
+            o.work_dev, o.work_cap = _ptr(work), int(work.numel())
+            b = SdxGeneralBatch(_ptr(gd["data"]), _ptr(gd["offsets"]), _ptr(gd["npat"]), _ptr(gd["pat_ids"]),
+                                _ptr(gd["pat_val"]), _ptr(gd["cp_slot"]), _ptr(gd["ms_ok"]), None, n, 0)
+            _check(self.lib, self.lib.sdx_demod_pulses_general(self.handle, kind, ctypes.byref(b), ctypes.byref(o),
+                                                               self.stream_ptr()))
+            desc, rec, heap = self.fetch(out)
+            if not (desc["status"] == ST_OVF_OUT).any():
+                return desc, rec, heap
+            rec_cap, heap_cap = 4 * rec_cap, 4 * heap_cap   # whole-batch re-run with grown outputs
+        raise RuntimeError("general path: result capacity overflow persists")
+
     def to_device_mn(self, hexes) -> Dict[str, "object"]:
         """MN frames (hex strings / bytes) -> device batch.  Contract: [0-9A-Fa-f]* and at most
         MN_HEX_MAX characters (checked here; ContractError-free callers check before)."""
@@ -378,9 +438,7 @@ class Engine:
                     raise NotImplementedError(f"MN frames longer than {MN_HEX_MAX} hex characters are outside "
                                               "the device contract")
             elif kind == KIND_MC:
-                if n and int(lengths.max(initial=0)) > MC_HEX_MAX:
-                    raise NotImplementedError(f"MC frames longer than {MC_HEX_MAX} hex characters are outside "
-                                              "the device contract")
+                pass   # frames longer than MC_HEX_MAX run on the general MC kernel (below)
             elif n and int(lengths.max(initial=0)) > LONG_MAX:
                 raise NotImplementedError(f"messages longer than {LONG_MAX} pulses are outside the device contract")
         rec_cap = rec_cap or (8 * n_work + 1024)
@@ -399,7 +457,14 @@ class Engine:
             if sel_long is not None and sel_long.numel():
                 self.launch_pulses(kind, bd, out, sel=sel_long, long_variant=True)
         elif kind == KIND_MC:
-            self.launch_mc(bd, out)
+            longf = lengths > MC_HEX_MAX
+            if not longf.any():
+                self.launch_mc(bd, out)
+            else:   # k_mc takes <= MC_HEX_MAX characters; longer frames: sdx_demod_mc_general
+                if not longf.all():
+                    self.launch_mc(bd, out, sel=t.from_numpy(np.nonzero(~longf)[0].astype(np.int32)).to(self.dev))
+                self.launch_mc_general(bd, out, t.from_numpy(np.nonzero(longf)[0].astype(np.int32)).to(self.dev),
+                                       int(lengths.max()))
         else:
             short = lengths <= SHORT_MAX
             if short.all():
@@ -426,7 +491,12 @@ class Engine:
             if kind == KIND_MN:
                 self.launch_mn(bd, out2, elig=mn_elig, method=mn_method, sel=sel)
             elif kind == KIND_MC:
-                self.launch_mc(bd, out2, sel=sel)
+                lr = bd["lengths"][redo] > MC_HEX_MAX
+                if (~lr).any():
+                    self.launch_mc(bd, out2, sel=t.from_numpy(redo[~lr]).to(self.dev))
+                if lr.any():
+                    self.launch_mc_general(bd, out2, t.from_numpy(redo[lr]).to(self.dev),
+                                           int(bd["lengths"][redo].max()))
             else:
                 self.launch_pulses(kind, bd, out2, sel=sel, long_variant=True)
             d2, r2, h2 = self.fetch(out2)

@@ -319,14 +319,20 @@ class SDProtocols(UnitsMixin):
         if msg_type not in ("MU", "MS"):
             return [self.demodulate(m, msg_type) for m in messages]
         packer = packing.PulsePacker(msg_type)
+        gen = packing.GeneralPacker(msg_type)   # multi-digit pattern ids / more than LONG_MAX pulses
+        gen_rows: List[int] = []
         pack_err: Dict[int, BaseException] = {}
         for i, m in enumerate(messages):
             try:
                 d = m.get("data", "")
-                if isinstance(d, str) and len(d) > runtime.LONG_MAX:
-                    raise packing.ContractError(f"messages longer than {runtime.LONG_MAX} pulses are outside "
-                                                "the device contract")
-                packer.add(m)
+                try:
+                    if isinstance(d, str) and len(d) > runtime.LONG_MAX:
+                        raise packing.GeneralPathMessage("longer than the long kernel's pulses")
+                    packer.add(m)
+                except packing.GeneralPathMessage:
+                    gen.add(m)                      # same gates and conversions, general layout
+                    gen_rows.append(i)
+                    packer.add({"data": ""})
             except Exception as e:  # the reference raises on this message (same class), or the
                 if raise_errors:    # message is outside the device contract (ContractError): per slot
                     raise
@@ -336,7 +342,13 @@ class SDProtocols(UnitsMixin):
         eng = self._ensure()
         kind = runtime.KIND_MU if msg_type == "MU" else runtime.KIND_MS
         desc, rec, heap = eng.run(kind, eng.to_device_pulses(pb))
-        return self._decode_pulses(msg_type, desc, rec, heap, packer, pack_err, raise_errors)
+        out = self._decode_pulses(msg_type, desc, rec, heap, packer, pack_err, raise_errors)
+        if gen_rows:
+            gd, gr, gh = eng.run_general(kind, eng.to_device_general(gen.arrays()))
+            res = self._decode_pulses(msg_type, gd, gr, gh, gen, {}, raise_errors)
+            for j, i in enumerate(gen_rows):
+                out[i] = res[j]
+        return out
 
     @staticmethod
     def _catch(fn, m, t, raise_errors):
@@ -358,9 +370,12 @@ class SDProtocols(UnitsMixin):
                 continue
             d = desc[i]
             if d["status"] == runtime.ST_RAISED:
-                exc = runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)(
-                    f"reference raises {runtime.RAISE_NAMES.get(int(d['raise_kind']), RuntimeError).__name__} "
-                    f"on this {kind} message")
+                if int(d["raise_kind"]) == runtime.RAISE_CONTRACT:
+                    exc = packing.ContractError(f"{kind} message exceeds a general-path limit (include/sdx.h SDX_GEN_*)")
+                else:
+                    exc = runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)(
+                        f"reference raises {runtime.RAISE_NAMES.get(int(d['raise_kind']), RuntimeError).__name__} "
+                        f"on this {kind} message")
                 if raise_errors:
                     raise exc
                 out.append(exc)
@@ -418,9 +433,8 @@ class SDProtocols(UnitsMixin):
                 clk = m.get("clock", m.get("C", 0))
                 L = m.get("mcbitnum", m.get("bit_length", m.get("L", 0)))
                 mt = m.get("messagetype", msg_type if msg_type in ("MC", "Mc") else "MC")
-                if not isinstance(hx, str) or len(hx) > runtime.MC_HEX_MAX:
-                    raise packing.ContractError(f"MC frames must be str of at most {runtime.MC_HEX_MAX} hex "
-                                                "characters for the device path")
+                if not isinstance(hx, str):
+                    raise packing.ContractError("MC frames must be str for the device path")
                 frames.append((hx, int(clk), int(L), mt, m.get("version", version)))
             except Exception as e:
                 if raise_errors:
@@ -440,7 +454,9 @@ class SDProtocols(UnitsMixin):
                 continue
             d = desc[i]
             if d["status"] == runtime.ST_RAISED:
-                exc = runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)("reference raises on this MC frame")
+                exc = (packing.ContractError("MC payload longer than 65535 bytes") if int(d["raise_kind"]) ==
+                       runtime.RAISE_CONTRACT else
+                       runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)("reference raises on this MC frame"))
                 if raise_errors:
                     raise exc
                 out.append(exc)

@@ -866,3 +866,106 @@ def mc_planted_frames(P: Dict[str, dict], n: int, seed: int = 51, corrupt_frac: 
         L = int(rng.integers(int(p.get("length_min", 8)), int(p.get("length_max", 64)) + 1))
         out.append((h, clock, L, mtype, ver))
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# inputs of the general path (include/sdx.h): multi-digit pattern ids, long messages and frames
+# ---------------------------------------------------------------------------------------------
+def _msg_ids(m: Dict[str, str]) -> List[str]:
+    return [k[1:] for k in m if k.startswith("P") and k[1:].isdigit()]
+
+
+def _rekey(m: Dict[str, str], ren: Dict[str, str], rewrite_data: bool, order=None) -> Dict[str, str]:
+    """m with pattern ids renamed (P<old> -> P<new>) -- the data characters of each renamed id
+    replaced by the new id string when rewrite_data -- and the P keys in `order` (dict order
+    decides pattern_exists ties)."""
+    pk = [k for k in m if k.startswith("P") and k[1:].isdigit()]
+    if order is not None:
+        pk = [pk[i] for i in order]
+    out: Dict[str, str] = {}
+    for k, v in m.items():
+        if k.startswith("P") and k[1:].isdigit():
+            continue
+        if k == "D" or k == "data":
+            continue
+        out[k] = v
+    for k in pk:
+        out["P" + ren.get(k[1:], k[1:])] = m[k]
+    d = m["D"]
+    if rewrite_data:
+        d = "".join(ren.get(c, c) for c in d)
+    for key in ("CP", "SP"):
+        if key in out and out[key] in ren:
+            out[key] = ren[out[key]]
+    out["D"] = d
+    out["data"] = d
+    return out
+
+
+def general_pulse_messages(P: Dict[str, dict], kind: str, n: int, seed: int = 60) -> List[Dict[str, str]]:
+    """n MU or MS msg_data dicts outside the fixed-layout kernels' contract: multi-digit pattern
+    ids (renamed ids with the data rewritten to the new strings, extra P1x patterns near the
+    message's values, zero-padded keys), more than 10 patterns, and messages of 4097..12000 pulses
+    (planted and corpus messages repeated), alone and combined."""
+    rng = np.random.default_rng(seed)
+    base = planted_pulse_messages(P, kind, max(8, n // 2), seed=seed + 1, corrupt_frac=0.1)
+    pb = (mu_corpus if kind == "MU" else ms_corpus)(P, max(8, n // 2), seed=seed + 2)
+    base += [pb.to_msg_dict(i) for i in range(pb.n)]
+    out: List[Dict[str, str]] = []
+    for j in range(n):
+        m = dict(base[int(rng.integers(0, len(base)))])
+        ids = _msg_ids(m)
+        mode = int(rng.integers(0, 6))
+        if mode in (0, 5) and ids:  # rename 1..3 ids to multi-digit strings, data rewritten
+            pick = [ids[int(x)] for x in rng.permutation(len(ids))[: int(rng.integers(1, min(3, len(ids)) + 1))]]
+            ren = {}
+            for o in pick:
+                cand = [str(10 + int(o)), o + o, "1" + o, str(int(rng.integers(10, 100))), o + "0"]
+                c = cand[int(rng.integers(0, len(cand)))]
+                if c not in ids and c not in ren.values():
+                    ren[o] = c
+            m = _rekey(m, ren, rewrite_data=True)
+        elif mode == 1 and ids:  # rename without rewriting the data (ids may then be absent / mixed)
+            o = ids[int(rng.integers(0, len(ids)))]
+            m = _rekey(m, {o: str(int(rng.integers(10, 40)))}, rewrite_data=False)
+        elif mode == 2:  # extra multi-digit patterns close to existing values (> 10 patterns possible)
+            vals = [float(m[k]) for k in m if k.startswith("P") and k[1:].isdigit()] or [400.0]
+            for t in range(int(rng.integers(1, 7))):
+                v = vals[int(rng.integers(0, len(vals)))] * float(rng.uniform(0.85, 1.15))
+                m["P" + str(10 + t + int(rng.integers(0, 3)) * 10)] = str(int(round(v)))
+            if rng.random() < 0.5:  # shuffled key order
+                m = _rekey(m, {}, rewrite_data=False, order=list(rng.permutation(len(_msg_ids(m)))))
+        elif mode == 3:  # zero-padded keys beside multi-digit ones
+            m = _rekey(m, {i: "0" + i for i in ids[:1]}, rewrite_data=False)
+            m["P12"] = str(int(rng.integers(-2000, 2000)))
+        if mode in (4, 5) or rng.random() < 0.15:  # long: the data repeated past LONG_MAX pulses
+            d = m["D"]
+            reps = max(2, (4097 + int(rng.integers(0, 8000))) // max(1, len(d)) + 1)
+            if kind == "MS":  # MS: one sync, then a long tail of the message's data chunks
+                d = d + d[len(d) // 3:] * reps
+            else:
+                d = d * reps
+            m["D"] = m["data"] = d
+        out.append(m)
+    return out
+
+
+def general_mc_frames(P: Dict[str, dict], n: int, seed: int = 61):
+    """MC frames of 129..800 hex characters (the fixed chain's frames of any length): planted
+    frames repeated / extended with random hex, and random hex; L inside and outside the gates."""
+    rng = np.random.default_rng(seed)
+    base = mc_planted_frames(P, max(8, n), seed=seed + 1, corrupt_frac=0.1)
+    out = []
+    for j in range(n):
+        h, clock, L, mt, ver = base[int(rng.integers(0, len(base)))]
+        target = int(rng.integers(129, 800))
+        if rng.random() < 0.5:
+            h2 = (h * (target // max(1, len(h)) + 1))[:target]
+        else:
+            h2 = h + "".join(_HEXD[int(x)] for x in rng.integers(0, 16, target - len(h)))
+        if rng.random() < 0.05:
+            h2 = h2[:40] + "g" + h2[41:]  # not hex
+        if rng.random() < 0.3:
+            L = 4 * len(h2)
+        out.append((h2, clock, L, mt, ver))
+    return out

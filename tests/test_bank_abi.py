@@ -160,12 +160,12 @@ def test_library_loads_and_exports_every_declared_symbol():
     from pysignalduino_amd import build, runtime
     build.build()  # hipcc cross-compiles gfx950 here; no GPU needed
     lib = runtime.load_library()
-    decl = set(re.findall(r"^\s*(?:int|size_t|const char\*|const void\*)\s+(sdx_\w+)\s*\(",
+    decl = set(re.findall(r"^\s*(?:int|size_t|uint64_t|const char\*|const void\*)\s+(sdx_\w+)\s*\(",
                           open(os.path.join(REPO, "include", "sdx.h")).read(), re.M))
     assert decl == set(runtime.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.sdx_abi_version() == 5
+    assert lib.sdx_abi_version() == 6
     runtime.check_layout(lib)
 
 

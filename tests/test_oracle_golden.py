@@ -85,3 +85,20 @@ def test_oracle_mc_methods(bank, golden):
         if got != [kind, rc, res if rc != -1 else None]:
             bad.append((pid, s, kind, rc, res, got))
     assert not bad, f"{len(bad)} mismatches, first: {bad[:3]}"
+
+
+def test_oracle_general_path_matches_reference(bank, golden):
+    """Multi-digit pattern ids, > 10 patterns, > 4096 pulses, MC frames > 128 hex characters:
+    the reference's own outputs (tests/golden/make_general_golden.py) pin the oracle there too."""
+    g = golden("general_golden.json.gz")
+    for kind in ("MU", "MS"):
+        bad = [(c["msg"], c["exp"], got) for c in g[kind.lower()]
+               if (got := _run(bank, c["msg"], kind)) != c["exp"]]
+        assert not bad, f"{kind}: {len(bad)} mismatches, first: {bad[:1]}"
+    for f in g["mc"]:
+        try:
+            got = {"results": [[r["protocol_id"], r["payload"]] for r in
+                               O.demod_mc_fixed(bank, f["hex"], f["clock"], f["L"], f["mtype"], f["version"])]}
+        except Exception as e:
+            got = {"raise": type(e).__name__}
+        assert got == f["fixed"], f
