@@ -55,6 +55,39 @@ def extract_payload(line: bytes) -> Optional[bytes]:
     return s[1:-1]
 
 
+_FLOAT_WS = b" \t\n\v\f\r\x1c\x1d\x1e\x1f"
+_DEC_RE = re.compile(rb"([+-]?)([0-9]*)(?:\.([0-9]*))?(?:[eE]([+-]?[0-9]+))?")
+
+
+def _float_class(v: bytes):
+    """float(v) as _patterns calls it (message_unsynced.py:31-35) and the device's modelled subset
+    (sdx_lines.hip parse_pyfloat): ("skip", None) when float() raises ValueError; ("ok", float(v))
+    for inf / nan / zero and decimals whose significant digits form M < 2^53 (<= 19 digits, trailing
+    zeros moved into the exponent) with |exp10| <= 22 (Clinger's fast path: exact); ("unsup", None)
+    for any other valid float."""
+    try:
+        x = float(v.decode("latin-1"))
+    except ValueError:
+        return "skip", None
+    t = v.strip(_FLOAT_WS).replace(b"_", b"")
+    if t.lstrip(b"+-").lower() in (b"inf", b"infinity", b"nan"):
+        return "ok", x
+    m = _DEC_RE.fullmatch(t)
+    if m is None:
+        return "unsup", None
+    digs = (m.group(2) + (m.group(3) or b"")).lstrip(b"0")
+    e10 = int(m.group(4) or b"0") - len(m.group(3) or b"")
+    if not digs.strip(b"0"):
+        return "ok", x
+    stripped = digs.rstrip(b"0")
+    e10 += len(digs) - len(stripped)
+    if len(digs) > 19 and digs[19:].strip(b"0"):
+        return "unsup", None
+    if int(stripped) >= 2 ** 53 or not -22 <= e10 <= 22:
+        return "unsup", None
+    return "ok", x
+
+
 class Unsupported(Exception):
     """Outside the device contract (the kernel reports SDX_LS_UNSUPPORTED)."""
 
@@ -212,12 +245,13 @@ def parse_line(line: bytes) -> Dict[str, Any]:
         slot: Dict[int, float] = {}
         for k, v in items:                                    # message_unsynced.py:28-35
             if k[:1] == b"P" and len(k) > 1 and k[1:].isdigit():
-                if not v:
-                    continue                                  # float('') raises -> skipped
-                if not _INT15.fullmatch(v) or int(k[1:]) >= 10:
+                cls, fv = _float_class(v)
+                if cls == "skip":
+                    continue                                  # float() raises ValueError -> skipped
+                if cls == "unsup" or int(k[1:]) >= 10:
                     r["status"] = UNSUPPORTED
                     return r
-                slot[int(k[1:])] = float(v)                  # "-0" -> -0.0, as the reference
+                slot[int(k[1:])] = fv                         # Python's own float(): "-0" -> -0.0
         ids, vals = list(slot.keys()), list(slot.values())
     if len(data) > LONG_MAX:
         r["status"] = UNSUPPORTED

@@ -315,23 +315,99 @@ LD bool mu_valid(const Str& P) {
   return hasd;
 }
 
-// float() of [-+]?[0-9]{1,15} (exact: |v| < 2^53; "-0" is -0.0 as in Python); 0 = empty,
-// 1 = ok, 2 = something else
-LD int parse_num15(const Str& P, int s, int e, double* v) {
+// Python float(str) (float_from_string): ASCII whitespace stripped, '_' only between two digits,
+// [+-]? (digits [. digits] | . digits) ([eE] [+-]? digits)?  or  [+-]? (inf | infinity | nan).
+// 0 = ValueError (the reference's _patterns skips the key), 1 = *v exact, 2 = a valid float outside
+// the modelled subset (SDX_LS_UNSUPPORTED).  Exact subset (Clinger's fast path): the significant
+// digits form M < 2^53 (at most 19 of them, trailing zeros moved into the exponent) and
+// |exp10| <= 22, so M * 10^exp10 (or M / 10^-exp10) is ONE IEEE operation on exact operands,
+// i.e. the correctly rounded value Python's strtod returns; zero keeps its sign; inf / nan.
+__constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+LD bool float_ws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f); }
+LD bool lower_is(const Str& P, int s, const char* w, int n) {
+  for (int k = 0; k < n; ++k) {
+    uint8_t c = P.p[s + k];
+    if (c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
+    if (c != (uint8_t)w[k]) return false;
+  }
+  return true;
+}
+LD int parse_pyfloat(const Str& P, int s, int e, double* v) {
+  while (s < e && float_ws(P.p[s])) ++s;
+  while (e > s && float_ws(P.p[e - 1])) --e;
   if (s == e) return 0;
+  for (int i = s; i < e; ++i)  // _Py_string_to_number_with_underscores: digit '_' digit only
+    if (P.p[i] == '_' && (i == s || i + 1 >= e || !digit(P.p[i - 1]) || !digit(P.p[i + 1]))) return 0;
   int i = s;
   bool neg = false;
   if (P.p[i] == '-' || P.p[i] == '+') {
     neg = P.p[i] == '-';
     ++i;
   }
-  if (i == e || e - i > 15) return 2;
-  long long x = 0;
-  for (; i < e; ++i) {
-    if (!digit(P.p[i])) return 2;
-    x = 10 * x + (P.p[i] - '0');
+  const int rem = e - i;
+  if ((rem == 3 && lower_is(P, i, "inf", 3)) || (rem == 8 && lower_is(P, i, "infinity", 8))) {
+    *v = neg ? -__builtin_inf() : __builtin_inf();
+    return 1;
   }
-  *v = neg ? -(double)x : (double)x;
+  if (rem == 3 && lower_is(P, i, "nan", 3)) {  // CPython: -nan keeps its sign bit
+    *v = __longlong_as_double(neg ? (long long)0xFFF8000000000000ull : 0x7FF8000000000000ll);
+    return 1;
+  }
+  uint64_t M = 0;
+  int sig = 0, e10 = 0;
+  bool anyd = false, lost = false;
+  auto take = [&](int d, bool frac) {
+    anyd = true;
+    if (M == 0 && d == 0) {
+      if (frac) --e10;
+      return;
+    }
+    if (sig < 19) {
+      M = 10 * M + (uint64_t)d;
+      ++sig;
+      if (frac) --e10;
+    } else {
+      if (d) lost = true;  // a 20th significant digit: outside the exact subset
+      if (!frac) ++e10;
+    }
+  };
+  for (; i < e && (digit(P.p[i]) || P.p[i] == '_'); ++i)
+    if (P.p[i] != '_') take(P.p[i] - '0', false);
+  if (i < e && P.p[i] == '.') {
+    ++i;
+    for (; i < e && (digit(P.p[i]) || P.p[i] == '_'); ++i)
+      if (P.p[i] != '_') take(P.p[i] - '0', true);
+  }
+  if (!anyd) return 0;
+  if (i < e && (P.p[i] == 'e' || P.p[i] == 'E')) {
+    int j = i + 1;
+    bool eneg = false;
+    if (j < e && (P.p[j] == '+' || P.p[j] == '-')) {
+      eneg = P.p[j] == '-';
+      ++j;
+    }
+    if (j < e && digit(P.p[j])) {  // otherwise the number ends before the 'e': trailing junk
+      long long x = 0;
+      for (; j < e && (digit(P.p[j]) || P.p[j] == '_'); ++j)
+        if (P.p[j] != '_' && x < 100000) x = 10 * x + (P.p[j] - '0');
+      e10 += (int)(eneg ? -x : x);
+      i = j;
+    }
+  }
+  if (i != e) return 0;
+  if (M == 0) {
+    *v = neg ? -0.0 : 0.0;
+    return 1;
+  }
+  if (lost) return 2;
+  while (M % 10 == 0) {
+    M /= 10;
+    ++e10;
+  }
+  if (M >= (1ull << 53) || e10 < -22 || e10 > 22) return 2;
+  const double x = e10 >= 0 ? (double)M * kPow10[e10] : (double)M / kPow10[-e10];
+  *v = neg ? -x : x;
   return 1;
 }
 // int() of [-+]?[0-9]+ (any length): 0 = empty, 1 = ok, 2 = not decimal, 3 = ok but |v| >= 2^31
@@ -865,9 +941,9 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
         const int d = (int)((order >> (4 * q)) & 15);
         const uint32_t w = pvt[64 * d];
         double v;
-        const int rv = parse_num15(P, (int)(w & 0xFFFF), (int)(w >> 16), &v);
-        if (rv == 0) continue;  // float('') -> ValueError -> skipped
-        if (rv == 2) {          // other float() syntax: not modelled
+        const int rv = parse_pyfloat(P, (int)(w & 0xFFFF), (int)(w >> 16), &v);
+        if (rv == 0) continue;  // float() raises ValueError -> skipped
+        if (rv == 2) {          // a float outside the exact subset: not modelled
           r.status = SDX_LS_UNSUPPORTED;
           return;
         }
@@ -906,9 +982,9 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
         for (int k = s + 1; k < ke; ++k)
           if (idv < 1000) idv = 10 * idv + (P.p[k] - '0');
         double v;
-        const int rv = parse_num15(P, vs, ve, &v);
+        const int rv = parse_pyfloat(P, vs, ve, &v);
         if (rv == 0) continue;
-        if (rv == 2 || idv >= 10) {  // other float() syntax / a multi-character pattern id
+        if (rv == 2 || idv >= 10) {  // a float outside the exact subset / a multi-character pattern id
           r.status = SDX_LS_UNSUPPORTED;
           return;
         }

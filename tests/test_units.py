@@ -332,24 +332,38 @@ def test_gpu_planted_large_vs_c_oracle(kind, n, seed):
 
 @pytest.mark.gpu
 def test_gpu_zero_padded_pattern_keys_and_per_message_contract(proto, golden):
-    """P01 / P001 keys name pattern "1" as in the reference; a message outside the device contract
-    (a pattern id >= 10, > 4096 pulses, an MC frame > 128 hex characters) yields ContractError in
-    its own slot while the rest of the batch decodes."""
+    """P01 / P001 keys name pattern "1" as in the reference; a pattern id >= 10, > 4096 pulses and
+    an MC frame > 128 hex characters run on the general path (equal to the oracle); a message
+    outside the device contract (17 patterns) yields ContractError in its own slot while the rest
+    of the batch decodes."""
+    from oracle import sd_oracle as O
     from pysignalduino_amd.packing import ContractError
     from pysignalduino_amd.sd_protocols import SDProtocols
+    ob = O.OracleBank()
     cases = golden("accept_golden.json.gz")["mu_p0x"]
     got = proto.demodulate_batch([c["msg"] for c in cases], "MU")
     assert [_flat(x) for x in got] == [c["exp"] for c in cases]
     msgs = [dict(c["msg"]) for c in cases[:20]]
     msgs[3] = dict(msgs[3], P10="500")
     msgs[7] = dict(msgs[7], data="0" * 5000, D="0" * 5000)
+    msgs[9] = dict(msgs[9], **{f"P{k}": str(50 * k) for k in range(10, 27)})
     got = proto.demodulate_batch(msgs, "MU")
-    assert isinstance(got[3], ContractError) and isinstance(got[7], ContractError)
-    assert [_flat(x) for i, x in enumerate(got) if i not in (3, 7)] == \
-        [c["exp"] for i, c in enumerate(cases[:20]) if i not in (3, 7)]
+    assert isinstance(got[9], ContractError)
+    for i in (3, 7):
+        try:
+            exp = _flat(O.demod(ob, dict(msgs[i]), "MU"))
+        except Exception as e:
+            exp = {"raise": type(e).__name__}
+        assert _flat(got[i]) == exp
+    assert [_flat(x) for i, x in enumerate(got) if i not in (3, 7, 9)] == \
+        [c["exp"] for i, c in enumerate(cases[:20]) if i not in (3, 7, 9)]
     pf = SDProtocols(mc_mode="fixed")
+    src = golden("accept_golden.json.gz")["mc"][:10]
     frames = [{"raw_hex": f["hex"], "clock": f["clock"], "mcbitnum": f["L"], "messagetype": f["mtype"],
-               "version": f["version"]} for f in golden("accept_golden.json.gz")["mc"][:10]]
+               "version": f["version"]} for f in src]
     frames[4] = dict(frames[4], raw_hex="A" * 200)
     got = pf.demodulate_mc_batch(frames)
-    assert isinstance(got[4], ContractError) and all(not isinstance(x, ContractError) for i, x in enumerate(got) if i != 4)
+    for f, g in zip(frames, got):
+        exp = [(r["protocol_id"], r["payload"]) for r in O.demod_mc_fixed(ob, f["raw_hex"], f["clock"], f["mcbitnum"],
+                                                                       f["messagetype"], f["version"])]
+        assert [(r["protocol_id"], r["payload"]) for r in g] == exp
