@@ -55,7 +55,7 @@ def extract_payload(line: bytes) -> Optional[bytes]:
     return s[1:-1]
 
 
-_FLOAT_WS = b" \t\n\v\f\r\x1c\x1d\x1e\x1f"
+_FLOAT_WS = b" \t\n\v\f\r"  # what float() strips (not \x1c-\x1f: float("5\x1c") raises)
 _DEC_RE = re.compile(rb"([+-]?)([0-9]*)(?:\.([0-9]*))?(?:[eE]([+-]?[0-9]+))?")
 
 

@@ -324,7 +324,8 @@ LD bool mu_valid(const Str& P) {
 // i.e. the correctly rounded value Python's strtod returns; zero keeps its sign; inf / nan.
 __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                   1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-LD bool float_ws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f); }
+// float() strips ' ' and \t\n\v\f\r (not \x1c-\x1f, which str.isspace() counts; non-ASCII never gets here)
+LD bool float_ws(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
 LD bool lower_is(const Str& P, int s, const char* w, int n) {
   for (int k = 0; k < n; ++k) {
     uint8_t c = P.p[s + k];
