@@ -364,6 +364,10 @@ def test_gpu_zero_padded_pattern_keys_and_per_message_contract(proto, golden):
     frames[4] = dict(frames[4], raw_hex="A" * 200)
     got = pf.demodulate_mc_batch(frames)
     for f, g in zip(frames, got):
-        exp = [(r["protocol_id"], r["payload"]) for r in O.demod_mc_fixed(ob, f["raw_hex"], f["clock"], f["mcbitnum"],
-                                                                       f["messagetype"], f["version"])]
+        try:
+            exp = [(r["protocol_id"], r["payload"]) for r in
+                   O.demod_mc_fixed(ob, f["raw_hex"], f["clock"], f["mcbitnum"], f["messagetype"], f["version"])]
+        except Exception as e:  # the reference raises on this frame (helpers.mcraw, id 57)
+            assert type(g) is type(e)
+            continue
         assert [(r["protocol_id"], r["payload"]) for r in g] == exp
