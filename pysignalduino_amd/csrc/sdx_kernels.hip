@@ -1513,39 +1513,70 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   uint8_t* st_id = st_f + TM * SDX_MAXPAT;                                 // [TM][10]
   double* st_clk = reinterpret_cast<double*>(st_id + TM * SDX_MAXPAT);     // [TM] (MS)
   uint8_t* st_np = reinterpret_cast<uint8_t*>(st_clk + TM);                // [TM]
+  int64_t pf_off = 0;
+  int pf_n = 0;
+  uint32_t pf_c[MPW][NW <= 4 ? NW : 1];
   if constexpr (NW <= 4) {
-    for (int i = tid; i < TM * SDX_MAXPAT; i += blockDim.x) {
+    // every header load of the tile is issued before any of them is used: the data offsets of the
+    // wave's messages, and per (message, pattern) thread npat, P, the id and (MS) the message's
+    // CP slot with all its values (five 16-B loads; the clock is selected in registers) -- two
+    // levels of dependent global loads (message index -> fields -> data) instead of five
+    if (lane < MPW && wave + lane * NWAVE < nvalid) {
+      const int msg = msg_of[wave + lane * NWAVE];
+      pf_off = b.offsets_dev[msg];
+      pf_n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - pf_off);
+      if (pf_n > 64 * NW) pf_n = 64 * NW;
+    }
+    constexpr int NTH = pulses_threads<KIND, NW>();
+    constexpr int NIT = (TM * SDX_MAXPAT + NTH - 1) / NTH;
+    int r_np[NIT], r_cp[NIT];
+    double r_v[NIT];
+    uint8_t r_id[NIT];
+    double2 r_all[NIT][KIND == SDX_KIND_MS ? SDX_MAXPAT / 2 : 1];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + it * NTH;
       const int m = i / SDX_MAXPAT, k = i - m * SDX_MAXPAT;
-      if (m >= nvalid) break;
-      const int msg = msg_of[m];
-      int np = b.npat_dev[msg];
-      np = np > SDX_MAXPAT ? SDX_MAXPAT : np;
+      const bool ok = i < TM * SDX_MAXPAT && m < nvalid;
+      const int msg = ok ? msg_of[m] : 0;
+      r_np[it] = ok ? (int)b.npat_dev[msg] : 0;
+      r_v[it] = ok ? b.pat_val_dev[msg * SDX_MAXPAT + k] : 0.0;  // n x 10 values: always in bounds
+      r_id[it] = ok ? b.pat_id_dev[msg * SDX_MAXPAT + k] : (uint8_t)'0';
+      r_cp[it] = -1;
+      if constexpr (KIND == SDX_KIND_MS) {
+        r_cp[it] = ok ? (int)b.cp_slot_dev[msg] : -1;
+        const double2* row = reinterpret_cast<const double2*>(b.pat_val_dev + msg * SDX_MAXPAT);
+#pragma unroll
+        for (int h = 0; h < SDX_MAXPAT / 2; ++h) r_all[it][h] = ok ? row[h] : make_double2(0.0, 0.0);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + it * NTH;
+      const int m = i / SDX_MAXPAT, k = i - m * SDX_MAXPAT;
+      if (!(i < TM * SDX_MAXPAT && m < nvalid)) continue;
+      const int np = r_np[it] > SDX_MAXPAT ? SDX_MAXPAT : r_np[it];
       if (k == 0) st_np[m] = (uint8_t)np;
       if (k >= np) continue;
-      const double v = b.pat_val_dev[msg * SDX_MAXPAT + k];
-      st_id[i] = (uint8_t)((b.pat_id_dev[msg * SDX_MAXPAT + k] - '0') & 15);
+      const double v = r_v[it];
+      st_id[i] = (uint8_t)((r_id[it] - '0') & 15);
       if constexpr (KIND == SDX_KIND_MU) {
         const double av = fabs(v);
         const bool fast = av < 67108864.0 && av == floor(av);  // 2^26; NaN fails
         st_x[i] = fast ? (uint32_t)av * 10u : 0u;
         st_f[i] = (uint8_t)((signbit(v) ? 1 : 0) | (fast ? 0 : 2));
       } else {
-        const int cp = b.cp_slot_dev[msg];
-        const double clk = (cp >= 0 && cp < np) ? fabs(b.pat_val_dev[msg * SDX_MAXPAT + cp]) : 0.0;
+        const int cp = r_cp[it];
+        double pc = 0.0;
+#pragma unroll
+        for (int h = 0; h < SDX_MAXPAT / 2; ++h) {
+          if (cp == 2 * h) pc = r_all[it][h].x;
+          if (cp == 2 * h + 1) pc = r_all[it][h].y;
+        }
+        const double clk = (cp >= 0 && cp < np) ? fabs(pc) : 0.0;
         if (k == 0) st_clk[m] = clk;
         st_x[i] = (uint32_t)(clk != 0.0 ? py_round1_k(v / clk) : SDX_K_NONE);
       }
-    }
-  }
-  int64_t pf_off = 0;
-  int pf_n = 0;
-  uint32_t pf_c[MPW][NW <= 4 ? NW : 1];
-  if constexpr (NW <= 4) {
-    if (lane < MPW && wave + lane * NWAVE < nvalid) {
-      const int msg = msg_of[wave + lane * NWAVE];
-      pf_off = b.offsets_dev[msg];
-      pf_n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - pf_off);
-      if (pf_n > 64 * NW) pf_n = 64 * NW;
     }
 #pragma unroll
     for (int k = 0; k < MPW; ++k) {
