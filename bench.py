@@ -169,12 +169,17 @@ def main():
                                  eng.pulses_work_bytes(n) if k != "MC" else 0)
             o[k]["cursor"] = cursors[s_, i]   # one fill per step resets a slot's cursors
         outs.append(o)
-    stream = torch.cuda.current_stream(dev)
+    # the launch stream at high priority, the grouping's side stream at low priority: the hardware
+    # scheduler dispatches the demodulation tiles first and the grouping's small kernels fill the
+    # gaps (measured: 2.153 vs 2.177 ms per step, tools/exp_group_cost.py)
+    lo_prio, hi_prio = torch.cuda.Stream.priority_range()
+    stream = torch.cuda.Stream(dev, priority=hi_prio)
+    torch.cuda.set_stream(stream)
     # MU/MS message grouping (sdx_group_pulses) on a side stream, one step ahead: the grouping of
     # step j+1 (latency-bound small kernels) runs while step j demodulates; order buffers are
     # double-buffered by step parity.  Every step still groups once.
     gkinds = [k for k in kinds if k != "MC"] if not args.no_group else []
-    side = torch.cuda.Stream(dev)
+    side = torch.cuda.Stream(dev, priority=lo_prio)
     gbufs = {k: [eng.group_buffers(corp[k].n) for _ in range(2)] for k in gkinds}
     gdone, used = {}, [None, None]
     gev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps + 1)]
