@@ -206,3 +206,38 @@ def test_compact_filter_records_roundtrip():
                     assert dec(fs, u) == (int(ps["klo"][u]), int(ps["khi"][u]), int(ps["rk_off"][u]))
                 assert (int(f[upk0]) if i == 0 else int(fs["upk"])) == int(ps["uidx_pk"])
         assert nfull < 10
+
+
+def test_mu_clock_divider_is_exact():
+    """The MU integer normalisation (sdx_mu_filt clk_c/clk_m/clk_sh, bank.clock_divider): for every
+    MU clock, floor(x / c) == (x * m) >> sh over the device's input range (x = 10|P| < 2^30), at
+    every multiple of c +- 1 on a grid and on random x; and the rounding built on it (half-even on
+    the exact remainder, ties to the fp64 path) equals Python's round(P / clockabs, 1) * 10."""
+    import numpy as np
+    bk = bankmod.Bank()
+    rng = np.random.default_rng(3)
+    clocks = sorted({float(c) for c in bk.mu_clock})
+    checked = 0
+    for clock in clocks:
+        c, m, shf = bankmod.clock_divider(clock)
+        if not (shf >> 8) & 1:
+            continue
+        sh = shf & 0xFF
+        q = np.unique(np.concatenate([np.arange(0, (1 << 30) // c, max(1, (1 << 30) // c // 4000)),
+                                      rng.integers(0, (1 << 30) // c, 4000)])).astype(np.uint64)
+        x = np.concatenate([q * c, q * c + 1, np.maximum(q * c, 1) - 1, rng.integers(0, 1 << 30, 20000).astype(np.uint64)])
+        x = x[x < (1 << 30)].astype(np.uint64)
+        assert np.array_equal((x * np.uint64(m)) >> np.uint64(sh), x // np.uint64(c)), clock
+        # integral P: k from the integer remainder vs round(P / clock, 1) (exact ties excluded:
+        # the device sends those to the fp64 path)
+        P = rng.integers(-(1 << 20), 1 << 20, 3000)
+        for p in P.tolist():
+            xx = 10 * abs(p)
+            qq, r = divmod(xx, c)
+            if 2 * r == c:
+                continue
+            k = qq + (1 if 2 * r > c else 0)
+            k = -k if (p < 0) != (clock < 0) else k
+            assert k == round(round(p / clock, 1) * 10), (p, clock)
+        checked += 1
+    assert checked >= 10
