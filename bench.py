@@ -42,6 +42,9 @@ def parse():
                     help="one stream per kind: MU, MS and MC of a step run concurrently, one kernel's tail "
                          "overlapping the others' tiles (+3.5 %% msgs/s measured; per-kernel times then include "
                          "the sharing, so the roofline line is quoted on the default serial launches)")
+    ap.add_argument("--serial", action="store_true",
+                    help="MU, MS and MC one after another on one stream (default: MC on a second stream, "
+                         "started when MU ends, so MC runs beside MS while MU runs alone)")
     ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
                     help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
@@ -207,6 +210,13 @@ def main():
     # --concurrent: one stream per kind, the three launches of a step run concurrently (the tail of
     # one kernel overlaps the others' tiles); default: one after another on the launch stream
     kstream = {k: (torch.cuda.Stream(dev) if args.concurrent else stream) for k in kinds}
+    # default: MU alone (the roofline kernel keeps an attributable duration), then MS and MC side by
+    # side -- MC fills the CUs MS's tail leaves idle (482 vs 471M msgs/s serial, 20 steps)
+    mc_beside_ms = not args.serial and not args.concurrent and "MC" in kinds and "MU" in kinds
+    if mc_beside_ms:
+        kstream["MC"] = torch.cuda.Stream(dev)
+
+    mu_done = [None]
 
     def step(j, si=None):
         s_ = j % nslot
@@ -224,7 +234,10 @@ def main():
         for k in kinds:
             ks = kstream[k]
             if ks is not stream:
-                ks.wait_event(start)
+                if mc_beside_ms and k == "MC":
+                    ks.wait_event(mu_done[0])
+                else:
+                    ks.wait_event(start)
             if k in gkinds:
                 ks.wait_event(gdone[(k, par)])
             with torch.cuda.stream(ks):
@@ -237,6 +250,9 @@ def main():
                                       sel=gbufs[k][par][0][:corp[k].n] if k in gkinds else None, group=False)
                 if si is not None:
                     ev[si][k][1].record(ks)
+                if k == "MU":
+                    mu_done[0] = torch.cuda.Event()
+                    mu_done[0].record(ks)
             if ks is not stream:
                 e = torch.cuda.Event()
                 e.record(ks)
@@ -329,7 +345,8 @@ def main():
                 (", noise-free dense corpus)" if args.corpus == "dense" else ")"),
         "config": {"workload": wl, "kind": args.kind, "corpus": args.corpus, "msgs_per_gpu": sum(per.values()),
                    "parallelism": f"dp{world}", "grouped": bool(gkinds),
-                   "streams": "one per kind" if args.concurrent and len(kinds) > 1 else "serial"},
+                   "streams": ("one per kind" if args.concurrent and len(kinds) > 1 else
+                               "MU, then MS beside MC" if mc_beside_ms else "serial")},
         "per_kernel_ms": {k: 1e3 * v for k, v in kt.items()},
         "group_ms": 1e3 * gtime,   # sdx_group_pulses of all kinds per step (side stream, one step ahead)
         "per_type_msgs_per_s": {k: per[k] / kt[k] for k in kinds},
