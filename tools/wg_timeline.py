@@ -21,7 +21,7 @@ def main():
     for kind, gen in (("MU", synth.mu_corpus), ("MS", synth.ms_corpus)):
         pb = gen(bk.protocols, n, seed=42)
         bd = eng.to_device_pulses(pb)
-        out = eng.alloc_out(pb.n, 8 * pb.n + 4096, 200 * pb.n + 65536)
+        out = eng.alloc_out(pb.n, 12 * pb.n + 4096, 320 * pb.n + 65536, eng.pulses_work_bytes(pb.n))
         k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
         for _ in range(3):
             out["cursor"].zero_()
