@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 6
+#define SDX_ABI_VERSION 7
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -191,6 +191,9 @@ typedef struct {
   const uint8_t* ms_ok_dev;    /* [n] MS: string gates passed and CP names a pattern (NULL for MU) */
   const int32_t* sel_dev;      /* optional [n_sel] subset to run, NULL = all */
   int32_t n, n_sel;
+  const int32_t* len_dev;      /* optional [n] lengths: message i = data[offsets[i], +len[i]) (slot layout) */
+  int64_t work_stride;         /* > 0: the j-th message run takes scratch at work_dev + j * work_stride
+                                * (>= 3 * (its length + 512)); 0: sdx_general_work_bytes layout */
 } sdx_general_batch;
 
 uint64_t sdx_general_work_bytes(int64_t total_chars, int32_t n);
@@ -221,10 +224,13 @@ enum sdx_line_status {
   SDX_LS_NOPARSER = 2,    /* no parser for the message type: ignored */
   SDX_LS_INVALID = 3,     /* the parser rejects the line (MU regex, MC header, MC hex, R/F): ignored */
   SDX_LS_NODATA = 4,      /* no D field: ignored */
-  SDX_LS_UNSUPPORTED = 5, /* outside the device contract (e.g. multi-digit P ids, non-integer P# values,
+  SDX_LS_UNSUPPORTED = 5, /* outside the device contract (e.g. P# values outside the exact float() subset,
                            * bytes >= 0x80 after decompression): the caller must not guess */
-  SDX_LS_RAISES = 6       /* handed to the demodulator, which raises (caught by the parser): no results
+  SDX_LS_RAISES = 6,      /* handed to the demodulator, which raises (caught by the parser): no results
                            * (MC: int(C) / int(L) of a hex-lettered value) */
+  SDX_LS_GENERAL = 7      /* an MU/MS line the fixed-layout kernels do not take (a multi-digit pattern id,
+                           * more than SDX_LONG_MAX pulses): D, meta and doff/dlen are written as for
+                           * SDX_LS_OK; sdx_lines_general builds its general-path batch */
 };
 
 typedef struct {
@@ -264,6 +270,26 @@ typedef struct {
  * mcbitnum/mcflags for OK MC lines, and plen plus the slot payload for OK decompressed lines.
  * meta_dev must be 16-byte aligned; bytes_dev and slot_dev 8-byte aligned. */
 int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out, void* hip_stream);
+
+/* The general-path batch of a parsed batch's SDX_LS_GENERAL lines: for the j-th entry of sel_dev
+ * (line i) the line's _parse_to_dict / _patterns fields in the sdx_general_batch layout --
+ * offsets[j] = doff[i], len[j] = dlen[i] (the D characters in slot_dev), the pattern ids as strings
+ * (str(int(key[1:]))), float(P#) values, MS cp_slot / ms_ok.  A line found outside the general
+ * path's contract (an id of more than 15 digits, more than SDX_GEN_MAXPAT patterns) gets
+ * status_dev[i] = SDX_LS_UNSUPPORTED and npat[j] = 0.  Run the result with
+ * sdx_demod_pulses_general(data_dev = slot_dev, sel_dev = NULL, n = n_sel). */
+typedef struct {
+  int64_t* offsets_dev;        /* [n_sel] */
+  int32_t* len_dev;            /* [n_sel] */
+  uint8_t* npat_dev;           /* [n_sel] */
+  uint8_t* pat_ids_dev;        /* [n_sel * SDX_GEN_MAXPAT * SDX_GEN_IDSTR] */
+  double* pat_val_dev;         /* [n_sel * SDX_GEN_MAXPAT] */
+  int8_t* cp_slot_dev;         /* [n_sel] */
+  uint8_t* ms_ok_dev;          /* [n_sel] */
+} sdx_lines_general_out;
+
+int sdx_lines_general(const sdx_lines* lines, const sdx_lines_out* out, const int32_t* sel_dev, int32_t n_sel,
+                      const sdx_lines_general_out* gen, void* hip_stream);
 
 /* ---- publish-ready JSON ------------------------------------------------------
  * The MQTT publication of a DecodedMessage, MqttPublisher._message_to_json (signalduino/mqtt.py:

@@ -23,7 +23,8 @@ import re
 from typing import Any, Dict, List, Optional, Tuple
 
 NONE, MU, MS, MC, MN = 0, 1, 2, 3, 4
-OK, NOFRAME, NOPARSER, INVALID, NODATA, UNSUPPORTED, RAISES = 0, 1, 2, 3, 4, 5, 6
+OK, NOFRAME, NOPARSER, INVALID, NODATA, UNSUPPORTED, RAISES, GENERAL = 0, 1, 2, 3, 4, 5, 6, 7
+GEN_MAXPAT, GEN_IDMAX = 16, 15   # include/sdx.h SDX_GEN_MAXPAT, SDX_GEN_IDSTR - 1
 SHORT_MAX, LONG_MAX, MC_HEX_MAX, MN_HEX_MAX = 256, 4096, 128, 4096
 
 _WS = set(range(9, 14)) | set(range(0x1C, 0x21)) | {0x85, 0xA0}          # str.isspace() on latin-1
@@ -241,6 +242,8 @@ def parse_line(line: bytes) -> Dict[str, Any]:
               and bool(kv.get(b"SP")) and kv[b"SP"].isdigit() and (b"R" not in kv or kv[b"R"].isdigit()))
     ids: List[int] = []
     vals: List[float] = []
+    gen = len(data) > LONG_MAX       # the fixed-layout kernels' limits: the general path (SDX_LS_GENERAL)
+    pats: Dict[str, float] = {}      # _patterns with string ids (the general layout)
     if (kind == MS and ok) or (kind == MU and data):
         slot: Dict[int, float] = {}
         for k, v in items:                                    # message_unsynced.py:28-35
@@ -248,23 +251,32 @@ def parse_line(line: bytes) -> Dict[str, Any]:
                 cls, fv = _float_class(v)
                 if cls == "skip":
                     continue                                  # float() raises ValueError -> skipped
-                if cls == "unsup" or int(k[1:]) >= 10:
+                if cls == "unsup":
                     r["status"] = UNSUPPORTED
                     return r
+                pats[str(int(k[1:]))] = fv
+                if int(k[1:]) >= 10:
+                    gen = True
+                    continue
                 slot[int(k[1:])] = fv                         # Python's own float(): "-0" -> -0.0
         ids, vals = list(slot.keys()), list(slot.values())
-    if len(data) > LONG_MAX:
-        r["status"] = UNSUPPORTED
-        return r
     cp_slot = -1
+    gcp = -1
     if kind == MS and ok:
         cp = int(kv[b"CP"])
         cp_slot = ids.index(cp) if cp in ids else -1
-        ok = cp_slot >= 0
+        gids = list(pats.keys())
+        gcp = gids.index(str(cp)) if str(cp) in gids else -1
+        ok = (gcp if gen else cp_slot) >= 0
     r.update(status=OK, data=data, ids=ids, vals=vals, cp_slot=cp_slot, ms_ok=int(ok),
              R=kv.get(b"R"), F=kv.get(b"F"))
+    if gen:
+        r.update(status=GENERAL, gids=list(pats.keys()), gvals=list(pats.values()), gcp=gcp)
     if not _meta_fits(r):
         r["status"] = UNSUPPORTED
+        return r
+    if gen and (len(pats) > GEN_MAXPAT or any(len(x) > GEN_IDMAX for x in pats)):
+        r["status"] = UNSUPPORTED   # outside the general path's contract too (sdx_lines_general)
         return r
     msg = [(k.decode("latin-1"), v.decode("latin-1")) for k, v in items]
     msg.append(("data", data.decode("latin-1")))

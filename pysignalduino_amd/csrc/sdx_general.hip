@@ -495,12 +495,13 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
   const int64_t off = b.offsets_dev[msg];
   Msg m;
   m.d = b.data_dev + off;
-  m.n = (int)(b.offsets_dev[msg + 1] - off);
+  m.n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
   m.npat = b.npat_dev[msg] < GP ? b.npat_dev[msg] : GP;
   m.ids = b.pat_ids_dev + (size_t)msg * GP * GID;
   m.val = b.pat_val_dev + (size_t)msg * GP;
   // per-message scratch: bits, postDemod output, payload text (include/sdx.h sdx_general_work_bytes)
-  uint8_t* B = out.work_dev + 3 * off + (int64_t)3 * GSLACK * msg;
+  uint8_t* B = b.work_stride > 0 ? out.work_dev + (int64_t)i * b.work_stride
+                                 : out.work_dev + 3 * off + (int64_t)3 * GSLACK * msg;
   uint8_t* B2 = B + m.n + GSLACK;
   uint8_t* T = B2 + m.n + GSLACK;
   const int cp = KIND == SDX_KIND_MS ? (int)b.cp_slot_dev[msg] : -1;
@@ -661,7 +662,7 @@ int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_b
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
   if (ntot <= 0) return SDX_OK;
   if (!batch->data_dev || !batch->offsets_dev || !batch->npat_dev || !batch->pat_ids_dev || !batch->pat_val_dev ||
-      !out->work_dev)
+      !out->work_dev || (batch->work_stride > 0 && out->work_cap < (uint64_t)batch->work_stride * (uint64_t)ntot))
     return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: missing buffer (work_dev: sdx_general_work_bytes)");
   const int grid = (ntot + 63) / 64;
   hipStream_t st = (hipStream_t)hip_stream;

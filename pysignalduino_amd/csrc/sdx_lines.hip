@@ -770,6 +770,7 @@ LD void mn_line(const Str& P, LineRes& r) {
 // fields of line i, returns kind/status and the D/R/F ranges.  pvt = this lane's column of the
 // fast P-key table (stride 64 words).
 LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i, uint32_t* pvt) {
+  bool gen = false;  // MU/MS: a multi-digit pattern id or > SDX_LONG_MAX pulses (SDX_LS_GENERAL)
   // ---- routing: payload[:2].upper()
   const uint8_t c0 = P.n > 0 ? up(P.p[0]) : 0, c1 = P.n > 1 ? up(P.p[1]) : 0;
   if (c0 != 'M' || !(c1 == 'S' || c1 == 'U' || c1 == 'C' || c1 == 'N')) {
@@ -985,17 +986,18 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
         double v;
         const int rv = parse_pyfloat(P, vs, ve, &v);
         if (rv == 0) continue;
-        if (rv == 2 || idv >= 10) {  // a float outside the exact subset / a multi-character pattern id
+        if (rv == 2) {  // a float outside the exact subset
           r.status = SDX_LS_UNSUPPORTED;
           return;
+        }
+        if (idv >= 10) {  // a multi-character pattern id: the general path (sdx_lines_general)
+          gen = true;
+          continue;
         }
         assign((int)idv, v);
       }
     }
-    if (fD.e - fD.s > SDX_LONG_MAX) {  // longer than the long demodulation variant takes
-      r.status = SDX_LS_UNSUPPORTED;
-      return;
-    }
+    if (fD.e - fD.s > SDX_LONG_MAX) gen = true;  // longer than the long variant takes: general path
     out.npat_dev[i] = (uint8_t)nslot;
     if (r.kind == SDX_LINE_MS) {
       int8_t slotv = -1;
@@ -1017,7 +1019,7 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
   }
   r.dS = fD.s;
   r.dE = fD.e;
-  r.status = SDX_LS_OK;
+  r.status = gen ? SDX_LS_GENERAL : SDX_LS_OK;
 }
 
 // 16 bytes of meta_dev: value characters, length at byte 15 (255 = absent); the value (<= 15
@@ -1101,7 +1103,7 @@ __global__ __launch_bounds__(PT) void k_parse_lines(sdx_lines in, sdx_lines_out 
         }
       }
     }
-    if (r.status == SDX_LS_OK) {
+    if (r.status == SDX_LS_OK || r.status == SDX_LS_GENERAL) {
       finish_fields(P, r, out, i);
       if (comp) {
         doff = 3 * lo + r.dS;
@@ -1156,7 +1158,7 @@ LD void parse_compressed(const sdx_lines& in, const sdx_lines_out& out, int i, u
       const Str P{out.slot_dev + 3 * lo, w.n};
       const uint8_t ty = P.n > 1 ? P.p[1] : 0;
       if (!((ty == 'U' || ty == 'S' || ty == 'C') && fast_payload(P.p, P.n, r, out, i))) parse_payload(P, r, out, i, pvt);
-      if (r.status == SDX_LS_OK) {
+      if (r.status == SDX_LS_OK || r.status == SDX_LS_GENERAL) {
         finish_fields(P, r, out, i);
         doff = 3 * lo + r.dS;
       }
@@ -1312,6 +1314,128 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sel_write(sdx_lines_out o, int 
   }
 }
 
+// ---- sdx_lines_general: the general-path batch of the SDX_LS_GENERAL lines (lane = line) --------
+// _parse_to_dict (mu.py:82-94, ms.py:65-78: first position, last value) and _patterns
+// (message_unsynced.py:28-35: id = str(int(key[1:])), float(value), ValueError skipped) with ids as
+// strings, the MS string gates and str(int(CP)) (message_synced.py:21-57).
+constexpr int GEN_P = SDX_GEN_MAXPAT, GEN_ID = SDX_GEN_IDSTR;
+
+// the key's digits with leading zeros removed (str(int(digits)) for ASCII digits); false if > 15
+LD bool id_string(const Str& P, int s, int e, uint8_t* dst) {
+  while (s < e - 1 && P.p[s] == '0') ++s;
+  if (e - s > GEN_ID - 1) return false;
+  dst[0] = (uint8_t)(e - s);
+  for (int k = s; k < e; ++k) dst[1 + k - s] = P.p[k];
+  return true;
+}
+
+__global__ __launch_bounds__(64) void k_lines_general(sdx_lines in, sdx_lines_out out, const int32_t* sel, int n_sel,
+                                                      sdx_lines_general_out g) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= n_sel) return;
+  const int i = sel[j];
+  const int64_t lo = in.offsets_dev[i];
+  const int len = (int)(in.offsets_dev[i + 1] - lo);
+  Str P;
+  if (out.plen_dev[i] >= 0) {  // decompressed into the slot
+    P = Str{out.slot_dev + 3 * lo, out.plen_dev[i]};
+  } else {  // the stripped line between STX and ETX (frame_check passed in sdx_parse_lines)
+    const uint8_t* L = in.bytes_dev + lo;
+    int a = 0, b = len;
+    while (a < b && py_space(L[a])) ++a;
+    while (b > a && py_space(L[b - 1])) --b;
+    P = Str{L + a + 1, b - a - 2};
+  }
+  g.offsets_dev[j] = out.doff_dev[i];
+  g.len_dev[j] = out.dlen_dev[i];
+  uint8_t* ids = g.pat_ids_dev + (int64_t)j * GEN_P * GEN_ID;
+  double* vals = g.pat_val_dev + (int64_t)j * GEN_P;
+  Field fD{-1, -1}, fCP{-1, -1}, fSP{-1, -1}, fR{-1, -1};
+  int pos = 0, s, e;
+  while (next_part(P, pos, s, e)) {
+    int k = s;
+    while (k < e && P.p[k] != '=') ++k;
+    const Field f{k < e ? k + 1 : e, e};
+    if (keq(P, s, k, "D")) fD = f;
+    else if (keq(P, s, k, "CP")) fCP = f;
+    else if (keq(P, s, k, "SP")) fSP = f;
+    else if (keq(P, s, k, "R")) fR = f;
+  }
+  const bool ms = out.kind_dev[i] == SDX_LINE_MS;
+  bool ms_ok = ms && fD.s >= 0 && all_digits(P, fD.s, fD.e) && fCP.s >= 0 && all_digits(P, fCP.s, fCP.e) &&
+               fSP.s >= 0 && all_digits(P, fSP.s, fSP.e) && (fR.s < 0 || all_digits(P, fR.s, fR.e));
+  const bool want = ms ? ms_ok : (fD.s >= 0 && fD.e > fD.s);
+  int np = 0;
+  bool bad = false;
+  pos = 0;
+  while (want && !bad && next_part(P, pos, s, e)) {
+    int ke = s;
+    while (ke < e && P.p[ke] != '=') ++ke;
+    if (!(P.p[s] == 'P' && ke - s >= 2 && all_digits(P, s + 1, ke))) continue;
+    bool dup = false;  // msg_data holds each key string once, at its first position ...
+    int p2 = 0, s2, e2;
+    while (!dup && next_part(P, p2, s2, e2) && s2 < s) {
+      int k2 = s2;
+      while (k2 < e2 && P.p[k2] != '=') ++k2;
+      dup = same_key(P, s, ke, s2, k2);
+    }
+    if (dup) continue;
+    int vs = ke < e ? ke + 1 : e, ve = e;  // ... with the value of its last occurrence
+    int p3 = pos, s3, e3;
+    while (next_part(P, p3, s3, e3)) {
+      int k3 = s3;
+      while (k3 < e3 && P.p[k3] != '=') ++k3;
+      if (same_key(P, s, ke, s3, k3)) {
+        vs = k3 < e3 ? k3 + 1 : e3;
+        ve = e3;
+      }
+    }
+    double v;
+    const int rv = parse_pyfloat(P, vs, ve, &v);
+    if (rv == 0) continue;  // float() raises ValueError: key skipped
+    uint8_t id[GEN_ID];
+    if (rv == 2 || !id_string(P, s + 1, ke, id)) {
+      bad = true;
+      break;
+    }
+    int z = 0;  // pats[id] = value: first assignment fixes the slot, the last one the value
+    for (; z < np; ++z) {
+      bool same = ids[z * GEN_ID] == id[0];
+      for (int q = 1; same && q <= id[0]; ++q) same = ids[z * GEN_ID + q] == id[q];
+      if (same) break;
+    }
+    if (z == np) {
+      if (np == GEN_P) {
+        bad = true;
+        break;
+      }
+      for (int q = 0; q <= id[0]; ++q) ids[z * GEN_ID + q] = id[q];
+      ++np;
+    }
+    vals[z] = v;
+  }
+  int8_t cp = -1;
+  if (!bad && ms && ms_ok) {  // str(int(CP)) in the pattern ids
+    uint8_t id[GEN_ID];
+    if (id_string(P, fCP.s, fCP.e, id)) {
+      for (int z = 0; z < np && cp < 0; ++z) {
+        bool same = ids[z * GEN_ID] == id[0];
+        for (int q = 1; same && q <= id[0]; ++q) same = ids[z * GEN_ID + q] == id[q];
+        if (same) cp = (int8_t)z;
+      }
+    }
+    ms_ok = cp >= 0;
+  }
+  if (bad) {
+    out.status_dev[i] = SDX_LS_UNSUPPORTED;
+    np = 0;
+    ms_ok = false;
+  }
+  g.npat_dev[j] = (uint8_t)np;
+  g.cp_slot_dev[j] = cp;
+  g.ms_ok_dev[j] = ms_ok ? 1 : 0;
+}
+
 }  // namespace sdxl
 
 extern "C" int sdx_select_lines(const sdx_lines_out* out, int32_t n, int32_t* sel_dev, int32_t* counts_dev,
@@ -1351,5 +1475,19 @@ extern "C" int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out,
                      dim3(256), 0, (hipStream_t)hip_stream, *lines, *out);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("sdx_parse_lines: ") + hipGetErrorString(e));
+  return SDX_OK;
+}
+
+extern "C" int sdx_lines_general(const sdx_lines* lines, const sdx_lines_out* out, const int32_t* sel_dev, int32_t n_sel,
+                                 const sdx_lines_general_out* gen, void* hip_stream) {
+  if (!lines || !out || !gen || n_sel < 0) return sdx::set_error(SDX_EINVAL, "sdx_lines_general: bad arguments");
+  if (n_sel == 0) return SDX_OK;
+  if (!sel_dev || !gen->offsets_dev || !gen->len_dev || !gen->npat_dev || !gen->pat_ids_dev || !gen->pat_val_dev ||
+      !gen->cp_slot_dev || !gen->ms_ok_dev)
+    return sdx::set_error(SDX_EINVAL, "sdx_lines_general: null buffer");
+  hipLaunchKernelGGL(sdxl::k_lines_general, dim3((n_sel + 63) / 64), dim3(64), 0, (hipStream_t)hip_stream, *lines, *out,
+                     sel_dev, n_sel, *gen);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("sdx_lines_general: ") + hipGetErrorString(e));
   return SDX_OK;
 }

@@ -22,6 +22,7 @@ There is no CPU fallback.
 """
 from __future__ import annotations
 
+import json
 import logging
 import re
 from dataclasses import dataclass, field
@@ -141,6 +142,35 @@ class LineBatch:
     def mn_batch(self):
         return {"hex": self.slot, "offsets": self.doff, "len": self.dlen, "n": self.n}
 
+    def general(self, status: np.ndarray, kind_np: np.ndarray, line_kind: int):
+        """The SDX_LS_GENERAL lines of one kind through sdx_lines_general + sdx_demod_pulses_general.
+        Returns (rows, desc, rec, heap, vals [rows, 16], cp_slot) or None when there are none; rows whose
+        general parse found them outside the contract are reported back in status (UNSUPPORTED)."""
+        import ctypes
+        rows = np.nonzero((status == runtime.LS_GENERAL) & (kind_np == line_kind))[0]
+        if not len(rows):
+            return None
+        t, d, eng = self.eng.torch, self.eng.dev, self.eng
+        m = len(rows)
+        sel = t.from_numpy(rows.astype(np.int32)).to(d)
+        g = {"offsets": t.empty(m, dtype=t.int64, device=d), "len": t.empty(m, dtype=t.int32, device=d),
+             "npat": t.empty(m, dtype=t.uint8, device=d), "pat_ids": t.empty(m * 256, dtype=t.uint8, device=d),
+             "pat_val": t.empty(m * 16, dtype=t.float64, device=d), "cp_slot": t.empty(m, dtype=t.int8, device=d),
+             "ms_ok": t.empty(m, dtype=t.uint8, device=d)}
+        p = runtime._ptr
+        go = runtime.SdxLinesGeneralOut(p(g["offsets"]), p(g["len"]), p(g["npat"]), p(g["pat_ids"]), p(g["pat_val"]),
+                                        p(g["cp_slot"]), p(g["ms_ok"]))
+        runtime._check(eng.lib, eng.lib.sdx_lines_general(ctypes.byref(self.c_lines), ctypes.byref(self.c_out),
+                                                          p(sel), m, ctypes.byref(go), eng.stream_ptr()))
+        lens = g["len"].cpu().numpy()
+        st = self.status[sel.long()].cpu().numpy()
+        status[rows] = st                                   # lines found outside the contract
+        g.update(data=self.slot, n=m, total=int(lens.sum()))
+        kd = runtime.KIND_MU if line_kind == runtime.LINE_MU else runtime.KIND_MS
+        desc, rec, heap = eng.run_general(kd, g, work_stride=3 * (int(lens.max()) + 512))
+        return (rows, desc, rec, heap, g["pat_val"].cpu().numpy().reshape(m, 16),
+                g["cp_slot"].cpu().numpy().astype(np.int64))
+
     def mc_batch(self):
         return {"hex": self.slot, "offsets": self.doff, "clock": self.clock, "mcbitnum": self.mcbitnum,
                 "flags": self.mcflags, "len": self.dlen, "n": self.n}
@@ -223,6 +253,13 @@ class SignalParser:
         # read-back of the per-line fields the Python objects need
         kind = lb.kind[:n].cpu().numpy()
         status = lb.status[:n].cpu().numpy()
+        # SDX_LS_GENERAL lines (multi-digit pattern ids, > 4096 pulses): the general path
+        gen = {name: lb.general(status, kind, lk) for name, lk in (("MU", runtime.LINE_MU), ("MS", runtime.LINE_MS))}
+        gen_of = {}
+        for name, gr in gen.items():
+            if gr is not None:
+                for j, i in enumerate(gr[0]):
+                    gen_of[int(i)] = (name, j)
         plen = lb.plen[:n].cpu().numpy()
         meta = lb.meta[: 32 * n].cpu().numpy().reshape(n, 32)
         need_slot = plen >= 0
@@ -246,6 +283,12 @@ class SignalParser:
                                          f"(kind {_KIND_NAME.get(int(kind[i]), '?')})"))
                 continue
             name = _KIND_NAME.get(int(kind[i]))
+            if st == runtime.LS_GENERAL:
+                gname, j = gen_of[i]
+                _, gdesc, grec, gheap, gvals, gcps = gen[gname]
+                out.append(self._general_messages(lines[i], i, plen, offsets, slot, meta, gname, gdesc[j], grec,
+                                                  gheap.tobytes(), abs(float(gvals[j, max(0, int(gcps[j]))]))))
+                continue
             if st != runtime.LS_OK or name not in res:
                 out.append([])
                 continue
@@ -276,6 +319,26 @@ class SignalParser:
                 msgs.append(DecodedMessage(protocol_id=str(pid), payload=payload, raw=fr, metadata=md))
             out.append(msgs)
         return out
+
+    def _general_messages(self, line, i, plen, offsets, slot, meta, name, d, rec, hb, ms_clock) -> List[DecodedMessage]:
+        """The DecodedMessage list of a general-path line (as the OK lines' records below)."""
+        bk = self.protocols._bank
+        if d["status"] == runtime.ST_RAISED or int(d["n_rec"]) == 0:
+            return []   # a demodulator exception is caught by the reference's parsers
+        if d["status"] != runtime.ST_OK:
+            raise RuntimeError(f"device status {int(d['status'])} for line {i}")
+        fr = self._frame(line, i, plen, offsets, slot, meta, name)
+        rssi_raw = self._meta_str(meta[i], 0)
+        msgs = []
+        for r in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
+            p = int(r["proto"])
+            off = int(r["payload_off"])
+            pid = bk.mu_pids[p] if name == "MU" else bk.ms_pids[p]
+            md = {"bit_length": int(r["bit_length"]), "rssi": rssi_raw,
+                  "clock": bk.mu_clock[p] if name == "MU" else ms_clock}
+            msgs.append(DecodedMessage(protocol_id=str(pid), payload=hb[off: off + int(r["payload_len"])].decode("latin-1"),
+                                       raw=fr, metadata=md))
+        return msgs
 
     def _payload(self, line, i, plen, offsets, slot) -> str:
         if plen[i] >= 0:
@@ -367,6 +430,14 @@ class SignalParser:
                 texts[int(i)] = blob[int(offs[i]): int(offs[i]) + int(lens[i])].decode("ascii")
         status = lb.status[:n].cpu().numpy()
         kinds = lb.kind[:n].cpu().numpy()
+        grows = [int(i) for i in np.nonzero(status == runtime.LS_GENERAL)[0] if int(i) not in bad]
+        if grows:  # general-path lines (rare): their objects through parse_lines, the text as _message_to_json
+            for i, g in zip(grows, self.parse_lines([lines[i] for i in grows])):
+                if isinstance(g, BaseException):
+                    texts[i] = g
+                elif g:
+                    texts[i] = json.dumps({"protocol_id": g[0].protocol_id, "payload": g[0].payload,
+                                           "metadata": g[0].metadata}, indent=4)
         for i in range(n):
             if i in bad:
                 texts[i] = bad[i]

@@ -38,7 +38,8 @@ EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_cr
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
             "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
             "sdx_exchange_pack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
-            "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general"]
+            "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general",
+            "sdx_lines_general"]
 GROUP_MIN = 4096   # SDX_GROUP_MIN
 
 
@@ -52,7 +53,12 @@ class SdxPulseBatch(Structure):
 class SdxGeneralBatch(Structure):
     _fields_ = [("data_dev", c_void_p), ("offsets_dev", c_void_p), ("npat_dev", c_void_p), ("pat_ids_dev", c_void_p),
                 ("pat_val_dev", c_void_p), ("cp_slot_dev", c_void_p), ("ms_ok_dev", c_void_p), ("sel_dev", c_void_p),
-                ("n", c_int32), ("n_sel", c_int32)]
+                ("n", c_int32), ("n_sel", c_int32), ("len_dev", c_void_p), ("work_stride", ctypes.c_int64)]
+
+
+class SdxLinesGeneralOut(Structure):
+    _fields_ = [(f, c_void_p) for f in ("offsets_dev", "len_dev", "npat_dev", "pat_ids_dev", "pat_val_dev",
+                                         "cp_slot_dev", "ms_ok_dev")]
 
 
 class SdxMcBatch(Structure):
@@ -106,7 +112,7 @@ class SdxLinesOut(Structure):
 
 # include/sdx.h front-end constants
 LINE_NONE, LINE_MU, LINE_MS, LINE_MC, LINE_MN = 0, 1, 2, 3, 4
-LS_OK, LS_NOFRAME, LS_NOPARSER, LS_INVALID, LS_NODATA, LS_UNSUPPORTED, LS_RAISES = 0, 1, 2, 3, 4, 5, 6
+LS_OK, LS_NOFRAME, LS_NOPARSER, LS_INVALID, LS_NODATA, LS_UNSUPPORTED, LS_RAISES, LS_GENERAL = 0, 1, 2, 3, 4, 5, 6, 7
 SEL_MU_SHORT, SEL_MU_LONG, SEL_MS_SHORT, SEL_MS_LONG, SEL_MC, SEL_MN, SEL_NCLASS = 0, 1, 2, 3, 4, 5, 6
 SEL_CHUNK = 1024
 
@@ -154,6 +160,9 @@ def load_library(path: Optional[str] = None):
     lib.sdx_mc_general_work_bytes.restype = ctypes.c_uint64
     lib.sdx_demod_mc_general.argtypes = [c_void_p, POINTER(SdxMcBatch), c_int32, POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mc_general.restype = c_int
+    lib.sdx_lines_general.argtypes = [POINTER(SdxLines), POINTER(SdxLinesOut), c_void_p, c_int32,
+                                      POINTER(SdxLinesGeneralOut), c_void_p]
+    lib.sdx_lines_general.restype = c_int
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mc.restype = c_int
     lib.sdx_demod_mn.argtypes = [c_void_p, POINTER(SdxMnBatch), POINTER(SdxOut), c_void_p]
@@ -168,7 +177,7 @@ def load_library(path: Optional[str] = None):
     lib.sdx_units.restype = c_int
     lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, c_void_p]
     lib.sdx_exchange_pack.restype = c_int
-    if lib.sdx_abi_version() != 6:
+    if lib.sdx_abi_version() != 7:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -356,19 +365,21 @@ class Engine:
         out["lengths"] = np.diff(arrs["offsets"])
         return out
 
-    def run_general(self, kind: int, gd):
-        """MU/MS messages on the general path; returns host (desc, rec, heap) like run()."""
+    def run_general(self, kind: int, gd, work_stride: int = 0):
+        """MU/MS messages on the general path; returns host (desc, rec, heap) like run().
+        ``work_stride`` > 0: per-message scratch of that many bytes (gd in slot layout, "len" set)."""
         n = gd["n"]
         rec_cap = 16 * n + 1024
         heap_cap = int(2 * gd["total"] + 256 * n + 65536)
-        work = self.torch.empty(int(self.lib.sdx_general_work_bytes(gd["total"], n)), dtype=self.torch.uint8,
-                                device=self.dev)
+        wb = n * work_stride if work_stride > 0 else int(self.lib.sdx_general_work_bytes(gd["total"], n))
+        work = self.torch.empty(max(wb, 1), dtype=self.torch.uint8, device=self.dev)
         for attempt in range(6):
             out = self.alloc_out(n, rec_cap, heap_cap)
             o = self._out_struct(out)
             o.work_dev, o.work_cap = _ptr(work), int(work.numel())
             b = SdxGeneralBatch(_ptr(gd["data"]), _ptr(gd["offsets"]), _ptr(gd["npat"]), _ptr(gd["pat_ids"]),
-                                _ptr(gd["pat_val"]), _ptr(gd["cp_slot"]), _ptr(gd["ms_ok"]), None, n, 0)
+                                _ptr(gd["pat_val"]), _ptr(gd["cp_slot"]), _ptr(gd["ms_ok"]), None, n, 0,
+                                _ptr(gd.get("len")), int(work_stride))
             _check(self.lib, self.lib.sdx_demod_pulses_general(self.handle, kind, ctypes.byref(b), ctypes.byref(o),
                                                                self.stream_ptr()))
             desc, rec, heap = self.fetch(out)
