@@ -276,7 +276,8 @@ def parse_line(line: bytes) -> Dict[str, Any]:
         r["status"] = UNSUPPORTED
         return r
     if gen and (len(pats) > GEN_MAXPAT or any(len(x) > GEN_IDMAX for x in pats)):
-        r["status"] = UNSUPPORTED   # outside the general path's contract too (sdx_lines_general)
+        r["status"] = UNSUPPORTED   # outside the general path's contract too: sdx_parse_lines reports
+        r["gen_contract"] = True    # GENERAL, sdx_lines_general then UNSUPPORTED
         return r
     msg = [(k.decode("latin-1"), v.decode("latin-1")) for k, v in items]
     msg.append(("data", data.decode("latin-1")))
