@@ -316,8 +316,8 @@ def test_lines_general_batch_matches_oracle(golden):
             d = bytes(slot[int(h["offsets"][j]): int(h["offsets"][j]) + int(h["len"][j])])
             assert d == r["data"]
             npat = int(h["npat"][j])
-            ids = [bytes(h["pat_ids"][256 * j + 16 * z + 1: 256 * j + 16 * z + 1 + h["pat_ids"][256 * j + 16 * z]]).decode()
-                   for z in range(npat)]
+            base = [256 * j + 16 * z for z in range(npat)]
+            ids = [bytes(h["pat_ids"][b + 1: b + 1 + int(h["pat_ids"][b])]).decode() for b in base]
             assert ids == r["gids"], (ids, r["gids"])
             assert h["pat_val"][16 * j: 16 * j + npat].tobytes() == np.array(r["gvals"], np.float64).tobytes()
             if lk == runtime.LINE_MS:
