@@ -156,7 +156,8 @@ int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
 /* same, for messages of 257..4096 pulses (4 messages per workgroup tile) */
 int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
                           void* hip_stream);
-/* MC "fixed" chain: every frame x every clockrange protocol */
+/* MC "fixed" chain: every frame x every clockrange protocol.  Frames of more than SDX_MC_HEX_MAX
+ * characters get status SDX_ST_OVF_TILE (cursor[2] bit 1): run them with sdx_demod_mc_general */
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream);
 /* MN (FSK): every frame x every 'modulation' protocol (parser mode) or one method (method mode).
  * Frames must hold hex digits only ([0-9A-Fa-f]; the front end guarantees [0-9A-F]) and at most
@@ -263,7 +264,7 @@ typedef struct {
 } sdx_lines_out;
 
 /* parse a batch of lines into out (device buffers, caller-owned; no allocation, no sync).  Lines
- * longer than the kernels' contract (SDX_LONG_MAX pulses, SDX_MC_HEX_MAX hex characters) are
+ * (MU/MS lines with multi-digit pattern ids or more than SDX_LONG_MAX pulses: SDX_LS_GENERAL) are
  * reported SDX_LS_UNSUPPORTED.  kind/status/doff/plen are written for every line; the other
  * fields only where they mean something: dlen and meta for SDX_LS_OK lines, the pattern fields
  * (npat, pat_id/pat_val[0..npat)) for OK MU/MS lines, cp_slot/ms_ok for OK MS lines, clock/

@@ -320,7 +320,7 @@ def _mc(q: bytes, r: Dict[str, Any]) -> Dict[str, Any]:
     if not _DEC.fullmatch(c) or not _DEC.fullmatch(l_):
         r.update(status=RAISES, msg=msg, rssi=rssi, freq_afc=afc)  # int() raises inside demodulate_mc
         return r
-    if not (-2**31 <= int(c) < 2**31) or not (-2**31 <= int(l_) < 2**31) or len(d[b"D"]) > MC_HEX_MAX:
+    if not (-2**31 <= int(c) < 2**31) or not (-2**31 <= int(l_) < 2**31):
         r["status"] = UNSUPPORTED
         return r
     if not _meta_fits({"R": d.get(b"R"), "F": d.get(b"F")}):

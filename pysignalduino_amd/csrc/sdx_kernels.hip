@@ -2215,9 +2215,23 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   const int gi = blockIdx.x * 256 + tid;
   bool valid = gi < ntot;
   const int msg = valid ? (b.sel_dev ? b.sel_dev[gi] : gi) : 0;
+  bool toolong = false;  // > MC_MAXW * 16 characters: left to sdx_demod_mc_general (status OVF_TILE)
   if (valid) {  // this launch's share: short frames (MW = 4) or long ones
     const int hl0 = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - b.offsets_dev[msg]);
     valid = LONG ? hl0 > MC_SHORTW * 16 : hl0 <= MC_SHORTW * 16;
+    if (LONG && valid && hl0 > MW * 16) {
+      toolong = true;
+      valid = false;
+    }
+  }
+  if (LONG && toolong) {
+    sdx_desc d;
+    d.rec_begin = 0;
+    d.n_rec = 0;
+    d.status = SDX_ST_OVF_TILE;
+    d.raise_kind = 0;
+    out.desc_dev[msg] = d;
+    atomicOr(&out.cursor_dev[2], 2u);
   }
   if (LONG && !__ballot(valid)) return;  // whole wave without long frames (nothing staged yet)
   if (lane == 0) { L.nrec[wave] = 0; L.nheap[wave] = 0; L.ovf[wave] = 0; }

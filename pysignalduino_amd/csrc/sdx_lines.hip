@@ -663,7 +663,7 @@ LD bool fast_payload(const uint8_t* P, int n, LineRes& r, const sdx_lines_out& o
   if (!(have & (1u << KD))) return false;
   if ((rS >= 0 && rE - rS > 15) || (fS >= 0 && fE - fS > 15)) return false;
   if (mc) {
-    if ((have & ((1u << KC) | (1u << KL))) != ((1u << KC) | (1u << KL)) || dE - dS > SDX_MC_HEX_MAX) return false;
+    if ((have & ((1u << KC) | (1u << KL))) != ((1u << KC) | (1u << KL))) return false;
     out.clock_dev[i] = (int32_t)cval;
     out.mcbitnum_dev[i] = (int32_t)lval;
     out.mcflags_dev[i] = 0;
@@ -869,7 +869,7 @@ LD void parse_payload(const Str& P, LineRes& r, const sdx_lines_out& out, int i,
       r.status = SDX_LS_RAISES;
       return;
     }
-    if (rc != 1 || rl != 1 || fD.e - fD.s > SDX_MC_HEX_MAX) {  // outside the int32 / frame-length contract
+    if (rc != 1 || rl != 1) {  // outside the int32 contract (long frames: the general MC kernel)
       r.status = SDX_LS_UNSUPPORTED;
       return;
     }

@@ -401,6 +401,7 @@ class SignalParser:
                          int(6 * len(data) + 400 * k + 65536), [(lb.mn_batch(), sels[runtime.SEL_MN], False)]))
         elig = self.protocols.mn_eligibility(self.rfmode)
         texts: List[Any] = [None] * n
+        host_rows: List[int] = []   # lines whose text is built from parse_lines' objects (general paths)
         for kind, rec_cap, heap_cap, json_cap, launches in jobs:
             for _attempt in range(4):
                 work = eng.pulses_work_bytes(n) if kind in (runtime.KIND_MU, runtime.KIND_MS) else 0
@@ -418,6 +419,12 @@ class SignalParser:
                 eng.launch_json(kind, out, lo, n, jo, first_only=True)
                 c1 = out["cursor"].cpu().numpy()
                 c2 = jo["cursor"].cpu().numpy()
+                if kind == runtime.KIND_MC and c1[2] == 2 and not c2[1]:
+                    # frames of > 128 hex characters were handed over (ST_OVF_TILE): their texts below
+                    sel = launches[0][1]
+                    st = out["desc"][: 8 * n].view(-1, 8)[:, 6][sel.long()].cpu().numpy()
+                    host_rows.extend(int(i) for i in sel.cpu().numpy()[st == runtime.ST_OVF_TILE])
+                    break
                 if not c1[2] and not c2[1]:
                     break
                 rec_cap, heap_cap, json_cap = 4 * rec_cap, 4 * heap_cap, 4 * json_cap
@@ -430,7 +437,7 @@ class SignalParser:
                 texts[int(i)] = blob[int(offs[i]): int(offs[i]) + int(lens[i])].decode("ascii")
         status = lb.status[:n].cpu().numpy()
         kinds = lb.kind[:n].cpu().numpy()
-        grows = [int(i) for i in np.nonzero(status == runtime.LS_GENERAL)[0] if int(i) not in bad]
+        grows = [int(i) for i in np.nonzero(status == runtime.LS_GENERAL)[0] if int(i) not in bad] + host_rows
         if grows:  # general-path lines (rare): their objects through parse_lines, the text as _message_to_json
             for i, g in zip(grows, self.parse_lines([lines[i] for i in grows])):
                 if isinstance(g, BaseException):

@@ -501,13 +501,16 @@ class Engine:
             sel = t.from_numpy(redo).to(self.dev)
             if kind == KIND_MN:
                 self.launch_mn(bd, out2, elig=mn_elig, method=mn_method, sel=sel)
-            elif kind == KIND_MC:
-                lr = bd["lengths"][redo] > MC_HEX_MAX
+            elif kind == KIND_MC:   # k_mc hands frames of > MC_HEX_MAX characters over as ST_OVF_TILE
+                if "lengths" in bd:
+                    rl = np.asarray(bd["lengths"])[redo]
+                else:                # a line batch: the frames' lengths are on the device
+                    rl = bd["len"][t.from_numpy(redo.astype(np.int64)).to(self.dev)].cpu().numpy()
+                lr = rl > MC_HEX_MAX
                 if (~lr).any():
                     self.launch_mc(bd, out2, sel=t.from_numpy(redo[~lr]).to(self.dev))
                 if lr.any():
-                    self.launch_mc_general(bd, out2, t.from_numpy(redo[lr]).to(self.dev),
-                                           int(bd["lengths"][redo].max()))
+                    self.launch_mc_general(bd, out2, t.from_numpy(redo[lr]).to(self.dev), int(rl.max()))
             else:
                 self.launch_pulses(kind, bd, out2, sel=sel, long_variant=True)
             d2, r2, h2 = self.fetch(out2)

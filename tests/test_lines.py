@@ -323,3 +323,34 @@ def test_lines_general_batch_matches_oracle(golden):
             if lk == runtime.LINE_MS:
                 assert int(h["ms_ok"][j]) == r["ms_ok"] and (not r["ms_ok"] or int(h["cp_slot"][j]) == r["gcp"])
     assert n_gen > 200
+
+
+@pytest.mark.gpu
+def test_long_mc_lines_fixed_mode_and_json():
+    """MC lines of more than 128 hex characters: sdx_parse_lines accepts them, k_mc hands them to
+    sdx_demod_mc_general; in fixed mode the DecodedMessages equal demodulate_mc_batch on the same
+    frames (the oracle-pinned dict path, tests/test_general.py), and parse_lines_json equals
+    json.dumps of the first message."""
+    import json
+    from pysignalduino_amd.frontend import SignalParser
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    p = SDProtocols(mc_mode="fixed")
+    P = p.get_protocol_list()
+    frames = synth.general_mc_frames(P, 300, seed=71) + synth.mc_planted_frames(P, 100, seed=72)
+    frames = [f for f in frames if all(c in "0123456789ABCDEFabcdef" for c in f[0])]
+    lines = ["\x02MC;LL=-1000;LH=900;SL=-500;SH=480;D=%s;C=%d;L=%d;R=40;\x03" % (h.upper(), c, L)
+             for h, c, L, _, _ in frames]
+    sp = SignalParser(p)
+    got = sp.parse_lines(lines)
+    ref = p.demodulate_mc_batch([{"raw_hex": h.upper(), "clock": c, "mcbitnum": L, "messagetype": "MC"}
+                                 for h, c, L, _, _ in frames])
+    nres = 0
+    for g, r in zip(got, ref):
+        exp = [] if isinstance(r, BaseException) else [(x["protocol_id"], x["payload"]) for x in r]
+        assert [(d.protocol_id, d.payload) for d in g] == exp
+        nres += len(exp)
+    assert sum(len(f[0]) > 128 for f in frames) > 200 and nres > 20
+    texts = sp.parse_lines_json(lines)
+    for g, t in zip(got, texts):
+        assert t == (json.dumps({"protocol_id": g[0].protocol_id, "payload": g[0].payload,
+                                 "metadata": g[0].metadata}, indent=4) if g else None)
