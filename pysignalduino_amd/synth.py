@@ -969,3 +969,22 @@ def general_mc_frames(P: Dict[str, dict], n: int, seed: int = 61):
             L = 4 * len(h2)
         out.append((h2, clock, L, mt, ver))
     return out
+
+
+def general_edge_messages(kind: str) -> List[Dict[str, str]]:
+    """Hand-written edge inputs of the general path (empty / one-character data, only multi-digit
+    ids, empty / non-numeric / nan / inf / -0 / 1e308 values, leading-zero keys beside multi-digit
+    ones, CP naming a multi-digit id, 16 patterns, ragged lengths around 4096)."""
+    base = {"CP": "10", "SP": "11", "R": "42"} if kind == "MS" else {"R": "42"}
+    return [
+        dict(base, data="", P10="400"),
+        dict(base, data="1", P10="400"),
+        dict(base, data="1010101110", P10="400", P11="-4000", P1="-400"),
+        dict(base, data="1011" * 30, P10="", P11="abc", P1="400", P0="-800"),
+        dict(base, data="1011" * 30, P10="nan", P11="inf", P1="-0", P0="1e308"),
+        dict(base, data="0010" * 40, P010="500", P10="-500", P0010="600", P0="-1000"),
+        dict(base, data="10" * 2100, P10="500", P1="-500", P0="-1000"),
+        dict(base, data="10" * 2048 + "1", P1="500", P0="-1000"),
+        dict(base, data="1" * 4097, P1="500"),
+        dict(base, data="1213" * 50, **{f"P{k}": str(100 * (k + 1)) for k in range(10, 26)}),
+    ]

@@ -88,23 +88,10 @@ def test_general_contract_limits(proto):
 
 @pytest.mark.parametrize("kind", ["MU", "MS"])
 def test_general_edge_cases_vs_oracle(proto, kind):
-    """Edge inputs on the general path: empty / one-character data, only multi-digit ids, empty,
-    non-numeric, nan / inf / -0 / 1e308 values, leading-zero keys mixed with multi-digit ones, CP
-    naming a multi-digit id, 16 patterns, ragged lengths around 4096."""
+    """synth.general_edge_messages (also in the reference goldens) against the oracle."""
+    from pysignalduino_amd import synth
     ob = O.OracleBank()
-    base = {"CP": "10", "SP": "11", "R": "42"} if kind == "MS" else {"R": "42"}
-    msgs = [
-        dict(base, data="", P10="400"),
-        dict(base, data="1", P10="400"),
-        dict(base, data="1010101110", P10="400", P11="-4000", P1="-400"),
-        dict(base, data="1011" * 30, P10="", P11="abc", P1="400", P0="-800"),
-        dict(base, data="1011" * 30, P10="nan", P11="inf", P1="-0", P0="1e308"),
-        dict(base, data="0010" * 40, P010="500", P10="-500", P0010="600", P0="-1000"),
-        dict(base, data="10" * 2100, P10="500", P1="-500", P0="-1000"),
-        dict(base, data="10" * 2048 + "1", P1="500", P0="-1000"),
-        dict(base, data="1" * 4097, P1="500"),
-        dict(base, data="1213" * 50, **{f"P{k}": str(100 * (k + 1)) for k in range(10, 26)}),
-    ]
+    msgs = synth.general_edge_messages(kind)
     got = proto.demodulate_batch(msgs, kind)
     for m, g in zip(msgs, got):
         assert _flat(g) == _oracle(ob, m, kind), (m.get("data", "")[:40], _flat(g), _oracle(ob, m, kind))
