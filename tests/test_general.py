@@ -95,3 +95,27 @@ def test_general_edge_cases_vs_oracle(proto, kind):
     got = proto.demodulate_batch(msgs, kind)
     for m, g in zip(msgs, got):
         assert _flat(g) == _oracle(ob, m, kind), (m.get("data", "")[:40], _flat(g), _oracle(ob, m, kind))
+
+
+@pytest.mark.parametrize("kind", ["MU", "MS"])
+def test_general_very_long_messages_vs_oracle(proto, kind):
+    """Messages of 20k-60k pulses (the reference has no length limit): repeated planted frames,
+    equal to the oracle (results, bit lengths, raises)."""
+    from pysignalduino_amd import synth
+    ob = O.OracleBank()
+    P = proto.get_protocol_list()
+    base = synth.planted_pulse_messages(P, kind, 6, seed=77, corrupt_frac=0.0)
+    msgs = []
+    for k, m in enumerate(base):
+        m = dict(m)
+        d = m["D"]
+        reps = (20000 + 8000 * k) // max(1, len(d)) + 1
+        m["D"] = m["data"] = (d + d[len(d) // 3:] * reps) if kind == "MS" else d * reps
+        msgs.append(m)
+    got = proto.demodulate_batch(msgs, kind)
+    nres = 0
+    for m, g in zip(msgs, got):
+        exp = _oracle(ob, m, kind)
+        assert _flat(g) == exp, (len(m["data"]), _flat(g).get("raise"), exp.get("raise"))
+        nres += len(exp.get("results", []))
+    assert nres > (100 if kind == "MU" else 0)
