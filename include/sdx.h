@@ -194,7 +194,7 @@ typedef struct {
   int32_t n, n_sel;
   const int32_t* len_dev;      /* optional [n] lengths: message i = data[offsets[i], +len[i]) (slot layout) */
   int64_t work_stride;         /* > 0: the j-th message run takes scratch at work_dev + j * work_stride
-                                * (>= 3 * (its length + 512)); 0: sdx_general_work_bytes layout */
+                                * (>= 5 * (its length + 512)); 0: sdx_general_work_bytes layout */
 } sdx_general_batch;
 
 uint64_t sdx_general_work_bytes(int64_t total_chars, int32_t n);

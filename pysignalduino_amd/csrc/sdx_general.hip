@@ -50,7 +50,35 @@ struct Msg {
   const uint8_t* ids;  // [GP][GID]
   const double* val;   // [GP]
   double nv[GP];       // round(P / clock, 1)
+  const uint64_t* bm;  // per digit character c: bm[c * nwp + w] bit j = d[64w + j] == '0' + c
+  int nwp;             // words per character bitmap (one zero word of padding)
 };
+
+// bits q .. q+63 of character c's occurrence bitmap (q >= 0; the padding word ends every row)
+GI uint64_t bm_at(const Msg& m, int c, int q) {
+  const uint64_t* r = m.bm + (size_t)c * m.nwp;
+  const int w = q >> 6, o = q & 63;
+  if (w >= m.nwp - 1) return 0ull;
+  const uint64_t lo = r[w];
+  return o ? (lo >> o) | (r[w + 1] << (64 - o)) : lo;
+}
+
+// str.find(s, from) over the bitmaps: 64 start positions per step, one AND per character of s
+// (pattern strings are digit strings: ids are str(int(key[1:])))
+GD int find_bm(const Msg& m, int from, const Str& s) {
+  if (s.len == 0) return from <= m.n ? from : -1;
+  const int last = m.n - s.len;
+  if (from < 0) from = 0;
+  if (from > last) return -1;
+  for (int w = from >> 6; w <= (last >> 6); ++w) {
+    uint64_t acc = ~0ull;
+    for (int i = 0; i < s.len && acc; ++i) acc &= bm_at(m, s.c[i] - '0', w * 64 + i);
+    if (w == (from >> 6)) acc &= ~0ull << (from & 63);
+    if (w == (last >> 6) && (last & 63) != 63) acc &= (1ull << ((last & 63) + 1)) - 1;
+    if (acc) return w * 64 + ffs64(acc);
+  }
+  return -1;
+}
 
 // result sink: pass 1 counts, pass 2 writes at the reserved bases
 struct Sink {
@@ -132,7 +160,7 @@ GD int pex(const Msg& m, const sdx_patspec* sp, int base, Str* out) {
         if (t.len + L > GS) return -1;
         for (int j = 0; j < L; ++j) t.c[t.len++] = m.ids[k * GID + 1 + j];
       }
-      if (find_str(m.d, m.n, base, t) >= 0) {  // (:133-134)
+      if (find_bm(m, base, t) >= 0) {  // (:133-134)
         *out = t;
         return 1;
       }
@@ -289,7 +317,7 @@ GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* 
       const int r = pex(m, &rec->start, 0, &S);
       if (r < 0) return SDX_RAISE_CONTRACT;
       if (r == 0) continue;
-      base = find_str(m.d, m.n, 0, S);
+      base = find_bm(m, 0, S);
     }
     // pattern_lookup (distinct strings, last writer), end_pattern_lookup (pstr[:-1], first writer)
     Str U[3], E[3];
@@ -337,7 +365,24 @@ GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* 
     while (pos <= nw) {  // matcher.finditer(current_raw_data) (:195)
       int gq = -1, ge = -1, s = pos;
       for (; s <= nw; ++s) {
-        if (S.len && !at(w, nw, s, S.c, S.len)) continue;
+        // jump to the next position where the start string (or, without one, any unit) occurs
+        if (S.len) {
+          const int f = find_bm(m, base + s, S);
+          if (f < 0) break;
+          s = f - base;
+        } else {
+          int f = -1;
+          for (int j = 0; j < nu; ++j) {
+            const int g = find_bm(m, base + s, U[j]);
+            if (g >= 0 && (f < 0 || g < f)) f = g;
+          }
+          if (f < 0) {
+            s = nw;  // no unit left: only an empty repetition (length_min 0) can match at the end
+            if (rec->length_min > 0) break;
+          } else {
+            s = f - base;
+          }
+        }
         bool over = false;
         const int e = rep_match(w, nw, s + S.len, U, nu, rec->length_min, &over);
         if (over) return SDX_RAISE_CONTRACT;
@@ -452,7 +497,7 @@ GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8
         }
       }
       if (k == 0) {  // (:145-158)
-        mstart = find_str(m.d, m.n, 0, t) + t.len;
+        mstart = find_bm(m, 0, t) + t.len;
         const double bl = W > 0 ? (double)(m.n - mstart) / (double)W : 0.0;
         if ((double)rec->lmin_sync > bl) {
           fail = true;
@@ -501,9 +546,26 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
   m.val = b.pat_val_dev + (size_t)msg * GP;
   // per-message scratch: bits, postDemod output, payload text (include/sdx.h sdx_general_work_bytes)
   uint8_t* B = b.work_stride > 0 ? out.work_dev + (int64_t)i * b.work_stride
-                                 : out.work_dev + 3 * off + (int64_t)3 * GSLACK * msg;
+                                 : out.work_dev + 5 * off + (int64_t)5 * GSLACK * msg;
   uint8_t* B2 = B + m.n + GSLACK;
   uint8_t* T = B2 + m.n + GSLACK;
+  // the message's digit-character bitmaps (find_bm), after the three byte areas, 8-byte aligned
+  uint64_t* bmw = reinterpret_cast<uint64_t*>(((uintptr_t)(T + m.n + GSLACK) + 7) & ~(uintptr_t)7);
+  m.nwp = ((m.n + 63) >> 6) + 1;
+  m.bm = bmw;
+  for (int w = 0; w < m.nwp; ++w) {
+    uint64_t a[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) a[c] = 0;
+    const int p0 = w * 64, pe = (m.n - p0 < 64) ? m.n - p0 : 64;
+    for (int j = 0; j < pe; ++j) {
+      const int c = (int)m.d[p0 + j] - '0';
+#pragma unroll
+      for (int k = 0; k < 10; ++k) a[k] |= (uint64_t)(c == k) << j;
+    }
+#pragma unroll
+    for (int c = 0; c < 10; ++c) bmw[(size_t)c * m.nwp + w] = a[c];
+  }
   const int cp = KIND == SDX_KIND_MS ? (int)b.cp_slot_dev[msg] : -1;
   const bool ok = KIND == SDX_KIND_MS ? b.ms_ok_dev[msg] != 0 : true;
   Sink sk{false, 0, 0u, out.rec_dev, out.heap_dev, 0u, 0u, (uint32_t)msg};
@@ -650,7 +712,7 @@ __global__ __launch_bounds__(256) void k_mc_general(const void* __restrict__ ban
 extern "C" {
 
 uint64_t sdx_general_work_bytes(int64_t total_chars, int32_t n) {
-  return (uint64_t)(3 * (total_chars > 0 ? total_chars : 0) + (int64_t)3 * sdxg::GSLACK * (n > 0 ? n : 0) + 256);
+  return (uint64_t)(5 * (total_chars > 0 ? total_chars : 0) + (int64_t)5 * sdxg::GSLACK * (n > 0 ? n : 0) + 256);
 }
 
 int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_batch* batch, const sdx_out* out,

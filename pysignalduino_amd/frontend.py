@@ -167,7 +167,7 @@ class LineBatch:
         status[rows] = st                                   # lines found outside the contract
         g.update(data=self.slot, n=m, total=int(lens.sum()))
         kd = runtime.KIND_MU if line_kind == runtime.LINE_MU else runtime.KIND_MS
-        desc, rec, heap = eng.run_general(kd, g, work_stride=3 * (int(lens.max()) + 512))
+        desc, rec, heap = eng.run_general(kd, g, work_stride=5 * (int(lens.max()) + 512))
         return (rows, desc, rec, heap, g["pat_val"].cpu().numpy().reshape(m, 16),
                 g["cp_slot"].cpu().numpy().astype(np.int64))
 
