@@ -7,8 +7,8 @@
 // id "10", message_unsynced.py:28-35, message_synced.py:50-57), builds candidate targets by string
 // concatenation (pattern_utils.py:120-130), matches MU with re.finditer over alternations of those
 // strings (message_unsynced.py:146-200) and slices chunks by characters (:203-221; MS :172-189).
-// This file restates that string semantics directly, lane = message, serially over the bank in
-// bank order (the order results and raises take in the reference):
+// This file restates that string semantics directly, one wave per message walking the bank in bank
+// order (the order results and raises take in the reference), the 64 lanes sharing the wide steps:
 //   * pattern_exists: candidates by the fp64 gap test, stable gap order, itertools.product order,
 //     no id reused, first target string that occurs (str `in`);
 //   * MU matching: Python sre's order for (?:S)((?:U1|U2|..){lmin,}(?:E1|..)?) -- leftmost start,
@@ -63,19 +63,27 @@ GI uint64_t bm_at(const Msg& m, int c, int q) {
   return o ? (lo >> o) | (r[w + 1] << (64 - o)) : lo;
 }
 
-// str.find(s, from) over the bitmaps: 64 start positions per step, one AND per character of s
-// (pattern strings are digit strings: ids are str(int(key[1:])))
+// str.find(s, from) over the bitmaps, the whole wave: lane l tests the 64 start positions of word
+// w0 + l (one AND per character of s; pattern strings are digit strings, ids are str(int(key[1:]))),
+// the lowest lane with a hit gives the position.  Called in wave-uniform control flow (every lane
+// holds the same message state, k_general), so 4096 start positions go per step.
 GD int find_bm(const Msg& m, int from, const Str& s) {
   if (s.len == 0) return from <= m.n ? from : -1;
   const int last = m.n - s.len;
   if (from < 0) from = 0;
   if (from > last) return -1;
-  for (int w = from >> 6; w <= (last >> 6); ++w) {
-    uint64_t acc = ~0ull;
-    for (int i = 0; i < s.len && acc; ++i) acc &= bm_at(m, s.c[i] - '0', w * 64 + i);
-    if (w == (from >> 6)) acc &= ~0ull << (from & 63);
-    if (w == (last >> 6) && (last & 63) != 63) acc &= (1ull << ((last & 63) + 1)) - 1;
-    if (acc) return w * 64 + ffs64(acc);
+  const int wf = from >> 6, wl = last >> 6, lane = lane_id();
+  for (int w0 = wf; w0 <= wl; w0 += 64) {
+    const int w = w0 + lane;
+    uint64_t acc = 0;
+    if (w <= wl) {
+      acc = ~0ull;
+      for (int i = 0; i < s.len && acc; ++i) acc &= bm_at(m, s.c[i] - '0', w * 64 + i);
+      if (w == wf) acc &= ~0ull << (from & 63);
+      if (w == wl && (last & 63) != 63) acc &= (1ull << ((last & 63) + 1)) - 1;
+    }
+    const uint64_t hit = ballot(acc != 0);
+    if (hit) return bcast_i(acc ? w * 64 + ffs64(acc) : 0, ffs64(hit));
   }
   return -1;
 }
@@ -102,15 +110,6 @@ GI bool str_eq(const Str& a, const Str& b) {
     if (a.c[i] != b.c[i]) return false;
   return true;
 }
-// str.find(s, from)
-GD int find_str(const uint8_t* d, int n, int from, const Str& s) {
-  if (s.len == 0) return from <= n ? from : -1;
-  const uint8_t c0 = s.c[0];
-  for (int p = from; p + s.len <= n; ++p)
-    if (d[p] == c0 && at(d, n, p, s.c, s.len)) return p;
-  return -1;
-}
-
 // pattern_exists(search, patterns, d[base:]) (pattern_utils.py:34-136): 1 found (*out = the target
 // string), 0 = -1, -1 = the target would exceed SDX_GEN_STRMAX characters (contract)
 GD int pex(const Msg& m, const sdx_patspec* sp, int base, Str* out) {
@@ -243,18 +242,19 @@ GD int emit(Sink& sk, const BankView& bv, int p, int pre_off, int pre_len, const
             int post_len, int bitlen) {
   const int total = pre_len + dl + post_len;
   if (total > 65535) return SDX_RAISE_CONTRACT;  // sdx_result.payload_len
-  if (sk.write) {
+  if (sk.write) {  // the payload bytes spread over the wave, the record from lane 0
     uint8_t* dst = sk.heap + sk.hbase + sk.nheap;
-    for (int i = 0; i < pre_len; ++i) dst[i] = bv.str[pre_off + i];
-    for (int i = 0; i < dl; ++i) dst[pre_len + i] = T[i];
-    for (int i = 0; i < post_len; ++i) dst[pre_len + dl + i] = bv.str[post_off + i];
-    sdx_result r;
-    r.payload_off = sk.hbase + sk.nheap;
-    r.payload_len = (uint16_t)total;
-    r.proto = (uint16_t)p;
-    r.bit_length = (uint32_t)bitlen;
-    r.msg = sk.msg;
-    sk.rec[sk.rbase + sk.nrec] = r;
+    for (int i = lane_id(); i < total; i += 64)
+      dst[i] = i < pre_len ? bv.str[pre_off + i] : i < pre_len + dl ? T[i - pre_len] : bv.str[post_off + i - pre_len - dl];
+    if (lane_id() == 0) {
+      sdx_result r;
+      r.payload_off = sk.hbase + sk.nheap;
+      r.payload_len = (uint16_t)total;
+      r.proto = (uint16_t)p;
+      r.bit_length = (uint32_t)bitlen;
+      r.msg = sk.msg;
+      sk.rec[sk.rbase + sk.nrec] = r;
+    }
   }
   ++sk.nrec;
   sk.nheap += (uint32_t)total;
@@ -530,12 +530,13 @@ GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8
   return 0;
 }
 
+// one wave per message: every lane runs the same serial walk over the bank on the same state (so
+// all control flow is wave-uniform), and the wide steps -- the character bitmaps, str.find, the
+// payload copies -- spread over the 64 lanes
 template <int KIND>
 __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, sdx_general_batch b, sdx_out out) {
   const BankView bv = bank_view(bank);
-  const int ntot = b.sel_dev ? b.n_sel : b.n;
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= ntot) return;
+  const int i = blockIdx.x, lane = threadIdx.x;
   const int msg = b.sel_dev ? b.sel_dev[i] : i;
   const int64_t off = b.offsets_dev[msg];
   Msg m;
@@ -544,16 +545,18 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
   m.npat = b.npat_dev[msg] < GP ? b.npat_dev[msg] : GP;
   m.ids = b.pat_ids_dev + (size_t)msg * GP * GID;
   m.val = b.pat_val_dev + (size_t)msg * GP;
-  // per-message scratch: bits, postDemod output, payload text (include/sdx.h sdx_general_work_bytes)
+  // per-message scratch: bits, postDemod output, payload text (include/sdx.h sdx_general_work_bytes);
+  // every lane writes the same bytes here and reads back only what it wrote itself
   uint8_t* B = b.work_stride > 0 ? out.work_dev + (int64_t)i * b.work_stride
                                  : out.work_dev + 5 * off + (int64_t)5 * GSLACK * msg;
   uint8_t* B2 = B + m.n + GSLACK;
   uint8_t* T = B2 + m.n + GSLACK;
-  // the message's digit-character bitmaps (find_bm), after the three byte areas, 8-byte aligned
+  // the message's digit-character bitmaps (find_bm), after the three byte areas, 8-byte aligned;
+  // lane l builds words l, l + 64, ..
   uint64_t* bmw = reinterpret_cast<uint64_t*>(((uintptr_t)(T + m.n + GSLACK) + 7) & ~(uintptr_t)7);
   m.nwp = ((m.n + 63) >> 6) + 1;
   m.bm = bmw;
-  for (int w = 0; w < m.nwp; ++w) {
+  for (int w = lane; w < m.nwp; w += 64) {
     uint64_t a[10];
 #pragma unroll
     for (int c = 0; c < 10; ++c) a[c] = 0;
@@ -566,6 +569,8 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
 #pragma unroll
     for (int c = 0; c < 10; ++c) bmw[(size_t)c * m.nwp + w] = a[c];
   }
+  __threadfence_block();
+  __syncthreads();  // the block is this one wave: the bitmaps are visible to every lane
   const int cp = KIND == SDX_KIND_MS ? (int)b.cp_slot_dev[msg] : -1;
   const bool ok = KIND == SDX_KIND_MS ? b.ms_ok_dev[msg] != 0 : true;
   Sink sk{false, 0, 0u, out.rec_dev, out.heap_dev, 0u, 0u, (uint32_t)msg};
@@ -577,11 +582,16 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
   d.status = raise ? SDX_ST_RAISED : SDX_ST_OK;
   if (!raise && sk.nrec) {
     const uint32_t nh = (sk.nheap + 15u) & ~15u;
-    const uint32_t rb = atomicAdd(&out.cursor_dev[0], (uint32_t)sk.nrec);
-    const uint32_t hb = atomicAdd(&out.cursor_dev[1], nh);
+    uint32_t rb = 0, hb = 0;
+    if (lane == 0) {
+      rb = atomicAdd(&out.cursor_dev[0], (uint32_t)sk.nrec);
+      hb = atomicAdd(&out.cursor_dev[1], nh);
+    }
+    rb = (uint32_t)bcast_i((int)rb, 0);
+    hb = (uint32_t)bcast_i((int)hb, 0);
     if (sk.nrec > 65535 || rb + sk.nrec > out.rec_cap || hb + nh > out.heap_cap) {
       d.status = SDX_ST_OVF_OUT;
-      atomicOr(&out.cursor_dev[2], 1u);
+      if (lane == 0) atomicOr(&out.cursor_dev[2], 1u);
     } else {
       Sink sw{true, 0, 0u, out.rec_dev, out.heap_dev, rb, hb, (uint32_t)msg};
       raise = KIND == SDX_KIND_MU ? mu_message(bv, m, B, B2, T, sw) : ms_message(bv, m, cp, ok, B, B2, T, sw);
@@ -589,7 +599,7 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
       d.n_rec = (uint16_t)sw.nrec;
     }
   }
-  out.desc_dev[msg] = d;
+  if (lane == 0) out.desc_dev[msg] = d;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -726,7 +736,7 @@ int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_b
   if (!batch->data_dev || !batch->offsets_dev || !batch->npat_dev || !batch->pat_ids_dev || !batch->pat_val_dev ||
       !out->work_dev || (batch->work_stride > 0 && out->work_cap < (uint64_t)batch->work_stride * (uint64_t)ntot))
     return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: missing buffer (work_dev: sdx_general_work_bytes)");
-  const int grid = (ntot + 63) / 64;
+  const int grid = ntot;  // one wave per message
   hipStream_t st = (hipStream_t)hip_stream;
   const void* bd = sdx::bank_dev_ptr(bank);
   if (kind == SDX_KIND_MU)
