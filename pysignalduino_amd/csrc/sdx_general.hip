@@ -43,7 +43,20 @@ struct Str {
   uint8_t c[GS];
 };
 
+// the wave's small working set, in LDS (all lanes write the same values and read them back):
+// dynamically indexed private arrays would live in scratch memory, at global-memory latency
+struct Wk {
+  Str str[8];                        // MU: S, U[3], E[3], the pex target; MS: K[4], E[3], the target
+  uint8_t sym[8];                    // symbols of the unit / end strings
+  uint8_t cand[SDX_MAXUNIQ][GP];     // pattern_exists candidates per unique value
+  int cnt[SDX_MAXUNIQ], digit[SDX_MAXUNIQ];
+  double gap[GP];
+  uint8_t ch[GREP];                  // rep_match choice stack
+  int ps[GREP];
+};
+
 struct Msg {
+  Wk* wk;
   const uint8_t* d;
   int n;
   int npat;
@@ -104,22 +117,27 @@ GI bool at(const uint8_t* d, int n, int p, const uint8_t* s, int len) {
     if (d[p + i] != s[i]) return false;
   return true;
 }
-GI bool str_eq(const Str& a, const Str& b) {
-  if (a.len != b.len) return false;
-  for (int i = 0; i < a.len; ++i)
+GI bool str_eq(const Str& a, const Str& b, int blen) {  // a == b[:blen]
+  if (a.len != blen) return false;
+  for (int i = 0; i < blen; ++i)
     if (a.c[i] != b.c[i]) return false;
   return true;
+}
+GI void str_set(Str& a, const Str& b, int blen) {  // a = b[:blen]
+  for (int i = 0; i < blen; ++i) a.c[i] = b.c[i];
+  a.len = blen;
 }
 // pattern_exists(search, patterns, d[base:]) (pattern_utils.py:34-136): 1 found (*out = the target
 // string), 0 = -1, -1 = the target would exceed SDX_GEN_STRMAX characters (contract)
 GD int pex(const Msg& m, const sdx_patspec* sp, int base, Str* out) {
   const int slen = sp->len, nu = sp->nuniq;
-  uint8_t cand[SDX_MAXUNIQ][GP];
-  int cnt[SDX_MAXUNIQ];
+  auto& cand = m.wk->cand;
+  int* cnt = m.wk->cnt;
+  int* digit = m.wk->digit;
+  double* gap = m.wk->gap;
   int total = 1;
   for (int u = 0; u < nu; ++u) {
     const double uv = sp->uval[u], tol = sp->utol[u];
-    double gap[GP];
     int c = 0;
     for (int k = 0; k < m.npat; ++k) {
       const double g = fabs(m.nv[k] - uv);
@@ -139,7 +157,6 @@ GD int pex(const Msg& m, const sdx_patspec* sp, int base, Str* out) {
     total *= c;
     if (total > 10000) return 0;  // (:88-95): the product only grows
   }
-  int digit[SDX_MAXUNIQ];
   for (int u = 0; u < SDX_MAXUNIQ; ++u) digit[u] = 0;
   for (int it = 0; it < total; ++it) {
     uint32_t used = 0;
@@ -149,20 +166,18 @@ GD int pex(const Msg& m, const sdx_patspec* sp, int base, Str* out) {
       if ((used >> k) & 1u) dup = true;
       used |= 1u << k;
     }
-    if (!dup) {  // (:111-113)
-      Str t;
-      t.len = 0;
+    if (!dup) {  // (:111-113); the target is built in *out
+      Str& t = *out;
+      int tl = 0;
       for (int s = 0; s < slen; ++s) {
         const int u = sp->uidx[s];
         const int k = cand[u][digit[u]];
         const int L = m.ids[k * GID];
-        if (t.len + L > GS) return -1;
-        for (int j = 0; j < L; ++j) t.c[t.len++] = m.ids[k * GID + 1 + j];
+        if (tl + L > GS) return -1;
+        for (int j = 0; j < L; ++j) t.c[tl++] = m.ids[k * GID + 1 + j];
       }
-      if (find_bm(m, base, t) >= 0) {  // (:133-134)
-        *out = t;
-        return 1;
-      }
+      t.len = tl;
+      if (find_bm(m, base, t) >= 0) return 1;  // (:133-134)
     }
     for (int u = nu - 1; u >= 0; --u) {  // itertools.product: the last list varies fastest
       if (digit[u] + 1 < cnt[u]) {
@@ -178,14 +193,12 @@ GD int pex(const Msg& m, const sdx_patspec* sp, int base, Str* out) {
 // (?:U0|U1|..){lmin,} at q in Python sre order: alternatives in order, another iteration before
 // stopping; a dead end below lmin iterations backtracks to the latest choice with a further
 // alternative.  Returns the end of the repetition or -1; *over on the step budget / depth limit.
-GD int rep_match(const uint8_t* d, int n, int q, const Str* U, int nu, int lmin, bool* over) {
+GD int rep_match(const uint8_t* d, int n, int q, const Str* U, int nu, int lmin, bool* over, uint8_t* ch, int* ps) {
   long long steps = 0;
   if (lmin > GREP) {
     *over = true;
     return -1;
   }
-  uint8_t ch[GREP];
-  int ps[GREP];
   int depth = 0, p = q, a0 = 0;
   while (true) {
     if (++steps > GBUDGET) {
@@ -311,7 +324,7 @@ GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* 
       for (int k = 0; k < m.npat; ++k) m.nv[k] = py_round1(m.val[k] / rec->clock);  // (:62-64)
     }
     int base = 0;
-    Str S;
+    Str& S = m.wk->str[0];
     S.len = 0;
     if (rec->has_start) {  // (:70-88)
       const int r = pex(m, &rec->start, 0, &S);
@@ -320,15 +333,17 @@ GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* 
       base = find_bm(m, 0, S);
     }
     // pattern_lookup (distinct strings, last writer), end_pattern_lookup (pstr[:-1], first writer)
-    Str U[3], E[3];
-    uint8_t us[3], es[3];
+    Str* U = m.wk->str + 1;
+    Str* E = m.wk->str + 4;
+    Str& t = m.wk->str[7];
+    uint8_t* us = m.wk->sym;
+    uint8_t* es = m.wk->sym + 3;
     int nu = 0, ne = 0;
     bool fail = false;
     const sdx_patspec* K[3] = {&rec->one, &rec->zero, &rec->flt};
     const uint8_t SYM[3] = {1, 0, 2};
     for (int k = 0; k < 3; ++k) {  // (:98-141)
       if (K[k]->len == 0) continue;
-      Str t;
       const int r = pex(m, K[k], base, &t);
       if (r < 0) return SDX_RAISE_CONTRACT;
       if (r == 0) {
@@ -340,17 +355,15 @@ GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* 
       }
       int j = 0;
       for (; j < nu; ++j)
-        if (str_eq(U[j], t)) break;
-      if (j == nu) U[nu++] = t;
+        if (str_eq(U[j], t, t.len)) break;
+      if (j == nu) str_set(U[nu++], t, t.len);
       us[j] = SYM[k];
       if (t.len > 0) {
-        Str e = t;
-        e.len -= 1;
         int i = 0;
         for (; i < ne; ++i)
-          if (str_eq(E[i], e)) break;
+          if (str_eq(E[i], t, t.len - 1)) break;
         if (i == ne) {
-          E[ne] = e;
+          str_set(E[ne], t, t.len - 1);
           es[ne] = SYM[k];
           ++ne;
         }
@@ -384,7 +397,7 @@ GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* 
           }
         }
         bool over = false;
-        const int e = rep_match(w, nw, s + S.len, U, nu, rec->length_min, &over);
+        const int e = rep_match(w, nw, s + S.len, U, nu, rec->length_min, &over, m.wk->ch, m.wk->ps);
         if (over) return SDX_RAISE_CONTRACT;
         if (e >= 0) {
           gq = s + S.len;
@@ -462,14 +475,16 @@ GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8
     if (rec->never) continue;
     if (rec->pclock > 0.0 && fabs(rec->pclock - clock) > clock * 0.3) continue;  // (:81-86)
     const int W = rec->width;
-    Str K[4], E[3];
-    uint8_t ks[4], es[3];
+    Str* K = m.wk->str;
+    Str* E = m.wk->str + 4;
+    Str& t = m.wk->str[7];
+    uint8_t* ks = m.wk->sym;
+    uint8_t* es = m.wk->sym + 4;
     int nk = 0, ne = 0, mstart = 0;
     bool fail = false;
     for (int k = 0; k < 4; ++k) {  // (:109-160)
       const sdx_patspec* sp = &rec->key[k];
       if (sp->len == 0) continue;
-      Str t;
       const int r = pex(m, sp, 0, &t);
       if (r < 0) return SDX_RAISE_CONTRACT;
       if (r == 0) {
@@ -481,17 +496,15 @@ GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8
       }
       int j = 0;
       for (; j < nk; ++j)
-        if (str_eq(K[j], t)) break;
-      if (j == nk) K[nk++] = t;
+        if (str_eq(K[j], t, t.len)) break;
+      if (j == nk) str_set(K[nk++], t, t.len);
       ks[j] = KS[k];
       if (t.len > 0) {
-        Str e = t;
-        e.len -= 1;
         int i = 0;
         for (; i < ne; ++i)
-          if (str_eq(E[i], e)) break;
+          if (str_eq(E[i], t, t.len - 1)) break;
         if (i == ne) {
-          E[ne] = e;
+          str_set(E[ne], t, t.len - 1);
           es[ne] = KS[k];
           ++ne;
         }
@@ -533,13 +546,20 @@ GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8
 // one wave per message: every lane runs the same serial walk over the bank on the same state (so
 // all control flow is wave-uniform), and the wide steps -- the character bitmaps, str.find, the
 // payload copies -- spread over the 64 lanes
+constexpr int GHEAD = (int)((sizeof(Msg) + sizeof(Wk) + 15) & ~(size_t)15);  // LDS: Msg, Wk, then data
+__host__ __device__ inline int lds_need(int n) { return GHEAD + ((n + 7) & ~7); }                        // + the message's characters
+__host__ __device__ inline int lds_need_bm(int n) { return lds_need(n) + 80 * (((n + 63) >> 6) + 1); }   // + its digit bitmaps
+
 template <int KIND>
-__global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, sdx_general_batch b, sdx_out out) {
+__global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, sdx_general_batch b, sdx_out out,
+                                                 int lds_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t glds[];
   const BankView bv = bank_view(bank);
   const int i = blockIdx.x, lane = threadIdx.x;
   const int msg = b.sel_dev ? b.sel_dev[i] : i;
   const int64_t off = b.offsets_dev[msg];
-  Msg m;
+  Msg& m = *reinterpret_cast<Msg*>(glds);
+  m.wk = reinterpret_cast<Wk*>(glds + sizeof(Msg));
   m.d = b.data_dev + off;
   m.n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
   m.npat = b.npat_dev[msg] < GP ? b.npat_dev[msg] : GP;
@@ -555,6 +575,12 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
   // lane l builds words l, l + 64, ..
   uint64_t* bmw = reinterpret_cast<uint64_t*>(((uintptr_t)(T + m.n + GSLACK) + 7) & ~(uintptr_t)7);
   m.nwp = ((m.n + 63) >> 6) + 1;
+  // the characters and the bitmaps go to LDS when they fit (the serial walks read them at LDS latency)
+  if (lds_need(m.n) <= lds_bytes) {
+    uint8_t* ld = glds + GHEAD;
+    for (int j = lane; j < m.n; j += 64) ld[j] = m.d[j];
+    if (lds_need_bm(m.n) <= lds_bytes) bmw = reinterpret_cast<uint64_t*>(glds + lds_need(m.n));
+  }
   m.bm = bmw;
   for (int w = lane; w < m.nwp; w += 64) {
     uint64_t a[10];
@@ -570,7 +596,8 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
     for (int c = 0; c < 10; ++c) bmw[(size_t)c * m.nwp + w] = a[c];
   }
   __threadfence_block();
-  __syncthreads();  // the block is this one wave: the bitmaps are visible to every lane
+  __syncthreads();  // the block is this one wave: the bitmaps and LDS characters are visible to every lane
+  if (lds_need(m.n) <= lds_bytes) m.d = glds + GHEAD;
   const int cp = KIND == SDX_KIND_MS ? (int)b.cp_slot_dev[msg] : -1;
   const bool ok = KIND == SDX_KIND_MS ? b.ms_ok_dev[msg] != 0 : true;
   Sink sk{false, 0, 0u, out.rec_dev, out.heap_dev, 0u, 0u, (uint32_t)msg};
@@ -737,12 +764,20 @@ int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_b
       !out->work_dev || (batch->work_stride > 0 && out->work_cap < (uint64_t)batch->work_stride * (uint64_t)ntot))
     return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: missing buffer (work_dev: sdx_general_work_bytes)");
   const int grid = ntot;  // one wave per message
+  // LDS per wave: the working set plus the longest message's characters and bitmaps when the
+  // stride names it (work_stride = 5 * (max len + GSLACK)), at most 64 KB; longer ones stay in HBM
+  int lds = 65536;
+  if (batch->work_stride > 0) {
+    const int64_t ml = batch->work_stride / 5 - sdxg::GSLACK;
+    lds = ml < 0 ? sdxg::GHEAD : ml >= 65536 ? 65536 : sdxg::lds_need_bm((int)ml);
+    if (lds > 65536) lds = 65536;
+  }
   hipStream_t st = (hipStream_t)hip_stream;
   const void* bd = sdx::bank_dev_ptr(bank);
   if (kind == SDX_KIND_MU)
-    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MU>), dim3(grid), dim3(64), 0, st, bd, *batch, *out);
+    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MU>), dim3(grid), dim3(64), lds, st, bd, *batch, *out, lds);
   else
-    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MS>), dim3(grid), dim3(64), 0, st, bd, *batch, *out);
+    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MS>), dim3(grid), dim3(64), lds, st, bd, *batch, *out, lds);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("k_general: ") + hipGetErrorString(e));
   return SDX_OK;
