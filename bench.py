@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--msgs", type=int, default=1_000_000, help="messages per rank (1/3 MU, 1/3 MS, 1/3 MC)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the N > 1 exchange (RCCL process group, overlapped all-gather) even at world size 1")
     ap.add_argument("--kind", default="mixed", choices=("mixed", "MU", "MS", "MC"),
                     help="mixed = config 5's per-GPU shard (1/3 each); MU/MS/MC = configs 2/3/4 (--msgs of one type)")
     ap.add_argument("--no-group", action="store_true",
@@ -132,7 +134,12 @@ def main():
     backend = os.environ.get("SDX_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    dist_on = world > 1 or args.exchange   # --exchange: the N > 1 path on a world-1 RCCL group
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29541")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -161,7 +168,7 @@ def main():
             corp[k] = synth.mc_corpus(P, per[k], seed=sd)
         bds[k] = eng.to_device_mc(corp[k]) if k == "MC" else eng.to_device_pulses(corp[k])
     caps = {"MU": (12, 320), "MS": (4, 64), "MC": (4, 96)}
-    nslot = 2 if world > 1 else 1   # double-buffered outputs: step k+1 computes while step k is exchanged
+    nslot = 2 if dist_on else 1   # double-buffered outputs: step k+1 computes while step k is exchanged
     outs = []
     cursors = torch.zeros((nslot, len(kinds), 4), dtype=torch.int32, device=dev)
     for s_ in range(nslot):
@@ -201,7 +208,7 @@ def main():
                 gdone[(k, par)] = e
             if si is not None:
                 gev[si][1].record(side)
-    exch = sdist.Exchange() if world > 1 else None
+    exch = sdist.Exchange() if dist_on else None
     done = [None] * nslot
     # one event pair per kernel and timed step: read after the closing synchronize
     ev = [{k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in kinds}
@@ -286,7 +293,7 @@ def main():
             ovf[k] = int(cur[2])
     if ovf and args.corpus != "dense":
         raise SystemExit(f"result capacity overflow in bench configuration ({ovf})")
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -294,13 +301,13 @@ def main():
         step(j, si)
         j += 1
     drain()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
     ktimes = {k: [ev[si][k][0].elapsed_time(ev[si][k][1]) * 1e-3 for si in range(args.steps)] for k in kinds}
     gtime = float(np.mean([gev[si][0].elapsed_time(gev[si][1]) * 1e-3 for si in range(args.steps)])) if gkinds else 0.0
     tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
     total_msgs = sum(per.values()) * world * args.steps
@@ -334,7 +341,7 @@ def main():
           "MU": "config 2: 256-pulse MU messages x 129-id MU bank",
           "MS": "config 3: MS sync+bits messages x 66-id MS bank, clock x U(0.6,1.4) sweep of the +-30 % gate",
           "MC": "config 4: MC frames x 12 clockrange ids ('fixed' chain, mc2dmc + postdemodulation methods)"}[args.kind]
-    if world > 1:
+    if dist_on:
         wl += "; N>1 adds the RCCL all-gather of dmsg buffers (config 5), overlapped with the next step"
     res = {
         "metric": "RF messages/sec demodulated (MU+MS+MC, full protocol bank)",
@@ -365,7 +372,7 @@ def main():
         res["cpu_baseline"] = cpu_baseline(corp.get("MU"), corp.get("MS"), corp.get("MC"), args.cpu_seconds, kinds)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

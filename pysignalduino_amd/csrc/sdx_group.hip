@@ -41,6 +41,9 @@ SDX_DEV uint64_t peers8(uint32_t v, bool active) {
 // the clock-grouped processing order.)
 // ---------------------------------------------------------------------------------------------
 constexpr int SIG_PROTOS = 32;
+#ifndef SDX_MS_KEY
+#define SDX_MS_KEY 0  // MS key form (A/B experiments; 0 = ascending signature)
+#endif
 template <int KIND>
 __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_pulse_batch b, uint32_t* __restrict__ key,
                                              uint32_t* __restrict__ msg_out) {
@@ -137,7 +140,16 @@ __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_
     // MU: descending signature order -- messages that pass the leading protocols, the tiles that
     // run the expensive search most, start first and the cheap tiles fill the kernel's tail
     // (MU 1.29 -> 1.21 ms; popcount-first keys measured 1.24 ms); MS measured better ascending
-    key[i] = KIND == SDX_KIND_MU ? ~sig : sig;
+#if SDX_MS_KEY == 1
+    const uint32_t ms_key = ~sig;
+#elif SDX_MS_KEY == 2  // survivor count descending, then signature
+    const uint32_t ms_key = ((uint32_t)(32 - popc64(sig)) << 26) | (sig >> 6);
+#elif SDX_MS_KEY == 3  // survivor count ascending, then signature
+    const uint32_t ms_key = ((uint32_t)popc64(sig) << 26) | (sig >> 6);
+#else
+    const uint32_t ms_key = sig;
+#endif
+    key[i] = KIND == SDX_KIND_MU ? ~sig : ms_key;
     msg_out[i] = (uint32_t)msg;
   }
 }

@@ -163,3 +163,17 @@ def test_exchange_pack_kernel_matches_torch_pack():
     sdist._pack_device(parts, S, 2, sec_off, base, b, torch.cuda.current_stream(dev))
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_exchange_rccl_world1():
+    """The bench's N > 1 exchange over a real RCCL process group (world size 1, cuda:0): the
+    pipelined count all-gather, device packing and data all-gather on the exchange stream, two
+    double-buffered steps of MU + MC launches; gathered buffers == the rank's own outputs.  Runs
+    in a child process (its own process group), bounded by a timeout."""
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_exchange_worker.py")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, worker], env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
