@@ -115,6 +115,7 @@ class Exchange:
         self.pending: Optional[_Pending] = None
         self.stream = None
         self._bufs = {}
+        self._ns = {}      # device copies of the launches' message counts
         self.last = None   # (recv, S, nb, sec_off, total) of the last completed exchange
 
     def _buf(self, name, n, dev):
@@ -124,9 +125,18 @@ class Exchange:
         return b[:n]
 
     def _counts(self, parts):
+        """(messages, records, heap bytes) per launch, flat, on the device.  The message counts are
+        host-known; their device copy is made once per distinct set and cached, because a fresh
+        ``torch.tensor(..., device=cuda)`` is a blocking copy on the current (exchange) stream,
+        which waits for the step's kernels and stalls the host's enqueue of the next step."""
         dev = parts[0][0].device
-        return torch.stack([torch.stack([torch.tensor(n, dtype=torch.int64, device=dev), cur[0].to(torch.int64),
-                                         cur[1].to(torch.int64)]) for _, _, _, n, cur in parts]).reshape(-1)
+        ns = tuple(int(n) for _, _, _, n, _ in parts)
+        key = (str(dev), ns)
+        nd = self._ns.get(key)
+        if nd is None:
+            nd = self._ns[key] = torch.tensor(ns, dtype=torch.int64).to(dev)
+        cur = torch.stack([c[:2] for _, _, _, _, c in parts]).to(torch.int64)   # [K, 2]
+        return torch.cat([nd.view(-1, 1), cur], dim=1).reshape(-1)
 
     def submit(self, parts, stream=None):
         parts = list(parts)

@@ -94,7 +94,9 @@ def main():
     n = len(lines)
     lb = frontend.LineBatch(eng, data, offsets)
     pb, mb = lb.pulse_batch(), lb.mc_batch()
-    outs = {"MU": eng.alloc_out(n, 8 * n + 4096, 160 * n + 65536), "MS": eng.alloc_out(n, 2 * n + 4096, 48 * n + 65536),
+    # MU/MS carry the spill workspace heavy tiles write into (sdx_out.work_dev, round 2)
+    outs = {"MU": eng.alloc_out(n, 8 * n + 4096, 160 * n + 65536, eng.pulses_work_bytes(n)),
+            "MS": eng.alloc_out(n, 2 * n + 4096, 48 * n + 65536, eng.pulses_work_bytes(n)),
             "MC": eng.alloc_out(n, 2 * n + 4096, 48 * n + 65536)}
     stream = torch.cuda.current_stream()
     names = ["parse+select", "MU", "MS", "MC"] + (["json"] if args.json else [])
@@ -173,7 +175,8 @@ def main():
     alg = int(offsets[-1]) + 8 * (n + 1) + 152 * n + int(dl[stv == runtime.LS_OK].sum())
     achieved = alg / km["parse"]
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "r01", "pmc_traffic_lines.json")
+    tpath = next((p for p in (os.path.join(REPO, "profiles", r, "pmc_traffic_lines.json") for r in ("r02", "r01"))
+                  if os.path.exists(p)), "")
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
         if tj.get("_config", {}).get("lines") == n and tj.get("k_parse_lines", {}).get("traffic_bytes"):
