@@ -1170,18 +1170,21 @@ LD void parse_compressed(const sdx_lines& in, const sdx_lines_out& out, int i, u
   out.status_dev[i] = r.status;
 }
 
-// the lines k_parse_lines left to it (ST_RARE): each wave scans COMP_CHUNK lines, queues the
-// compressed ones in LDS and parses them 64 at a time (lane = line), so the decompression work of
-// the ~20 % compressed lines of a mixed stream runs on full waves
-constexpr int COMP_CHUNK = 192;  // lines scanned per wave (~40 compressed at the bench mix): measured best of 128-2048
-__global__ __launch_bounds__(256) void k_parse_comp(sdx_lines in, sdx_lines_out out) {
+// the lines k_parse_lines left to it (ST_RARE): each wave scans `chunk` lines (a multiple of 64),
+// queues the compressed ones in LDS and parses them 64 at a time (lane = line), so the
+// decompression work of the ~20 % compressed lines of a mixed stream runs on full waves.  A wave's
+// time is about one line's serial decompress + parse, so the host sizes `chunk` for the grid to fit
+// the GPU's resident waves in one round (comp_chunk below)
+constexpr int COMP_CHUNK = 192;         // lower bound of the chunk (~40 compressed at the bench mix)
+constexpr int COMP_WAVES_PER_CU = 16;   // k_parse_comp: 118 VGPRs -> 4 waves/SIMD
+__global__ __launch_bounds__(256) void k_parse_comp(sdx_lines in, sdx_lines_out out, int chunk) {
   __shared__ uint32_t pv[4][10 * 64];
   __shared__ int q[4][128];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* pvt = pv[wave] + lane;
-  const int64_t base = ((int64_t)blockIdx.x * 4 + wave) * COMP_CHUNK;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + wave) * chunk;
   int qn = 0;
-  for (int c = 0; c < COMP_CHUNK; c += 64) {
+  for (int c = 0; c < chunk; c += 64) {
     const int64_t i = base + c + lane;
     const bool rare = i < in.n && out.status_dev[i] == ST_RARE;
     const uint64_t m = __ballot(rare);
@@ -1202,6 +1205,20 @@ __global__ __launch_bounds__(256) void k_parse_comp(sdx_lines in, sdx_lines_out 
     }
   }
   if (lane < qn) parse_compressed(in, out, q[wave][lane], pvt);
+}
+
+// lines per k_parse_comp wave: at least COMP_CHUNK, and enough that the grid's waves fit the
+// device's resident waves in one round (1M lines on 256 CUs: 256 -> 3907 waves <= 4096; the fixed
+// 192 needed 5208 waves, a second round 27 % full)
+int comp_chunk(int n) {
+  int dev = 0, cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cu <= 0)
+    cu = 256;
+  const int64_t waves = (int64_t)cu * COMP_WAVES_PER_CU;
+  int64_t c = ((int64_t)n + waves - 1) / waves;
+  c = (c + 63) / 64 * 64;
+  return (int)(c < COMP_CHUNK ? COMP_CHUNK : c);
 }
 
 // ---- selection lists (sdx_select_lines): class of a parsed line, -1 = not demodulated
@@ -1471,8 +1488,9 @@ extern "C" int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out,
     return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: bytes_dev and slot_dev must be 8-byte aligned");
   const int grid = (lines->n + sdxl::PT - 1) / sdxl::PT;
   hipLaunchKernelGGL(sdxl::k_parse_lines, dim3(grid), dim3(sdxl::PT), 0, (hipStream_t)hip_stream, *lines, *out);
-  hipLaunchKernelGGL(sdxl::k_parse_comp, dim3((lines->n + 4 * sdxl::COMP_CHUNK - 1) / (4 * sdxl::COMP_CHUNK)),
-                     dim3(256), 0, (hipStream_t)hip_stream, *lines, *out);
+  const int chunk = sdxl::comp_chunk(lines->n);
+  hipLaunchKernelGGL(sdxl::k_parse_comp, dim3((int)(((int64_t)lines->n + 4 * chunk - 1) / (4 * chunk))), dim3(256), 0,
+                     (hipStream_t)hip_stream, *lines, *out, chunk);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("sdx_parse_lines: ") + hipGetErrorString(e));
   return SDX_OK;
