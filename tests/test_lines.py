@@ -354,3 +354,24 @@ def test_long_mc_lines_fixed_mode_and_json():
     for g, t in zip(got, texts):
         assert t == (json.dumps({"protocol_id": g[0].protocol_id, "payload": g[0].payload,
                                  "metadata": g[0].metadata}, indent=4) if g else None)
+
+
+@pytest.mark.gpu
+def test_parse_lines_large_batch_comp_chunk():
+    """A batch large enough that the host sizes k_parse_comp's chunk above its 192-line minimum
+    (the grid fits the resident waves in one round): the same 8000 lines repeated 110 times, and
+    the first, a middle and the last copy compared with the oracle."""
+    import torch
+    P = B.Bank().protocols
+    base, _ = synth.line_corpus(P, 8000, seed=31, compress_frac=0.3)
+    reps = 110
+    cu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert len(base) * reps > cu * 16 * 192, "batch too small to leave the minimum chunk"
+    dv = _device_parse(base * reps)
+    nb = len(base)
+    for c in (0, reps // 2, reps - 1):
+        lo, hi = c * nb, (c + 1) * nb
+        sl = {k: (v[lo:hi] if isinstance(v, np.ndarray) and k not in ("slot", "offsets") else v) for k, v in dv.items()}
+        sl["offsets"] = dv["offsets"][lo:hi + 1]
+        bad = _compare(base, sl)
+        assert not bad, f"copy {c}: {len(bad)} mismatches; first: {bad[:3]}"
