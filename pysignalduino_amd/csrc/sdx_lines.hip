@@ -1052,7 +1052,9 @@ LD void finish_fields(const Str& P, const LineRes& r, const sdx_lines_out& out, 
 
 constexpr uint8_t ST_RARE = 0xFF;  // internal: compressed, but not recognisably at its first byte
 
-__global__ __launch_bounds__(PT) void k_parse_lines(sdx_lines in, sdx_lines_out out) {
+// 6 waves/SIMD: the kernel needs 81 VGPRs unconstrained (5 waves); at 80 it fits 6 with no scratch
+__global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(6))) void k_parse_lines(sdx_lines in,
+                                                                                           sdx_lines_out out) {
   __shared__ uint32_t pv[PT / 64][10 * 64];  // parse_payload's P-key table, per lane
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * PT + threadIdx.x;
