@@ -52,6 +52,50 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo), for the cpu_baseline line."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def launch_ranks(args) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script (one GPU each,
+    LOCAL_RANK = rank) and wait for them.  Runs before anything touches the GPU (this process never
+    initialises HIP: the ranks are children, not exec'd replacements).  If one rank fails the others
+    are stopped (they would wait in a collective) and its exit status is returned."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:          # the exact PIDs this function started
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def cpu_baseline(mu, ms, mc, budget_s: float, kinds=("MU", "MS", "MC")):
     """The plain-C oracle (oracle/sd_oracle_c.c, a restatement of the reference path: kind 'port')
     timed on this host over a bounded sample of the SAME corpora the GPU demodulates (1:1:1
@@ -86,7 +130,7 @@ def cpu_baseline(mu, ms, mc, budget_s: float, kinds=("MU", "MS", "MC")):
     return {"value": vn, "unit": "msgs/s", "cores": cores, "kind": "port", "value_1core": v1,
             "sample": f"oracle/sd_oracle_c.c (plain C, gcc -O2): {len(kinds) * kn} messages ({mix}, the "
                       f"first {kn} of each bench corpus) on {cores} threads; 1-core rate on {len(kinds) * k1} "
-                      f"messages; {platform.processor() or platform.machine()}"}
+                      f"messages; host CPU: {cpu_model()}"}
 
 
 def issue_view(pmc, t_kernel):
@@ -124,9 +168,13 @@ def latest_pmc():
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # SDX_DIST_BACKEND=gloo rehearses the N > 1 code path on fewer GPUs than ranks (ranks share
@@ -144,6 +192,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    if dist_on and dist.get_world_size() != args.gpus:
+        raise SystemExit(f"bench.py: the process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -269,16 +319,15 @@ def main():
             u.record(stream)
             used[par] = u
         if exch is not None:  # RCCL all-gather of the decoded dmsg buffers (config 5), overlapped
-            d = exch.submit([(outs[s_][k]["desc"], outs[s_][k]["rec"], outs[s_][k]["heap"], bds[k]["n"],
-                              outs[s_][k]["cursor"]) for k in kinds], stream)
-            done[(j - 1) % nslot] = d
+            done[s_] = exch.submit([(outs[s_][k]["desc"], outs[s_][k]["rec"], outs[s_][k]["heap"], bds[k]["n"],
+                                     outs[s_][k]["cursor"]) for k in kinds], stream)
 
     def drain():
         stream.wait_stream(side)
         if exch is not None:
-            d = exch.flush()
-            if d is not None:
-                stream.wait_event(d)
+            exch.flush()
+            if exch.stream is not None:     # the last step's pack and data all-gather
+                stream.wait_stream(exch.stream)
         torch.cuda.synchronize()
 
     j = 0
@@ -362,6 +411,13 @@ def main():
                      "alg_bytes_per_launch": alg, "layout_bytes_per_launch": layout,
                      "results_per_launch": int(cur[0]), "issue": issue},
     }
+    if exch is not None and exch.bytes_sent:
+        nb = exch.bytes_sent[-args.steps:]
+        wb = exch.wire_bytes[-args.steps:]
+        res["exchange"] = {"format": "wire (include/sdx.h): 4 B/message + 8 B/record + payload bytes",
+                           "send_bytes_per_rank_per_step": float(np.mean(nb)),
+                           "wire_bytes_per_rank_per_step": float(np.mean(wb)),
+                           "recv_bytes_per_rank_per_step": float(np.mean(nb)) * world}
     if ovf:   # dense corpus: messages whose results did not fit the on-chip staging (the product re-runs them)
         res["overflow"] = {}
         for k in ovf:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 7
+#define SDX_ABI_VERSION 8
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -91,6 +91,8 @@ typedef struct {
   const int32_t* len_dev;      /* optional [n] frame lengths (as sdx_pulse_batch.len_dev) */
   const int32_t* sel_dev;
   int32_t n, n_sel;
+  const int16_t* only_dev;     /* optional [n]: evaluate only MC protocol only[i] (table index; -1 = every
+                                * protocol) -- demodulate_mc(msg_data) with a protocol_id (sd_protocols.py:79) */
 } sdx_mc_batch;
 
 /* MN (FSK) batch: the hex characters of each frame (MN_PATTERN group 2, parser/mn.py:17) */
@@ -122,7 +124,7 @@ typedef struct {
                                 * aligned: spill regions of result-heavy tiles (112 KB each, see
                                 * sdx_pulses_work_bytes); without it a tile whose results overflow
                                 * LDS is re-run (ST_OVF_TILE) */
-  uint64_t work_cap;           /* bytes at work_dev */
+  uint64_t work_cap;           /* bytes at work_dev (< 4 GiB - 112 KB: spill offsets are 32-bit) */
 } sdx_out;
 
 typedef struct sdx_bank sdx_bank;
@@ -379,20 +381,60 @@ typedef struct {
 int sdx_units(const sdx_unit_batch* batch, const sdx_out* out, void* hip_stream);
 
 /* ---- multi-GPU exchange (BASELINE config 5) --------------------------------------
- * The packing step of the all-gather of decoded dmsg buffers (pysignalduino_amd/dist.py): one
- * launch copies K (<= 8) demodulation launches' descriptors, records and heap into the caller's
- * send buffer, re-basing them to the whole job (rec_begin += base_rec; payload_off += base_heap,
- * msg += base_msg).  Section offsets and heap_dev must be 16-byte aligned. */
+ * The all-gather of decoded dmsg buffers (pysignalduino_amd/dist.py) moves a WIRE form of each
+ * demodulation launch, per rank and in message order (the canonical order: the same bytes whether
+ * the stream ran sharded or not):
+ *   msg section   uint32 per message: n_rec | status << 16 | raise_kind << 24  (sdx_desc minus rec_begin)
+ *   rec section   sdx_wire_rec per record                                      (sdx_result minus payload_off, msg)
+ *   heap section  the payloads concatenated in record order
+ * rec_begin, payload_off and msg are prefix sums: sdx_exchange_unpack rebuilds them on the receiver.
+ * A rank's send buffer holds, for launch 0, 1, ..., K-1 in turn, its msg, rec and heap sections, each
+ * zero-padded to 16 bytes -- a layout that follows from the counts alone (dist.py _layout).
+ * Sender: sdx_exchange_count (device counts per launch + the layout), then sdx_exchange_pack into the
+ * send buffer, both without a host round trip; the host needs the counts only to size the collective.
+ * A message whose status is an overflow, or whose descriptor / records lie outside what the launch
+ * wrote (cursor clamped to the capacities), is counted in counts[3] ("bad") and shipped with n_rec 0
+ * and status SDX_ST_OVF_OUT: the caller must re-run such a launch instead of exchanging it. */
+#define SDX_XCHG_MAX_RANKS 32
 typedef struct {
-  const uint8_t* desc_dev;     /* sdx_desc[n_msgs] */
-  const uint8_t* rec_dev;      /* sdx_result[n_rec] */
-  const uint8_t* heap_dev;     /* n_heap payload bytes */
-  uint32_t n_msgs, n_rec, n_heap;
-  uint32_t base_msg, base_rec, base_heap;  /* the lower ranks' messages / records / heap bytes */
-  uint64_t off_desc, off_rec, off_heap;    /* section offsets in send_dev */
+  uint16_t proto;
+  uint16_t payload_len;
+  uint32_t bit_length;
+} sdx_wire_rec;
+
+typedef struct {
+  const uint8_t* desc_dev;     /* sdx_desc[n_msgs] of one demodulation launch */
+  const uint8_t* rec_dev;      /* its sdx_result records */
+  const uint8_t* heap_dev;     /* its payload heap */
+  const uint32_t* cursor_dev;  /* its cursor: [0] records, [1] heap bytes written (clamped to rec_cap / heap_cap) */
+  uint32_t n_msgs, rec_cap, heap_cap, res;
 } sdx_xchg_part;
 
-int sdx_exchange_pack(const sdx_xchg_part* parts, int k, uint8_t* send_dev, void* hip_stream);
+/* workspace of count + pack (kept between the two: 8 B per message + block sums + the layout);
+ * 256-byte aligned and ZEROED once at allocation (the kernels leave their counters at zero) */
+uint64_t sdx_exchange_work_bytes(const uint32_t* n_msgs, int k);
+/* send buffer capacity for any outcome of the launches (from their capacities) */
+uint64_t sdx_exchange_send_bytes(const sdx_xchg_part* parts, int k);
+/* counts_dev[4*i + 0..3] = messages, records, payload bytes, bad messages of launch i */
+int sdx_exchange_count(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, uint32_t* counts_dev,
+                       void* hip_stream);
+int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, uint8_t* send_dev,
+                      uint64_t send_cap, void* hip_stream);
+
+/* receiver: one launch's wire sections of every rank (rank order = global message order) -> the
+ * whole job's sdx_desc[sum n_msgs], sdx_result[sum n_rec] and one contiguous heap (sum n_heap bytes,
+ * heap_dev 4-byte aligned).  work_dev: sdx_exchange_unpack_work_bytes(total messages, total records),
+ * 64-byte aligned, zeroed once. */
+typedef struct {
+  const uint8_t* msg_dev;
+  const uint8_t* rec_dev;
+  const uint8_t* heap_dev;
+  uint32_t n_msgs, n_rec, n_heap, res;     /* n_heap: payload bytes (without the padding) */
+} sdx_xchg_wire;
+
+uint64_t sdx_exchange_unpack_work_bytes(uint32_t n_msgs, uint32_t n_rec);
+int sdx_exchange_unpack(const sdx_xchg_wire* ranks, int nranks, void* work_dev, uint64_t work_cap, sdx_desc* desc_dev,
+                        sdx_result* rec_dev, uint8_t* heap_dev, void* hip_stream);
 
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */
 #define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */

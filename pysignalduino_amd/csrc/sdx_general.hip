@@ -634,9 +634,10 @@ __global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, s
 // in global memory (LaneBits layout: word w of lane t at base[w * 256 + t])
 // ---------------------------------------------------------------------------------------------
 GD int mc_frame(const BankView& bv, const LaneBits& BN, const LaneBits& BI, int nN, int nI, bool hex_ok, int clock,
-                int mcbit, int flags, int mw, Sink& sk) {
+                int mcbit, int flags, int mw, int only, Sink& sk) {
   const int nmc = (int)bv.hdr->n_mc;
   for (int p = 0; p < nmc; ++p) {
+    if (only >= 0 && p != only) continue;
     const sdx_mc_proto* r = bv.mc + p;
     // gates of _demodulate_mc_data (manchester.py:70-89; clockrange fixed to [0] / [1])
     if (mcbit < (r->has_lmin ? r->lmin : -1)) continue;
@@ -720,8 +721,9 @@ __global__ __launch_bounds__(256) void k_mc_general(const void* __restrict__ ban
   for (int w = nI >> 6; w < mw; ++w) { bi[(size_t)w * 256] = (w == (nI >> 6)) ? wi : 0ull; }
   const LaneBits BN{bn, mw, false}, BI{bi, mw, false};
   const int clock = b.clock_dev[msg], mcbit = b.mcbitnum_dev[msg], flags = b.flags_dev[msg];
+  const int only = b.only_dev ? b.only_dev[msg] : -1;
   Sink sk{false, 0, 0u, out.rec_dev, out.heap_dev, 0u, 0u, (uint32_t)msg};
-  int raise = mc_frame(bv, BN, BI, nN, nI, hex_ok, clock, mcbit, flags, mw, sk);
+  int raise = mc_frame(bv, BN, BI, nN, nI, hex_ok, clock, mcbit, flags, mw, only, sk);
   sdx_desc d;
   d.rec_begin = 0;
   d.n_rec = 0;
@@ -736,7 +738,7 @@ __global__ __launch_bounds__(256) void k_mc_general(const void* __restrict__ ban
       atomicOr(&out.cursor_dev[2], 1u);
     } else {
       Sink sw{true, 0, 0u, out.rec_dev, out.heap_dev, rb, hb, (uint32_t)msg};
-      mc_frame(bv, BN, BI, nN, nI, hex_ok, clock, mcbit, flags, mw, sw);
+      mc_frame(bv, BN, BI, nN, nI, hex_ok, clock, mcbit, flags, mw, only, sw);
       d.rec_begin = rb;
       d.n_rec = (uint16_t)sw.nrec;
     }

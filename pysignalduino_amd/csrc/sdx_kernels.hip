@@ -127,7 +127,7 @@ constexpr int MATCH_CAP = 768;  // per tile in LDS (bench corpus: mean 290, max 
 constexpr uint32_t SPILL_M = 2048, SPILL_R = 2048, SPILL_H = 49152;
 constexpr uint32_t SPILL_OFF_R = SPILL_M * 16, SPILL_OFF_H = SPILL_OFF_R + SPILL_R * 16;
 constexpr uint32_t SPILL_BYTES = SPILL_OFF_H + SPILL_H;  // 112 KB
-constexpr uint32_t SPILL_NONE = 0xFFFFFFFFu, SPILL_PENDING = 0xFFFFFFFEu;
+constexpr uint32_t SPILL_NONE = 0xFFFFFFFFu, SPILL_PENDING = 0xFFFFFFFEu, SPILL_FULL = 0xFFFFFFFDu;
 constexpr uint32_t HEAP_SPILLED = 0x80000000u;  // StageRec.off: payload in the spill region
 constexpr uint8_t REC_HOLE = 0xFF;              // StageRec.msg: LDS slot left unused (result spilled)
 static_assert(sizeof(MuMatch) == 16, "MuMatch spill layout");
@@ -249,7 +249,19 @@ SDX_DEV uint32_t spill_region(T& L, const sdx_out& out) {
     if (lane_id() == leader) {
       uint32_t cur = atomicCAS(&L.spill_base, SPILL_NONE, SPILL_PENDING);
       if (cur == SPILL_NONE) {
-        cur = atomicAdd(&out.cursor_dev[3], SPILL_BYTES);
+        // claim a region with a CAS loop that stops at work_cap: the cursor never moves past the
+        // workspace, so it cannot wrap however many tiles ask (SPILL_FULL: exhausted)
+        uint32_t c = __hip_atomic_load(&out.cursor_dev[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+          if (!out.work_dev || (uint64_t)c + SPILL_BYTES > out.work_cap) {
+            c = SPILL_FULL;
+            break;
+          }
+          const uint32_t seen = atomicCAS(&out.cursor_dev[3], c, c + SPILL_BYTES);
+          if (seen == c) break;
+          c = seen;
+        }
+        cur = c;
         __hip_atomic_store(&L.spill_base, cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       while (cur == SPILL_PENDING) cur = __hip_atomic_load(&L.spill_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -257,7 +269,7 @@ SDX_DEV uint32_t spill_region(T& L, const sdx_out& out) {
     }
     b = (uint32_t)__shfl((int)b, leader);
   }
-  if (!out.work_dev || (uint64_t)b + SPILL_BYTES > out.work_cap) return SPILL_NONE;
+  if (b == SPILL_FULL || !out.work_dev || (uint64_t)b + SPILL_BYTES > out.work_cap) return SPILL_NONE;
   return b;
 }
 
@@ -2239,13 +2251,14 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   // hex -> bits for both polarities (helpers.py:168-188: leading zero nibbles are dropped)
   int nN = 0, nI = 0;
   bool hex_ok = false;
-  int clock = 0, mcbit = 0, flags = 0;
+  int clock = 0, mcbit = 0, flags = 0, only = -1;
   if (valid) {
     const int64_t off = b.offsets_dev[msg];
     const int hl = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
     clock = b.clock_dev[msg];
     mcbit = b.mcbitnum_dev[msg];
     flags = b.flags_dev[msg];
+    if (b.only_dev) only = b.only_dev[msg];
     hex_ok = hl > 0 && hl <= MW * 16;
     if constexpr (!LONG) {
       if (hex_ok) mc_stage_short(b.hex_dev + off, hl, &L.bn[tid], &L.bi[tid], &nN, &nI, &hex_ok);
@@ -2280,7 +2293,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   int raise = 0, mycnt = 0;
   for (int p = 0; p < nmc; ++p) {
     const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
-    bool go = valid && !raise;
+    bool go = valid && !raise && (only < 0 || only == p);
     // gates of _demodulate_mc_data (manchester.py:70-89; clockrange fixed to [0] / [1])
     if (go && mcbit < (cld(&r->has_lmin) ? cld(&r->lmin) : -1)) go = false;
     if (go && mcbit > (cld(&r->has_lmax) ? cld(&r->lmax) : 9999)) go = false;
@@ -2467,6 +2480,9 @@ int sdx_layout_size(int which) {
     case 9: return (int)sizeof(sdx_json_rec);
     case 10: return (int)sizeof(sdx_mu_filt);
     case 11: return (int)sizeof(sdx_ms_filt);
+    case 12: return (int)sizeof(sdx_xchg_part);
+    case 13: return (int)sizeof(sdx_xchg_wire);
+    case 14: return (int)sizeof(sdx_wire_rec);
   }
   return -1;
 }
@@ -2514,6 +2530,9 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
   if (kind != SDX_KIND_MU && kind != SDX_KIND_MS) return fail(SDX_EINVAL, "kind must be MU or MS");
   if (kind == SDX_KIND_MS && (!batch->cp_slot_dev || !batch->ms_ok_dev)) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+  // spill regions are addressed with 32-bit offsets (the workspace cursor is cursor_dev[3])
+  if (out->work_dev && out->work_cap > 0xFFFFFFFFull - sdx::SPILL_BYTES)
+    return fail(SDX_EINVAL, "work_cap above 4 GiB - 112 KB: spill offsets are 32-bit");
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
   if (ntot <= 0) return SDX_OK;
   hipStream_t st = (hipStream_t)hip_stream;

@@ -176,6 +176,13 @@ class LineBatch:
                 "flags": self.mcflags, "len": self.dlen, "n": self.n}
 
 
+def _contract(i: int, name) -> ContractError:
+    """The slot value of a line whose demodulation hit a device limit (SDX_RAISE_CONTRACT): not a
+    reference outcome, so it is reported, never turned into an empty result list."""
+    return ContractError(f"line {i} ({name}) exceeds a limit of the device's general path "
+                         "(include/sdx.h SDX_GEN_*, payloads > 65535 bytes)")
+
+
 def pack_lines(lines: Sequence[Union[str, bytes]]):
     """Concatenate lines into (data uint8, offsets int64[n+1]); per-line ContractError where a line
     cannot be represented (returned in ``bad``; such lines are replaced by an empty line)."""
@@ -294,6 +301,9 @@ class SignalParser:
                 continue
             desc, rec, _ = res[name]
             d = desc[i]
+            if d["status"] == runtime.ST_RAISED and int(d["raise_kind"]) == runtime.RAISE_CONTRACT:
+                out.append(_contract(i, name))   # a device limit (MC frames > 128 hex: k_mc_general)
+                continue
             if d["status"] == runtime.ST_RAISED or int(d["n_rec"]) == 0:
                 out.append([])  # a demodulator exception is caught by the reference's parsers
                 continue
@@ -323,6 +333,8 @@ class SignalParser:
     def _general_messages(self, line, i, plen, offsets, slot, meta, name, d, rec, hb, ms_clock) -> List[DecodedMessage]:
         """The DecodedMessage list of a general-path line (as the OK lines' records below)."""
         bk = self.protocols._bank
+        if d["status"] == runtime.ST_RAISED and int(d["raise_kind"]) == runtime.RAISE_CONTRACT:
+            return _contract(i, name)   # a general-path limit (SDX_GEN_*), not a reference outcome
         if d["status"] == runtime.ST_RAISED or int(d["n_rec"]) == 0:
             return []   # a demodulator exception is caught by the reference's parsers
         if d["status"] != runtime.ST_OK:

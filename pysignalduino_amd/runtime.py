@@ -37,7 +37,8 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
             "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
-            "sdx_exchange_pack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
+            "sdx_exchange_work_bytes", "sdx_exchange_send_bytes", "sdx_exchange_count", "sdx_exchange_pack", "sdx_exchange_unpack_work_bytes",
+            "sdx_exchange_unpack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
             "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general",
             "sdx_lines_general"]
 GROUP_MIN = 4096   # SDX_GROUP_MIN
@@ -64,7 +65,7 @@ class SdxLinesGeneralOut(Structure):
 class SdxMcBatch(Structure):
     _fields_ = [("hex_dev", c_void_p), ("offsets_dev", c_void_p), ("clock_dev", c_void_p),
                 ("mcbitnum_dev", c_void_p), ("flags_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p),
-                ("n", c_int32), ("n_sel", c_int32)]
+                ("n", c_int32), ("n_sel", c_int32), ("only_dev", c_void_p)]
 
 
 class SdxMnBatch(Structure):
@@ -89,10 +90,18 @@ class SdxUnitBatch(Structure):
 
 
 class SdxXchgPart(Structure):
-    _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("n_msgs", c_uint32),
-                ("n_rec", c_uint32), ("n_heap", c_uint32), ("base_msg", c_uint32), ("base_rec", c_uint32),
-                ("base_heap", c_uint32), ("off_desc", ctypes.c_uint64), ("off_rec", ctypes.c_uint64),
-                ("off_heap", ctypes.c_uint64)]
+    _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("cursor_dev", c_void_p),
+                ("n_msgs", c_uint32), ("rec_cap", c_uint32), ("heap_cap", c_uint32), ("res", c_uint32)]
+
+
+class SdxXchgWire(Structure):
+    _fields_ = [("msg_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("n_msgs", c_uint32),
+                ("n_rec", c_uint32), ("n_heap", c_uint32), ("res", c_uint32)]
+
+
+# the exchange's wire form (include/sdx.h): one word per message, 8 bytes per record, packed payloads
+WIRE_REC_DT = np.dtype([("proto", "<u2"), ("payload_len", "<u2"), ("bit_length", "<u4")])
+XCHG_MAX_RANKS = 32
 
 
 class SdxOut(Structure):
@@ -175,9 +184,21 @@ def load_library(path: Optional[str] = None):
     lib.sdx_select_lines.restype = c_int
     lib.sdx_units.argtypes = [POINTER(SdxUnitBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_units.restype = c_int
-    lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, c_void_p]
+    lib.sdx_exchange_work_bytes.argtypes = [c_void_p, c_int]
+    lib.sdx_exchange_work_bytes.restype = ctypes.c_uint64
+    lib.sdx_exchange_send_bytes.argtypes = [POINTER(SdxXchgPart), c_int]
+    lib.sdx_exchange_send_bytes.restype = ctypes.c_uint64
+    lib.sdx_exchange_count.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p]
+    lib.sdx_exchange_count.restype = c_int
+    lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p,
+                                      ctypes.c_uint64, c_void_p]
     lib.sdx_exchange_pack.restype = c_int
-    if lib.sdx_abi_version() != 7:
+    lib.sdx_exchange_unpack_work_bytes.argtypes = [c_uint32, c_uint32]
+    lib.sdx_exchange_unpack_work_bytes.restype = ctypes.c_uint64
+    lib.sdx_exchange_unpack.argtypes = [POINTER(SdxXchgWire), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
+                                        c_void_p, c_void_p]
+    lib.sdx_exchange_unpack.restype = c_int
+    if lib.sdx_abi_version() != 8:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -190,7 +211,8 @@ def check_layout(lib) -> None:
     want = {0: struct.calcsize(bankmod.HDR_FMT), 1: bankmod.PATSPEC.itemsize, 2: bankmod.MU_REC.itemsize, 3: bankmod.MS_REC.itemsize,
             4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize,
             8: bankmod.MN_REC.itemsize, 9: bankmod.JSON_REC.itemsize, 10: bankmod.MU_FILT.itemsize,
-            11: bankmod.MS_FILT.itemsize}
+            11: bankmod.MS_FILT.itemsize, 12: ctypes.sizeof(SdxXchgPart), 13: ctypes.sizeof(SdxXchgWire),
+            14: WIRE_REC_DT.itemsize}
     for k, v in want.items():
         got = lib.sdx_layout_size(k)
         if got != v:
@@ -272,7 +294,9 @@ class Engine:
         """Workspace of an MU/MS launch over n messages: spill room for `spill_frac` of its
         64-message tiles (a grouped order makes tiles of result-heavy messages)."""
         tiles = (n + 63) // 64
-        return int(self.lib.sdx_pulses_work_bytes(int(max(16, spill_frac * tiles))))
+        region = int(self.lib.sdx_pulses_work_bytes(1))
+        most = (2 ** 32 - 2 * region) // region          # spill offsets are 32-bit (include/sdx.h)
+        return int(self.lib.sdx_pulses_work_bytes(int(min(most, max(16, spill_frac * tiles)))))
 
     def group_buffers(self, n: int):
         """(order, work) device buffers for sdx_group_pulses over n messages."""
@@ -338,7 +362,7 @@ class Engine:
     def launch_mc(self, bd, out, sel=None) -> None:
         b = SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
                        _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"],
-                       0 if sel is None else int(sel.numel()))
+                       0 if sel is None else int(sel.numel()), _ptr(bd.get("only")))
         o = self._out_struct(out)
         _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 
@@ -347,7 +371,8 @@ class Engine:
         wb = int(self.lib.sdx_mc_general_work_bytes(int(sel.numel()), int(max_hex)))
         work = self.torch.empty(max(wb, 1), dtype=self.torch.uint8, device=self.dev)
         b = SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
-                       _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"], int(sel.numel()))
+                       _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"], int(sel.numel()),
+                       _ptr(bd.get("only")))
         o = self._out_struct(out)
         o.work_dev, o.work_cap = _ptr(work), wb
         _check(self.lib, self.lib.sdx_demod_mc_general(self.handle, ctypes.byref(b), int(max_hex), ctypes.byref(o),

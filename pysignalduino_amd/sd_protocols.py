@@ -443,9 +443,16 @@ class SDProtocols(UnitsMixin):
                 frames.append(("", 0, 0, "MC", None))
         mb = packing.mc_batch_from_frames(frames)
         eng = self._ensure()
-        desc, rec, heap = eng.run(runtime.KIND_MC, eng.to_device_mc(mb))
-        only = [m.get("protocol_id") for m in messages]
         bk = self._bank
+        bd = eng.to_device_mc(mb)
+        # demodulate_mc(msg_data) with a protocol_id evaluates that protocol only (sd_protocols.py:
+        # 79-99): a raise of another id must not surface for it, so the device skips the others
+        only = [m.get("protocol_id") for m in messages]
+        if any(only):
+            idx = {str(p): i for i, p in enumerate(bk.mc_pids)}
+            sel_only = np.array([-1 if not o else idx.get(str(o), len(bk.mc_pids)) for o in only], np.int16)
+            bd["only"] = eng.torch.from_numpy(sel_only).to(eng.dev)
+        desc, rec, heap = eng.run(runtime.KIND_MC, bd)
         hb = heap.tobytes()
         out: List[Any] = []
         for i in range(len(desc)):
@@ -466,8 +473,6 @@ class SDProtocols(UnitsMixin):
             res = []
             for r in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
                 pid = bk.mc_pids[int(r["proto"])]
-                if only[i] and pid != only[i]:
-                    continue
                 off = int(r["payload_off"])
                 res.append({"protocol_id": str(pid), "payload": hb[off: off + int(r["payload_len"])].decode("latin-1"),
                             "meta": {"protocol_id": pid, "rssi": None, "freq_afc": None}})

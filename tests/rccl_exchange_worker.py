@@ -4,7 +4,7 @@ Runs the pipelined dist.Exchange the bench uses for N > 1 over a real RCCL ("ncc
 group of world size 1 on cuda:0: two steps of MU + MC launches into double-buffered outputs,
 each step's exchange (count all-gather, sdx_exchange_pack, data all-gather on the exchange
 stream) overlapping the next step's kernels.  At world size 1 the gathered buffers must equal
-the rank's own outputs byte for byte (re-basing by zero lower ranks).  Prints "OK" on success.
+the rank's own outputs in canonical form (dist.canonical) byte for byte.  Prints "OK" on success.
 """
 import os
 import sys
@@ -49,13 +49,12 @@ def main():
     for j, got in enumerate(snaps):
         o = outs[j % 2]
         for (gd, gr, gh), k in zip(got, ("MU", "MC")):
-            cur = o[k]["cursor"].cpu()
-            nrec, nheap = int(cur[0]), int(cur[1])
-            assert nrec > 0, f"step {j} {k}: no results"
-            n = bds[k]["n"]
-            assert torch.equal(gd, o[k]["desc"][: n * runtime.DESC_DT.itemsize]), f"step {j} {k}: desc differs"
-            assert torch.equal(gr, o[k]["rec"][: nrec * runtime.RES_DT.itemsize]), f"step {j} {k}: records differ"
-            assert torch.equal(gh, o[k]["heap"][:nheap]), f"step {j} {k}: heap differs"
+            d, r, h = eng.fetch(o[k])
+            assert len(r) > 0, f"step {j} {k}: no results"
+            cd, cr, ch = sdist.canonical(d, r, h)
+            assert gd.cpu().numpy().tobytes() == cd.tobytes(), f"step {j} {k}: desc differs"
+            assert gr.cpu().numpy().tobytes() == cr.tobytes(), f"step {j} {k}: records differ"
+            assert gh.cpu().numpy().tobytes() == ch.tobytes(), f"step {j} {k}: heap differs"
     dist.destroy_process_group()
     print("OK", flush=True)
 

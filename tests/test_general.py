@@ -119,3 +119,4 @@ def test_general_very_long_messages_vs_oracle(proto, kind):
         assert _flat(g) == exp, (len(m["data"]), _flat(g).get("raise"), exp.get("raise"))
         nres += len(exp.get("results", []))
     assert nres > (100 if kind == "MU" else 0)
+

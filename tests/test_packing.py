@@ -40,3 +40,24 @@ def test_contract_and_reference_exceptions():
 def test_non_ascii_digits_keep_isdigit():
     assert packing._encode_data("01٣") == b"01\xfe"
     assert packing._encode_data("01é") == b"01\xff"
+
+
+def test_frontend_contract_raise_is_reported():
+    """SDX_RAISE_CONTRACT (a general-path device limit, include/sdx.h) is not a reference outcome:
+    the front end reports it as a ContractError in the line's slot instead of the empty list a
+    reference-caught exception gives (host logic; the device side is covered by test_general.py)."""
+    import types
+
+    import numpy as np
+
+    from pysignalduino_amd import runtime
+    from pysignalduino_amd.frontend import SignalParser
+    sp = SignalParser.__new__(SignalParser)
+    sp.protocols = types.SimpleNamespace(_bank=None)
+    d = np.zeros(1, runtime.DESC_DT)[0]
+    d["status"] = runtime.ST_RAISED
+    d["raise_kind"] = runtime.RAISE_CONTRACT
+    got = sp._general_messages(b"", 3, None, None, None, None, "MU", d, None, b"", 0.0)
+    assert isinstance(got, packing.ContractError)
+    d["raise_kind"] = 1   # IndexError: caught by the reference's MUParser -> no messages
+    assert sp._general_messages(b"", 3, None, None, None, None, "MU", d, None, b"", 0.0) == []

@@ -371,3 +371,31 @@ def test_gpu_zero_padded_pattern_keys_and_per_message_contract(proto, golden):
             assert type(g) is type(e)
             continue
         assert [(r["protocol_id"], r["payload"]) for r in g] == exp
+
+
+@pytest.mark.gpu
+def test_gpu_mc_fixed_protocol_id_evaluates_only_that_id(obank):
+    """Fixed-mode demodulate_mc(msg_data) with a protocol_id runs that protocol only
+    (sd_protocols.py:79-99): on a user-modified bank where id 57 (helpers.mcraw, which raises
+    TypeError) overlaps TFA (58), a 58 frame raises without an id but decodes with protocol_id 58."""
+    from pysignalduino_amd import synth
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    p = SDProtocols(mc_mode="fixed")
+    P = p.get_protocol_list()
+    frames = [f for f in synth.mc_planted_frames(P, 600, seed=9) if 460 < f[1] < 520 and f[2] == 52][:40]
+    assert frames
+    p._protocols["57"]["clockrange"] = [300, 600]
+    p._protocols["57"]["length_max"] = "60"
+    msgs = [{"raw_hex": h, "clock": c, "mcbitnum": L, "messagetype": t, "version": v} for h, c, L, t, v in frames]
+    got_all = p.demodulate_mc_batch(msgs)
+    assert all(isinstance(g, TypeError) for g in got_all), got_all[:3]
+    got = p.demodulate_mc_batch([dict(m, protocol_id="58") for m in msgs])
+    n_ok = 0
+    for (h, c, L, t, v), g in zip(frames, got):
+        exp = O.demod_mc_fixed_one(obank, "58", h, c, L, t, v)
+        assert g == ([exp] if exp is not None else []), (h, g, exp)
+        n_ok += exp is not None
+    assert n_ok > 0
+    assert p.demodulate_mc(dict(msgs[0], protocol_id="58"), "MC") == got[0]
+    # an id outside the MC table: nothing, and no raise from the others
+    assert p.demodulate_mc_batch([dict(msgs[0], protocol_id="0")]) == [[]]
