@@ -118,7 +118,7 @@ typedef struct {
   sdx_result* rec_dev;         /* [rec_cap] */
   uint8_t* heap_dev;           /* [heap_cap] */
   uint32_t* cursor_dev;        /* [4] zeroed by the caller before the first launch: rec, heap, ovf,
-                                * workspace bytes taken */
+                                * spill regions handed out (including refused ones past work_cap) */
   uint32_t rec_cap, heap_cap;
   uint8_t* work_dev;           /* optional device workspace (MU/MS short variant, NULL = none), 256-B
                                 * aligned: spill regions of result-heavy tiles (112 KB each, see
@@ -173,10 +173,11 @@ int sdx_demod_mn(const sdx_bank* bank, const sdx_mn_batch* batch, const sdx_out*
  * pattern_utils.py:120-130), more than 10 patterns, and more than SDX_LONG_MAX pulses.  The
  * reference's string semantics run as they are: candidate targets are character strings, MU's
  * re.finditer over (?:start)((?:u1|u2|..){length_min,}(?:e1|..)?) is emulated with Python sre's
- * backtracking order, chunks are sliced by characters.  Lane = message, serial over the bank in
- * bank order; every result list is counted, reserved (one atomic pair per message) and written in
- * a second pass.  out->work_dev must hold sdx_general_work_bytes(offsets[n], n) bytes (per message
- * scratch for bit lists and payload text).  Limits (status SDX_ST_RAISED + SDX_RAISE_CONTRACT when
+ * backtracking order, chunks are sliced by characters.  A wave walks a chunk of the bank (a few
+ * protocols in bank order) for one message, the chunks of a message run on separate waves (the
+ * first raise in bank order decides, as in the reference); every result list is counted, reserved
+ * (one atomic pair per message) and written in a second pass.  out->work_dev must hold
+ * sdx_general_work_bytes(...) bytes.  Limits (status SDX_ST_RAISED + SDX_RAISE_CONTRACT when
  * exceeded): SDX_GEN_MAXPAT patterns of <= 15 digits, target strings of <= SDX_GEN_STRMAX
  * characters, length_min <= SDX_GEN_REPMAX, 2^22 sre steps per repetition match, payloads of
  * <= 65535 bytes. */
@@ -195,11 +196,16 @@ typedef struct {
   const int32_t* sel_dev;      /* optional [n_sel] subset to run, NULL = all */
   int32_t n, n_sel;
   const int32_t* len_dev;      /* optional [n] lengths: message i = data[offsets[i], +len[i]) (slot layout) */
-  int64_t work_stride;         /* > 0: the j-th message run takes scratch at work_dev + j * work_stride
-                                * (>= 5 * (its length + 512)); 0: sdx_general_work_bytes layout */
+  int64_t work_stride;         /* > 0: the j-th message run takes its region at j * work_stride
+                                * (>= 5 * (max_len + 512)); 0: regions by offsets (5 * offsets[i] + 2560 * i) */
+  int32_t max_len;             /* the longest message run (characters): per-wave scratch and LDS sizing */
+  int32_t res;
 } sdx_general_batch;
 
-uint64_t sdx_general_work_bytes(int64_t total_chars, int32_t n);
+/* workspace of a general-path launch of n messages (sel'd or not): a head (work queue counters, the
+ * per (message, chunk of protocols) table, per-wave scratch) and the per-message regions */
+uint64_t sdx_general_work_bytes(const sdx_bank* bank, int kind, int64_t total_chars, int32_t n, int32_t max_len,
+                                int64_t work_stride);
 int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_batch* batch, const sdx_out* out,
                              void* hip_stream);
 /* MC frames of any length (the "fixed" chain of sdx_demod_mc without its SDX_MC_HEX_MAX limit): lane =
@@ -418,8 +424,9 @@ uint64_t sdx_exchange_send_bytes(const sdx_xchg_part* parts, int k);
 /* counts_dev[4*i + 0..3] = messages, records, payload bytes, bad messages of launch i */
 int sdx_exchange_count(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, uint32_t* counts_dev,
                        void* hip_stream);
-int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, uint8_t* send_dev,
-                      uint64_t send_cap, void* hip_stream);
+/* after sdx_exchange_count on the same stream (reads its counts_dev and workspace) */
+int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, const uint32_t* counts_dev,
+                      uint8_t* send_dev, uint64_t send_cap, void* hip_stream);
 
 /* receiver: one launch's wire sections of every rank (rank order = global message order) -> the
  * whole job's sdx_desc[sum n_msgs], sdx_result[sum n_rec] and one contiguous heap (sum n_heap bytes,

@@ -8,20 +8,19 @@
 // per message instead of 8 + 16 * records + the (padded) heap.
 //
 // Sender, two launches around the host's count exchange:
-//   k_xw_count  lane = 4 consecutive messages: validate each descriptor and its records against the
-//               launch's cursor / capacities, count records and payload bytes, block-scan them
-//               (per-message local prefixes into the workspace); the last block of a launch to
-//               finish scans the block totals and publishes the launch's counts (no inter-block
-//               waiting: a block that is not last just leaves).
-//   k_xw_pack   lane = message (its wire word) and lane = source record (its wire record at the
-//               message's prefix + its rank in the message, and its payload bytes).  The source
+//   k_xw_count  lane = message: validate the descriptor and its records against the launch's
+//               cursor / capacities, count records and payload bytes, block-scan them (per-message
+//               local prefixes into the workspace), block totals;
+//   k_xw_scan   one block per launch: exclusive block offsets, the launch's counts;
+//   k_xw_pack   block = the count block's 256 messages: wire words and wire records (lane =
+//               message), then the payloads as coalesced dwords (lane = output dword).  The source
 //               records are in tile order (k_pulses places them per tile); the wire is in message
 //               order, so the pack is also the canonicalisation that makes sharded and un-sharded
 //               runs compare byte for byte.
 // Receiver:
-//   k_xu_scan / k_xu_write  rebuild sdx_desc / sdx_result / one contiguous heap of the whole job from
-//               the gathered wire sections of every rank (the same last-block scan, over the
-//               rank-concatenated messages and records).
+//   k_xu_sum / k_xu_scan / k_xu_write  rebuild sdx_desc / sdx_result / one contiguous heap of the whole
+//               job from the gathered wire sections of every rank (the same block-sum / scan / apply
+//               passes over the rank-concatenated messages and records).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,18 +34,20 @@ int set_error(int code, const std::string& msg);  // sdx_kernels.hip
 
 namespace sdxx {
 
-constexpr int XT = 256;       // threads per block
-constexpr int IPT = 1;        // items per thread in the scans (one message: its loads all in flight)
-constexpr int XB = XT * IPT;  // items per block
+constexpr int XT = 256;       // threads per block; one message per thread in the scans
+constexpr int XB = XT;        // items per block
 constexpr int XMAX = 8;       // launches per exchange
 constexpr int XRANKS = SDX_XCHG_MAX_RANKS;
+constexpr int LREC = 1536;    // records of a pack block staged in LDS for the coalesced payload copy
 constexpr uint64_t BADBIT = 1ull << 63;
+
+// Inter-block results travel through kernel boundaries only (count -> scan -> pack): a grid-wide
+// "last block" protocol needs agent-scope release fences, and on a multi-XCD part each one writes
+// back the whole L2 -- under a concurrently running demodulation kernel that cost ~100 us per launch.
 
 __host__ __device__ inline uint32_t nblk_of(uint64_t n) { return n ? (uint32_t)((n + XB - 1) / XB) : 1u; }
 __host__ __device__ inline uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
-// workspace: header (256 B: launches done, the send layout) | per launch: [ctr, bad, tot[2]] (64 B),
-// loc u64[n], blk u64[nblk]
-constexpr uint64_t HDR = 256;
+// per-launch workspace: [bad, records, bytes, -] (64 B) | loc u64[n] | blk u64[nblk]
 __host__ __device__ inline uint64_t part_work_bytes(uint32_t n) {
   return (64 + 8ull * n + 8ull * nblk_of(n) + 255) / 256 * 256;
 }
@@ -57,27 +58,18 @@ struct Parts {
   int k;
 };
 
-struct Hdr {
-  uint32_t done;             // launches whose count finished (reset by the last)
-  uint32_t res;
-  uint64_t off[XMAX][3];     // the send layout: msg / rec / heap section offsets per launch
-  uint64_t total;
-};
-
 struct PartWork {
-  uint32_t* ctr;   // blocks done (reset by the last block)
-  uint32_t* bad;   // bad messages (reset by the last block)
-  uint32_t* tot;   // [2]: records, payload bytes of the launch (read by k_xw_pack)
-  uint64_t* loc;   // per message: BADBIT | local record prefix << 32 | local byte prefix
+  uint32_t* bad;   // bad messages (reset by k_xw_scan)
+  uint32_t* tot;   // [2]: records, payload bytes of the launch (written by k_xw_scan)
+  uint64_t* loc;   // per message: BADBIT | local record prefix << 32 | local byte prefix (in its block)
   uint64_t* blk;   // block totals -> exclusive block offsets (records << 32 | bytes)
 };
 
 __device__ inline PartWork part_work(uint8_t* work, uint64_t off, uint32_t n) {
   PartWork w;
-  uint8_t* b = work + HDR + off;
-  w.ctr = reinterpret_cast<uint32_t*>(b);
-  w.bad = w.ctr + 1;
-  w.tot = w.ctr + 2;
+  uint8_t* b = work + off;
+  w.bad = reinterpret_cast<uint32_t*>(b);
+  w.tot = w.bad + 1;
   w.loc = reinterpret_cast<uint64_t*>(b + 64);
   w.blk = w.loc + n;
   return w;
@@ -115,32 +107,18 @@ __device__ inline uint64_t block_excl(uint64_t v, uint64_t* total) {
   return base + inc - v;
 }
 
-// in-place exclusive scan of blk[0, nb) by one block (after an acquire fence); returns the sum
+// in-place exclusive scan of blk[0, nb) by one block; returns the sum
 __device__ inline uint64_t block_scan_array(uint64_t* blk, uint32_t nb) {
   uint64_t carry = 0;
   for (uint32_t c = 0; c < nb; c += XT) {
     const uint32_t i = c + threadIdx.x;
-    const uint64_t v = i < nb ? __hip_atomic_load(&blk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const uint64_t v = i < nb ? blk[i] : 0;
     uint64_t tot;
     const uint64_t ex = block_excl(v, &tot);
     if (i < nb) blk[i] = carry + ex;
     carry += tot;
   }
   return carry;
-}
-
-// last-block protocol: publish this block's total, count the block in; true in every thread of the
-// block that finished last (which then sees every block's total after its acquire fence)
-__device__ inline bool arrive_last(uint64_t* blk_slot, uint64_t total, uint32_t* ctr, uint32_t nb) {
-  __shared__ bool s_last;
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(blk_slot, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();
-    s_last = atomicAdd(ctr, 1u) == nb - 1;
-  }
-  __syncthreads();
-  if (s_last) __threadfence();
-  return s_last;
 }
 
 __device__ inline void clamp_counts(const sdx_xchg_part& x, uint32_t* nrec_c, uint32_t* nheap_c) {
@@ -173,73 +151,53 @@ __device__ inline uint64_t msg_counts(const sdx_xchg_part& x, uint32_t nrec_c, u
   return good ? (((uint64_t)d.n_rec << 32) | bytes) : 0;
 }
 
-// the send layout, in launch order: [msg | rec | heap] sections of each launch, 16-byte aligned
-__device__ inline void make_layout(Hdr* h, const uint32_t* counts, int K) {
-  uint64_t off = 0;
-  for (int k = 0; k < K; ++k) {
-    h->off[k][0] = off;
-    off += r16(4ull * counts[4 * k]);
-    h->off[k][1] = off;
-    off += r16(8ull * counts[4 * k + 1]);
-    h->off[k][2] = off;
-    off += r16(counts[4 * k + 2]);
-  }
-  h->total = off;
-}
-
-__global__ __launch_bounds__(XT) void k_xw_count(Parts P, uint8_t* __restrict__ work, uint32_t* __restrict__ counts) {
+// lane = message: validate, count, block-local prefixes; block totals for k_xw_scan
+__global__ __launch_bounds__(XT) void k_xw_count(Parts P, uint8_t* __restrict__ work) {
   const int k = blockIdx.y;
   const sdx_xchg_part& x = P.p[k];
-  const uint32_t nb = nblk_of(x.n_msgs);
-  if (blockIdx.x >= nb) return;
+  if (blockIdx.x >= nblk_of(x.n_msgs)) return;
   PartWork w = part_work(work, P.work_off[k], x.n_msgs);
   uint32_t nrec_c, nheap_c;
   clamp_counts(x, &nrec_c, &nheap_c);
   const uint32_t m = blockIdx.x * XB + threadIdx.x;
   bool ok = true;
-  uint64_t v = m < x.n_msgs ? msg_counts(x, nrec_c, nheap_c, m, &ok) : 0;
+  const uint64_t v = m < x.n_msgs ? msg_counts(x, nrec_c, nheap_c, m, &ok) : 0;
   uint64_t tot;
   const uint64_t pre = block_excl(v, &tot);
   if (m < x.n_msgs) w.loc[m] = pre | (ok ? 0 : BADBIT);
   const uint64_t bad_wave = __ballot(!ok);
   if (lane_id() == 0 && bad_wave) atomicAdd(w.bad, (uint32_t)__popcll(bad_wave));
-  if (!arrive_last(&w.blk[blockIdx.x], tot, w.ctr, nb)) return;
-  const uint64_t all = block_scan_array(w.blk, nb);
-  __shared__ bool s_lastk;
+  if (threadIdx.x == 0) w.blk[blockIdx.x] = tot;
+}
+
+// one block per launch: block offsets, the launch's counts
+__global__ __launch_bounds__(XT) void k_xw_scan(Parts P, uint8_t* __restrict__ work, uint32_t* __restrict__ counts) {
+  const int k = blockIdx.x;
+  const sdx_xchg_part& x = P.p[k];
+  PartWork w = part_work(work, P.work_off[k], x.n_msgs);
+  const uint64_t all = block_scan_array(w.blk, nblk_of(x.n_msgs));
   if (threadIdx.x == 0) {
-    const uint32_t bd = __hip_atomic_load(w.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     w.tot[0] = (uint32_t)(all >> 32);
     w.tot[1] = (uint32_t)all;
     counts[4 * k + 0] = x.n_msgs;
     counts[4 * k + 1] = (uint32_t)(all >> 32);
     counts[4 * k + 2] = (uint32_t)all;
-    counts[4 * k + 3] = bd;
+    counts[4 * k + 3] = *w.bad;
     *w.bad = 0;
-    *w.ctr = 0;
-    // the launch that finishes last lays out the send buffer from every launch's counts
-    Hdr* h = reinterpret_cast<Hdr*>(work);
-    __threadfence();
-    s_lastk = atomicAdd(&h->done, 1u) == (uint32_t)P.k - 1;
-    if (s_lastk) {
-      __threadfence();
-      uint32_t c[4 * XMAX];
-      for (int i = 0; i < 4 * P.k; ++i) c[i] = __hip_atomic_load(&counts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      make_layout(h, c, P.k);
-      h->done = 0;
-    }
   }
 }
 
-// copy n payload bytes (arbitrary alignment on both sides): 16 independent byte loads in flight per
-// step, then their stores
-__device__ inline void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n) {
-  for (uint32_t c = 0; c < n; c += 16) {
-    uint8_t b[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) b[i] = c + i < n ? src[c + i] : 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (c + i < n) dst[c + i] = b[i];
+// the send layout, in launch order: [msg | rec | heap] sections of each launch, 16-byte aligned
+__device__ inline void section_offsets(const uint32_t* counts, int K, int k, uint64_t* o) {
+  uint64_t off = 0;
+  for (int i = 0; i < K; ++i) {
+    if (i == k) {
+      o[0] = off;
+      o[1] = off + r16(4ull * counts[4 * i]);
+      o[2] = o[1] + r16(8ull * counts[4 * i + 1]);
+      return;
+    }
+    off += r16(4ull * counts[4 * i]) + r16(8ull * counts[4 * i + 1]) + r16(counts[4 * i + 2]);
   }
 }
 
@@ -247,38 +205,50 @@ __device__ inline void zero_tail(uint8_t* sec, uint64_t used, uint32_t lane) {
   if (lane < 16 && used + lane < r16(used)) sec[used + lane] = 0;
 }
 
-// lane = message (grid-stride), grid.y = launch: the message's wire word, its records (contiguous in
-// the source, from rec_begin) as wire records at its record prefix, its payloads at its byte prefix
-__global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
+// block = 256 consecutive messages (the count blocks), grid.y = launch.
+// A (lane = message): the wire word, the wire records (contiguous per message) and the message's
+//   records' (source, destination, length) into an LDS list in output order;
+// B (lane = output dword of the block's payload range): the payload bytes, gathered through the
+//   list (binary search for the first byte's record), stored as coalesced dwords (byte stores only
+//   at the two ends of the range, which neighbouring blocks share).
+__global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restrict__ counts,
+                                                uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
+  __shared__ uint32_t l_src[LREC], l_dst[LREC];
+  __shared__ uint16_t l_len[LREC];
   const int k = blockIdx.y;
   const sdx_xchg_part& x = P.p[k];
-  const Hdr* h = reinterpret_cast<const Hdr*>(work);
-  PartWork w = part_work(const_cast<uint8_t*>(work), P.work_off[k], x.n_msgs);
-  uint8_t* s_msg = send + h->off[k][0];
-  sdx_wire_rec* s_rec = reinterpret_cast<sdx_wire_rec*>(send + h->off[k][1]);
-  uint8_t* s_heap = send + h->off[k][2];
-  const uint32_t g0 = blockIdx.x * XT + threadIdx.x;
+  const uint32_t nb = nblk_of(x.n_msgs);
+  if (blockIdx.x >= nb) return;
+  PartWork w = part_work(work, P.work_off[k], x.n_msgs);
+  uint64_t so[3];
+  section_offsets(counts, P.k, k, so);
+  uint8_t* s_msg = send + so[0];
+  sdx_wire_rec* s_rec = reinterpret_cast<sdx_wire_rec*>(send + so[1]);
+  uint8_t* s_heap = send + so[2];
   if (blockIdx.x == 0) {  // deterministic section padding
     zero_tail(s_msg, 4ull * x.n_msgs, threadIdx.x);
-    zero_tail(reinterpret_cast<uint8_t*>(s_rec), 8ull * w.tot[0], threadIdx.x);
-    zero_tail(s_heap, w.tot[1], threadIdx.x);
+    zero_tail(reinterpret_cast<uint8_t*>(s_rec), 8ull * counts[4 * k + 1], threadIdx.x);
+    zero_tail(s_heap, counts[4 * k + 2], threadIdx.x);
   }
-  const sdx_desc* desc = reinterpret_cast<const sdx_desc*>(x.desc_dev);
-  const sdx_result* rec = reinterpret_cast<const sdx_result*>(x.rec_dev);
-  for (uint32_t m = g0; m < x.n_msgs; m += gridDim.x * XT) {
-    const sdx_desc d = desc[m];
+  const uint64_t boff = w.blk[blockIdx.x];
+  const uint64_t bnext = blockIdx.x + 1 < nb ? w.blk[blockIdx.x + 1]
+                                             : (((uint64_t)counts[4 * k + 1] << 32) | counts[4 * k + 2]);
+  const uint32_t brec = (uint32_t)((bnext >> 32) - (boff >> 32));   // the block's records
+  const uint32_t m = blockIdx.x * XB + threadIdx.x;
+  if (m < x.n_msgs) {
+    const sdx_desc d = reinterpret_cast<const sdx_desc*>(x.desc_dev)[m];
     const uint64_t loc = w.loc[m];
-    const uint64_t base = w.blk[m / XB] + (loc & ~BADBIT);
     const bool bad = (loc & BADBIT) != 0;
     const uint32_t nr = (bad || d.status != SDX_ST_OK) ? 0u : d.n_rec;
     reinterpret_cast<uint32_t*>(s_msg)[m] =
         nr | ((uint32_t)(bad ? SDX_ST_OVF_OUT : d.status) << 16) | ((uint32_t)d.raise_kind << 24);
-    uint32_t ri = (uint32_t)(base >> 32), byte = (uint32_t)base;
+    const sdx_result* rec = reinterpret_cast<const sdx_result*>(x.rec_dev) + d.rec_begin;
+    uint32_t lr = (uint32_t)((loc & ~BADBIT) >> 32), lb = (uint32_t)loc;   // block-local
     for (uint32_t j = 0; j < nr; j += 4) {
       sdx_result r4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (j + i < nr) r4[i] = rec[d.rec_begin + j + i];
+        if (j + i < nr) r4[i] = rec[j + i];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (j + i >= nr) break;
@@ -286,10 +256,54 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint8_t* __restri
         o.proto = r4[i].proto;
         o.payload_len = r4[i].payload_len;
         o.bit_length = r4[i].bit_length;
-        s_rec[ri++] = o;
-        copy_bytes(s_heap + byte, x.heap_dev + r4[i].payload_off, r4[i].payload_len);
-        byte += r4[i].payload_len;
+        s_rec[(uint32_t)(boff >> 32) + lr] = o;
+        if (lr < LREC) {
+          l_src[lr] = r4[i].payload_off;
+          l_dst[lr] = lb;
+          l_len[lr] = r4[i].payload_len;
+        } else {  // past the LDS list (a block of unusually many records): copy here, byte by byte
+          uint8_t* dst = s_heap + (uint32_t)boff + lb;
+          const uint8_t* src = x.heap_dev + r4[i].payload_off;
+          for (uint32_t b = 0; b < r4[i].payload_len; ++b) dst[b] = src[b];
+        }
+        ++lr;
+        lb += r4[i].payload_len;
       }
+    }
+  }
+  __syncthreads();
+  // B: the block's payload range [G, G + lim) of the heap section, dword by dword
+  const uint32_t nl = brec < LREC ? brec : LREC;
+  if (nl == 0) return;
+  const uint32_t lim = nl ? l_dst[nl - 1] + l_len[nl - 1] : 0;   // bytes covered by the list
+  const uint64_t G = (uint64_t)(s_heap - send) + (uint32_t)boff;  // absolute offset in send
+  const uint64_t A0 = G & ~3ull, A1 = G + lim;
+  for (uint64_t a = A0 + 4ull * threadIdx.x; a < A1; a += 4ull * XT) {
+    // bytes [a, a + 4) -> block-local p = a - G + i
+    const int64_t p0 = (int64_t)(a - G);
+    uint32_t lo = 0, hi = nl - 1;   // the last record with l_dst <= max(p0, 0)
+    const uint32_t q = p0 < 0 ? 0u : (uint32_t)p0;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (l_dst[mid] <= q) lo = mid;
+      else hi = mid - 1;
+    }
+    uint32_t r = lo;
+    uint32_t word = 0, have = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t p = p0 + i;
+      if (p < 0 || p >= (int64_t)lim) continue;
+      while ((uint32_t)p >= l_dst[r] + l_len[r]) ++r;   // empty payloads are skipped here too
+      word |= (uint32_t)x.heap_dev[l_src[r] + ((uint32_t)p - l_dst[r])] << (8 * i);
+      have |= 1u << i;
+    }
+    if (have == 0xFu) {
+      *reinterpret_cast<uint32_t*>(send + a) = word;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (have & (1u << i)) send[a + i] = (uint8_t)(word >> (8 * i));
     }
   }
 }
@@ -327,23 +341,23 @@ __device__ inline uint64_t xu_item(const Wire& W, bool is_msg, uint32_t g, uint3
   return reinterpret_cast<const sdx_wire_rec*>(W.r[r].rec_dev)[g - W.rec0[r]].payload_len;
 }
 
-__global__ __launch_bounds__(XT) void k_xu_scan(Wire W, uint8_t* __restrict__ work) {
+__global__ __launch_bounds__(XT) void k_xu_sum(Wire W, uint8_t* __restrict__ work) {
   const uint32_t M = W.msg0[W.nranks], R = W.rec0[W.nranks];
-  const uint32_t nbm = nblk_of(M), nbr = nblk_of(R);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(work);
+  const uint32_t nbm = nblk_of(M);
   uint64_t* blk = reinterpret_cast<uint64_t*>(work + 64);
   const bool is_msg = blockIdx.x < nbm;
   const uint32_t b = is_msg ? blockIdx.x : blockIdx.x - nbm;
-  const uint32_t g0 = b * XB + threadIdx.x * IPT;
-  uint64_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < IPT; ++j) sum += xu_item(W, is_msg, g0 + j, M, R);
   uint64_t tot;
-  (void)block_excl(sum, &tot);
-  if (!arrive_last(&blk[blockIdx.x], tot, ctr, nbm + nbr)) return;
+  (void)block_excl(xu_item(W, is_msg, b * XB + threadIdx.x, M, R), &tot);
+  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(XT) void k_xu_scan(Wire W, uint8_t* __restrict__ work) {
+  const uint32_t M = W.msg0[W.nranks], R = W.rec0[W.nranks];
+  const uint32_t nbm = nblk_of(M), nbr = nblk_of(R);
+  uint64_t* blk = reinterpret_cast<uint64_t*>(work + 64);
   block_scan_array(blk, nbm);
   block_scan_array(blk + nbm, nbr);
-  if (threadIdx.x == 0) *ctr = 0;
 }
 
 // blocks [0, nbm): descriptors (and each record's msg field); [nbm, nbm + nbr): records;
@@ -373,39 +387,28 @@ __global__ __launch_bounds__(XT) void k_xu_write(Wire W, const uint8_t* __restri
     return;
   }
   const bool is_msg = blockIdx.x < nbm;
-  const uint32_t b = is_msg ? blockIdx.x : blockIdx.x - nbm;
-  const uint32_t g0 = b * XB + threadIdx.x * IPT;
-  uint64_t v[IPT], sum = 0;
-#pragma unroll
-  for (int j = 0; j < IPT; ++j) {
-    v[j] = xu_item(W, is_msg, g0 + j, M, R);
-    sum += v[j];
-  }
+  const uint32_t g = (is_msg ? blockIdx.x : blockIdx.x - nbm) * XB + threadIdx.x;
+  const uint64_t v = xu_item(W, is_msg, g, M, R);
   uint64_t tot;
-  uint64_t pre = block_excl(sum, &tot) + blk[blockIdx.x];
-#pragma unroll
-  for (int j = 0; j < IPT; ++j) {
-    const uint32_t g = g0 + j;
-    if (is_msg && g < M) {
-      const int r = rank_of(W.msg0, W.nranks, g);
-      const uint32_t word = reinterpret_cast<const uint32_t*>(W.r[r].msg_dev)[g - W.msg0[r]];
-      sdx_desc o;
-      o.rec_begin = (uint32_t)(pre >> 32);
-      o.n_rec = (uint16_t)(word & 0xffffu);
-      o.status = (uint8_t)(word >> 16);
-      o.raise_kind = (uint8_t)(word >> 24);
-      desc[g] = o;
-      for (uint32_t i = 0; i < o.n_rec; ++i) rec[o.rec_begin + i].msg = g;
-    } else if (!is_msg && g < R) {
-      const int r = rank_of(W.rec0, W.nranks, g);
-      const sdx_wire_rec wr = reinterpret_cast<const sdx_wire_rec*>(W.r[r].rec_dev)[g - W.rec0[r]];
-      sdx_result* o = rec + g;
-      o->payload_off = (uint32_t)pre;
-      o->payload_len = wr.payload_len;
-      o->proto = wr.proto;
-      o->bit_length = wr.bit_length;
-    }
-    pre += v[j];
+  const uint64_t pre = block_excl(v, &tot) + blk[blockIdx.x];
+  if (is_msg && g < M) {
+    const int r = rank_of(W.msg0, W.nranks, g);
+    const uint32_t word = reinterpret_cast<const uint32_t*>(W.r[r].msg_dev)[g - W.msg0[r]];
+    sdx_desc o;
+    o.rec_begin = (uint32_t)(pre >> 32);
+    o.n_rec = (uint16_t)(word & 0xffffu);
+    o.status = (uint8_t)(word >> 16);
+    o.raise_kind = (uint8_t)(word >> 24);
+    desc[g] = o;
+    for (uint32_t i = 0; i < o.n_rec; ++i) rec[o.rec_begin + i].msg = g;
+  } else if (!is_msg && g < R) {
+    const int r = rank_of(W.rec0, W.nranks, g);
+    const sdx_wire_rec wr = reinterpret_cast<const sdx_wire_rec*>(W.r[r].rec_dev)[g - W.rec0[r]];
+    sdx_result* o = rec + g;
+    o->payload_off = (uint32_t)pre;
+    o->payload_len = wr.payload_len;
+    o->proto = wr.proto;
+    o->bit_length = wr.bit_length;
   }
 }
 
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(XT) void k_xu_write(Wire W, const uint8_t* __restri
 using namespace sdxx;
 
 extern "C" uint64_t sdx_exchange_work_bytes(const uint32_t* n_msgs, int k) {
-  uint64_t s = HDR;
+  uint64_t s = 0;
   for (int i = 0; i < k; ++i) s += part_work_bytes(n_msgs[i]);
   return s;
 }
@@ -459,30 +462,33 @@ static bool work_ok(const sdx_xchg_part* parts, int k, const void* work_dev, uin
   return work_dev && ((uintptr_t)work_dev & 255u) == 0 && work_cap >= sdx_exchange_work_bytes(ns, k);
 }
 
+static uint32_t max_blocks(const sdx_xchg_part* parts, int k) {
+  uint32_t nb = 1;
+  for (int i = 0; i < k; ++i) nb = nblk_of(parts[i].n_msgs) > nb ? nblk_of(parts[i].n_msgs) : nb;
+  return nb;
+}
+
 extern "C" int sdx_exchange_count(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
                                   uint32_t* counts_dev, void* hip_stream) {
   if (int rc = check_parts(parts, k, "sdx_exchange_count")) return rc;
   if (!counts_dev || !work_ok(parts, k, work_dev, work_cap))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_count: workspace too small / unaligned, or no counts buffer");
-  uint32_t nbmax = 1;
-  for (int i = 0; i < k; ++i) nbmax = nblk_of(parts[i].n_msgs) > nbmax ? nblk_of(parts[i].n_msgs) : nbmax;
-  hipLaunchKernelGGL(k_xw_count, dim3(nbmax, k), dim3(XT), 0, (hipStream_t)hip_stream, make_parts(parts, k),
-                     (uint8_t*)work_dev, counts_dev);
-  return launched("k_xw_count");
+  const Parts P = make_parts(parts, k);
+  hipLaunchKernelGGL(k_xw_count, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream, P,
+                     (uint8_t*)work_dev);
+  if (int rc = launched("k_xw_count")) return rc;
+  hipLaunchKernelGGL(k_xw_scan, dim3(k), dim3(XT), 0, (hipStream_t)hip_stream, P, (uint8_t*)work_dev, counts_dev);
+  return launched("k_xw_scan");
 }
 
 extern "C" int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
-                                 uint8_t* send_dev, uint64_t send_cap, void* hip_stream) {
+                                 const uint32_t* counts_dev, uint8_t* send_dev, uint64_t send_cap, void* hip_stream) {
   if (int rc = check_parts(parts, k, "sdx_exchange_pack")) return rc;
-  if (!send_dev || ((uintptr_t)send_dev & 15u) || send_cap < sdx_exchange_send_bytes(parts, k) ||
+  if (!counts_dev || !send_dev || ((uintptr_t)send_dev & 15u) || send_cap < sdx_exchange_send_bytes(parts, k) ||
       !work_ok(parts, k, work_dev, work_cap))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack: workspace or send buffer too small / unaligned");
-  uint64_t most = 1;
-  for (int i = 0; i < k; ++i) most = parts[i].n_msgs > most ? parts[i].n_msgs : most;
-  uint64_t blocks = (most + XT - 1) / XT;
-  blocks = blocks > 8192 ? 8192 : blocks;
-  hipLaunchKernelGGL(k_xw_pack, dim3((unsigned)blocks, k), dim3(XT), 0, (hipStream_t)hip_stream,
-                     make_parts(parts, k), (const uint8_t*)work_dev, send_dev);
+  hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream,
+                     make_parts(parts, k), counts_dev, (uint8_t*)work_dev, send_dev);
   return launched("k_xw_pack");
 }
 
@@ -525,9 +531,12 @@ extern "C" int sdx_exchange_unpack(const sdx_xchg_wire* ranks, int nranks, void*
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_unpack: bad workspace or output buffers");
   const uint32_t nb = nblk_of(m) + nblk_of(r);
   const uint32_t nh = (uint32_t)((h + 4ull * XT - 1) / (4ull * XT));
-  hipLaunchKernelGGL(k_xu_scan, dim3(nb), dim3(XT), 0, (hipStream_t)hip_stream, W, (uint8_t*)work_dev);
+  hipStream_t st = (hipStream_t)hip_stream;
+  hipLaunchKernelGGL(k_xu_sum, dim3(nb), dim3(XT), 0, st, W, (uint8_t*)work_dev);
+  if (int rc = launched("k_xu_sum")) return rc;
+  hipLaunchKernelGGL(k_xu_scan, dim3(1), dim3(XT), 0, st, W, (uint8_t*)work_dev);
   if (int rc = launched("k_xu_scan")) return rc;
-  hipLaunchKernelGGL(k_xu_write, dim3(nb + nh), dim3(XT), 0, (hipStream_t)hip_stream, W, (const uint8_t*)work_dev,
-                     desc_dev, rec_dev, heap_dev);
+  hipLaunchKernelGGL(k_xu_write, dim3(nb + nh), dim3(XT), 0, st, W, (const uint8_t*)work_dev, desc_dev, rec_dev,
+                     heap_dev);
   return launched("k_xu_write");
 }

@@ -26,6 +26,7 @@
 namespace sdx {
 int set_error(int code, const std::string& msg);  // sdx_kernels.hip
 const void* bank_dev_ptr(const sdx_bank* b);
+const sdx_bank_hdr* bank_hdr(const sdx_bank* b);
 }  // namespace sdx
 
 namespace sdxg {
@@ -312,11 +313,14 @@ GD int finish_mu_g(const BankView& bv, const sdx_mu_proto* rec, int p, uint8_t* 
   return emit(sk, bv, p, rec->pre_off, rec->pre_len, T, dl, rec->post_off, rec->post_len, nbp);
 }
 
-GD int mu_message(const BankView& bv, Msg& m, uint8_t* B, uint8_t* B2, uint8_t* T, Sink& sk) {
+// protocols [p0, p1) of the bank (a chunk of the walk; chunks run in parallel, k_general_walk):
+// returns the raise kind of the first protocol that raises (*raise_p = its index), else 0
+GD int mu_chunk(const BankView& bv, Msg& m, int p0, int p1, uint8_t* B, uint8_t* B2, uint8_t* T, Sink& sk,
+                int* raise_p) {
   if (m.n == 0) return 0;  // `if not raw_data` (:22-25)
   double last = __builtin_nan("");
-  const int nmu = (int)bv.hdr->n_mu;
-  for (int p = 0; p < nmu; ++p) {
+  for (int p = p0; p < p1; ++p) {
+    *raise_p = p;
     const sdx_mu_proto* rec = bv.mu + p;
     if (!rec->active || rec->never) continue;  // (:47-48); never = the key loop always fails
     if (!(rec->clock == last)) {
@@ -463,14 +467,15 @@ GD int finish_ms_g(const BankView& bv, const sdx_ms_proto* rec, int p, uint8_t* 
   return emit(sk, bv, p, rec->pre_off, rec->pre_len, T, dl, rec->post_off, rec->post_len, nb);
 }
 
-GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8_t* B2, uint8_t* T, Sink& sk) {
+GD int ms_chunk(const BankView& bv, Msg& m, int cp, bool ok, int p0, int p1, uint8_t* B, uint8_t* B2, uint8_t* T,
+                Sink& sk, int* raise_p) {
   if (!ok || cp < 0 || cp >= m.npat) return 0;  // the string gates and `str(CP) in patterns` (:21-57)
   const double clock = fabs(m.val[cp]);
   if (clock == 0.0) return 0;  // (:60-62)
   for (int k = 0; k < m.npat; ++k) m.nv[k] = py_round1(m.val[k] / clock);  // (:64-72)
-  const int nms = (int)bv.hdr->n_ms;
   const uint8_t KS[4] = {3, 1, 0, 2};  // sync '', one '1', zero '0', float 'F'
-  for (int p = 0; p < nms; ++p) {
+  for (int p = p0; p < p1; ++p) {
+    *raise_p = p;
     const sdx_ms_proto* rec = bv.ms + p;
     if (rec->never) continue;
     if (rec->pclock > 0.0 && fabs(rec->pclock - clock) > clock * 0.3) continue;  // (:81-86)
@@ -543,90 +548,193 @@ GD int ms_message(const BankView& bv, Msg& m, int cp, bool ok, uint8_t* B, uint8
   return 0;
 }
 
-// one wave per message: every lane runs the same serial walk over the bank on the same state (so
-// all control flow is wave-uniform), and the wide steps -- the character bitmaps, str.find, the
-// payload copies -- spread over the 64 lanes
+// Work split: the bank walk of a message is cut into chunks of GCH protocols, and a (message, chunk)
+// item is one wave's work.  A persistent grid of waves takes items from a device counter (heaviest
+// messages first: the host orders them by length), every lane of a wave running the same serial
+// walk on the same state (all control flow wave-uniform) with the wide steps -- str.find over the
+// character bitmaps, payload copies -- spread over the 64 lanes.  A message's results and raise are
+// the concatenation of its chunks in bank order up to the first raising protocol (message_unsynced.py
+// :45-49: an exception leaves the protocol loop), so:
+//   k_gen_prep     wave per message: its digit-character bitmaps into its workspace region;
+//   k_gen_walk<0>  every item: count its chunk's results and payload bytes, note the first raise;
+//   k_gen_reserve  thread per message: first raise over its chunks in bank order, else one
+//                  record / heap reservation for the message and each chunk's base;
+//   k_gen_walk<1>  items with results of messages that did not raise: the same walk, writing.
+constexpr int GCH = 1;          // protocols per chunk (one: the most parallel; staging a message costs ~us)
+constexpr int GSLOTS = 1024;    // resident waves of the walk (scratch slots)
 constexpr int GHEAD = (int)((sizeof(Msg) + sizeof(Wk) + 15) & ~(size_t)15);  // LDS: Msg, Wk, then data
 __host__ __device__ inline int lds_need(int n) { return GHEAD + ((n + 7) & ~7); }                        // + the message's characters
 __host__ __device__ inline int lds_need_bm(int n) { return lds_need(n) + 80 * (((n + 63) >> 6) + 1); }   // + its digit bitmaps
 
-template <int KIND>
-__global__ __launch_bounds__(64) void k_general(const void* __restrict__ bank, sdx_general_batch b, sdx_out out,
-                                                 int lds_bytes) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t glds[];
-  const BankView bv = bank_view(bank);
+struct GenChunk {  // per (message, chunk); 24 bytes
+  uint32_t nrec, nheap, rbase, hbase;
+  uint32_t raise;  // raise kind << 16 | protocol (0: none)
+  uint32_t res;
+};
+
+// workspace: [item counters (256 B) | chunk table | slot scratch | per-message regions]
+struct GenPlan {
+  int64_t tab, head;  // byte offsets of the slot scratch and of the per-message regions
+  int nproto, nch, max_len, slots, lds;
+};
+
+// the per-message region: the message's bitmaps (k_gen_prep)
+GI uint8_t* gen_region(const sdx_general_batch& b, const sdx_out& out, const GenPlan& g, int i, int msg) {
+  return out.work_dev + g.head +
+         (b.work_stride > 0 ? (int64_t)i * b.work_stride : 5 * b.offsets_dev[msg] + (int64_t)5 * GSLACK * msg);
+}
+GI uint32_t* gen_ctr(const sdx_out& out) { return reinterpret_cast<uint32_t*>(out.work_dev); }
+GI GenChunk* gen_table(const sdx_out& out) { return reinterpret_cast<GenChunk*>(out.work_dev + 256); }
+GI uint8_t* gen_slot(const sdx_out& out, const GenPlan& g, int slot) {
+  return out.work_dev + g.tab + (int64_t)slot * 3 * (g.max_len + GSLACK);
+}
+
+__global__ __launch_bounds__(64) void k_gen_prep(sdx_general_batch b, sdx_out out, GenPlan g) {
   const int i = blockIdx.x, lane = threadIdx.x;
   const int msg = b.sel_dev ? b.sel_dev[i] : i;
   const int64_t off = b.offsets_dev[msg];
-  Msg& m = *reinterpret_cast<Msg*>(glds);
-  m.wk = reinterpret_cast<Wk*>(glds + sizeof(Msg));
-  m.d = b.data_dev + off;
-  m.n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
-  m.npat = b.npat_dev[msg] < GP ? b.npat_dev[msg] : GP;
-  m.ids = b.pat_ids_dev + (size_t)msg * GP * GID;
-  m.val = b.pat_val_dev + (size_t)msg * GP;
-  // per-message scratch: bits, postDemod output, payload text (include/sdx.h sdx_general_work_bytes);
-  // every lane writes the same bytes here and reads back only what it wrote itself
-  uint8_t* B = b.work_stride > 0 ? out.work_dev + (int64_t)i * b.work_stride
-                                 : out.work_dev + 5 * off + (int64_t)5 * GSLACK * msg;
-  uint8_t* B2 = B + m.n + GSLACK;
-  uint8_t* T = B2 + m.n + GSLACK;
-  // the message's digit-character bitmaps (find_bm), after the three byte areas, 8-byte aligned;
-  // lane l builds words l, l + 64, ..
-  uint64_t* bmw = reinterpret_cast<uint64_t*>(((uintptr_t)(T + m.n + GSLACK) + 7) & ~(uintptr_t)7);
-  m.nwp = ((m.n + 63) >> 6) + 1;
-  // the characters and the bitmaps go to LDS when they fit (the serial walks read them at LDS latency)
-  if (lds_need(m.n) <= lds_bytes) {
-    uint8_t* ld = glds + GHEAD;
-    for (int j = lane; j < m.n; j += 64) ld[j] = m.d[j];
-    if (lds_need_bm(m.n) <= lds_bytes) bmw = reinterpret_cast<uint64_t*>(glds + lds_need(m.n));
-  }
-  m.bm = bmw;
-  for (int w = lane; w < m.nwp; w += 64) {
+  const uint8_t* d = b.data_dev + off;
+  const int n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
+  const int nwp = ((n + 63) >> 6) + 1;
+  uint64_t* bmw = reinterpret_cast<uint64_t*>(gen_region(b, out, g, i, msg));
+  if (i == 0 && lane < 2) gen_ctr(out)[lane] = 0;  // the two walk passes' item counters
+  for (int w = lane; w < nwp; w += 64) {  // lane l builds words l, l + 64, ..
     uint64_t a[10];
 #pragma unroll
     for (int c = 0; c < 10; ++c) a[c] = 0;
-    const int p0 = w * 64, pe = (m.n - p0 < 64) ? m.n - p0 : 64;
+    const int p0 = w * 64, pe = (n - p0 < 64) ? n - p0 : 64;
     for (int j = 0; j < pe; ++j) {
-      const int c = (int)m.d[p0 + j] - '0';
+      const int c = (int)d[p0 + j] - '0';
 #pragma unroll
       for (int k = 0; k < 10; ++k) a[k] |= (uint64_t)(c == k) << j;
     }
 #pragma unroll
-    for (int c = 0; c < 10; ++c) bmw[(size_t)c * m.nwp + w] = a[c];
+    for (int c = 0; c < 10; ++c) bmw[(size_t)c * nwp + w] = a[c];
   }
-  __threadfence_block();
-  __syncthreads();  // the block is this one wave: the bitmaps and LDS characters are visible to every lane
-  if (lds_need(m.n) <= lds_bytes) m.d = glds + GHEAD;
-  const int cp = KIND == SDX_KIND_MS ? (int)b.cp_slot_dev[msg] : -1;
-  const bool ok = KIND == SDX_KIND_MS ? b.ms_ok_dev[msg] != 0 : true;
-  Sink sk{false, 0, 0u, out.rec_dev, out.heap_dev, 0u, 0u, (uint32_t)msg};
-  int raise = KIND == SDX_KIND_MU ? mu_message(bv, m, B, B2, T, sk) : ms_message(bv, m, cp, ok, B, B2, T, sk);
+}
+
+template <int KIND, int PASS>
+__global__ __launch_bounds__(64) void k_gen_walk(const void* __restrict__ bank, sdx_general_batch b, sdx_out out,
+                                                 GenPlan g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t glds[];
+  const BankView bv = bank_view(bank);
+  const int lane = threadIdx.x;
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int nitems = ntot * g.nch;
+  uint32_t* ctr = gen_ctr(out) + PASS;
+  GenChunk* tab = gen_table(out);
+  // per-slot scratch: bits, postDemod output, payload text (every lane writes the same bytes and reads
+  // back only what it wrote itself)
+  uint8_t* B = gen_slot(out, g, blockIdx.x);
+  uint8_t* B2 = B + g.max_len + GSLACK;
+  uint8_t* T = B2 + g.max_len + GSLACK;
+  Msg& m = *reinterpret_cast<Msg*>(glds);
+  m.wk = reinterpret_cast<Wk*>(glds + sizeof(Msg));
+  int cur = -1;  // the item's message whose characters / bitmaps are staged
+  while (true) {
+    int item = 0;
+    if (lane == 0) item = (int)atomicAdd(ctr, 1u);
+    item = bcast_i(item, 0);
+    if (item >= nitems) break;
+    const int i = item / g.nch, c = item - i * g.nch;
+    const int msg = b.sel_dev ? b.sel_dev[i] : i;
+    GenChunk& e = tab[item];
+    if (PASS == 1 && (e.nrec == 0 || out.desc_dev[msg].status != SDX_ST_OK)) continue;
+    const int p0 = c * GCH, p1 = (p0 + GCH < g.nproto) ? p0 + GCH : g.nproto;
+    if (GCH == 1 && PASS == 0) {  // a protocol the walk skips anyway: no staging
+      const bool skip = KIND == SDX_KIND_MU ? (!bv.mu[p0].active || bv.mu[p0].never) : (bool)bv.ms[p0].never;
+      if (skip) {
+        if (lane == 0) {
+          e.nrec = 0;
+          e.nheap = 0;
+          e.raise = 0;
+        }
+        continue;
+      }
+    }
+    if (i != cur) {  // stage the message (the LDS holds one)
+      cur = i;
+      const int64_t off = b.offsets_dev[msg];
+      m.d = b.data_dev + off;
+      m.n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
+      m.npat = b.npat_dev[msg] < GP ? b.npat_dev[msg] : GP;
+      m.ids = b.pat_ids_dev + (size_t)msg * GP * GID;
+      m.val = b.pat_val_dev + (size_t)msg * GP;
+      m.nwp = ((m.n + 63) >> 6) + 1;
+      const uint64_t* gbm = reinterpret_cast<const uint64_t*>(gen_region(b, out, g, i, msg));
+      m.bm = gbm;
+      __syncthreads();  // the previous item's reads of the LDS copy are done
+      if (lds_need(m.n) <= g.lds) {  // the serial walks read characters / bitmaps at LDS latency
+        uint8_t* ld = glds + GHEAD;
+        for (int j = lane; j < m.n; j += 64) ld[j] = m.d[j];
+        if (lds_need_bm(m.n) <= g.lds) {
+          uint64_t* lb = reinterpret_cast<uint64_t*>(glds + lds_need(m.n));
+          for (int j = lane; j < 10 * m.nwp; j += 64) lb[j] = gbm[j];
+          m.bm = lb;
+        }
+        m.d = ld;
+      }
+      __syncthreads();
+    }
+    Sink sk{PASS == 1, 0, 0u, out.rec_dev, out.heap_dev, PASS == 1 ? e.rbase : 0u, PASS == 1 ? e.hbase : 0u,
+            (uint32_t)msg};
+    int rp = 0, raise;
+    if (KIND == SDX_KIND_MU) {
+      raise = mu_chunk(bv, m, p0, p1, B, B2, T, sk, &rp);
+    } else {
+      const int cp = (int)b.cp_slot_dev[msg];
+      raise = ms_chunk(bv, m, cp, b.ms_ok_dev[msg] != 0, p0, p1, B, B2, T, sk, &rp);
+    }
+    if (PASS == 0 && lane == 0) {
+      e.nrec = (uint32_t)sk.nrec;
+      e.nheap = sk.nheap;
+      e.raise = raise ? ((uint32_t)raise << 16) | (uint32_t)rp : 0u;
+    }
+  }
+}
+
+// thread per message: its chunks in bank order -> the first raise, or one reservation and the chunk bases
+__global__ __launch_bounds__(256) void k_gen_reserve(sdx_general_batch b, sdx_out out, GenPlan g) {
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ntot) return;
+  const int msg = b.sel_dev ? b.sel_dev[i] : i;
+  GenChunk* e = gen_table(out) + (int64_t)i * g.nch;
   sdx_desc d;
   d.rec_begin = 0;
   d.n_rec = 0;
-  d.raise_kind = (uint8_t)raise;
-  d.status = raise ? SDX_ST_RAISED : SDX_ST_OK;
-  if (!raise && sk.nrec) {
-    const uint32_t nh = (sk.nheap + 15u) & ~15u;
-    uint32_t rb = 0, hb = 0;
-    if (lane == 0) {
-      rb = atomicAdd(&out.cursor_dev[0], (uint32_t)sk.nrec);
-      hb = atomicAdd(&out.cursor_dev[1], nh);
+  d.status = SDX_ST_OK;
+  d.raise_kind = 0;
+  uint64_t nr = 0, nh = 0;
+  for (int c = 0; c < g.nch; ++c) {
+    if (e[c].raise) {
+      d.status = SDX_ST_RAISED;
+      d.raise_kind = (uint8_t)(e[c].raise >> 16);
+      break;
     }
-    rb = (uint32_t)bcast_i((int)rb, 0);
-    hb = (uint32_t)bcast_i((int)hb, 0);
-    if (sk.nrec > 65535 || rb + sk.nrec > out.rec_cap || hb + nh > out.heap_cap) {
+    nr += e[c].nrec;
+    nh += e[c].nheap;
+  }
+  if (d.status == SDX_ST_OK && nr) {
+    const uint32_t nh16 = (uint32_t)((nh + 15) & ~15ull);
+    const uint32_t rb = atomicAdd(&out.cursor_dev[0], (uint32_t)nr);
+    const uint32_t hb = atomicAdd(&out.cursor_dev[1], nh16);
+    if (nr > 65535 || nh > 0xFFFFFFF0ull || (uint64_t)rb + nr > out.rec_cap || (uint64_t)hb + nh16 > out.heap_cap) {
       d.status = SDX_ST_OVF_OUT;
-      if (lane == 0) atomicOr(&out.cursor_dev[2], 1u);
+      atomicOr(&out.cursor_dev[2], 1u);
     } else {
-      Sink sw{true, 0, 0u, out.rec_dev, out.heap_dev, rb, hb, (uint32_t)msg};
-      raise = KIND == SDX_KIND_MU ? mu_message(bv, m, B, B2, T, sw) : ms_message(bv, m, cp, ok, B, B2, T, sw);
+      uint32_t r = rb, h = hb;
+      for (int c = 0; c < g.nch; ++c) {
+        e[c].rbase = r;
+        e[c].hbase = h;
+        r += e[c].nrec;
+        h += e[c].nheap;
+      }
       d.rec_begin = rb;
-      d.n_rec = (uint16_t)sw.nrec;
+      d.n_rec = (uint16_t)nr;
     }
   }
-  if (lane == 0) out.desc_dev[msg] = d;
+  out.desc_dev[msg] = d;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -750,8 +858,32 @@ __global__ __launch_bounds__(256) void k_mc_general(const void* __restrict__ ban
 
 extern "C" {
 
-uint64_t sdx_general_work_bytes(int64_t total_chars, int32_t n) {
-  return (uint64_t)(5 * (total_chars > 0 ? total_chars : 0) + (int64_t)5 * sdxg::GSLACK * (n > 0 ? n : 0) + 256);
+static sdxg::GenPlan gen_plan(const sdx_bank* bank, int kind, int32_t n, int32_t max_len) {
+  sdxg::GenPlan g;
+  const sdx_bank_hdr* h = sdx::bank_hdr(bank);
+  g.nproto = kind == SDX_KIND_MU ? (int)h->n_mu : (int)h->n_ms;
+  g.nch = (g.nproto + sdxg::GCH - 1) / sdxg::GCH;
+  if (g.nch < 1) g.nch = 1;
+  g.max_len = max_len > 0 ? max_len : 0;
+  const int64_t items = (int64_t)(n > 0 ? n : 0) * g.nch;
+  g.slots = (int)(items < sdxg::GSLOTS ? (items > 0 ? items : 1) : sdxg::GSLOTS);
+  g.tab = 256 + (((int64_t)(n > 0 ? n : 0) * g.nch * (int64_t)sizeof(sdxg::GenChunk) + 255) & ~(int64_t)255);
+  g.head = g.tab + (((int64_t)g.slots * 3 * (g.max_len + sdxg::GSLACK) + 255) & ~(int64_t)255);
+  // LDS per wave: the working set plus the longest message's characters and bitmaps, at most 64 KB
+  // (longer messages keep them in HBM)
+  const int64_t need = sdxg::lds_need_bm(g.max_len);
+  g.lds = need <= 65536 ? (int)need : (sdxg::lds_need(g.max_len) <= 65536 ? sdxg::lds_need(g.max_len) : sdxg::GHEAD);
+  return g;
+}
+
+uint64_t sdx_general_work_bytes(const sdx_bank* bank, int kind, int64_t total_chars, int32_t n, int32_t max_len,
+                                int64_t work_stride) {
+  if (!bank || (kind != SDX_KIND_MU && kind != SDX_KIND_MS)) return 0;
+  const sdxg::GenPlan g = gen_plan(bank, kind, n, max_len);
+  const int64_t regions = work_stride > 0 ? work_stride * (int64_t)(n > 0 ? n : 0)
+                                          : 5 * (total_chars > 0 ? total_chars : 0) +
+                                                (int64_t)5 * sdxg::GSLACK * (n > 0 ? n : 0);
+  return (uint64_t)(g.head + regions + 256);
 }
 
 int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_batch* batch, const sdx_out* out,
@@ -763,25 +895,29 @@ int sdx_demod_pulses_general(const sdx_bank* bank, int kind, const sdx_general_b
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
   if (ntot <= 0) return SDX_OK;
   if (!batch->data_dev || !batch->offsets_dev || !batch->npat_dev || !batch->pat_ids_dev || !batch->pat_val_dev ||
-      !out->work_dev || (batch->work_stride > 0 && out->work_cap < (uint64_t)batch->work_stride * (uint64_t)ntot))
-    return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: missing buffer (work_dev: sdx_general_work_bytes)");
-  const int grid = ntot;  // one wave per message
-  // LDS per wave: the working set plus the longest message's characters and bitmaps when the
-  // stride names it (work_stride = 5 * (max len + GSLACK)), at most 64 KB; longer ones stay in HBM
-  int lds = 65536;
-  if (batch->work_stride > 0) {
-    const int64_t ml = batch->work_stride / 5 - sdxg::GSLACK;
-    lds = ml < 0 ? sdxg::GHEAD : ml >= 65536 ? 65536 : sdxg::lds_need_bm((int)ml);
-    if (lds > 65536) lds = 65536;
-  }
+      !out->work_dev || batch->max_len < 0)
+    return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: missing buffer");
+  if (batch->work_stride > 0 && batch->work_stride < 5 * ((int64_t)batch->max_len + sdxg::GSLACK))
+    return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: work_stride < 5 * (max_len + 512)");
+  // the regions' part of the workspace is the caller's (sdx_general_work_bytes); the head is checked here
+  const sdxg::GenPlan g = gen_plan(bank, kind, ntot, batch->max_len);
+  if (out->work_cap < (uint64_t)g.head) return sdx::set_error(SDX_EINVAL, "sdx_demod_pulses_general: work_cap < sdx_general_work_bytes");
   hipStream_t st = (hipStream_t)hip_stream;
   const void* bd = sdx::bank_dev_ptr(bank);
+  const int nitems = ntot * g.nch;
+  const int grid = nitems < g.slots ? nitems : g.slots;
+  hipLaunchKernelGGL(sdxg::k_gen_prep, dim3(ntot), dim3(64), 0, st, *batch, *out, g);
   if (kind == SDX_KIND_MU)
-    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MU>), dim3(grid), dim3(64), lds, st, bd, *batch, *out, lds);
+    hipLaunchKernelGGL((sdxg::k_gen_walk<SDX_KIND_MU, 0>), dim3(grid), dim3(64), g.lds, st, bd, *batch, *out, g);
   else
-    hipLaunchKernelGGL((sdxg::k_general<SDX_KIND_MS>), dim3(grid), dim3(64), lds, st, bd, *batch, *out, lds);
+    hipLaunchKernelGGL((sdxg::k_gen_walk<SDX_KIND_MS, 0>), dim3(grid), dim3(64), g.lds, st, bd, *batch, *out, g);
+  hipLaunchKernelGGL(sdxg::k_gen_reserve, dim3((ntot + 255) / 256), dim3(256), 0, st, *batch, *out, g);
+  if (kind == SDX_KIND_MU)
+    hipLaunchKernelGGL((sdxg::k_gen_walk<SDX_KIND_MU, 1>), dim3(grid), dim3(64), g.lds, st, bd, *batch, *out, g);
+  else
+    hipLaunchKernelGGL((sdxg::k_gen_walk<SDX_KIND_MS, 1>), dim3(grid), dim3(64), g.lds, st, bd, *batch, *out, g);
   const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("k_general: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("k_gen_*: ") + hipGetErrorString(e));
   return SDX_OK;
 }
 

@@ -249,19 +249,11 @@ SDX_DEV uint32_t spill_region(T& L, const sdx_out& out) {
     if (lane_id() == leader) {
       uint32_t cur = atomicCAS(&L.spill_base, SPILL_NONE, SPILL_PENDING);
       if (cur == SPILL_NONE) {
-        // claim a region with a CAS loop that stops at work_cap: the cursor never moves past the
-        // workspace, so it cannot wrap however many tiles ask (SPILL_FULL: exhausted)
-        uint32_t c = __hip_atomic_load(&out.cursor_dev[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-          if (!out.work_dev || (uint64_t)c + SPILL_BYTES > out.work_cap) {
-            c = SPILL_FULL;
-            break;
-          }
-          const uint32_t seen = atomicCAS(&out.cursor_dev[3], c, c + SPILL_BYTES);
-          if (seen == c) break;
-          c = seen;
-        }
-        cur = c;
+        // cursor[3] counts the regions handed out (one per tile at most, so it cannot wrap); a
+        // region past the workspace is SPILL_FULL
+        const uint32_t idx = atomicAdd(&out.cursor_dev[3], 1u);
+        const uint64_t o = (uint64_t)idx * SPILL_BYTES;
+        cur = (out.work_dev && o + SPILL_BYTES <= out.work_cap) ? (uint32_t)o : SPILL_FULL;
         __hip_atomic_store(&L.spill_base, cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       while (cur == SPILL_PENDING) cur = __hip_atomic_load(&L.spill_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1527,7 +1519,15 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   uint8_t* st_np = reinterpret_cast<uint8_t*>(st_clk + TM);                // [TM]
   int64_t pf_off = 0;
   int pf_n = 0;
+#ifdef SDX_STAGE_BALLOT
   uint32_t pf_c[MPW][NW <= 4 ? NW : 1];
+#else
+  // SWAR staging (short variants): 16 characters per lane, 4 messages per pass over the wave
+  constexpr int SMSG = 64 / 16;                    // messages per pass
+  constexpr int SPASS = (MPW + SMSG - 1) / SMSG;   // passes per wave
+  static_assert(NW > 4 || NW == 4, "SWAR staging: 256-character rows, 16 lanes per message");
+  uint32_t sx[NW <= 4 ? SPASS : 1][5];
+#endif
   if constexpr (NW <= 4) {
     // every header load of the tile is issued before any of them is used: the data offsets of the
     // wave's messages, and per (message, pattern) thread npat, P, the id and (MS) the message's
@@ -1590,6 +1590,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         st_x[i] = (uint32_t)(clk != 0.0 ? py_round1_k(v / clk) : SDX_K_NONE);
       }
     }
+    PROF_ADD(17, t_stage);
+#ifdef SDX_STAGE_BALLOT
 #pragma unroll
     for (int k = 0; k < MPW; ++k) {
       const int lo = __shfl((int)(uint32_t)pf_off, k), hi = __shfl((int)(uint32_t)((uint64_t)pf_off >> 32), k);
@@ -1601,14 +1603,88 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         pf_c[k][w] = pos < n ? (uint32_t)b.data_dev[off + pos] : 0xFFu;
       }
     }
+#else
+    // 16 characters per lane: lane group g = lane / 16 holds tile message 4 * pass + g, lane j = lane % 16
+    // its characters [16 j, 16 j + 16) as five aligned dwords (realigned below; a dword that holds a
+    // byte of the message cannot cross a page, so the loads past the message end stay in bounds)
+#pragma unroll
+    for (int ps = 0; ps < SPASS; ++ps) {
+      const int k = ps * SMSG + (lane >> 4);
+      const int lo = __shfl((int)(uint32_t)pf_off, k), hi = __shfl((int)(uint32_t)((uint64_t)pf_off >> 32), k);
+      const int64_t off = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+      const int n = __shfl(pf_n, k);
+      const int64_t base = off + 16 * (lane & 15);
+      const int64_t a = base & ~(int64_t)3;
+      const bool on = wave + k * NWAVE < nvalid;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(b.data_dev + a);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) sx[ps][i] = (on && a + 4 * i < off + n) ? src[i] : 0xFFFFFFFFu;
+    }
+#endif
   }
+  PROF_T(t_bm);
   if constexpr (NW <= 4) {
+#ifndef SDX_STAGE_BALLOT
+  // per pass: the lane's 16 characters -> 10 id masks of 16 bits (SWAR on 4 characters per dword),
+  // written as 16-bit pieces of the per-id bitmaps; non-digit characters per message by ballot
+  uint32_t ndmsg = 0;  // bit k: tile message k of the wave holds a non-digit character
+#pragma unroll
+  for (int ps = 0; ps < SPASS; ++ps) {
+    const int k = ps * SMSG + (lane >> 4), j = lane & 15;
+    const int mi = wave + k * NWAVE;
+    const int n = __shfl(pf_n, k);
+    const int lo = __shfl((int)(uint32_t)pf_off, k);
+    const uint32_t r = (uint32_t)lo & 3u;  // realignment of the message's rows
+    uint32_t V = 0, P0 = 0, P1 = 0, P2 = 0, P3 = 0, FE = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t c = __builtin_amdgcn_alignbyte(sx[ps][i + 1], sx[ps][i], r);  // bytes r.. of the pair
+      const int rem = n - (16 * j + 4 * i);  // characters of this dword inside the message
+      c = rem >= 4 ? c : (rem <= 0 ? 0xFFFFFFFFu : (c | (0xFFFFFFFFu << (8 * rem))));
+      const uint32_t t = c ^ 0x30303030u;        // digits -> 0x00..0x09
+      const uint32_t lo4 = t & 0x0F0F0F0Fu;
+      const uint32_t bad = (t & 0xF0F0F0F0u) | ((lo4 + 0x06060606u) & 0x10101010u);  // byte != 0 <=> not a digit
+      const uint32_t nz = ((bad & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | bad;               // bit 7: byte != 0
+      const uint32_t dg = (~nz >> 7) & 0x01010101u;                                // byte bit 0: digit
+      V |= ((dg * 0x01020408u) >> 24) << (4 * i);
+      P0 |= (((lo4 & 0x01010101u) * 0x01020408u) >> 24) << (4 * i);
+      P1 |= (((lo4 & 0x02020202u) * 0x00810204u) >> 24) << (4 * i);
+      P2 |= (((lo4 & 0x04040404u) * 0x00408102u) >> 24) << (4 * i);
+      P3 |= (((lo4 & 0x08080808u) * 0x00204081u) >> 24) << (4 * i);
+      if (__builtin_expect(bad != 0 && rem > 0, 0)) {  // 0xFE counts as isdigit() (packing.py), not as an id
+        const uint32_t fe = c ^ 0xFEFEFEFEu;
+        const uint32_t fz = ~(((fe & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | fe) & 0x80808080u;
+        FE |= ((((fz >> 7) & 0x01010101u) * 0x01020408u) >> 24) << (4 * i);
+      }
+    }
+    const uint32_t posm = n - 16 * j >= 16 ? 0xFFFFu : (n - 16 * j <= 0 ? 0u : (1u << (n - 16 * j)) - 1u);
+    const bool nondigit = (posm & ~V & ~FE) != 0;
+    const uint64_t ndb = ballot(nondigit);
+#pragma unroll
+    for (int g = 0; g < SMSG; ++g)
+      if ((ndb >> (16 * g)) & 0xFFFFull) ndmsg |= 1u << (ps * SMSG + g);
+    if (mi < nvalid) {
+      const uint32_t N0 = ~P0, N1 = ~P1, N2 = ~P2, N3 = ~P3;
+      uint16_t* row = reinterpret_cast<uint16_t*>(&L.bm[mi * T::MSTRIDE + (j >> 2)]) + (j & 3);
+#pragma unroll
+      for (int id = 0; id < 10; ++id) {
+        const uint32_t m = V & ((id & 1) ? P0 : N0) & ((id & 2) ? P1 : N1) & ((id & 4) ? P2 : N2) &
+                           ((id & 8) ? P3 : N3);
+        row[id * T::WS * 4] = (uint16_t)m;
+      }
+    }
+  }
+  wave_sync();
+#endif
+  PROF_ADD(18, t_bm);
+  PROF_T(t_pairs);
 #pragma unroll
   for (int k = 0; k < MPW; ++k) {
     const int mi = wave + k * NWAVE;
     if (mi >= nvalid) break;
     const int n = __shfl(pf_n, k);
     const int nwu = (n + 63) >> 6;  // words holding pulses (wave-uniform); the rest are empty
+#ifdef SDX_STAGE_BALLOT
     bool nondigit = false;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
@@ -1627,6 +1703,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       if (lane < 10) L.bm[mi * T::MSTRIDE + lane * T::WS + w] = mine;
     }
     const uint64_t nd = ballot(nondigit);
+#else
+    const uint64_t nd = (ndmsg >> k) & 1u;
+#endif
     if constexpr (NW <= 4) {  // pair presence: lane = id pair (a, b), a = q / 10, b = q % 10
       wave_sync();
       uint64_t pr[2];
@@ -1653,6 +1732,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       L.digit_ok[mi] = (nd == 0 && n > 0) ? 1u : 0u;
     }
   }
+  PROF_ADD(19, t_pairs);
   }
   if constexpr (NW > 4) {  // long variants: one message per wave
     for (int mi = wave; mi < nvalid; mi += NWAVE) {
@@ -2530,7 +2610,7 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
   if (kind != SDX_KIND_MU && kind != SDX_KIND_MS) return fail(SDX_EINVAL, "kind must be MU or MS");
   if (kind == SDX_KIND_MS && (!batch->cp_slot_dev || !batch->ms_ok_dev)) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
-  // spill regions are addressed with 32-bit offsets (the workspace cursor is cursor_dev[3])
+  // spill regions are addressed with 32-bit offsets (region index cursor_dev[3] x SPILL_BYTES)
   if (out->work_dev && out->work_cap > 0xFFFFFFFFull - sdx::SPILL_BYTES)
     return fail(SDX_EINVAL, "work_cap above 4 GiB - 112 KB: spill offsets are 32-bit");
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;

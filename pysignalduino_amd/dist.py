@@ -230,7 +230,8 @@ class Exchange:
         cap = int(lib.sdx_exchange_send_bytes(xp, len(parts)))
         send = self._buf("send", cap, dev)
         runtime._check(lib, lib.sdx_exchange_pack(xp, len(parts), ctypes.c_void_p(work.data_ptr()), wb,
-                                                  ctypes.c_void_p(send.data_ptr()), send.numel(), sp))
+                                                  ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(send.data_ptr()),
+                                                  send.numel(), sp))
         return cnt
 
     # -- host path (CPU tensors) ------------------------------------------------------------------------

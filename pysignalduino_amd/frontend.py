@@ -165,7 +165,7 @@ class LineBatch:
         lens = g["len"].cpu().numpy()
         st = self.status[sel.long()].cpu().numpy()
         status[rows] = st                                   # lines found outside the contract
-        g.update(data=self.slot, n=m, total=int(lens.sum()))
+        g.update(data=self.slot, n=m, total=int(lens.sum()), lens_host=lens)
         kd = runtime.KIND_MU if line_kind == runtime.LINE_MU else runtime.KIND_MS
         desc, rec, heap = eng.run_general(kd, g, work_stride=5 * (int(lens.max()) + 512))
         return (rows, desc, rec, heap, g["pat_val"].cpu().numpy().reshape(m, 16),

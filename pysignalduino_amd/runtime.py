@@ -54,7 +54,8 @@ class SdxPulseBatch(Structure):
 class SdxGeneralBatch(Structure):
     _fields_ = [("data_dev", c_void_p), ("offsets_dev", c_void_p), ("npat_dev", c_void_p), ("pat_ids_dev", c_void_p),
                 ("pat_val_dev", c_void_p), ("cp_slot_dev", c_void_p), ("ms_ok_dev", c_void_p), ("sel_dev", c_void_p),
-                ("n", c_int32), ("n_sel", c_int32), ("len_dev", c_void_p), ("work_stride", ctypes.c_int64)]
+                ("n", c_int32), ("n_sel", c_int32), ("len_dev", c_void_p), ("work_stride", ctypes.c_int64),
+                ("max_len", c_int32), ("res", c_int32)]
 
 
 class SdxLinesGeneralOut(Structure):
@@ -161,7 +162,7 @@ def load_library(path: Optional[str] = None):
     lib.sdx_group_work_bytes.restype = c_size_t
     lib.sdx_group_pulses.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), c_void_p, c_void_p, c_size_t, c_void_p]
     lib.sdx_group_pulses.restype = c_int
-    lib.sdx_general_work_bytes.argtypes = [ctypes.c_int64, c_int32]
+    lib.sdx_general_work_bytes.argtypes = [c_void_p, c_int, ctypes.c_int64, c_int32, c_int32, ctypes.c_int64]
     lib.sdx_general_work_bytes.restype = ctypes.c_uint64
     lib.sdx_demod_pulses_general.argtypes = [c_void_p, c_int, POINTER(SdxGeneralBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_pulses_general.restype = c_int
@@ -190,7 +191,7 @@ def load_library(path: Optional[str] = None):
     lib.sdx_exchange_send_bytes.restype = ctypes.c_uint64
     lib.sdx_exchange_count.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p]
     lib.sdx_exchange_count.restype = c_int
-    lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p,
+    lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
                                       ctypes.c_uint64, c_void_p]
     lib.sdx_exchange_pack.restype = c_int
     lib.sdx_exchange_unpack_work_bytes.argtypes = [c_uint32, c_uint32]
@@ -396,15 +397,20 @@ class Engine:
         n = gd["n"]
         rec_cap = 16 * n + 1024
         heap_cap = int(2 * gd["total"] + 256 * n + 65536)
-        wb = n * work_stride if work_stride > 0 else int(self.lib.sdx_general_work_bytes(gd["total"], n))
+        lens = gd["lens_host"] if "lens_host" in gd else np.asarray(gd["lengths"])
+        max_len = int(lens.max(initial=0))
+        wb = int(self.lib.sdx_general_work_bytes(self.handle, kind, int(gd["total"]), n, max_len, int(work_stride)))
         work = self.torch.empty(max(wb, 1), dtype=self.torch.uint8, device=self.dev)
+        # the longest messages first: the device's work queue then ends on short ones
+        order = np.argsort(-lens, kind="stable").astype(np.int32)
+        sel = self.torch.from_numpy(order).to(self.dev)
         for attempt in range(6):
             out = self.alloc_out(n, rec_cap, heap_cap)
             o = self._out_struct(out)
             o.work_dev, o.work_cap = _ptr(work), int(work.numel())
             b = SdxGeneralBatch(_ptr(gd["data"]), _ptr(gd["offsets"]), _ptr(gd["npat"]), _ptr(gd["pat_ids"]),
-                                _ptr(gd["pat_val"]), _ptr(gd["cp_slot"]), _ptr(gd["ms_ok"]), None, n, 0,
-                                _ptr(gd.get("len")), int(work_stride))
+                                _ptr(gd["pat_val"]), _ptr(gd["cp_slot"]), _ptr(gd["ms_ok"]), _ptr(sel), n, n,
+                                _ptr(gd.get("len")), int(work_stride), max_len, 0)
             _check(self.lib, self.lib.sdx_demod_pulses_general(self.handle, kind, ctypes.byref(b), ctypes.byref(o),
                                                                self.stream_ptr()))
             desc, rec, heap = self.fetch(out)

@@ -14,7 +14,8 @@ from pysignalduino_amd import bank as bankmod, runtime, synth
 NAMES = {0: "stage bitmaps", 1: "MU normalise", 2: "MU pexists(start)", 3: "MU pexists(one/zero/float)",
          4: "MU decode setup", 5: "MU finditer scan", 6: "MU chunk->bits", 7: "MU postDemod",
          8: "MU payload write", 9: "MU format+DFA", 10: "MS decode", 11: "MS finish", 12: "MU decode total",
-         13: "flush", 14: "end barrier wait", 15: "kernel total", 16: "MU finish phase (lane = match)", 20: "#results(MU)", 21: "#survivors(MU)",
+         13: "flush", 14: "end barrier wait", 15: "kernel total", 16: "MU finish phase (lane = match)",
+         17: "  stage: headers + pattern tables", 18: "  stage: id bitmaps", 19: "  stage: pairs + lengths", 20: "#results(MU)", 21: "#survivors(MU)",
          22: "#matches(MU)", 23: "#survivors(MS)"}
 
 
@@ -28,7 +29,7 @@ def main():
     for kind, gen in (("MU", synth.mu_corpus), ("MS", synth.ms_corpus)):
         pb = gen(bk.protocols, n, seed=42)
         bd = eng.to_device_pulses(pb)
-        out = eng.alloc_out(pb.n, 8 * pb.n + 4096, 200 * pb.n + 65536)
+        out = eng.alloc_out(pb.n, 12 * pb.n + 4096, 320 * pb.n + 65536, eng.pulses_work_bytes(pb.n))
         k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
         eng.launch_pulses(k, bd, out)
         torch.cuda.synchronize()

@@ -1,0 +1,66 @@
+"""Standalone time of the exchange's sender kernels (sdx_exchange_count + sdx_exchange_pack) on the
+bench step's outputs (1M messages: MU/MS/MC 1/3 each), and of the receiver rebuild
+(sdx_exchange_unpack) at world 1.  usage: python tools/time_exchange.py [msgs] [reps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from pysignalduino_amd import bank as bankmod, dist as sdist, runtime, synth
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    bk = bankmod.Bank()
+    eng = runtime.Engine(bk, 0)
+    P = bk.protocols
+    per = {"MU": n // 3, "MS": n // 3, "MC": n - 2 * (n // 3)}
+    parts = []
+    for k, s in (("MU", 42), ("MS", 43), ("MC", 44)):
+        c = (synth.mu_corpus if k == "MU" else synth.ms_corpus if k == "MS" else synth.mc_corpus)(P, per[k], seed=s)
+        bd = eng.to_device_mc(c) if k == "MC" else eng.to_device_pulses(c)
+        caps = {"MU": (12, 320), "MS": (4, 64), "MC": (4, 96)}[k]
+        o = eng.alloc_out(c.n, caps[0] * c.n + 4096, caps[1] * c.n + 65536, eng.pulses_work_bytes(c.n) if k != "MC" else 0)
+        if k == "MC":
+            eng.launch_mc(bd, o)
+        else:
+            eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, o)
+        parts.append((o["desc"], o["rec"], o["heap"], c.n, o["cursor"]))
+    torch.cuda.synchronize()
+    ex = sdist.Exchange.__new__(sdist.Exchange)
+    ex._bufs = {}
+    pt = [sdist._part_tuple(p) for p in parts]
+    s = torch.cuda.current_stream()
+    cnt = ex._count_pack_device(pt, s)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        cnt = ex._count_pack_device(pt, s)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    S = cnt.cpu().numpy().astype(np.int64).reshape(1, 3, 4)
+    offs, nb, T = sdist._layout(S)
+    wire = int(nb.sum())
+    src = sum(int(p[4][0]) * 16 + int(p[4][1]) + 8 * p[3] for p in parts)
+    tu = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for k in range(3):
+            sdist.unpack_device(ex._bufs["send"], S[:, k, :3], [offs[0, k]])
+        e1.record()
+        torch.cuda.synchronize()
+        tu.append(e0.elapsed_time(e1))
+    print(f"count+pack {np.median(ts) * 1e3:.1f} us (min {min(ts) * 1e3:.1f}); wire {wire / 1e6:.2f} MB "
+          f"(source desc+rec+heap {src / 1e6:.2f} MB); {wire / (min(ts) * 1e-3) / 1e9:.0f} GB/s of wire; "
+          f"unpack x3 (world 1, incl. host sync) {min(tu) * 1e3:.0f} us; counts {S[0].tolist()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

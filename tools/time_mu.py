@@ -33,7 +33,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         cur = out["cursor"].cpu().numpy()
-        res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) >> 20} MB)")
+        res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) * 112 >> 10} MB)")
     tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped")
     print(tag, " | ".join(res), flush=True)
 
