@@ -38,7 +38,7 @@ constexpr int XT = 256;       // threads per block; one message per thread in th
 constexpr int XB = XT;        // items per block
 constexpr int XMAX = 8;       // launches per exchange
 constexpr int XRANKS = SDX_XCHG_MAX_RANKS;
-constexpr int LREC = 1536;    // records of a pack block staged in LDS for the coalesced payload copy
+constexpr int LREC = 2048;    // records of a pack block listed in LDS for the coalesced payload copy
 constexpr uint64_t BADBIT = 1ull << 63;
 
 // Inter-block results travel through kernel boundaries only (count -> scan -> pack): a grid-wide
@@ -208,13 +208,12 @@ __device__ inline void zero_tail(uint8_t* sec, uint64_t used, uint32_t lane) {
 // block = 256 consecutive messages (the count blocks), grid.y = launch.
 // A (lane = message): the wire word, the wire records (contiguous per message) and the message's
 //   records' (source, destination, length) into an LDS list in output order;
-// B (lane = output dword of the block's payload range): the payload bytes, gathered through the
-//   list (binary search for the first byte's record), stored as coalesced dwords (byte stores only
-//   at the two ends of the range, which neighbouring blocks share).
+// B (lane = 32 consecutive output bytes of the block's payload range): one binary search for the
+//   first byte's record, a linear walk through the list, 32 independent source byte loads, two
+//   16-byte stores (byte stores only at the two ends of the range, which neighbouring blocks share).
 __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restrict__ counts,
                                                 uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
-  __shared__ uint32_t l_src[LREC], l_dst[LREC];
-  __shared__ uint16_t l_len[LREC];
+  __shared__ uint32_t l_src[LREC], l_dst[LREC + 1];
   const int k = blockIdx.y;
   const sdx_xchg_part& x = P.p[k];
   const uint32_t nb = nblk_of(x.n_msgs);
@@ -260,50 +259,67 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
         if (lr < LREC) {
           l_src[lr] = r4[i].payload_off;
           l_dst[lr] = lb;
-          l_len[lr] = r4[i].payload_len;
         } else {  // past the LDS list (a block of unusually many records): copy here, byte by byte
+          if (lr == LREC) l_dst[LREC] = lb;   // the list's end
           uint8_t* dst = s_heap + (uint32_t)boff + lb;
           const uint8_t* src = x.heap_dev + r4[i].payload_off;
-          for (uint32_t b = 0; b < r4[i].payload_len; ++b) dst[b] = src[b];
+          for (uint32_t q = 0; q < r4[i].payload_len; ++q) dst[q] = src[q];
         }
         ++lr;
         lb += r4[i].payload_len;
       }
     }
   }
-  __syncthreads();
-  // B: the block's payload range [G, G + lim) of the heap section, dword by dword
   const uint32_t nl = brec < LREC ? brec : LREC;
+  const uint32_t bbytes = (uint32_t)bnext - (uint32_t)boff;
+  if (threadIdx.x == 0 && nl == brec) l_dst[nl] = bbytes;   // the list's end (truncated lists: set above)
+  __syncthreads();
   if (nl == 0) return;
-  const uint32_t lim = nl ? l_dst[nl - 1] + l_len[nl - 1] : 0;   // bytes covered by the list
-  const uint64_t G = (uint64_t)(s_heap - send) + (uint32_t)boff;  // absolute offset in send
-  const uint64_t A0 = G & ~3ull, A1 = G + lim;
-  for (uint64_t a = A0 + 4ull * threadIdx.x; a < A1; a += 4ull * XT) {
-    // bytes [a, a + 4) -> block-local p = a - G + i
-    const int64_t p0 = (int64_t)(a - G);
-    uint32_t lo = 0, hi = nl - 1;   // the last record with l_dst <= max(p0, 0)
+#ifdef SDX_XP_NOB
+  return;
+#endif
+  // B: bytes [0, lim) of the block's range go through the list
+  const uint32_t lim = l_dst[nl];
+  const uint64_t G = so[2] + (uint32_t)boff;   // absolute offset of the block's first byte in send
+  const uint64_t A0 = G & ~15ull;               // 16-byte aligned 32-byte pieces
+  for (uint64_t a = A0 + 32ull * threadIdx.x; a < G + lim; a += 32ull * XT) {
+    const int64_t p0 = (int64_t)(a - G);        // block-local position of the piece's first byte
     const uint32_t q = p0 < 0 ? 0u : (uint32_t)p0;
+    uint32_t lo = 0, hi = nl - 1;               // the last record with l_dst <= q
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
       if (l_dst[mid] <= q) lo = mid;
       else hi = mid - 1;
     }
     uint32_t r = lo;
-    uint32_t word = 0, have = 0;
+    // source offsets first (LDS only), then 32 loads without control flow between them
+    uint32_t so32[32];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 32; ++i) {
       const int64_t p = p0 + i;
-      if (p < 0 || p >= (int64_t)lim) continue;
-      while ((uint32_t)p >= l_dst[r] + l_len[r]) ++r;   // empty payloads are skipped here too
-      word |= (uint32_t)x.heap_dev[l_src[r] + ((uint32_t)p - l_dst[r])] << (8 * i);
-      have |= 1u << i;
+      so32[i] = 0;  // heap[0]: a harmless in-bounds read for bytes outside the list's range
+      if (p >= 0 && p < (int64_t)lim) {
+        while (r + 1 < nl && (uint32_t)p >= l_dst[r + 1]) ++r;   // zero-length payloads are passed over
+        so32[i] = l_src[r] + ((uint32_t)p - l_dst[r]);
+      }
     }
-    if (have == 0xFu) {
-      *reinterpret_cast<uint32_t*>(send + a) = word;
+    uint8_t bb[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) bb[i] = x.heap_dev[so32[i]];
+    uint32_t wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      wv[i] = (uint32_t)bb[4 * i] | ((uint32_t)bb[4 * i + 1] << 8) | ((uint32_t)bb[4 * i + 2] << 16) |
+              ((uint32_t)bb[4 * i + 3] << 24);
+    if (p0 >= 0 && p0 + 32 <= (int64_t)lim) {
+      reinterpret_cast<uint4*>(send + a)[0] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      reinterpret_cast<uint4*>(send + a)[1] = make_uint4(wv[4], wv[5], wv[6], wv[7]);
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (have & (1u << i)) send[a + i] = (uint8_t)(word >> (8 * i));
+      for (int i = 0; i < 32; ++i) {
+        const int64_t p = p0 + i;
+        if (p >= 0 && p < (int64_t)lim) send[a + i] = bb[i];
+      }
     }
   }
 }
