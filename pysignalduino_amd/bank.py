@@ -264,6 +264,29 @@ def _gap_ranks(v: float, klo: int, khi: int) -> List[int]:
     return [order[g] for g in gaps]
 
 
+# Per-protocol work of the MU protocol loop in thousands of wave-cycles per 64-message tile on the
+# bench corpus (tools/prof_phases.py, r03; group cost minus one normalisation, split evenly over the
+# group's protocols), and the normalisation's cost per group: the work-list order of Bank (LPT).
+MU_NORM_KCYC = 3.8
+MU_COST_KCYC = {
+    "15": 19.3, "121": 18.1, "34": 16.2, "120": 14.6, "9": 14.6, "111": 14.6, "118.1": 11.9, "118": 11.9,
+    "8": 11.7, "39": 11.1, "1": 11.1, "86": 11.0, "14": 11.0, "25": 11.0, "13": 10.9, "63": 10.9, "13.1": 10.9,
+    "130": 10.4, "33.2": 10.4, "91": 10.4, "74": 10.4, "88": 10.4, "87": 10.4, "21": 10.4, "82": 10.4,
+    "70": 10.4, "61": 10.4, "80": 10.4, "74.1": 10.4, "91.1": 10.4, "73": 10.4, "40": 10.2, "72": 9.9,
+    "72.1": 9.9, "135": 9.8, "27": 9.8, "71": 9.4, "20": 8.6, "20.1": 8.6, "64": 8.4, "55": 7.7, "19": 7.7,
+    "7.1": 7.7, "90": 7.6, "16": 7.6, "35": 7.6, "54": 7.5, "77": 7.5, "78": 7.5, "85": 7.5, "54.1": 7.5,
+    "89": 7.5, "38": 7.5, "97": 7.5, "113": 7.5, "37": 7.5, "48": 7.5, "92": 7.2, "75": 7.1, "41": 7.1,
+    "106": 7.1, "33": 7.1, "5": 7.1, "44.1": 7.1, "51": 7.1, "2": 7.1, "42": 7.1, "50": 7.1, "44": 7.1,
+    "81": 7.1, "98": 7.1, "36": 7.1, "76": 7.1, "99": 7.1, "104": 7.1, "93": 6.8, "31": 6.8, "127": 6.7,
+    "127.1": 6.7, "45": 6.5, "110": 6.1, "128": 5.9, "128.1": 5.9, "68": 5.9, "84": 5.9, "53": 5.7, "28": 5.7,
+    "49.2": 5.6, "49": 5.6, "6": 5.5, "7": 5.4, "95": 5.4, "26": 5.4, "122": 5.4, "56": 5.1, "23": 5.1,
+    "114": 5.1, "22": 5.1, "65": 4.9, "17.1": 4.9, "59": 4.9, "13.2": 4.7, "30": 4.6, "105": 4.6, "132": 4.6,
+    "79": 4.6, "33.1": 4.6, "67": 4.2, "66": 4.2, "60": 4.2, "83": 4.2, "46": 4.1, "94": 4.1, "29": 4.1,
+    "0.5": 4.0, "69": 3.8, "0.4": 3.8, "49.1": 3.7, "32": 3.3, "62": 3.0, "0.2": 2.7, "0.1": 2.7, "3": 2.7,
+    "4": 2.7, "3.1": 2.7, "17": 2.7, "0.3": 2.7, "0": 2.7, "24": 1.9
+}
+
+
 class Bank:
     """A compiled bank: the device blob plus host-side metadata for result building."""
 
@@ -581,10 +604,20 @@ class Bank:
         # MU sorted by clock so consecutive protocols reuse the normalised patterns
         # MU: clock groups (one normalisation per group and tile), largest group first so that the
         # waves' dynamic grabbing ends on small groups; group g = mu_order[gstart[g]:gstart[g+1]]
+        # Groups are taken in descending estimated cost (longest-processing-time first): the cost of a
+        # group is one normalisation plus its protocols' filter + decode costs, MU_COST_KCYC
+        # (profile-guided, tools/prof_phases.py per-group cycles on the bench corpus; protocols
+        # missing from the table count as the table's median).  Scheduling only: results are placed
+        # by protocol index.
         groups: Dict[float, List[int]] = {}
         for r in range(len(self.mu_pids)):
             groups.setdefault(float(mu[r]["clock"]), []).append(r)
-        glist = sorted(groups.values(), key=lambda g: -len(g))
+        med = float(np.median(list(MU_COST_KCYC.values())))
+        gcost = lambda g: MU_NORM_KCYC + sum(MU_COST_KCYC.get(str(self.mu_pids[r]), med) for r in g)  # noqa: E731
+        if os.environ.get("SDX_MU_ORDER") == "size":   # A/B: the round-2 order (largest group first)
+            glist = sorted(groups.values(), key=lambda g: -len(g))
+        else:
+            glist = sorted(groups.values(), key=lambda g: (-gcost(g), -len(g)))
         self.mu_order = [r for g in glist for r in g]
         self.mu_gstart = list(np.cumsum([0] + [len(g) for g in glist]))
         self.ms_order = list(range(len(self.ms_pids)))

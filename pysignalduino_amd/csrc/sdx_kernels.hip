@@ -32,6 +32,7 @@ __device__ unsigned long long g_wgt[2 * 65536];
 #endif
 #ifdef SDX_PROF
 __device__ unsigned long long g_prof[32];
+__device__ unsigned long long g_gprof[2][128];  // per MU clock group / MS protocol: wave-cycles, grabs
 #define PROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, v)                                                                   \
   do {                                                                                      \
@@ -1886,11 +1887,23 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   const int ngrab = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu_groups : nproto;
   const uint16_t* gstart = bv.order + bv.hdr->n_mu + bv.hdr->n_ms;
   int cur = 0, cend = 0;
+#ifdef SDX_PROF
+  int g_cur = -1;
+  unsigned long long g_t0 = 0;
+#endif
   while (true) {
     if (cur == cend) {
       int g = 0;
       if (lane == 0) g = atomicAdd(&L.next_p, 1);
       g = __builtin_amdgcn_readfirstlane(g);
+#ifdef SDX_PROF
+      if (g_cur >= 0 && g_cur < 128 && lane == 0) {
+        atomicAdd(&g_gprof[0][g_cur], __builtin_amdgcn_s_memtime() - g_t0);
+        atomicAdd(&g_gprof[1][g_cur], 1ull);
+      }
+      g_cur = g;
+      g_t0 = __builtin_amdgcn_s_memtime();
+#endif
       if (g >= ngrab) break;
       if (KIND == SDX_KIND_MU) {
         cur = cld(&gstart[g]);
@@ -2529,6 +2542,14 @@ extern "C" {
 int sdx_abi_version(void) { return SDX_ABI_VERSION; }
 
 #ifdef SDX_PROF
+int sdx_gprof_read(unsigned long long* out256, int reset) {
+  HIPCHK(hipMemcpyFromSymbol(out256, HIP_SYMBOL(g_gprof), sizeof(unsigned long long) * 256));
+  if (reset) {
+    unsigned long long z[256] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_gprof), z, sizeof z));
+  }
+  return SDX_OK;
+}
 int sdx_prof_read(unsigned long long* out32, int reset) {
   HIPCHK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 32));
   if (reset) {

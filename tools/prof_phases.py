@@ -23,6 +23,7 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 333333
     lib = runtime.load_library()
     lib.sdx_prof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    lib.sdx_gprof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     bk = bankmod.Bank()
     eng = runtime.Engine(bk, 0)
     buf = (ctypes.c_ulonglong * 32)()
@@ -34,6 +35,7 @@ def main():
         eng.launch_pulses(k, bd, out)
         torch.cuda.synchronize()
         lib.sdx_prof_read(buf, 1)
+        lib.sdx_gprof_read((ctypes.c_ulonglong * 256)(), 1)
         out["cursor"].zero_()
         t = time.perf_counter()
         eng.launch_pulses(k, bd, out)
@@ -41,6 +43,8 @@ def main():
         dt = time.perf_counter() - t
         lib.sdx_prof_read(buf, 1)
         v = np.array(list(buf), dtype=np.float64)
+        gb = (ctypes.c_ulonglong * 256)()
+        lib.sdx_gprof_read(gb, 1)
         tot = v[15]
         print(f"== {kind}: {pb.n} msgs, {dt*1e3:.2f} ms wall; wave-cycles total {tot:.3e} "
               f"({tot/pb.n:.0f} per message)")
@@ -51,6 +55,13 @@ def main():
                 print(f"  {NAMES[i]:28s} {v[i]:.0f}  ({v[i]/pb.n:.2f} per message)")
             else:
                 print(f"  {NAMES[i]:28s} {v[i]/tot*100:6.2f} %   {v[i]/pb.n:9.0f} wave-cycles/msg")
+        g = np.array(list(gb), dtype=np.float64).reshape(2, 128)
+        unit = "clock group" if kind == "MU" else "protocol"
+        order = np.argsort(-g[0])
+        print(f"  per {unit} (processing order index: share of the work-loop cycles, cycles per grab):")
+        tot_g = g[0].sum()
+        print("   " + " ".join(f"{int(i)}:{g[0, i] / tot_g * 100:.1f}%/{g[0, i] / max(g[1, i], 1):.0f}"
+                              for i in order if g[1, i] > 0))
 
 
 if __name__ == "__main__":

@@ -34,7 +34,7 @@ def main():
             ts.append(e0.elapsed_time(e1))
         cur = out["cursor"].cpu().numpy()
         res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) * 112 >> 10} MB)")
-    tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped")
+    tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped") + (" order=" + os.environ.get("SDX_MU_ORDER", "lpt"))
     print(tag, " | ".join(res), flush=True)
 
 
