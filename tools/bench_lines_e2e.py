@@ -117,8 +117,25 @@ def main():
             results[0] = (host_out[s][: T + 2 * C].numpy().copy(), offs, nb, T)
 
     nsteps = nck * args.passes
+    h2d_ev = [None] * 2
+
+    def enqueue_h2d(k):
+        """chunk k's lines to slot k % 2 (its line buffers are free once chunk k-2's parse read them)."""
+        nonlocal h2d_bytes
+        s, c = k % 2, k % nck
+        with torch.cuda.stream(cin):
+            if parse_done[s] is not None:
+                cin.wait_event(parse_done[s])
+            lbs[s].bytes[: hb[c].numel()].copy_(hb[c], non_blocking=True)
+            lbs[s].offsets.copy_(ho[c], non_blocking=True)
+            e = ev()
+            e.record(cin)
+            h2d_ev[s] = e
+        h2d_bytes += int(hb[c].numel()) + 8 * (C + 1)
+
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    enqueue_h2d(0)
     for k in range(nsteps):
         s, c = k % 2, k % nck
         lb = lbs[s]
@@ -126,18 +143,9 @@ def main():
         #    kind/status and wire buffer, which chunk k overwrites below
         if k >= 2:
             enqueue_d2h(k - 2)
-        # 1. H2D of chunk k (slot s's line buffers are free once chunk k-2's parse has read them)
-        with torch.cuda.stream(cin):
-            if parse_done[s] is not None:
-                cin.wait_event(parse_done[s])
-            lb.bytes[: hb[c].numel()].copy_(hb[c], non_blocking=True)
-            lb.offsets.copy_(ho[c], non_blocking=True)
-            h2d = ev()
-            h2d.record(cin)
-        h2d_bytes += int(hb[c].numel()) + 8 * (C + 1)
-        # 2. parse + select (slot s's parse outputs are free once chunk k-2's demodulation ran)
+        # 1. parse + select (slot s's parse outputs are free once chunk k-2's demodulation ran)
         with torch.cuda.stream(sp):
-            sp.wait_event(h2d)
+            sp.wait_event(h2d_ev[s])
             if demod_done[s] is not None:
                 sp.wait_event(demod_done[s])
             if d2h_done[s] is not None:
@@ -152,6 +160,9 @@ def main():
             counts_ev[s] = ce
             parse_done[s] = e1
             tev.setdefault("parse", []).append((e0, e1))
+        # 2. chunk k+1's H2D, ahead of the wait below: it overlaps chunk k's parse and demodulation
+        if k + 1 < nsteps:
+            enqueue_h2d(k + 1)
         # 3. demodulate + serialise chunk k (the class counts size the launches)
         ce.synchronize()
         cnt = host_counts[s].numpy()[: runtime.SEL_NCLASS].copy()
