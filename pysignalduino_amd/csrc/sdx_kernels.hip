@@ -1350,30 +1350,39 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
     }
   __syncthreads();
   const uint32_t nh_l16 = ((uint32_t)nh_l + 15u) & ~15u;
-  if (tid == 0) {
-    int bad = ovf ? 1 : 0;
-    uint32_t nrec = 0;
-    for (int m = 0; m < nvalid; ++m) {
-      L.mbase[m] = nrec;
-      if (L.raise_key[m] == 0xFFFFFFFFu && !bad) nrec += cntm[m];
+  static_assert(TM <= 64, "one wave scans the tile's messages");
+  if (tid < 64) {  // wave 0, lane = message: the record base of every message (exclusive scan)
+    const int lane = tid;
+    const bool live = !ovf && lane < nvalid && L.raise_key[lane] == 0xFFFFFFFFu;
+    const uint32_t c = live ? cntm[lane] : 0u;
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
     }
+    if (lane < nvalid) L.mbase[lane] = x - c;
+    const uint32_t nrec = __shfl(x, 63);
     // 16-B pieces: full-width copies
-    const uint32_t nheap = bad ? 0u : nh_l16 + (((uint32_t)nh_s + 15u) & ~15u);
-    uint32_t rb = 0, hb = 0;
-    if (!bad) {
-      rb = atomicAdd(&out.cursor_dev[0], nrec);
-      hb = atomicAdd(&out.cursor_dev[1], nheap);
-      if (rb + nrec > out.rec_cap || hb + nheap > out.heap_cap) {
-        bad = 2;
-        atomicOr(&out.cursor_dev[2], 1u);
+    const uint32_t nheap = ovf ? 0u : nh_l16 + (((uint32_t)nh_s + 15u) & ~15u);
+    uint32_t got = 0;  // both cursors reserved by one instruction (lanes 0 and 1)
+    if (!ovf && lane < 2) got = atomicAdd(&out.cursor_dev[lane], lane == 0 ? nrec : nheap);
+    const uint32_t rb = __shfl(got, 0), hb = __shfl(got, 1);
+    if (lane == 0) {
+      int bad = ovf ? 1 : 0;
+      if (!bad) {
+        if (rb + nrec > out.rec_cap || hb + nheap > out.heap_cap) {
+          bad = 2;
+          atomicOr(&out.cursor_dev[2], 1u);
+        }
+      } else {
+        atomicOr(&out.cursor_dev[2], 2u);
       }
-    } else {
-      atomicOr(&out.cursor_dev[2], 2u);
+      L.tile_bad = bad;
+      L.rec_base = rb;
+      L.heap_base = hb;
+      L.tot_rec = nrec;
     }
-    L.tile_bad = bad;
-    L.rec_base = rb;
-    L.heap_base = hb;
-    L.tot_rec = nrec;
   }
   __syncthreads();
   const int bad = L.tile_bad;  // block-uniform
@@ -2124,6 +2133,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     PROF_T(t_dec);
     const int ns = L.nsurv < MS_SURV_CAP ? L.nsurv : MS_SURV_CAP;
     if (!L.ovf) {
+      // survivors packed into the first waves (dealing them round-robin over all 8 measured
+      // 0.73 vs 0.645 ms: more waves on the same divergent decode path)
       for (int i = tid; i < ns; i += blockDim.x) {
         const MsItem it = L.slist[i];
         const int qm = it.mi, qp = it.p;
