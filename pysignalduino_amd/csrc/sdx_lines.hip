@@ -30,6 +30,19 @@ namespace sdxl {
 
 #define LD __device__ __forceinline__
 
+#ifdef SDX_LPROF  // k_parse_comp phase profile (variant builds only): per-lane s_memtime deltas
+__device__ unsigned long long g_lprof[16];
+#define LP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define LP_ADD(slot, t0) lp[slot] += __builtin_amdgcn_s_memtime() - (t0)
+#define LP_ARG , unsigned long long* lp
+#define LP_PASS , lp
+#else
+#define LP_T(v)
+#define LP_ADD(slot, t0)
+#define LP_ARG
+#define LP_PASS
+#endif
+
 struct Str {
   const uint8_t* p;
   int n;
@@ -89,18 +102,91 @@ struct Writer8 {
     } while (v);
     while (k) put((uint8_t)t[--k]);
   }
+  // 8 characters (x's bytes, lowest first): one aligned 8-byte store, the characters that spill
+  // into the next word stay in acc
+  LD void put8(uint64_t x) {
+    if (head || n + 8 > cap) {
+      for (int t = 0; t < 8; ++t) put((uint8_t)(x >> (8 * t)));
+      return;
+    }
+    n += 8;
+    if (fill == 0) {
+      *reinterpret_cast<uint64_t*>(w) = x;
+    } else {
+      *reinterpret_cast<uint64_t*>(w) = acc | (x << (8 * fill));
+      acc = x >> (64 - 8 * fill);
+    }
+    w += 8;
+  }
   LD void finish() {
     for (int k = head; k < fill; ++k) w[k] = (uint8_t)(acc >> (8 * k));
     fill = head = 0;
   }
+  LD void mark_d(bool) {}
 };
+
+// appends bytes to a lane's LDS buffer: one byte store per character, no word assembly (the
+// assembling Writer8's flush branch diverges across a wave's lanes on almost every character)
+struct LdsWriter {
+  uint8_t* p;
+  int n, cap;
+  bool ovf;
+  LD LdsWriter(uint8_t* dst, int capacity) : p(dst), n(0), cap(capacity), ovf(false) {}
+  LD void put(uint8_t c) {
+    if (n < cap) p[n] = c;
+    else ovf = true;
+    ++n;
+  }
+  LD void put_uint(uint32_t v) {
+    char t[10];
+    int k = 0;
+    do {
+      t[k++] = (char)('0' + v % 10);
+      v /= 10;
+    } while (v);
+    while (k) put((uint8_t)t[--k]);
+  }
+  LD void put8(uint64_t x) {
+    for (int t = 0; t < 8; ++t) put((uint8_t)(x >> (8 * t)));
+  }
+  LD void finish() {}
+  LD void mark_d(bool) {}
+};
+
+// the first ';' at or after s, or P.n: aligned 8-byte words, SWAR ';' test (no byte at or after
+// P.n counts; the words read are the ones holding bytes of [s, P.n))
+LD int find_semi(const Str& P, int s) {
+  if (s >= P.n) return P.n;
+  const uint8_t* q = P.p + s;
+  const int al = (int)((uintptr_t)q & 7);
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(q - al);
+  int base = s - al;
+  uint64_t x = *w;
+  uint64_t valid = ~0ull << (8 * al);  // bytes of the first word before s do not count
+  while (true) {
+    const uint64_t t = x ^ 0x3B3B3B3B3B3B3B3Bull;
+    uint64_t z = ~(((t & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | t) & 0x8080808080808080ull;
+    z &= valid;
+    const int left = P.n - base;  // bytes of this word inside P (> 0)
+    if (left < 8) z &= ~0ull >> (64 - 8 * left);
+    if (z) return base + (__builtin_ctzll(z) >> 3);
+    if (left <= 8) return P.n;
+    base += 8;
+    x = *++w;
+    valid = ~0ull;
+  }
+}
 
 // next non-empty ';'-separated part at or after pos: [s, e); returns false at the end
 LD bool next_part(const Str& P, int& pos, int& s, int& e) {
   while (pos <= P.n) {
     s = pos;
+#ifdef SDX_NEXTPART_BYTES
     e = s;
     while (e < P.n && P.p[e] != ';') ++e;
+#else
+    e = find_semi(P, s);
+#endif
     pos = e + 1;
     if (e > s) return true;
   }
@@ -126,7 +212,8 @@ LD bool d_field(const Str& P, int s, int e) {
 // decompress_payload (base.py:13-186) into w; returns false when an upper() of a non-ASCII
 // character would be needed (UNSUPPORTED)
 // one non-D part of decompress_payload (base.py:142-181); false: str.upper() of a non-ASCII byte
-LD bool dec_part(const Str& P, int s, int e, Writer8& w) {
+template <class W>
+LD bool dec_part(const Str& P, int s, int e, W& w) {
   const uint8_t m0 = P.p[s];
   const int m1s = s + 1, m1n = e - s - 1;
   if (m0 == 'M') {  // :144-146
@@ -174,11 +261,21 @@ LD bool dec_emits(const Str& P, int s, int e) {
 }
 
 // a D/d part (:59-140) starting at part [s, e); pos = where the part loop resumes
-LD void dec_data(const Str& P, int s, int e, int& pos, Writer8& w) {
+// four data bytes c (all < 0x80) -> the eight characters '0' + (c >> 4), '0' + (c & 7), in order
+LD uint64_t expand_word(uint32_t v) {
+  uint64_t y = v;
+  y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
+  y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;  // byte t -> the low byte of 16-bit lane t
+  return ((y >> 4) & 0x000F000F000F000Full) | ((y & 0x0007000700070007ull) << 8) | 0x3030303030303030ull;
+}
+
+template <class W>
+LD void dec_data(const Str& P, int s, int e, int& pos, W& w) {
   const uint8_t m0 = P.p[s];
   const int m1s = s + 1;
   w.put('D');
   w.put('=');
+  w.mark_d(true);
   // extent: the first part plus the following parts that do not start a field
   int lastend = e, j = pos, s2, e2;
   while (true) {
@@ -204,6 +301,17 @@ LD void dec_data(const Str& P, int s, int e, int& pos, Writer8& w) {
   const uint64_t* wp = reinterpret_cast<const uint64_t*>(q - al);
   for (int k0 = m1s - al; k0 < lastend; k0 += 8) {
     const uint64_t x = *wp++;
+    // a whole word inside the value, past its first character, not the last one of a 'd' part,
+    // no byte >= 0x80 and no ';': two characters per byte, '0' + (c >> 4) and '0' + (c & 7)
+    const uint64_t ts = x ^ 0x3B3B3B3B3B3B3B3Bull;
+    const uint64_t semi = ~(((ts & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | ts) & 0x8080808080808080ull;
+    if (!firstc && k0 >= m1s && k0 + 8 <= lastend && !(m0 == 'd' && k0 + 8 == lastend) &&
+        ((x & 0x8080808080808080ull) | semi) == 0) {
+      w.put8(expand_word((uint32_t)x));
+      w.put8(expand_word((uint32_t)(x >> 32)));
+      prev = (uint8_t)(x >> 56);
+      continue;
+    }
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const int k = k0 + b;
@@ -223,12 +331,14 @@ LD void dec_data(const Str& P, int s, int e, int& pos, Writer8& w) {
       if (!(m0 == 'd' && k == lastend - 1)) w.put((uint8_t)('0' + (c & 0x7)));
     }
   }
+  w.mark_d(false);
 }
 
 // decompress_payload (base.py:13-186) of a payload that has a byte > 127 after its header.  The
 // parts before the first D/d part, that part, and the rest are three loops, so that the lanes of
 // a wave expand their (long) data parts together.
-LD bool decompress(const Str& P, Writer8& w) {
+template <class W>
+LD bool decompress(const Str& P, W& w) {
   int pos = 0, s = 0, e = 0;
   bool first = true, dpart = false;
   while (next_part(P, pos, s, e)) {  // parts before the data
@@ -1136,9 +1246,69 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(6))) void k_
   }
 }
 
-// one compressed line (ST_RARE): extract_payload's checks, decompress_payload into the line's slot,
-// then the fast path on the decompressed payload with the general parser behind it
-LD void parse_compressed(const sdx_lines& in, const sdx_lines_out& out, int i, uint32_t* pvt) {
+// decompress_payload's output goes to the slot (RawFrame.line) and, without the characters of
+// the data value, to a lane-private LDS "skeleton": the parse runs on the skeleton, so the payload
+// is never read back from the slot.  The data value is all digits (dec_data emits nothing else);
+// the skeleton keeps min(n, 2) of them -- every decision fast_payload takes on the value
+// (n >= 2 for MU, n >= 1 for MS, digits only) is the same on both -- and its length travels
+// beside.  Anything else (a second data part, a skeleton past its buffer, data longer than
+// SDX_LONG_MAX, a payload the fast path declines) is parsed from the slot as before.
+constexpr int SKEL = 136;  // skeleton bytes per lane (8 * 17: lanes spread over the LDS banks)
+#ifdef SDX_NO_SKEL
+constexpr bool kSkel = false;  // A/B: parse from the slot
+#else
+constexpr bool kSkel = true;
+#endif
+struct SkelWriter {
+  Writer8 g;    // the slot
+  LdsWriter k;  // the skeleton
+  bool in_d = false;
+  int nd = 0, dlen = 0;  // data parts, characters of the data value
+  int n = 0;
+  bool ovf = false;
+  // scans read up to 7 bytes past the skeleton's end (the aligned word holding its last byte)
+  LD SkelWriter(uint8_t* slot, int cap, uint8_t* skel) : g(slot, cap), k(skel, SKEL - 8) {}
+  LD void put(uint8_t c) {
+    g.put(c);
+    if (!in_d || dlen < 2) k.put(c);
+    dlen += in_d ? 1 : 0;
+    n = g.n;
+    ovf = g.ovf;
+  }
+  LD void put_uint(uint32_t v) {
+    char t[10];
+    int q = 0;
+    do {
+      t[q++] = (char)('0' + v % 10);
+      v /= 10;
+    } while (v);
+    while (q) put((uint8_t)t[--q]);
+  }
+  LD void put8(uint64_t x) {
+    if (!in_d || dlen < 2) {  // the skeleton takes (some of) these
+      for (int t = 0; t < 8; ++t) put((uint8_t)(x >> (8 * t)));
+      return;
+    }
+    g.put8(x);
+    dlen += 8;
+    n = g.n;
+    ovf = g.ovf;
+  }
+  LD void mark_d(bool on) {
+    in_d = on;
+    if (on) {
+      ++nd;
+      dlen = 0;
+    }
+  }
+  LD void finish() { g.finish(); }
+};
+
+// one compressed line (ST_RARE): extract_payload's checks, decompress_payload into the line's slot
+// (and the skeleton), then the fast path on the skeleton, or on the slot with the general parser
+// behind it
+LD void parse_compressed(const sdx_lines& in, const sdx_lines_out& out, int i, uint32_t* pvt, uint8_t* skel LP_ARG) {
+  LP_T(t0);
   const int64_t lo = in.offsets_dev[i];
   const int len = (int)(in.offsets_dev[i + 1] - lo);
   const uint8_t* L = in.bytes_dev + lo;
@@ -1149,41 +1319,81 @@ LD void parse_compressed(const sdx_lines& in, const sdx_lines_out& out, int i, u
   int plen = -1;
   int64_t doff = 3 * lo;
   bool comp = false;
-  if (!frame_check(L, a, b, comp)) {
+  const bool framed = frame_check(L, a, b, comp);
+  LP_ADD(1, t0);
+  if (!framed) {
     r.status = SDX_LS_NOFRAME;
   } else {  // comp holds: the first payload byte, or another one, has the high bit set
-    Writer8 w(out.slot_dev + 3 * lo, 3 * len);
-    if (!(decompress(Str{L + a + 1, b - a - 2}, w) && !w.ovf)) {
+    LP_T(t1);
+    SkelWriter w(out.slot_dev + 3 * lo, 3 * len, skel);
+    const bool dec = decompress(Str{L + a + 1, b - a - 2}, w);
+    LP_ADD(2, t1);
+    if (!(dec && !w.g.ovf)) {
       r.status = SDX_LS_UNSUPPORTED;
     } else {
-      plen = w.n;
-      const Str P{out.slot_dev + 3 * lo, w.n};
-      const uint8_t ty = P.n > 1 ? P.p[1] : 0;
-      if (!((ty == 'U' || ty == 'S' || ty == 'C') && fast_payload(P.p, P.n, r, out, i))) parse_payload(P, r, out, i, pvt);
-      if (r.status == SDX_LS_OK || r.status == SDX_LS_GENERAL) {
-        finish_fields(P, r, out, i);
+      plen = w.g.n;
+      const Str P{out.slot_dev + 3 * lo, w.g.n};
+      const Str K{skel, w.k.n};
+      const uint8_t ty = K.n > 1 ? K.p[1] : 0;
+      LP_T(t2);
+      bool fast = false;
+      if (kSkel && !w.k.ovf && w.nd == 1 && w.dlen <= SDX_LONG_MAX && (ty == 'U' || ty == 'S') && fast_payload(K.p, K.n, r, out, i)) {
+        fast = true;
+        r.dE = r.dS + w.dlen;  // the data value's real extent (its position is the skeleton's)
+        finish_fields(K, r, out, i);
         doff = 3 * lo + r.dS;
+      }
+      LP_ADD(3, t2);
+      if (!fast) {
+        LP_T(t3);
+        r = LineRes{};
+        const uint8_t tp = P.n > 1 ? P.p[1] : 0;
+        if (!((tp == 'U' || tp == 'S' || tp == 'C') && fast_payload(P.p, P.n, r, out, i))) parse_payload(P, r, out, i, pvt);
+        if (r.status == SDX_LS_OK || r.status == SDX_LS_GENERAL) {
+          finish_fields(P, r, out, i);
+          doff = 3 * lo + r.dS;
+        }
+        LP_ADD(4, t3);
+#ifdef SDX_LPROF
+        lp[8] += 1;
+#endif
       }
     }
   }
+  LP_T(t5);
   out.doff_dev[i] = doff;
   out.plen_dev[i] = plen;
   out.kind_dev[i] = r.kind;
   out.status_dev[i] = r.status;
+  LP_ADD(6, t5);
+#ifdef SDX_LPROF
+  lp[9] += 1;
+#endif
 }
 
 // the lines k_parse_lines left to it (ST_RARE): each wave scans `chunk` lines (a multiple of 64),
 // queues the compressed ones in LDS and parses them 64 at a time (lane = line), so the
 // decompression work of the ~20 % compressed lines of a mixed stream runs on full waves.  A wave's
 // time is about one line's serial decompress + parse, so the host sizes `chunk` for the grid to fit
-// the GPU's resident waves in one round (comp_chunk below)
+// the GPU's resident waves in one round (comp_chunk below).  Measured alternative: staging the raw
+// lines and the decompressed payloads in 38 KB of LDS per wave (1 wave/SIMD) ran 1.74 vs 1.13 ms
+// for the parse (profiles/r03/lines_comp_ab.log): the per-lane work is issue-bound, and needs
+// the 4 waves/SIMD this layout keeps.
 constexpr int COMP_CHUNK = 192;         // lower bound of the chunk (~40 compressed at the bench mix)
-constexpr int COMP_WAVES_PER_CU = 16;   // k_parse_comp: 118 VGPRs -> 4 waves/SIMD
-__global__ __launch_bounds__(256) void k_parse_comp(sdx_lines in, sdx_lines_out out, int chunk) {
-  __shared__ uint32_t pv[4][10 * 64];
+constexpr int COMP_WAVES_PER_CU = 16;   // 4 waves/SIMD (VGPRs; LDS 36.8 KB per 4-wave block)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_parse_comp(sdx_lines in, sdx_lines_out out, int chunk) {
   __shared__ int q[4][128];
+  __shared__ uint64_t sk[4][64][SKEL / 8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* pvt = pv[wave] + lane;
+  uint8_t* skel = reinterpret_cast<uint8_t*>(sk[wave][lane]);
+  // parse_payload's P-key table (10 x 64 words per wave) aliases the wave's skeletons: it is used
+  // only after every lane of the wave has left its skeleton (parse_compressed's second block)
+  static_assert(10 * 64 * 4 <= 64 * SKEL, "the P-key table fits the wave's skeletons");
+  uint32_t* pvt = reinterpret_cast<uint32_t*>(sk[wave]) + lane;
+#ifdef SDX_LPROF
+  unsigned long long lp[16] = {};
+  const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
+#endif
   const int64_t base = ((int64_t)blockIdx.x * 4 + wave) * chunk;
   int qn = 0;
   for (int c = 0; c < chunk; c += 64) {
@@ -1201,17 +1411,28 @@ __global__ __launch_bounds__(256) void k_parse_comp(sdx_lines in, sdx_lines_out 
       __builtin_amdgcn_wave_barrier();
       if (lane < qn - 64) q[wave][lane] = rest;
       qn -= 64;
-      parse_compressed(in, out, li, pvt);
+      parse_compressed(in, out, li, pvt, skel LP_PASS);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
   }
-  if (lane < qn) parse_compressed(in, out, q[wave][lane], pvt);
+  if (lane < qn) parse_compressed(in, out, q[wave][lane], pvt, skel LP_PASS);
+#ifdef SDX_LPROF
+  lp[0] = __builtin_amdgcn_s_memtime() - tk0;  // the wave's whole time
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {  // phases: max over lanes (the wave runs while any lane does); counts: sum
+    unsigned long long v = lp[k];
+    for (int o = 32; o; o >>= 1) {
+      const unsigned long long y = (unsigned long long)__shfl_xor((long long)v, o);
+      v = k >= 8 ? v + y : (y > v ? y : v);
+    }
+    if (lane == 0) atomicAdd(&g_lprof[k], v);
+  }
+#endif
 }
 
 // lines per k_parse_comp wave: at least COMP_CHUNK, and enough that the grid's waves fit the
-// device's resident waves in one round (1M lines on 256 CUs: 256 -> 3907 waves <= 4096; the fixed
-// 192 needed 5208 waves, a second round 27 % full)
+// device's resident waves in one round
 int comp_chunk(int n) {
   int dev = 0, cu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -1475,6 +1696,17 @@ extern "C" int sdx_select_lines(const sdx_lines_out* out, int32_t n, int32_t* se
   if (e != hipSuccess) return sdx::set_error(SDX_EHIP, std::string("sdx_select_lines: ") + hipGetErrorString(e));
   return SDX_OK;
 }
+
+#ifdef SDX_LPROF
+extern "C" int sdx_lprof_read(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(sdxl::g_lprof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sdxl::g_lprof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 extern "C" int sdx_parse_lines(const sdx_lines* lines, const sdx_lines_out* out, void* hip_stream) {
   if (!lines || !out || lines->n < 0) return sdx::set_error(SDX_EINVAL, "sdx_parse_lines: bad arguments");

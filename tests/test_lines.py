@@ -222,6 +222,37 @@ def test_parse_lines_long_and_multi_chunk():
     _check_selection(lines, dv)
 
 
+@pytest.mark.gpu
+def test_parse_comp_lds_buffer_edges():
+    """k_parse_comp stages a compressed line (<= 176 raw bytes) and its decompressed payload
+    (<= 344 bytes) in per-lane LDS buffers; lines past either bound take the global path.  A batch
+    of compressed lines on both sides of both bounds, interleaved, matches the oracle."""
+    P = B.Bank().protocols
+    lines = []
+    for k, npulse in enumerate((200, 240, 260, 280, 300, 320, 360, 600)):
+        ls, _ = synth.line_corpus(P, 240, seed=50 + k, mix=(1, 1, 0), compress_frac=1.0, mu_npulse=npulse)
+        lines += ls
+    # data bytes with a high nibble >= 10 expand to three characters: short raw lines whose
+    # payload passes 344 bytes
+    pp = bytes([0x80 | 0, 0x80 | 0x74, 0x80 | 1]) + b";" + bytes([0x80 | 0x20 | 1, 0x80 | 0x58, 0x80 | 15]) + b";"
+    for nd in (90, 100, 105, 110, 115, 120, 130, 140, 150, 160):
+        for t in (b"u", b"s"):
+            d = bytes((0xA0 + 17 * j) & 0xF7 | 0xA0 for j in range(nd))
+            lines.append(synth.frame(b"M" + t + b";" + pp + b"D" + d + b";C0;" + (b"S1;" if t == b"s" else b"") + b"R2A;"))
+    rng = np.random.default_rng(5)
+    lines = [lines[j] for j in rng.permutation(len(lines))]
+    comp = [ln for ln in lines if any(c > 127 for c in ln)]
+    raw_fit = [len(ln) <= 176 for ln in comp]
+    plens = [LO.parse_line(ln)["plen"] for ln in comp]
+    assert sum(1 for f, p in zip(raw_fit, plens) if f and 0 <= p <= 344) > 100
+    assert sum(1 for f, p in zip(raw_fit, plens) if f and p > 344) > 10  # payload overflows the LDS buffer
+    assert sum(1 for f in raw_fit if not f) > 100                      # raw line overflows the LDS buffer
+    dv = _device_parse(lines)
+    bad = _compare(lines, dv)
+    assert not bad, f"{len(bad)} mismatches; first: {bad[:3]}"
+    _check_selection(lines, dv)
+
+
 def _flat_msgs(res):
     return [[d.protocol_id, d.payload, d.metadata, [d.raw.line, d.raw.message_type, d.raw.rssi, d.raw.freq_afc]]
             for d in res]
