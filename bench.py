@@ -47,6 +47,12 @@ def parse():
     ap.add_argument("--serial", action="store_true",
                     help="MU, MS and MC one after another on one stream (default: MC on a second stream, "
                          "started when MU ends, so MC runs beside MS while MU runs alone)")
+    ap.add_argument("--mrec", action="store_true",
+                    help="the grouping writes message records (sdx_msg_rec) and k_pulses reads its header fields "
+                         "from them instead of the scattered SoA fields: less HBM traffic, measured slower (A/B)")
+    ap.add_argument("--mc-tail", action="store_true",
+                    help="MC on a low-priority stream started with MU (the dispatcher gives its workgroups "
+                         "the CUs MU's tail leaves idle) instead of beside MS")
     ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
                     help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
@@ -203,6 +209,7 @@ def main():
     bk = bankmod.Bank()
     P = bk.protocols
     eng = runtime.Engine(bk, local)
+    eng.use_mrec = args.mrec  # the grouping writes message records only when the launches read them
     kinds = ("MU", "MS", "MC") if args.kind == "mixed" else (args.kind,)
     per = {k: (args.msgs // 3 if k != "MC" else args.msgs - 2 * (args.msgs // 3)) if args.kind == "mixed" else args.msgs
            for k in kinds}
@@ -269,9 +276,11 @@ def main():
     kstream = {k: (torch.cuda.Stream(dev) if args.concurrent else stream) for k in kinds}
     # default: MU alone (the roofline kernel keeps an attributable duration), then MS and MC side by
     # side -- MC fills the CUs MS's tail leaves idle (482 vs 471M msgs/s serial, 20 steps)
-    mc_beside_ms = not args.serial and not args.concurrent and "MC" in kinds and "MU" in kinds
+    mc_beside_ms = not args.serial and not args.concurrent and not args.mc_tail and "MC" in kinds and "MU" in kinds
     if mc_beside_ms:
         kstream["MC"] = torch.cuda.Stream(dev)
+    if args.mc_tail and "MC" in kinds:
+        kstream["MC"] = torch.cuda.Stream(dev, priority=lo_prio)
 
     mu_done = [None]
 
@@ -304,7 +313,8 @@ def main():
                     eng.launch_mc(bds[k], outs[s_][k])
                 else:
                     eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[s_][k],
-                                      sel=gbufs[k][par][0][:corp[k].n] if k in gkinds else None, group=False)
+                                      sel=gbufs[k][par][0][:corp[k].n] if k in gkinds else None, group=False,
+                                      mrec=gbufs[k][par][2] if k in gkinds and args.mrec else None)
                 if si is not None:
                     ev[si][k][1].record(ks)
                 if k == "MU":

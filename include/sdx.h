@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 8
+#define SDX_ABI_VERSION 9
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -64,6 +64,23 @@ typedef struct {
   uint32_t msg;         /* message index (into the batch) */
 } sdx_result;
 
+/* One message's header fields packed into one 128-byte record (sdx_group_pulses writes them while it
+ * reads the batch in message order; sdx_pulse_batch.mrec_dev).  A grouped launch visits its messages
+ * in the grouped order, so read from the SoA arrays every field is its own scattered 32-64 B memory
+ * sector per message; from the record they are one aligned line. */
+typedef struct {
+  int64_t off;          /* offsets[i] */
+  int32_t len;          /* the message's length (len_dev[i], or offsets[i+1] - offsets[i]) */
+  uint8_t npat;         /* npat[i] */
+  int8_t cp_slot;       /* MS: cp_slot[i]; MU: -1 */
+  uint8_t ms_ok;        /* MS: ms_ok[i]; MU: 0 */
+  uint8_t res0;
+  uint8_t pat_id[10];   /* pat_id[10 i, 10 i + 10) */
+  uint8_t res1[6];
+  double pat_val[10];   /* pat_val[10 i, 10 i + 10) (slots >= npat: 0) */
+  uint8_t res2[16];
+} sdx_msg_rec;          /* 128 bytes */
+
 /* MU / MS batch: structure-of-arrays in HBM (see DESIGN.md "Data layout") */
 typedef struct {
   const uint8_t* data_dev;     /* pulse-id characters, all messages concatenated */
@@ -78,6 +95,9 @@ typedef struct {
   const int32_t* sel_dev;      /* optional [n_sel] subset of message indices to run, NULL = all */
   int32_t n;                   /* messages in the batch */
   int32_t n_sel;               /* entries in sel_dev (ignored when sel_dev == NULL) */
+  const sdx_msg_rec* mrec_dev; /* optional [n]: the header fields of every message the launch visits,
+                                * as sdx_group_pulses wrote them (the short MU/MS variant reads them
+                                * from here; the SoA arrays must still be given); NULL = SoA only */
 } sdx_pulse_batch;
 
 /* MC batch */
@@ -152,8 +172,10 @@ size_t sdx_pulses_work_bytes(int spill_tiles);
  * sel_dev) gives the same results with fewer instructions (tiles of messages that survive the same
  * protocols).  work_dev: sdx_group_work_bytes(n) bytes.  Worth it from a few thousand messages. */
 size_t sdx_group_work_bytes(int n);
-int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, int32_t* order_dev, void* work_dev,
-                     size_t work_cap, void* hip_stream);
+/* mrec_dev: optional [batch->n] records (sdx_msg_rec) written for every message grouped -- pass them
+ * as the launch's batch->mrec_dev; NULL = none written */
+int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, int32_t* order_dev,
+                     sdx_msg_rec* mrec_dev, void* work_dev, size_t work_cap, void* hip_stream);
 #define SDX_GROUP_MIN 4096  /* batches from this size are grouped by the host wrappers */
 /* same, for messages of 257..4096 pulses (4 messages per workgroup tile) */
 int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,

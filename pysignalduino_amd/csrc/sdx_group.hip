@@ -46,7 +46,7 @@ constexpr int SIG_PROTOS = 32;
 #endif
 template <int KIND>
 __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_pulse_batch b, uint32_t* __restrict__ key,
-                                             uint32_t* __restrict__ msg_out) {
+                                             uint32_t* __restrict__ msg_out, sdx_msg_rec* __restrict__ mrec) {
   const BankView bv = bank_view(bank);
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int ntot = b.sel_dev ? b.n_sel : b.n;
@@ -135,6 +135,25 @@ __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_
       }
       sig |= (uint32_t)ok << (31 - r);
     }
+  }
+  if (valid && mrec) {  // the message's 128-byte record (sdx_msg_rec), eight 16-byte stores
+    const int64_t off = b.offsets_dev[msg];
+    const int32_t len = b.len_dev ? b.len_dev[msg] : (int32_t)(b.offsets_dev[msg + 1] - off);
+    uint32_t id[4] = {0, 0, 0, 0};  // bytes 16..31: pat_id[10], then zeros
+#pragma unroll
+    for (int k = 0; k < SDX_MAXPAT; ++k) id[k >> 2] |= (uint32_t)b.pat_id_dev[msg * SDX_MAXPAT + k] << (8 * (k & 3));
+    const uint32_t w3 = (uint32_t)(valid ? b.npat_dev[msg] : 0) |
+                        ((uint32_t)(uint8_t)(KIND == SDX_KIND_MS ? b.cp_slot_dev[msg] : -1) << 8) |
+                        ((uint32_t)(KIND == SDX_KIND_MS ? b.ms_ok_dev[msg] : 0) << 16);
+    uint4* d = reinterpret_cast<uint4*>(mrec + msg);
+    d[0] = make_uint4((uint32_t)off, (uint32_t)((uint64_t)off >> 32), (uint32_t)len, w3);
+    d[1] = make_uint4(id[0], id[1], id[2], 0u);
+#pragma unroll
+    for (int h = 0; h < SDX_MAXPAT / 2; ++h) {
+      const uint64_t a = (uint64_t)__double_as_longlong(val[2 * h]), c = (uint64_t)__double_as_longlong(val[2 * h + 1]);
+      d[2 + h] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)c, (uint32_t)(c >> 32));
+    }
+    d[7] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (valid) {
     // MU: descending signature order -- messages that pass the leading protocols, the tiles that
@@ -264,8 +283,8 @@ size_t group_bytes(int n) {
 
 // The grouped order of a batch's messages (or of its sel_dev subset): order[0, n) = message indices
 // (the sel_dev of the k_pulses launch that follows).
-bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, int32_t* order, uint8_t* work,
-                    size_t bytes, hipStream_t st) {
+bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, int32_t* order, sdx_msg_rec* mrec,
+                    uint8_t* work, size_t bytes, hipStream_t st) {
   const int n = b.sel_dev ? b.n_sel : b.n;
   const size_t need = group_bytes(n);
   if (!need || bytes < need) return false;
@@ -279,9 +298,9 @@ bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, in
   uint32_t* tot = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)np));
   const int grid = (n + 255) / 256;
   if (kind == SDX_KIND_MU)
-    hipLaunchKernelGGL((k_sig<SDX_KIND_MU>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0);
+    hipLaunchKernelGGL((k_sig<SDX_KIND_MU>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec);
   else
-    hipLaunchKernelGGL((k_sig<SDX_KIND_MS>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0);
+    hipLaunchKernelGGL((k_sig<SDX_KIND_MS>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec);
   // the key's top RS_PASSES bytes (LSD order): (k0, v0) -> (k1, v1) -> (k0, v0) -> ..., the last
   // pass writing the message indices to order
   for (int pi = 0; pi < RS_PASSES; ++pi) {

@@ -1543,10 +1543,19 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     // wave's messages, and per (message, pattern) thread npat, P, the id and (MS) the message's
     // CP slot with all its values (five 16-B loads; the clock is selected in registers) -- two
     // levels of dependent global loads (message index -> fields -> data) instead of five
+    // with message records (b.mrec_dev, written by the grouping in message order) every header
+    // field of a message comes from its one 128-byte line instead of a scattered sector per field
+    const sdx_msg_rec* __restrict__ mrec = b.mrec_dev;
     if (lane < MPW && wave + lane * NWAVE < nvalid) {
       const int msg = msg_of[wave + lane * NWAVE];
-      pf_off = b.offsets_dev[msg];
-      pf_n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - pf_off);
+      if (mrec) {
+        const int4 h = *reinterpret_cast<const int4*>(mrec + msg);
+        pf_off = (int64_t)(((uint64_t)(uint32_t)h.y << 32) | (uint32_t)h.x);
+        pf_n = h.z;
+      } else {
+        pf_off = b.offsets_dev[msg];
+        pf_n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - pf_off);
+      }
       if (pf_n > 64 * NW) pf_n = 64 * NW;
     }
     constexpr int NTH = pulses_threads<KIND, NW>();
@@ -1561,13 +1570,21 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const int m = i / SDX_MAXPAT, k = i - m * SDX_MAXPAT;
       const bool ok = i < TM * SDX_MAXPAT && m < nvalid;
       const int msg = ok ? msg_of[m] : 0;
-      r_np[it] = ok ? (int)b.npat_dev[msg] : 0;
-      r_v[it] = ok ? b.pat_val_dev[msg * SDX_MAXPAT + k] : 0.0;  // n x 10 values: always in bounds
-      r_id[it] = ok ? b.pat_id_dev[msg * SDX_MAXPAT + k] : (uint8_t)'0';
+      if (mrec) {
+        const sdx_msg_rec* r = mrec + msg;
+        r_np[it] = ok ? (int)r->npat : 0;
+        r_v[it] = ok ? r->pat_val[k] : 0.0;
+        r_id[it] = ok ? r->pat_id[k] : (uint8_t)'0';
+      } else {
+        r_np[it] = ok ? (int)b.npat_dev[msg] : 0;
+        r_v[it] = ok ? b.pat_val_dev[msg * SDX_MAXPAT + k] : 0.0;  // n x 10 values: always in bounds
+        r_id[it] = ok ? b.pat_id_dev[msg * SDX_MAXPAT + k] : (uint8_t)'0';
+      }
       r_cp[it] = -1;
       if constexpr (KIND == SDX_KIND_MS) {
-        r_cp[it] = ok ? (int)b.cp_slot_dev[msg] : -1;
-        const double2* row = reinterpret_cast<const double2*>(b.pat_val_dev + msg * SDX_MAXPAT);
+        r_cp[it] = ok ? (int)(mrec ? mrec[msg].cp_slot : b.cp_slot_dev[msg]) : -1;
+        const double2* row = mrec ? reinterpret_cast<const double2*>(mrec[msg].pat_val)
+                                  : reinterpret_cast<const double2*>(b.pat_val_dev + msg * SDX_MAXPAT);
 #pragma unroll
         for (int h = 0; h < SDX_MAXPAT / 2; ++h) r_all[it][h] = ok ? row[h] : make_double2(0.0, 0.0);
       }
@@ -1837,8 +1854,10 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   if (KIND == SDX_KIND_MS && mvalid) {
     // gates (message_synced.py:21-66): data.isdigit(), CP/SP/R string checks, CP in patterns, clock != 0
     const int msg = msg_of[mi];
-    const int cp = b.cp_slot_dev[msg];
-    lane_ok = lane_ok && L.digit_ok[mi] && b.ms_ok_dev[msg] && cp >= 0 && cp < npat;
+    const bool use_rec = NW <= 4 && b.mrec_dev;
+    const int cp = use_rec ? b.mrec_dev[msg].cp_slot : b.cp_slot_dev[msg];
+    const bool ok_ms = use_rec ? b.mrec_dev[msg].ms_ok : b.ms_ok_dev[msg];
+    lane_ok = lane_ok && L.digit_ok[mi] && ok_ms && cp >= 0 && cp < npat;
     if constexpr (NW <= 4) {  // clock and k were staged (st_clk / st_x)
       clock = st_clk[mi];
       lane_ok = lane_ok && clock != 0.0;
@@ -2534,7 +2553,7 @@ static int fail(int code, const std::string& msg) {
 }
 namespace sdx {
 size_t group_bytes(int n);  // sdx_group.hip
-bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, int32_t* order, uint8_t* work,
+bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, int32_t* order, sdx_msg_rec* mrec, uint8_t* work,
                     size_t bytes, hipStream_t st);
 // for the other translation units (sdx_lines.hip, sdx_mn.hip): the error text of sdx_last_error()
 // and the bank handle's fields
@@ -2595,6 +2614,8 @@ int sdx_layout_size(int which) {
     case 12: return (int)sizeof(sdx_xchg_part);
     case 13: return (int)sizeof(sdx_xchg_wire);
     case 14: return (int)sizeof(sdx_wire_rec);
+    case 15: static_assert(sizeof(sdx_msg_rec) == 128, "sdx_msg_rec is one 128-byte line"); return (int)sizeof(sdx_msg_rec);
+    case 16: return (int)sizeof(sdx_pulse_batch);
   }
   return -1;
 }
@@ -2642,6 +2663,7 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
   if (kind != SDX_KIND_MU && kind != SDX_KIND_MS) return fail(SDX_EINVAL, "kind must be MU or MS");
   if (kind == SDX_KIND_MS && (!batch->cp_slot_dev || !batch->ms_ok_dev)) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+  if ((uintptr_t)batch->mrec_dev & 127) return fail(SDX_EINVAL, "mrec_dev must be 128-byte aligned");
   // spill regions are addressed with 32-bit offsets (region index cursor_dev[3] x SPILL_BYTES)
   if (out->work_dev && out->work_cap > 0xFFFFFFFFull - sdx::SPILL_BYTES)
     return fail(SDX_EINVAL, "work_cap above 4 GiB - 112 KB: spill offsets are 32-bit");
@@ -2668,15 +2690,17 @@ size_t sdx_pulses_work_bytes(int spill_tiles) { return (size_t)(spill_tiles > 0 
 
 size_t sdx_group_work_bytes(int n) { return sdx::group_bytes(n); }
 
-int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, int32_t* order_dev, void* work_dev,
-                     size_t work_cap, void* hip_stream) {
+int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, int32_t* order_dev,
+                     sdx_msg_rec* mrec_dev, void* work_dev, size_t work_cap, void* hip_stream) {
   if (!bank || !batch || !order_dev || !work_dev) return fail(SDX_EINVAL, "null argument");
   if (kind != SDX_KIND_MU && kind != SDX_KIND_MS) return fail(SDX_EINVAL, "kind must be MU or MS");
   if (kind == SDX_KIND_MS && (!batch->cp_slot_dev || !batch->ms_ok_dev)) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
   if (ntot <= 0) return SDX_OK;
   if (work_cap < sdx::group_bytes(ntot)) return fail(SDX_EINVAL, "grouping workspace smaller than sdx_group_work_bytes(n)");
-  if (!sdx::group_messages(bank->dev, kind, *batch, order_dev, (uint8_t*)work_dev, work_cap, (hipStream_t)hip_stream))
+  if ((uintptr_t)mrec_dev & 127) return fail(SDX_EINVAL, "mrec_dev must be 128-byte aligned");
+  if (!sdx::group_messages(bank->dev, kind, *batch, order_dev, mrec_dev, (uint8_t*)work_dev, work_cap,
+                           (hipStream_t)hip_stream))
     return fail(SDX_EHIP, "message grouping (k_sig / radix sort) launch failed");
   return SDX_OK;
 }

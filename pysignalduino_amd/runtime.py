@@ -31,6 +31,10 @@ MC_HEX_MAX = 128   # MC_MAXW * 16 hex characters
 MN_HEX_MAX = 4096  # SDX_MN_HEX_MAX
 
 DESC_DT = np.dtype([("rec_begin", "<u4"), ("n_rec", "<u2"), ("status", "u1"), ("raise_kind", "u1")])
+# sdx_msg_rec (include/sdx.h): one message's header fields, written by sdx_group_pulses
+MREC_DT = np.dtype([("off", "<i8"), ("len", "<i4"), ("npat", "u1"), ("cp_slot", "i1"), ("ms_ok", "u1"), ("res0", "u1"),
+                    ("pat_id", "u1", (10,)), ("res1", "u1", (6,)), ("pat_val", "<f8", (10,)), ("res2", "u1", (16,))])
+MREC_BYTES = 128
 RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u2"), ("bit_length", "<u4"),
                    ("msg", "<u4")])
 
@@ -48,7 +52,7 @@ class SdxPulseBatch(Structure):
     _fields_ = [("data_dev", c_void_p), ("offsets_dev", c_void_p), ("npat_dev", c_void_p),
                 ("pat_id_dev", c_void_p), ("pat_val_dev", c_void_p), ("cp_slot_dev", c_void_p),
                 ("ms_ok_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p), ("n", c_int32),
-                ("n_sel", c_int32)]
+                ("n_sel", c_int32), ("mrec_dev", c_void_p)]
 
 
 class SdxGeneralBatch(Structure):
@@ -160,7 +164,8 @@ def load_library(path: Optional[str] = None):
     lib.sdx_pulses_work_bytes.restype = c_size_t
     lib.sdx_group_work_bytes.argtypes = [c_int]
     lib.sdx_group_work_bytes.restype = c_size_t
-    lib.sdx_group_pulses.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.sdx_group_pulses.argtypes = [c_void_p, c_int, POINTER(SdxPulseBatch), c_void_p, c_void_p, c_void_p, c_size_t,
+                                     c_void_p]
     lib.sdx_group_pulses.restype = c_int
     lib.sdx_general_work_bytes.argtypes = [c_void_p, c_int, ctypes.c_int64, c_int32, c_int32, ctypes.c_int64]
     lib.sdx_general_work_bytes.restype = ctypes.c_uint64
@@ -199,7 +204,7 @@ def load_library(path: Optional[str] = None):
     lib.sdx_exchange_unpack.argtypes = [POINTER(SdxXchgWire), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
                                         c_void_p, c_void_p]
     lib.sdx_exchange_unpack.restype = c_int
-    if lib.sdx_abi_version() != 8:
+    if lib.sdx_abi_version() != 9:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -213,7 +218,7 @@ def check_layout(lib) -> None:
             4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize,
             8: bankmod.MN_REC.itemsize, 9: bankmod.JSON_REC.itemsize, 10: bankmod.MU_FILT.itemsize,
             11: bankmod.MS_FILT.itemsize, 12: ctypes.sizeof(SdxXchgPart), 13: ctypes.sizeof(SdxXchgWire),
-            14: WIRE_REC_DT.itemsize}
+            14: WIRE_REC_DT.itemsize, 15: MREC_DT.itemsize, 16: ctypes.sizeof(SdxPulseBatch)}
     for k, v in want.items():
         got = lib.sdx_layout_size(k)
         if got != v:
@@ -241,6 +246,10 @@ class Engine:
         self.bank = bank
         self.device = device
         self.dev = torch.device("cuda", device)
+        # message records (sdx_msg_rec): the grouping writes them and k_pulses reads its header
+        # fields from them.  Off by default: 18 % / 44 % less HBM traffic for k_pulses<MU> / <MS>,
+        # but 3.5 % slower on the bench corpus; SDX_MREC=1 turns them on
+        self.use_mrec = os.environ.get("SDX_MREC", "0") == "1"
         h = c_void_p()
         blob = ctypes.create_string_buffer(bank.blob, len(bank.blob))
         with torch.cuda.device(device):
@@ -299,25 +308,32 @@ class Engine:
         most = (2 ** 32 - 2 * region) // region          # spill offsets are 32-bit (include/sdx.h)
         return int(self.lib.sdx_pulses_work_bytes(int(min(most, max(16, spill_frac * tiles)))))
 
-    def group_buffers(self, n: int):
-        """(order, work) device buffers for sdx_group_pulses over n messages."""
+    def group_buffers(self, n: int, n_batch: Optional[int] = None):
+        """(order, work, mrec) device buffers for sdx_group_pulses over n messages of a batch of
+        n_batch (default n): mrec holds one 128-byte sdx_msg_rec per batch message."""
         t = self.torch
+        nb = n if n_batch is None else n_batch
+        mrec = t.empty(max(nb, 1) * MREC_BYTES + 128, dtype=t.uint8, device=self.dev)
+        off = (-mrec.data_ptr()) % 128  # 128-byte aligned records
         return (t.empty(max(n, 1), dtype=t.int32, device=self.dev),
-                t.empty(max(int(self.lib.sdx_group_work_bytes(int(n))), 1), dtype=t.uint8, device=self.dev))
+                t.empty(max(int(self.lib.sdx_group_work_bytes(int(n))), 1), dtype=t.uint8, device=self.dev),
+                mrec[off: off + max(nb, 1) * MREC_BYTES])
 
     def group(self, kind: int, bd, sel=None, bufs=None):
         """The grouped message order of a batch (or of `sel`) as a device int32 tensor: the sel of
         the launch_pulses that follows (same results, fewer instructions; sdx_group.hip).  `bufs`:
-        group_buffers() to use; default: a per-engine cache (one stream at a time)."""
+        group_buffers() to use; default: a per-engine cache (one stream at a time).  The grouping
+        also writes the batch's message records into bufs[2] (launch_pulses(mrec=...))."""
         n = int(sel.numel()) if sel is not None else bd["n"]
         if bufs is None:
             c = getattr(self, "_gcache", None)
-            if c is None or c[0].numel() < n:
-                c = self._gcache = self.group_buffers(n)
+            if c is None or c[0].numel() < n or c[2].numel() < bd["n"] * MREC_BYTES:
+                c = self._gcache = self.group_buffers(n, max(n, bd["n"]))
             bufs = c
-        order, work = bufs
+        order, work, mrec = bufs
         b = self._pulse_batch(bd, sel)
-        _check(self.lib, self.lib.sdx_group_pulses(self.handle, kind, ctypes.byref(b), _ptr(order), _ptr(work),
+        _check(self.lib, self.lib.sdx_group_pulses(self.handle, kind, ctypes.byref(b), _ptr(order),
+                                                   _ptr(mrec) if self.use_mrec else None, _ptr(work),
                                                    int(work.numel()), self.stream_ptr()))
         return order[:n]
 
@@ -344,18 +360,22 @@ class Engine:
 
     # -- launches -------------------------------------------------------------------------------
     @staticmethod
-    def _pulse_batch(bd, sel) -> SdxPulseBatch:
+    def _pulse_batch(bd, sel, mrec=None) -> SdxPulseBatch:
         return SdxPulseBatch(_ptr(bd["data"]), _ptr(bd["offsets"]), _ptr(bd["npat"]), _ptr(bd["pat_id"]),
                              _ptr(bd["pat_val"]), _ptr(bd["cp_slot"]), _ptr(bd["ms_ok"]), _ptr(bd.get("len")),
-                             _ptr(sel), bd["n"], 0 if sel is None else int(sel.numel()))
+                             _ptr(sel), bd["n"], 0 if sel is None else int(sel.numel()), _ptr(mrec))
 
-    def launch_pulses(self, kind: int, bd, out, sel=None, long_variant: bool = False, group: bool = True) -> None:
+    def launch_pulses(self, kind: int, bd, out, sel=None, long_variant: bool = False, group: bool = True,
+                      mrec=None) -> None:
         """MU/MS launch; the short variant runs batches of >= GROUP_MIN messages in the grouped
-        order (group()) unless `group` is False (`sel` then runs in its own order)."""
+        order (group()) unless `group` is False (`sel` then runs in its own order).  `mrec`: the
+        message records a group() call wrote for this batch (its bufs[2]), read by the short
+        variant instead of the scattered SoA fields."""
         n = int(sel.numel()) if sel is not None else bd["n"]
         if group and not long_variant and n >= GROUP_MIN:
             sel = self.group(kind, bd, sel)
-        b = self._pulse_batch(bd, sel)
+            mrec = self._gcache[2] if self.use_mrec else None
+        b = self._pulse_batch(bd, sel, None if long_variant else mrec)
         o = self._out_struct(out)
         fn = self.lib.sdx_demod_pulses_long if long_variant else self.lib.sdx_demod_pulses
         _check(self.lib, fn(self.handle, kind, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))

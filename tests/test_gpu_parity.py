@@ -253,6 +253,44 @@ def test_grouped_order_and_spill_regions_vs_c_oracle(kind, n, seed):
     _compare_c_oracle(kind, d2, r2, h2, cres, cls_pids, cb)
 
 
+@pytest.mark.parametrize("kind", ["MU", "MS"])
+def test_message_records_match_soa_and_results(kind):
+    """sdx_group_pulses writes one 128-byte sdx_msg_rec per grouped message: its fields equal the
+    SoA arrays (pattern values bitwise; slots past npat 0), and k_pulses reading the records gives
+    byte-identical descriptors, records and heap to k_pulses reading the SoA fields."""
+    import torch
+    from pysignalduino_amd import bank as B, runtime, synth
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    n = 20000
+    gen = synth.mu_corpus if kind == "MU" else synth.ms_corpus
+    batch = gen(bk.protocols, n, seed=9301)
+    k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
+    bd = eng.to_device_pulses(batch)
+    bufs = eng.group_buffers(n)
+    eng.use_mrec = True
+    order = eng.group(k, bd, bufs=bufs)
+    torch.cuda.synchronize()
+    mr = bufs[2][: n * runtime.MREC_BYTES].cpu().numpy().view(runtime.MREC_DT)
+    assert np.array_equal(mr["off"], batch.offsets[:-1])
+    assert np.array_equal(mr["len"], np.diff(batch.offsets))
+    assert np.array_equal(mr["npat"], batch.npat)
+    assert np.array_equal(mr["pat_id"], batch.pat_id.reshape(n, 10))
+    pv = batch.pat_val.reshape(n, 10).copy()
+    pv[np.arange(10)[None, :] >= np.minimum(batch.npat, 10)[:, None]] = 0.0
+    assert mr["pat_val"].tobytes() == pv.tobytes()
+    if kind == "MS":
+        assert np.array_equal(mr["cp_slot"], batch.cp_slot) and np.array_equal(mr["ms_ok"], batch.ms_ok)
+    outs = []
+    for use in (True, False):
+        out = eng.alloc_out(n, 40 * n + 4096, 1024 * n + 65536, eng.pulses_work_bytes(n))
+        eng.launch_pulses(k, bd, out, sel=order, group=False, mrec=bufs[2] if use else None)
+        outs.append(eng.fetch(out))
+    from pysignalduino_amd import dist
+    a, b = (dist.canonical(*o) for o in outs)  # record placement follows the tiles' atomics: compare canonically
+    assert all(x.tobytes() == y.tobytes() for x, y in zip(a, b))
+
+
 @pytest.mark.gpu
 def test_mc_long_frames_vs_oracle():
     """Frames of 1..128 hex characters: the short (<= 64) and long (65..128) k_mc launches together
