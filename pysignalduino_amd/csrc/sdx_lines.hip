@@ -607,29 +607,43 @@ LD uint64_t sw_hexalpha(uint64_t x) {  // 'a'..'f' / 'A'..'F'
 }
 
 // position of the first ';' at or after s, or -1 when a byte outside the class comes first
-// (CLS_ANY: any ASCII byte).  P must end with ';'; the aligned 8-byte words around it are read.
-LD int scan_run(const uint8_t* P, int s, int cls) {
+// (CLS_ANY: any ASCII byte).  P[0, n) must end with ';'.  The aligned 8-byte words are loaded
+// SCAN_W at a time (independent loads: one memory round trip per SCAN_W words of a long field
+// instead of one per word); a word holding no byte of [0, n) is not loaded.
+#ifndef SDX_SCAN_W
+#define SDX_SCAN_W 4
+#endif
+constexpr int SCAN_W = SDX_SCAN_W;
+LD int scan_run(const uint8_t* P, int n, int s, int cls) {
   const uint8_t* q = P + s;
   const int a = (int)((uintptr_t)q & 7);
   const uint64_t* w = reinterpret_cast<const uint64_t*>(q - a);
   int base = s - a;
-  const uint64_t pre = a ? (~0ull >> (64 - 8 * a)) : 0ull;  // bytes before s: neutral '0'
-  uint64_t x = (*w & ~pre) | (SW_L1 * 0x30 & pre);
+  uint64_t pre = a ? (~0ull >> (64 - 8 * a)) : 0ull;  // bytes before s: neutral '0'
   while (true) {
-    const uint64_t t = x ^ (SW_L1 * 0x3B);
-    const uint64_t semi = (t - SW_L1) & ~t & SW_H;
-    const uint64_t dg = sw_digits(x);
-    const uint64_t tn = x ^ (SW_L1 * 0x0A);  // CLS_ANY: ASCII, not a newline
-    const uint64_t nl = ((tn & ~SW_H) + ~SW_H | tn) & SW_H;  // high bit: byte != '\n'
-    const uint64_t ok = cls == CLS_DIGIT ? dg : cls == CLS_HEX ? (dg | sw_hexalpha(x)) : (~x & nl & SW_H);
-    const uint64_t bad = ~ok & SW_H;
-    if (semi) {
-      if (bad & ((semi & (0 - semi)) - 1)) return -1;  // a bad byte before the ';'
-      return base + (__builtin_ctzll(semi) >> 3);
+    uint64_t xs[SCAN_W];
+#pragma unroll
+    for (int k = 0; k < SCAN_W; ++k) xs[k] = base + 8 * k < n ? w[k] : SW_L1 * 0x3B;  // past P: ';' (never reached)
+#pragma unroll
+    for (int k = 0; k < SCAN_W; ++k) {
+      uint64_t x = xs[k];
+      if (k == 0) x = (x & ~pre) | (SW_L1 * 0x30 & pre);
+      const uint64_t t = x ^ (SW_L1 * 0x3B);
+      const uint64_t semi = (t - SW_L1) & ~t & SW_H;
+      const uint64_t dg = sw_digits(x);
+      const uint64_t tn = x ^ (SW_L1 * 0x0A);  // CLS_ANY: ASCII, not a newline
+      const uint64_t nl = ((tn & ~SW_H) + ~SW_H | tn) & SW_H;  // high bit: byte != '\n'
+      const uint64_t ok = cls == CLS_DIGIT ? dg : cls == CLS_HEX ? (dg | sw_hexalpha(x)) : (~x & nl & SW_H);
+      const uint64_t bad = ~ok & SW_H;
+      if (semi) {
+        if (bad & ((semi & (0 - semi)) - 1)) return -1;  // a bad byte before the ';'
+        return base + 8 * k + (__builtin_ctzll(semi) >> 3);
+      }
+      if (bad) return -1;
     }
-    if (bad) return -1;
-    base += 8;
-    x = *++w;
+    pre = 0;
+    base += 8 * SCAN_W;
+    w += SCAN_W;
   }
 }
 
@@ -706,7 +720,7 @@ LD bool fast_payload(const uint8_t* P, int n, LineRes& r, const sdx_lines_out& o
       ++v0;
     }
     // 2. one scan for every kind of part
-    const int e = scan_run(P, v0, cls);
+    const int e = scan_run(P, n, v0, cls);
     if (e < 0) return false;
     const int nv = e - v0;
     // 3. the key's rule
