@@ -1460,7 +1460,9 @@ constexpr int pulses_threads() { return NW <= 4 ? 64 * LANE_WAVES : 256; }
 template <int KIND, int NW>
 constexpr int pulses_min_blocks() { return NW <= 4 ? 16 / LANE_WAVES : 1; }
 
-template <int KIND, int NW, int TM>
+// MR = 1: the short variant reads its header fields from the message records (b.mrec_dev); a
+// separate instantiation, so the default one carries no trace of that path
+template <int KIND, int NW, int TM, int MR = 0>
 __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
     (NW <= 4 ? 4 : 1)))) void k_pulses(
     const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
@@ -1545,7 +1547,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     // levels of dependent global loads (message index -> fields -> data) instead of five
     // with message records (b.mrec_dev, written by the grouping in message order) every header
     // field of a message comes from its one 128-byte line instead of a scattered sector per field
-    const sdx_msg_rec* __restrict__ mrec = b.mrec_dev;
+    const sdx_msg_rec* __restrict__ mrec = MR ? b.mrec_dev : nullptr;
     if (lane < MPW && wave + lane * NWAVE < nvalid) {
       const int msg = msg_of[wave + lane * NWAVE];
       if (mrec) {
@@ -1854,7 +1856,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   if (KIND == SDX_KIND_MS && mvalid) {
     // gates (message_synced.py:21-66): data.isdigit(), CP/SP/R string checks, CP in patterns, clock != 0
     const int msg = msg_of[mi];
-    const bool use_rec = NW <= 4 && b.mrec_dev;
+    const bool use_rec = MR && NW <= 4;
     const int cp = use_rec ? b.mrec_dev[msg].cp_slot : b.cp_slot_dev[msg];
     const bool ok_ms = use_rec ? b.mrec_dev[msg].ms_ok : b.ms_ok_dev[msg];
     lane_ok = lane_ok && L.digit_ok[mi] && ok_ms && cp >= 0 && cp < npat;
@@ -2676,12 +2678,16 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   const sdx_out& o = *out;
   constexpr int TM = 64;
   const int grid = (ntot + TM - 1) / TM;
-  if (kind == SDX_KIND_MU)
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), dim3(sdx::pulses_threads<SDX_KIND_MU, 4>()),
-                       0, st, bank->dev, b, o);
+  const dim3 blk(sdx::pulses_threads<SDX_KIND_MU, 4>());
+  static_assert(sdx::pulses_threads<SDX_KIND_MU, 4>() == sdx::pulses_threads<SDX_KIND_MS, 4>(), "one block shape");
+  if (kind == SDX_KIND_MU && b.mrec_dev)
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
+  else if (kind == SDX_KIND_MU)
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
+  else if (b.mrec_dev)
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
   else
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), dim3(sdx::pulses_threads<SDX_KIND_MS, 4>()),
-                       0, st, bank->dev, b, o);
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
   HIPCHK(hipGetLastError());
   return SDX_OK;
 }
