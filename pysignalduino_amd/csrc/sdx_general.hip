@@ -35,6 +35,21 @@ using namespace sdx;
 #define GD __device__ __attribute__((noinline))
 #define GI __device__ __forceinline__
 
+// SDX_GPROF (variant builds only, tools/prof_general.py): s_memtime cycles per phase of the MU walk,
+// summed over items (lane 0 adds), and each pass-0 item's cycles in GenChunk.res
+#ifdef SDX_GPROF
+__device__ unsigned long long g_genprof[16];
+#define GP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define GP_ADD(slot, t0) \
+  do { if (lane_id() == 0) atomicAdd(&g_genprof[slot], __builtin_amdgcn_s_memtime() - (t0)); } while (0)
+#define GP_CNT(slot) \
+  do { if (lane_id() == 0) atomicAdd(&g_genprof[slot], 1ull); } while (0)
+#else
+#define GP_T(v)
+#define GP_ADD(slot, t0)
+#define GP_CNT(slot)
+#endif
+
 constexpr int GP = SDX_GEN_MAXPAT, GID = SDX_GEN_IDSTR, GS = SDX_GEN_STRMAX, GREP = SDX_GEN_REPMAX;
 constexpr long long GBUDGET = 1ll << 22;  // sre steps per repetition match (catastrophic backtracking)
 constexpr int GSLACK = 512;               // per-message scratch beyond n: padding, postDemo prefixes, texts
@@ -66,7 +81,34 @@ struct Msg {
   double nv[GP];       // round(P / clock, 1)
   const uint64_t* bm;  // per digit character c: bm[c * nwp + w] bit j = d[64w + j] == '0' + c
   int nwp;             // words per character bitmap (one zero word of padding)
+  uint64_t* tb;        // the MU match tables (position bitmaps, mu_tables): LDS or the slot's scratch
+  int nwt;             // words per table bitmap (three zero words of padding)
+  uint8_t* ld;         // the LDS copy of the characters (nullptr: they do not fit), made by stage()
+  int staged;          // 1 once the characters are in the LDS copy (m.d points there)
 };
+
+// The serial steps (sre fallback, chunk compares) read the message's characters: copy them to the LDS
+// once per message, and only when a protocol gets past its key lookups (most items stop before).
+GD void stage(Msg& m) {
+  if (m.staged || !m.ld) return;
+  const uint8_t* src = m.d;
+  uint8_t* dst = m.ld;
+  const int n = m.n;
+  __syncthreads();
+  for (int j = lane_id(); j < n; j += 64) dst[j] = src[j];
+  m.d = dst;
+  m.staged = 1;
+  __syncthreads();
+}
+
+// MU match tables, one position bitmap each (bit p of word p >> 6), nwt = (n >> 6) + 3 words:
+//   UA[a]   unit string a occurs at p (a < 3)
+//   SA      the start string occurs at p
+//   D0, D1  {p : (?:U0|U1|..){r} can match at p} for the round r (double buffer)
+//   G0, G1  the same for the greedy path (first matching unit at every step)
+constexpr int TB_ARRAYS = 8;
+__host__ __device__ inline int tb_words(int n) { return (n >> 6) + 3; }
+__host__ __device__ inline int64_t tb_bytes(int n) { return (int64_t)TB_ARRAYS * 8 * tb_words(n); }
 
 // bits q .. q+63 of character c's occurrence bitmap (q >= 0; the padding word ends every row)
 GI uint64_t bm_at(const Msg& m, int c, int q) {
@@ -230,25 +272,173 @@ GD int rep_match(const uint8_t* d, int n, int q, const Str* U, int nu, int lmin,
   }
 }
 
-GI bool any_f(const uint8_t* b, int n) {
-  for (int i = 0; i < n; ++i)
-    if (b[i] == 2) return true;
+// bits q .. q+63 of a match-table row (q >= 0; the padding words end every row)
+GI uint64_t tb_at(const uint64_t* X, int nwt, int q) {
+  const int w = q >> 6, o = q & 63;
+  if (w >= nwt - 1) return 0ull;
+  const uint64_t lo = X[w];
+  return o ? (lo >> o) | (X[w + 1] << (64 - o)) : lo;
+}
+
+// The match tables of one (message, protocol) over the positions [base, n], lane = word: the unit and
+// start occurrence bitmaps, then lmin rounds of
+//   D_r = OR_a UA[a] & (D_{r-1} >> |U_a|),  D_0 = [base, n]
+// -- the positions from which some sequence of r units matches.  sre's repetition below lmin backtracks
+// over exactly these alternatives, so (?:U0|U1|..){lmin,} matches at q iff q is in D_lmin.  When one
+// unit is a proper prefix of another (the only way two units match at one position, amb), the same
+// rounds run over the first matching unit only (G_lmin: the greedy path reaches lmin units, so it is
+// the path sre takes).  Returns 0 when D_lmin is empty, -1 when lmin exceeds the fallback's choice
+// stack and the old step-by-step search would have tried a repetition (contract), else 1 with
+// *succ = D_lmin, *gsucc = G_lmin (D_lmin when !amb).
+GD int mu_tables(const Msg& m, int base, const Str* U, int nu, const Str& S, int lmin, bool amb,
+                 const uint64_t** succ, const uint64_t** gsucc) {
+  const int nwt = m.nwt, lane = lane_id();
+  uint64_t* UA = m.tb;
+  uint64_t* SA = UA + 3 * nwt;
+  uint64_t* D[2] = {SA + nwt, SA + 2 * nwt};
+  uint64_t* G[2] = {SA + 3 * nwt, SA + 4 * nwt};
+  const int wb = base >> 6, we = m.n >> 6;
+  const uint64_t lastm = (m.n & 63) == 63 ? ~0ull : (1ull << ((m.n & 63) + 1)) - 1;  // positions <= n
+  uint64_t any = 0;
+  for (int w = lane; w < nwt; w += 64) {
+    const bool in = w >= wb && w <= we;
+    uint64_t rng = in ? ~0ull : 0ull;
+    if (w == wb) rng &= ~0ull << (base & 63);
+    if (w == we) rng &= lastm;
+    for (int a = 0; a < 3; ++a) {
+      uint64_t acc = 0;
+      if (a < nu && in) {
+        acc = rng;
+        for (int i = 0; i < U[a].len && acc; ++i) acc &= bm_at(m, U[a].c[i] - '0', w * 64 + i);
+      }
+      UA[a * nwt + w] = acc;
+      any |= acc;
+    }
+    uint64_t sacc = 0;
+    if (S.len && in) {
+      sacc = rng;
+      for (int i = 0; i < S.len && sacc; ++i) sacc &= bm_at(m, S.c[i] - '0', w * 64 + i);
+    }
+    SA[w] = sacc;
+    D[0][w] = rng;
+    D[1][w] = 0;
+    G[0][w] = rng;
+    G[1][w] = 0;
+  }
+  __syncthreads();  // (one wave per workgroup) the rows, LDS or global, are visible to every lane
+  if (lmin > GREP && (S.len || ballot(any != 0))) return -1;
+  int cur = 0;
+  for (int r = 1; r <= lmin; ++r) {
+    uint64_t nz = 0;
+    for (int w = wb + lane; w <= we; w += 64) {
+      uint64_t d = 0, g = 0, seen = 0;
+      for (int a = 0; a < nu; ++a) {
+        const uint64_t ua = UA[a * nwt + w];
+        const int L = U[a].len;
+        d |= ua & tb_at(D[cur], nwt, w * 64 + L);
+        if (amb) {
+          g |= ua & ~seen & tb_at(G[cur], nwt, w * 64 + L);
+          seen |= ua;
+        }
+      }
+      D[cur ^ 1][w] = d;
+      if (amb) G[cur ^ 1][w] = g;
+      nz |= d;
+    }
+    cur ^= 1;
+    __syncthreads();
+    if (!ballot(nz != 0)) return 0;  // no position starts r units: no match anywhere
+  }
+  *succ = D[cur];
+  *gsucc = amb ? G[cur] : D[cur];
+  return 1;
+}
+
+// first s >= from with the start string at s (every s without one) and s + |S| in succ, or -1:
+// 64 words (4096 positions) per step, as find_bm
+GD int find_ok(const Msg& m, int from, int slen, const uint64_t* succ) {
+  const int nwt = m.nwt, we = m.n >> 6;
+  const uint64_t* SA = m.tb + 3 * nwt;
+  if (from < 0) from = 0;
+  if (from > m.n) return -1;
+  const int wf = from >> 6;
+  for (int w0 = wf; w0 <= we; w0 += 64) {
+    const int w = w0 + lane_id();
+    uint64_t acc = 0;
+    if (w <= we) {
+      acc = tb_at(succ, nwt, w * 64 + slen);
+      if (slen) acc &= SA[w];
+      if (w == wf) acc &= ~0ull << (from & 63);
+    }
+    const uint64_t hit = ballot(acc != 0);
+    if (hit) return bcast_i(acc ? w * 64 + ffs64(acc) : 0, ffs64(hit));
+  }
+  return -1;
+}
+
+// end of the greedy repetition from q: the first matching unit at every step until none matches.
+// Units of one length L (the usual case) step 64 units per wave step (lane = unit).
+GD int greedy_end(const Msg& m, const Str* U, int nu, int q) {
+  const int nwt = m.nwt;
+  const uint64_t* UA = m.tb;
+  bool same = true;
+  for (int a = 1; a < nu; ++a) same = same && U[a].len == U[0].len;
+  if (same) {
+    const int L = U[0].len;
+    while (true) {
+      const int p = q + lane_id() * L;
+      bool hit = false;
+      if (p <= m.n)
+        for (int a = 0; a < nu; ++a) hit = hit || ((UA[a * nwt + (p >> 6)] >> (p & 63)) & 1ull);
+      const uint64_t miss = ballot(!hit);
+      if (miss) return q + ffs64(miss) * L;
+      q += 64 * L;
+    }
+  }
+  while (true) {
+    int a = 0;
+    for (; a < nu; ++a)
+      if ((UA[a * nwt + (q >> 6)] >> (q & 63)) & 1ull) break;
+    if (a == nu) return q;
+    q += U[a].len;
+  }
+}
+
+// any bit symbol 'F' (2) in b[0, n): 64 positions per step (wave-uniform callers)
+GD bool any_f(const uint8_t* b, int n) {
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane_id();
+    if (ballot(i < n && b[i] == 2)) return true;
+  }
   return false;
 }
 
-// hex digits of bits b[0, nb) (helpers.py:28-64) into T; returns the count (after lstrip('0'))
+// hex digits of bits b[0, nb) (helpers.py:28-64) into T; returns the count (after lstrip('0')).
+// Lane = digit, 64 digits per step, compacted by ballot; T is read back by every lane afterwards
+// (the barrier: T may be the slot's global scratch)
 GD int hex_text(const uint8_t* b, int nb, int strip_zero, uint8_t* T) {
-  const int nd = (nb + 3) >> 2;
+  const int nd = (nb + 3) >> 2, lane = lane_id();
   int q = 0;
   bool lead = strip_zero != 0;
-  for (int d = 0; d < nd; ++d) {
-    const int e = nb - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+  for (int d0 = 0; d0 < nd; d0 += 64) {
+    const int d = d0 + lane;
     int v = 0;
-    for (int i = a; i < e; ++i) v = (v << 1) | b[i];
-    if (lead && v == 0) continue;
-    lead = false;
-    T[q++] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+    if (d < nd) {
+      const int e = nb - 4 * (nd - 1 - d), a = (e - 4 > 0) ? e - 4 : 0;
+      for (int i = a; i < e; ++i) v = (v << 1) | b[i];
+    }
+    bool keep = d < nd;
+    if (lead) {  // leading zero digits are dropped up to the first non-zero one
+      const uint64_t nz = ballot(d < nd && v != 0);
+      if (!nz) continue;
+      keep = keep && lane >= ffs64(nz);
+      lead = false;
+    }
+    const uint64_t km = ballot(keep);
+    if (keep) T[q + popc64(km & ((1ull << lane) - 1))] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+    q += popc64(km);
   }
+  __syncthreads();  // one wave per workgroup: the digits of every lane are visible to all
   return q;
 }
 
@@ -330,6 +520,7 @@ GD int mu_chunk(const BankView& bv, Msg& m, int p0, int p1, uint8_t* B, uint8_t*
     int base = 0;
     Str& S = m.wk->str[0];
     S.len = 0;
+    GP_T(tp0);
     if (rec->has_start) {  // (:70-88)
       const int r = pex(m, &rec->start, 0, &S);
       if (r < 0) return SDX_RAISE_CONTRACT;
@@ -373,43 +564,47 @@ GD int mu_chunk(const BankView& bv, Msg& m, int p0, int p1, uint8_t* B, uint8_t*
         }
       }
     }
+    GP_ADD(0, tp0);
     if (fail || nu == 0) continue;
+    GP_CNT(8);
     if (!rec->recon) ne = 0;  // the regex tail and the chunk fallback both need reconstructBit
+    stage(m);
     const uint8_t* w = m.d + base;
     const int nw = m.n - base;
     const int W = rec->width;
+    const int lmin = rec->length_min;
+    bool amb = false;  // a unit that is a proper prefix of another: two units can match at one position
+    for (int a = 0; a < nu; ++a)
+      for (int b = 0; b < nu; ++b)
+        if (U[a].len < U[b].len && str_eq(U[a], U[b], U[a].len)) amb = true;
+    GP_T(tt0);
+    const uint64_t *succ = nullptr, *gsucc = nullptr;
+    const int tr = mu_tables(m, base, U, nu, S, lmin, amb, &succ, &gsucc);
+    GP_ADD(11, tt0);
+    if (tr < 0) return SDX_RAISE_CONTRACT;
+    if (tr == 0) continue;
     int pos = 0;
     while (pos <= nw) {  // matcher.finditer(current_raw_data) (:195)
-      int gq = -1, ge = -1, s = pos;
-      for (; s <= nw; ++s) {
-        // jump to the next position where the start string (or, without one, any unit) occurs
-        if (S.len) {
-          const int f = find_bm(m, base + s, S);
-          if (f < 0) break;
-          s = f - base;
-        } else {
-          int f = -1;
-          for (int j = 0; j < nu; ++j) {
-            const int g = find_bm(m, base + s, U[j]);
-            if (g >= 0 && (f < 0 || g < f)) f = g;
-          }
-          if (f < 0) {
-            s = nw;  // no unit left: only an empty repetition (length_min 0) can match at the end
-            if (rec->length_min > 0) break;
-          } else {
-            s = f - base;
-          }
-        }
+      GP_T(tf0);
+      const int sa = find_ok(m, base + pos, S.len, succ);  // the leftmost position the regex matches at
+      GP_ADD(1, tf0);
+      if (sa < 0) break;
+      const int s = sa - base, gq = s + S.len;
+      int ge;
+      GP_T(tr0);
+      if ((gsucc[(sa + S.len) >> 6] >> ((sa + S.len) & 63)) & 1ull) {
+        ge = greedy_end(m, U, nu, sa + S.len) - base;
+      } else {  // below lmin the greedy path dead-ends: sre's backtracking order, step by step
         bool over = false;
-        const int e = rep_match(w, nw, s + S.len, U, nu, rec->length_min, &over, m.wk->ch, m.wk->ps);
+        ge = rep_match(w, nw, gq, U, nu, lmin, &over, m.wk->ch, m.wk->ps);
+        GP_CNT(12);
         if (over) return SDX_RAISE_CONTRACT;
-        if (e >= 0) {
-          gq = s + S.len;
-          ge = e;
-          break;
+        if (ge < 0) {  // unreachable: gq is in D_lmin
+          pos = s + 1;
+          continue;
         }
       }
-      if (gq < 0) break;
+      GP_ADD(2, tr0);
       for (int j = 0; j < ne; ++j)  // (?:E0|E1|..)? : the first key that matches
         if (at(w, nw, ge, E[j].c, E[j].len)) {
           ge += E[j].len;
@@ -421,17 +616,28 @@ GD int mu_chunk(const BankView& bv, Msg& m, int p0, int p1, uint8_t* B, uint8_t*
       if (glen == 0) return SDX_RAISE_INDEX;  // chunks[-1] on [] (:212)
       const int nch = (glen + W - 1) / W;
       if (nch > rec->length_max) continue;  // (:217-218); INT32_MAX = no length_max
+      GP_CNT(10);
+      GP_T(tc0);
       int nb = 0;
-      for (int c = 0; c < nch; ++c) {  // (:220-229)
-        const int x = gq + c * W, cl = (ge - x < W) ? ge - x : W;
+      for (int c0 = 0; c0 < nch; c0 += 64) {  // (:220-229), lane = chunk; unmatched chunks are skipped
+        const int c = c0 + lane_id();
         int sy = -1;
-        for (int j = 0; j < nu && sy < 0; ++j)
-          if (U[j].len == cl && at(w, nw, x, U[j].c, cl)) sy = us[j];
-        for (int j = 0; j < ne && sy < 0; ++j)
-          if (E[j].len == cl && at(w, nw, x, E[j].c, cl)) sy = es[j];
-        if (sy >= 0) B[nb++] = (uint8_t)sy;
+        if (c < nch) {
+          const int x = gq + c * W, cl = (ge - x < W) ? ge - x : W;
+          for (int j = 0; j < nu && sy < 0; ++j)
+            if (U[j].len == cl && at(w, nw, x, U[j].c, cl)) sy = us[j];
+          for (int j = 0; j < ne && sy < 0; ++j)
+            if (E[j].len == cl && at(w, nw, x, E[j].c, cl)) sy = es[j];
+        }
+        const uint64_t hit = ballot(sy >= 0);
+        if (sy >= 0) B[nb + popc64(hit & ((1ull << lane_id()) - 1))] = (uint8_t)sy;
+        nb += popc64(hit);
       }
+      __syncthreads();  // B (the slot's global scratch) is read by every lane from here on
+      GP_ADD(3, tc0);
+      GP_T(tz0);
       const int rr = finish_mu_g(bv, rec, p, B, B2, T, nb, sk);
+      GP_ADD(4, tz0);
       if (rr) return rr;
     }
   }
@@ -525,6 +731,7 @@ GD int ms_chunk(const BankView& bv, Msg& m, int cp, bool ok, int p0, int p1, uin
       }
     }
     if (fail || nk == 0 || W <= 0) continue;
+    stage(m);
     int nb = 0;
     for (int i = mstart; i < m.n; i += W) {  // (:172-189)
       const int cl = (m.n - i < W) ? m.n - i : W;
@@ -563,8 +770,13 @@ GD int ms_chunk(const BankView& bv, Msg& m, int cp, bool ok, int p0, int p1, uin
 constexpr int GCH = 1;          // protocols per chunk (one: the most parallel; staging a message costs ~us)
 constexpr int GSLOTS = 1024;    // resident waves of the walk (scratch slots)
 constexpr int GHEAD = (int)((sizeof(Msg) + sizeof(Wk) + 15) & ~(size_t)15);  // LDS: Msg, Wk, then data
-__host__ __device__ inline int lds_need(int n) { return GHEAD + ((n + 7) & ~7); }                        // + the message's characters
-__host__ __device__ inline int lds_need_bm(int n) { return lds_need(n) + 80 * (((n + 63) >> 6) + 1); }   // + its digit bitmaps
+__host__ __device__ inline int lds_need(int n) { return GHEAD + ((n + 7) & ~7); }                   // + the message's characters
+__host__ __device__ inline int64_t lds_need_tb(int n) { return lds_need(n) + tb_bytes(n); }             // + the match tables
+// per-slot scratch: bits, postDemod output and payload text (max_len + GSLACK bytes each), then the
+// match tables of a message whose tables do not fit the LDS
+__host__ __device__ inline int64_t slot_bytes(int max_len) {
+  return ((3 * ((int64_t)max_len + GSLACK) + 255) & ~(int64_t)255) + ((tb_bytes(max_len) + 255) & ~(int64_t)255);
+}
 
 struct GenChunk {  // per (message, chunk); 24 bytes
   uint32_t nrec, nheap, rbase, hbase;
@@ -586,7 +798,7 @@ GI uint8_t* gen_region(const sdx_general_batch& b, const sdx_out& out, const Gen
 GI uint32_t* gen_ctr(const sdx_out& out) { return reinterpret_cast<uint32_t*>(out.work_dev); }
 GI GenChunk* gen_table(const sdx_out& out) { return reinterpret_cast<GenChunk*>(out.work_dev + 256); }
 GI uint8_t* gen_slot(const sdx_out& out, const GenPlan& g, int slot) {
-  return out.work_dev + g.tab + (int64_t)slot * 3 * (g.max_len + GSLACK);
+  return out.work_dev + g.tab + (int64_t)slot * slot_bytes(g.max_len);
 }
 
 __global__ __launch_bounds__(64) void k_gen_prep(sdx_general_batch b, sdx_out out, GenPlan g) {
@@ -628,6 +840,7 @@ __global__ __launch_bounds__(64) void k_gen_walk(const void* __restrict__ bank, 
   uint8_t* B = gen_slot(out, g, blockIdx.x);
   uint8_t* B2 = B + g.max_len + GSLACK;
   uint8_t* T = B2 + g.max_len + GSLACK;
+  uint64_t* TBG = reinterpret_cast<uint64_t*>(B + ((3 * ((int64_t)g.max_len + GSLACK) + 255) & ~(int64_t)255));
   Msg& m = *reinterpret_cast<Msg*>(glds);
   m.wk = reinterpret_cast<Wk*>(glds + sizeof(Msg));
   int cur = -1;  // the item's message whose characters / bitmaps are staged
@@ -652,6 +865,7 @@ __global__ __launch_bounds__(64) void k_gen_walk(const void* __restrict__ bank, 
         continue;
       }
     }
+    GP_T(ti0);
     if (i != cur) {  // stage the message (the LDS holds one)
       cur = i;
       const int64_t off = b.offsets_dev[msg];
@@ -662,20 +876,17 @@ __global__ __launch_bounds__(64) void k_gen_walk(const void* __restrict__ bank, 
       m.val = b.pat_val_dev + (size_t)msg * GP;
       m.nwp = ((m.n + 63) >> 6) + 1;
       const uint64_t* gbm = reinterpret_cast<const uint64_t*>(gen_region(b, out, g, i, msg));
-      m.bm = gbm;
-      __syncthreads();  // the previous item's reads of the LDS copy are done
-      if (lds_need(m.n) <= g.lds) {  // the serial walks read characters / bitmaps at LDS latency
-        uint8_t* ld = glds + GHEAD;
-        for (int j = lane; j < m.n; j += 64) ld[j] = m.d[j];
-        if (lds_need_bm(m.n) <= g.lds) {
-          uint64_t* lb = reinterpret_cast<uint64_t*>(glds + lds_need(m.n));
-          for (int j = lane; j < 10 * m.nwp; j += 64) lb[j] = gbm[j];
-          m.bm = lb;
-        }
-        m.d = ld;
+      m.bm = gbm;  // the digit bitmaps are read by the wide steps only (64 lanes): they stay in HBM / L2
+      m.nwt = tb_words(m.n);
+      m.tb = TBG;
+      m.ld = nullptr;
+      m.staged = 0;
+      if (lds_need(m.n) <= g.lds) {  // the characters (stage()) and the match tables at LDS latency
+        m.ld = glds + GHEAD;
+        if (lds_need_tb(m.n) <= g.lds) m.tb = reinterpret_cast<uint64_t*>(glds + lds_need(m.n));
       }
-      __syncthreads();
     }
+    GP_ADD(5, ti0);
     Sink sk{PASS == 1, 0, 0u, out.rec_dev, out.heap_dev, PASS == 1 ? e.rbase : 0u, PASS == 1 ? e.hbase : 0u,
             (uint32_t)msg};
     int rp = 0, raise;
@@ -689,7 +900,11 @@ __global__ __launch_bounds__(64) void k_gen_walk(const void* __restrict__ bank, 
       e.nrec = (uint32_t)sk.nrec;
       e.nheap = sk.nheap;
       e.raise = raise ? ((uint32_t)raise << 16) | (uint32_t)rp : 0u;
+#ifdef SDX_GPROF
+      e.res = (uint32_t)(__builtin_amdgcn_s_memtime() - ti0);
+#endif
     }
+    GP_ADD(6 + PASS, ti0);
   }
 }
 
@@ -858,6 +1073,17 @@ __global__ __launch_bounds__(256) void k_mc_general(const void* __restrict__ ban
 
 extern "C" {
 
+#ifdef SDX_GPROF
+int sdx_genprof_read(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(sdxg::g_genprof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sdxg::g_genprof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
 static sdxg::GenPlan gen_plan(const sdx_bank* bank, int kind, int32_t n, int32_t max_len) {
   sdxg::GenPlan g;
   const sdx_bank_hdr* h = sdx::bank_hdr(bank);
@@ -868,11 +1094,11 @@ static sdxg::GenPlan gen_plan(const sdx_bank* bank, int kind, int32_t n, int32_t
   const int64_t items = (int64_t)(n > 0 ? n : 0) * g.nch;
   g.slots = (int)(items < sdxg::GSLOTS ? (items > 0 ? items : 1) : sdxg::GSLOTS);
   g.tab = 256 + (((int64_t)(n > 0 ? n : 0) * g.nch * (int64_t)sizeof(sdxg::GenChunk) + 255) & ~(int64_t)255);
-  g.head = g.tab + (((int64_t)g.slots * 3 * (g.max_len + sdxg::GSLACK) + 255) & ~(int64_t)255);
-  // LDS per wave: the working set plus the longest message's characters and bitmaps, at most 64 KB
-  // (longer messages keep them in HBM)
-  const int64_t need = sdxg::lds_need_bm(g.max_len);
-  g.lds = need <= 65536 ? (int)need : (sdxg::lds_need(g.max_len) <= 65536 ? sdxg::lds_need(g.max_len) : sdxg::GHEAD);
+  g.head = g.tab + (int64_t)g.slots * sdxg::slot_bytes(g.max_len);
+  // LDS per wave: the working set plus the longest message's characters and match tables, at most
+  // 64 KB (what does not fit stays in HBM: the tables first)
+  const int64_t ntb = sdxg::lds_need_tb(g.max_len);
+  g.lds = ntb <= 65536 ? (int)ntb : (sdxg::lds_need(g.max_len) <= 65536 ? sdxg::lds_need(g.max_len) : sdxg::GHEAD);
   return g;
 }
 
