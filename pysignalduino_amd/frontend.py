@@ -278,18 +278,31 @@ class SignalParser:
             ok_ms = (kind == runtime.LINE_MS) & (status == runtime.LS_OK)  # cp_slot is written for these
             cps = np.where(ok_ms, np.clip(cps, 0, 9), 0)
             ms_clock = np.abs(pv[np.arange(n), cps])
-        hb = {k: v[2].tobytes() for k, v in res.items()}
+        # the host assembly reads Python lists / str slices, not numpy rows: one bulk conversion per
+        # array instead of a numpy scalar access per field (the per-line objects dominate this path)
+        cols = {}
+        for k, (desc, rec, heap) in res.items():
+            cols[k] = (desc["status"].tolist(), desc["raise_kind"].tolist(), desc["n_rec"].tolist(),
+                       desc["rec_begin"].tolist(), rec["proto"].tolist(), rec["payload_off"].tolist(),
+                       rec["payload_len"].tolist(), rec["bit_length"].tolist(), heap.tobytes().decode("latin-1"))
+        mb = meta.tobytes()
+        sb = slot.tobytes() if slot is not None else b""
+        hb_mn = res["MN"][2].tobytes() if "MN" in res else b""
+        status_l, kind_l, plen_l, off_l = status.tolist(), kind.tolist(), plen.tolist(), offsets.tolist()
+        ms_clock_l = ms_clock.tolist() if ms_clock is not None else None
+        mu_pids, ms_pids, mc_pids, mu_clock = bk.mu_pids, bk.ms_pids, bk.mc_pids, bk.mu_clock
+        ST_OK, ST_RAISED, R_CONTRACT = runtime.ST_OK, runtime.ST_RAISED, runtime.RAISE_CONTRACT
         out: List[Any] = []
         for i in range(n):
             if i in bad:
                 out.append(bad[i])
                 continue
-            st = int(status[i])
+            st = status_l[i]
             if st == runtime.LS_UNSUPPORTED:
                 out.append(ContractError(f"line {i} is outside the device contract of the front end "
-                                         f"(kind {_KIND_NAME.get(int(kind[i]), '?')})"))
+                                         f"(kind {_KIND_NAME.get(kind_l[i], '?')})"))
                 continue
-            name = _KIND_NAME.get(int(kind[i]))
+            name = _KIND_NAME.get(kind_l[i])
             if st == runtime.LS_GENERAL:
                 gname, j = gen_of[i]
                 _, gdesc, grec, gheap, gvals, gcps = gen[gname]
@@ -299,33 +312,59 @@ class SignalParser:
             if st != runtime.LS_OK or name not in res:
                 out.append([])
                 continue
-            desc, rec, _ = res[name]
-            d = desc[i]
-            if d["status"] == runtime.ST_RAISED and int(d["raise_kind"]) == runtime.RAISE_CONTRACT:
+            d_st, d_rk, d_nr, d_rb, r_p, r_off, r_len, r_bl, hs = cols[name]
+            dst = d_st[i]
+            if dst == ST_RAISED and d_rk[i] == R_CONTRACT:
                 out.append(_contract(i, name))   # a device limit (MC frames > 128 hex: k_mc_general)
                 continue
-            if d["status"] == runtime.ST_RAISED or int(d["n_rec"]) == 0:
+            nr = d_nr[i]
+            if dst == ST_RAISED or nr == 0:
                 out.append([])  # a demodulator exception is caught by the reference's parsers
                 continue
-            if d["status"] != runtime.ST_OK:
-                raise RuntimeError(f"device status {int(d['status'])} for line {i}")
+            if dst != ST_OK:
+                raise RuntimeError(f"device status {dst} for line {i}")
             if name == "MN":
-                out.append(self._mn_messages(lines[i], i, plen, offsets, slot, meta, d, rec, hb["MN"]))
+                out.append(self._mn_messages(lines[i], i, plen, offsets, slot, meta, res[name][0][i], res[name][1],
+                                             hb_mn))
                 continue
-            fr = self._frame(lines[i], i, plen, offsets, slot, meta, name)
-            rssi_raw = self._meta_str(meta[i], 0)
+            # RawFrame(line=payload) + _extract_metadata (mu.py:96-108, mc.py:141-155)
+            pl = plen_l[i]
+            if pl >= 0:
+                s0 = 3 * off_l[i]
+                payload_line = sb[s0: s0 + pl].decode("latin-1")
+            else:
+                ln = lines[i]
+                payload_line = (ln.decode("latin-1") if isinstance(ln, (bytes, bytearray, memoryview)) else ln).strip()[1:-1]
+            fr = RawFrame(line=payload_line, message_type=name)
+            m0 = 32 * i
+            rl, fl = mb[m0 + 15], mb[m0 + 31]
+            rssi_raw = None if rl == 255 else mb[m0: m0 + rl].decode("latin-1")
+            if rssi_raw is not None:
+                try:
+                    fr.rssi = calc_rssi(int(rssi_raw))
+                except ValueError:
+                    self.logger.warning("Could not parse %s value: %s", "RSSI", rssi_raw)
+            if fl != 255:
+                afc_raw = mb[m0 + 16: m0 + 16 + fl].decode("latin-1")
+                try:
+                    fr.freq_afc = calc_afc(int(afc_raw))
+                except ValueError:
+                    self.logger.warning("Could not parse %s value: %s", "AFC", afc_raw)
             msgs = []
-            for r in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
-                p = int(r["proto"])
-                off = int(r["payload_off"])
-                payload = hb[name][off: off + int(r["payload_len"])].decode("latin-1")
+            rb = d_rb[i]
+            for r in range(rb, rb + nr):
+                p = r_p[r]
+                o = r_off[r]
+                payload = hs[o: o + r_len[r]]
                 if name == "MC":
-                    pid = bk.mc_pids[p]
+                    pid = mc_pids[p]
                     md = {"protocol_id": pid, "rssi": None, "freq_afc": None}
+                elif name == "MU":
+                    pid = mu_pids[p]
+                    md = {"bit_length": r_bl[r], "rssi": rssi_raw, "clock": mu_clock[p]}
                 else:
-                    pid = bk.mu_pids[p] if name == "MU" else bk.ms_pids[p]
-                    clock = bk.mu_clock[p] if name == "MU" else float(ms_clock[i])
-                    md = {"bit_length": int(r["bit_length"]), "rssi": rssi_raw, "clock": clock}
+                    pid = ms_pids[p]
+                    md = {"bit_length": r_bl[r], "rssi": rssi_raw, "clock": ms_clock_l[i]}
                 msgs.append(DecodedMessage(protocol_id=str(pid), payload=payload, raw=fr, metadata=md))
             out.append(msgs)
         return out

@@ -362,36 +362,43 @@ class SDProtocols(UnitsMixin):
     def _decode_pulses(self, kind, desc, rec, heap, packer, pack_err, raise_errors):
         bk = self._bank
         pids = bk.mu_pids if kind == "MU" else bk.ms_pids
-        hb = heap.tobytes()
+        hs = heap.tobytes().decode("latin-1")   # latin-1 maps bytes 1:1: str slices == decoded byte slices
+        # bulk conversions: Python lists instead of a numpy scalar access per field and record
+        d_st, d_rk, d_rb, d_nr = (desc["status"].tolist(), desc["raise_kind"].tolist(), desc["rec_begin"].tolist(),
+                                  desc["n_rec"].tolist())
+        r_p, r_off, r_len, r_bl = (rec["proto"].tolist(), rec["payload_off"].tolist(), rec["payload_len"].tolist(),
+                                   rec["bit_length"].tolist())
+        mu = kind == "MU"
+        clocks = bk.mu_clock if mu else None
         out: List[Any] = []
-        for i in range(len(desc)):
+        for i in range(len(d_st)):
             if i in pack_err:
                 out.append(pack_err[i])
                 continue
-            d = desc[i]
-            if d["status"] == runtime.ST_RAISED:
-                if int(d["raise_kind"]) == runtime.RAISE_CONTRACT:
+            st = d_st[i]
+            if st == runtime.ST_RAISED:
+                rk = d_rk[i]
+                if rk == runtime.RAISE_CONTRACT:
                     exc = packing.ContractError(f"{kind} message exceeds a general-path limit (include/sdx.h SDX_GEN_*)")
                 else:
-                    exc = runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)(
-                        f"reference raises {runtime.RAISE_NAMES.get(int(d['raise_kind']), RuntimeError).__name__} "
+                    exc = runtime.RAISE_NAMES.get(rk, RuntimeError)(
+                        f"reference raises {runtime.RAISE_NAMES.get(rk, RuntimeError).__name__} "
                         f"on this {kind} message")
                 if raise_errors:
                     raise exc
                 out.append(exc)
                 continue
-            if d["status"] != runtime.ST_OK:
-                raise RuntimeError(f"device status {int(d['status'])} for message {i}")
-            rs = rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]
+            if st != runtime.ST_OK:
+                raise RuntimeError(f"device status {st} for message {i}")
             res = []
             rssi = packer.rssi[i]
-            for r in rs:
-                p = int(r["proto"])
-                off = int(r["payload_off"])
-                payload = hb[off: off + int(r["payload_len"])].decode("latin-1")
-                clock = bk.mu_clock[p] if kind == "MU" else packer.clock_abs[i]
-                res.append({"protocol_id": pids[p], "payload": payload,
-                            "meta": {"bit_length": int(r["bit_length"]), "rssi": rssi, "clock": clock}})
+            b = d_rb[i]
+            for r in range(b, b + d_nr[i]):
+                p = r_p[r]
+                o = r_off[r]
+                res.append({"protocol_id": pids[p], "payload": hs[o: o + r_len[r]],
+                            "meta": {"bit_length": r_bl[r], "rssi": rssi,
+                                     "clock": clocks[p] if mu else packer.clock_abs[i]}})
             out.append(res)
         return out
 
@@ -453,28 +460,32 @@ class SDProtocols(UnitsMixin):
             sel_only = np.array([-1 if not o else idx.get(str(o), len(bk.mc_pids)) for o in only], np.int16)
             bd["only"] = eng.torch.from_numpy(sel_only).to(eng.dev)
         desc, rec, heap = eng.run(runtime.KIND_MC, bd)
-        hb = heap.tobytes()
+        hs = heap.tobytes().decode("latin-1")
+        d_st, d_rk, d_rb, d_nr = (desc["status"].tolist(), desc["raise_kind"].tolist(), desc["rec_begin"].tolist(),
+                                  desc["n_rec"].tolist())
+        r_p, r_off, r_len = rec["proto"].tolist(), rec["payload_off"].tolist(), rec["payload_len"].tolist()
         out: List[Any] = []
-        for i in range(len(desc)):
+        for i in range(len(d_st)):
             if i in slot_err:
                 out.append(slot_err[i])
                 continue
-            d = desc[i]
-            if d["status"] == runtime.ST_RAISED:
-                exc = (packing.ContractError("MC payload longer than 65535 bytes") if int(d["raise_kind"]) ==
+            st = d_st[i]
+            if st == runtime.ST_RAISED:
+                exc = (packing.ContractError("MC payload longer than 65535 bytes") if d_rk[i] ==
                        runtime.RAISE_CONTRACT else
-                       runtime.RAISE_NAMES.get(int(d["raise_kind"]), RuntimeError)("reference raises on this MC frame"))
+                       runtime.RAISE_NAMES.get(d_rk[i], RuntimeError)("reference raises on this MC frame"))
                 if raise_errors:
                     raise exc
                 out.append(exc)
                 continue
-            if d["status"] != runtime.ST_OK:
-                raise RuntimeError(f"device status {int(d['status'])} for frame {i}")
+            if st != runtime.ST_OK:
+                raise RuntimeError(f"device status {st} for frame {i}")
             res = []
-            for r in rec[int(d["rec_begin"]): int(d["rec_begin"]) + int(d["n_rec"])]:
-                pid = bk.mc_pids[int(r["proto"])]
-                off = int(r["payload_off"])
-                res.append({"protocol_id": str(pid), "payload": hb[off: off + int(r["payload_len"])].decode("latin-1"),
+            b = d_rb[i]
+            for r in range(b, b + d_nr[i]):
+                pid = bk.mc_pids[r_p[r]]
+                o = r_off[r]
+                res.append({"protocol_id": str(pid), "payload": hs[o: o + r_len[r]],
                             "meta": {"protocol_id": pid, "rssi": None, "freq_afc": None}})
             out.append(res)
         return out

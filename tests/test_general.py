@@ -124,22 +124,24 @@ def test_general_very_long_messages_vs_oracle(proto, kind):
 
 def test_general_modified_bank_repetition_bounds_vs_oracle():
     """The match-table rounds (sdx_general.hip mu_tables) for repetition bounds the shipped bank does
-    not have: length_min 0 on a protocol without a start string (sre matches an empty repetition at
-    the search position, and chunks[-1] raises IndexError, message_unsynced.py:212), length_min 1,
-    and length_min at the general path's limit (SDX_GEN_REPMAX 128); oracle on the same bank."""
+    not have: length_min 1 (one unit: every unit occurrence starts a match), length_min 0 after a start
+    string (an empty repetition raises IndexError at chunks[-1], message_unsynced.py:212) and
+    length_min at the general path's limit (SDX_GEN_REPMAX 128); oracle on the same edited bank.
+    (No start and length_min 0 -- empty matches everywhere -- is outside the bank compiler's model.)"""
     from pysignalduino_amd import synth
     from pysignalduino_amd.sd_protocols import SDProtocols
     p = SDProtocols()
     P = p.get_protocol_list()
     nostart = [pid for pid, v in P.items() if "clockabs" in v and "start" not in v and v.get("active", True)]
     withstart = [pid for pid, v in P.items() if "clockabs" in v and "start" in v and v.get("active", True)]
-    edits = {nostart[0]: 0, nostart[1]: 1, nostart[2]: 128, withstart[0]: 0, withstart[1]: 128}
+    edits = {nostart[1]: 1, nostart[2]: 128, withstart[0]: 0, withstart[1]: 128, withstart[2]: 1}
     for pid, lmin in edits.items():
         p._protocols[pid]["length_min"] = lmin
     ob = O.OracleBank(p.get_protocol_list())
     msgs = synth.general_pulse_messages(P, "MU", 300, seed=611)
     got = p.demodulate_batch(msgs, "MU")
-    bad = [(i, _oracle(ob, m, "MU"), _flat(g)) for i, (m, g) in enumerate(zip(msgs, got))
-           if _flat(g) != _oracle(ob, m, "MU")]
+    exp = [_oracle(ob, m, "MU") for m in msgs]
+    bad = [(i, e, _flat(g)) for i, (e, g) in enumerate(zip(exp, got)) if _flat(g) != e]
     assert not bad, f"{len(bad)}/{len(msgs)} mismatches; first: {bad[:2]}"
-    assert sum(1 for g in got if isinstance(g, IndexError)) > 0  # the empty repetition at the start
+    edited = sum(1 for e in exp for r in e.get("results", []) if r[0] in edits)
+    assert edited > 1000 and sum(1 for e in exp if e.get("raise") == "IndexError") > 0
