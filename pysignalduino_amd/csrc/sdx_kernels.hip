@@ -2736,9 +2736,7 @@ int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out*
   hipStream_t st = (hipStream_t)hip_stream;
   const int grid = (ntot + 255) / 256;
   hipLaunchKernelGGL((sdx::k_mc<sdx::MC_SHORTW, false>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
-#ifndef SDX_X_NOMCLONG
   hipLaunchKernelGGL((sdx::k_mc<sdx::MC_MAXW, true>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
-#endif
   HIPCHK(hipGetLastError());
   return SDX_OK;
 }
