@@ -268,6 +268,7 @@ def _gap_ranks(v: float, klo: int, khi: int) -> List[int]:
 # bench corpus (tools/prof_phases.py, r03; group cost minus one normalisation, split evenly over the
 # group's protocols), and the normalisation's cost per group: the work-list order of Bank (LPT).
 MU_NORM_KCYC = 3.8
+MU_SPLIT_KCYC = 60.0
 MU_COST_KCYC = {
     "15": 19.3, "121": 18.1, "34": 16.2, "120": 14.6, "9": 14.6, "111": 14.6, "118.1": 11.9, "118": 11.9,
     "8": 11.7, "39": 11.1, "1": 11.1, "86": 11.0, "14": 11.0, "25": 11.0, "13": 10.9, "63": 10.9, "13.1": 10.9,
@@ -618,6 +619,32 @@ class Bank:
             glist = sorted(groups.values(), key=lambda g: -len(g))
         else:
             glist = sorted(groups.values(), key=lambda g: (-gcost(g), -len(g)))
+        # work items of at most ~MU_SPLIT_KCYC: a clock group whose cost exceeds it is cut at protocol
+        # boundaries into pieces of about equal cost (each repeats the normalisation).  The tile's 8
+        # waves then end closer together at the end-of-loop barrier: the largest group (≈ 146 kcyc,
+        # ≈ one wave's whole share) sets the tile's critical path whenever the other groups of the
+        # tile run cheaper than average.  Measured (profiles/r03/s2/mu_split_*.log): k_pulses<MU>
+        # 1.098-1.101 ms unsplit, 1.042-1.050 ms at 50-100 kcyc.  SDX_MU_SPLIT=0 disables (A/B).
+        split = float(os.environ.get("SDX_MU_SPLIT", str(MU_SPLIT_KCYC)))
+        if split > 0:
+            pieces = []
+            for g in glist:
+                m = int(np.ceil((gcost(g) - MU_NORM_KCYC) / split))
+                if m <= 1:
+                    pieces.append(g)
+                    continue
+                tot = gcost(g) - MU_NORM_KCYC
+                # cut by cumulative cost into m pieces of about equal cost
+                cum, cut, cur = 0.0, 1, []
+                for r in g:
+                    cur.append(r)
+                    cum += MU_COST_KCYC.get(str(self.mu_pids[r]), med)
+                    if cum >= tot * cut / m and cut < m:
+                        pieces.append(cur)
+                        cur, cut = [], cut + 1
+                if cur:
+                    pieces.append(cur)
+            glist = sorted(pieces, key=lambda g: (-gcost(g), -len(g)))
         self.mu_order = [r for g in glist for r in g]
         self.mu_gstart = list(np.cumsum([0] + [len(g) for g in glist]))
         self.ms_order = list(range(len(self.ms_pids)))
