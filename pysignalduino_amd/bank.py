@@ -287,6 +287,20 @@ MU_COST_KCYC = {
     "4": 2.7, "3.1": 2.7, "17": 2.7, "0.3": 2.7, "0": 2.7, "24": 1.9
 }
 
+# MS per-protocol cost of the filter loop in k_pulses<MS> (kcyc per tile and grab, tools/prof_phases.py
+# on the bench corpus, profiles/r03/s2/phases_split.log): the processing order is descending cost
+# (LPT), so the 8 waves of a tile end their protocol loops closer together
+MS_COST_KCYC = {
+    "54.1": 16.7, "1": 14.9, "4": 14.6, "17": 13.4, "13.2": 13.0, "88": 12.9, "15": 12.8, "13": 12.4,
+    "53": 12.0, "0.1": 11.6, "128.1": 11.5, "87": 11.2, "33.2": 10.2, "7.1": 10.2, "41": 10.2, "3": 10.1,
+    "49": 10.0, "0": 9.9, "0.2": 9.8, "51": 9.7, "33": 9.6, "2": 9.4, "106": 9.4, "25": 9.3, "0.4": 9.3,
+    "33.1": 9.0, "6": 8.9, "93": 8.8, "3.1": 8.7, "0.3": 8.4, "100": 8.4, "65": 8.3, "23": 8.2, "112": 7.4,
+    "123": 7.4, "74.1": 7.3, "134": 7.1, "125": 7.1, "68": 7.1, "109": 7.1, "91.1": 7.0, "103": 7.0,
+    "14": 6.9, "107": 6.8, "0.5": 6.6, "35": 6.6, "127.1": 6.5, "116": 6.4, "131": 6.4, "113": 6.0,
+    "116.1": 6.0, "72.1": 6.0, "107.1": 6.0, "126": 5.7, "20": 5.5, "7": 5.3, "55": 5.1, "130": 5.1,
+    "118.1": 5.0, "90": 4.8, "117": 3.3, "101": 3.2, "108": 3.0, "133": 2.8, "115": 2.8, "102": 2.8
+}
+
 
 class Bank:
     """A compiled bank: the device blob plus host-side metadata for result building."""
@@ -647,7 +661,12 @@ class Bank:
             glist = sorted(pieces, key=lambda g: (-gcost(g), -len(g)))
         self.mu_order = [r for g in glist for r in g]
         self.mu_gstart = list(np.cumsum([0] + [len(g) for g in glist]))
-        self.ms_order = list(range(len(self.ms_pids)))
+        if os.environ.get("SDX_MS_ORDER") == "bank":   # A/B: bank order
+            self.ms_order = list(range(len(self.ms_pids)))
+        else:   # descending profile-guided cost; results are placed by protocol index
+            ms_med = float(np.median(list(MS_COST_KCYC.values())))
+            self.ms_order = sorted(range(len(self.ms_pids)),
+                                   key=lambda r: -MS_COST_KCYC.get(str(self.ms_pids[r]), ms_med))
         order = np.asarray(self.mu_order + self.ms_order + self.mu_gstart, dtype=np.uint16)
         ranks = np.asarray(self._ranks, dtype=np.uint16)
         sections = [mu.tobytes(), ms.tobytes(), mc.tobytes(), drec.tobytes(), cls_arr.tobytes(),
