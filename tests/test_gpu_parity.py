@@ -291,6 +291,33 @@ def test_message_records_match_soa_and_results(kind):
     assert all(x.tobytes() == y.tobytes() for x, y in zip(a, b))
 
 
+@pytest.mark.parametrize("kind,n", [("MU", 333333), ("MS", 5000), ("MU", 2049), ("MS", 1)])
+def test_grouping_is_a_stable_sort_of_the_keys(kind, n):
+    """sdx_group_pulses (k_sig + the 2-launch-per-pass radix sort, sdx_group.hip): the order is a
+    permutation of the messages, the sorted keys it leaves in the workspace's first array are
+    non-decreasing, and equal keys keep ascending message indices (stable) -- at the bench size
+    (163 partitions), a partition boundary plus one, and a single message."""
+    import torch
+    from pysignalduino_amd import bank as B, runtime, synth
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    gen = synth.mu_corpus if kind == "MU" else synth.ms_corpus
+    batch = gen(bk.protocols, n, seed=9400 + n)
+    k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
+    bd = eng.to_device_pulses(batch)
+    bufs = eng.group_buffers(n)
+    order = eng.group(k, bd, bufs=bufs)
+    torch.cuda.synchronize()
+    o = order.cpu().numpy().astype(np.int64)
+    keys = bufs[1][: 4 * n].cpu().numpy().view(np.uint32).astype(np.int64)
+    assert np.array_equal(np.sort(o), np.arange(n))
+    assert (np.diff(keys) >= 0).all()
+    same = np.diff(keys) == 0
+    assert (np.diff(o)[same] > 0).all()
+    if n > 1000:
+        assert len(np.unique(keys)) > 1   # the keys actually differ: the sort was exercised
+
+
 @pytest.mark.gpu
 def test_mc_long_frames_vs_oracle():
     """Frames of 1..128 hex characters: the short (<= 64) and long (65..128) k_mc launches together
