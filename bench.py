@@ -329,8 +329,10 @@ def main():
             u.record(stream)
             used[par] = u
         if exch is not None:  # RCCL all-gather of the decoded dmsg buffers (config 5), overlapped
-            done[s_] = exch.submit([(outs[s_][k]["desc"], outs[s_][k]["rec"], outs[s_][k]["heap"], bds[k]["n"],
-                                     outs[s_][k]["cursor"]) for k in kinds], stream)
+            rel = exch.submit([(outs[s_][k]["desc"], outs[s_][k]["rec"], outs[s_][k]["heap"], bds[k]["n"],
+                               outs[s_][k]["cursor"]) for k in kinds], stream)
+            if rel is not None:             # the previous step's pack has read its slot
+                done[(j - 1) % nslot] = rel
 
     def drain():
         stream.wait_stream(side)

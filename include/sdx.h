@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 9
+#define SDX_ABI_VERSION 10
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -449,6 +449,12 @@ int sdx_exchange_count(const sdx_xchg_part* parts, int k, void* work_dev, uint64
 /* after sdx_exchange_count on the same stream (reads its counts_dev and workspace) */
 int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, const uint32_t* counts_dev,
                       uint8_t* send_dev, uint64_t send_cap, void* hip_stream);
+/* ABI 10: the same pack after the counts have reached the host (counts_host = the same u32[4k]):
+ * dst_dev needs only the exact wire size (16-byte aligned), so the wire can be written straight into
+ * this rank's chunk of an in-place all-gather's receive buffer (no send buffer, no local copy) */
+int sdx_exchange_pack_into(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
+                           const uint32_t* counts_dev, const uint32_t* counts_host, uint8_t* dst_dev, uint64_t dst_cap,
+                           void* hip_stream);
 
 /* receiver: one launch's wire sections of every rank (rank order = global message order) -> the
  * whole job's sdx_desc[sum n_msgs], sdx_result[sum n_rec] and one contiguous heap (sum n_heap bytes,

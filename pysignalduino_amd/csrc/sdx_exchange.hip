@@ -508,6 +508,26 @@ extern "C" int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_d
   return launched("k_xw_pack");
 }
 
+// the pack into a buffer sized from the host's copy of the counts (the exact layout), e.g. the rank's
+// own chunk of an in-place all-gather's receive buffer
+extern "C" int sdx_exchange_pack_into(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
+                                      const uint32_t* counts_dev, const uint32_t* counts_host, uint8_t* dst_dev,
+                                      uint64_t dst_cap, void* hip_stream) {
+  if (int rc = check_parts(parts, k, "sdx_exchange_pack_into")) return rc;
+  if (!counts_dev || !counts_host || !dst_dev || ((uintptr_t)dst_dev & 15u) || !work_ok(parts, k, work_dev, work_cap))
+    return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: missing / unaligned buffer or workspace too small");
+  uint64_t need = 0;
+  for (int i = 0; i < k; ++i) {
+    if (counts_host[4 * i] != parts[i].n_msgs)
+      return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: counts_host are not this exchange's counts");
+    need += r16(4ull * counts_host[4 * i]) + r16(8ull * counts_host[4 * i + 1]) + r16(counts_host[4 * i + 2]);
+  }
+  if (dst_cap < need) return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: destination smaller than the wire");
+  hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream,
+                     make_parts(parts, k), counts_dev, (uint8_t*)work_dev, dst_dev);
+  return launched("k_xw_pack");
+}
+
 extern "C" uint64_t sdx_exchange_unpack_work_bytes(uint32_t n_msgs, uint32_t n_rec) {
   return 64 + 8ull * (nblk_of(n_msgs) + nblk_of(n_rec));
 }

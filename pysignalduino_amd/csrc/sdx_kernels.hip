@@ -187,7 +187,7 @@ struct TileLds {
   int nsurv;
   MsDesc msdesc[LM == 2 ? MS_DESC_LDS : 1];
 #ifdef SDX_PROF
-  unsigned int prof[LM != 0 ? LANE_WAVES : 4][24];  // s_memtime deltas per wave (< 2^32 per kernel)
+  unsigned int prof[LM != 0 ? LANE_WAVES : 4][28];  // s_memtime deltas per wave (< 2^32 per kernel)
 #endif
 };
 
@@ -1507,7 +1507,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     for (int i = tid; i < nd; i += blockDim.x) L.msdesc[i] = ms_desc(bv.ms + i);
   }
 #ifdef SDX_PROF
-  if (lane < 24) L.prof[wave][lane] = 0;
+  if (lane < 28) L.prof[wave][lane] = 0;
 #endif
   __syncthreads();
   PROF_T(t_kernel);
@@ -2156,7 +2156,13 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     if (!L.ovf) {
       // survivors packed into the first waves (dealing them round-robin over all 8 measured
       // 0.73 vs 0.645 ms: more waves on the same divergent decode path)
+#ifdef SDX_MSDEC_BLOCK
+      const int per = (ns + LANE_WAVES - 1) / LANE_WAVES;
+      const int i_end = (wave + 1) * per < ns ? (wave + 1) * per : ns;
+      for (int i = wave * per + lane; i < i_end; i += 64) {
+#else
       for (int i = tid; i < ns; i += blockDim.x) {
+#endif
         const MsItem it = L.slist[i];
         const int qm = it.mi, qp = it.p;
         const uint32_t rk = L.raise_key[qm];
@@ -2219,7 +2225,17 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       for (int m = tid; m < nm; m += blockDim.x) perm[atomicAdd(&bin[L.mlist[m].p], 1u)] = (uint16_t)m;
       __syncthreads();
     }
+    PROF_ADD(24, t_fin);
+    PROF_T(t_fl0);
+#ifdef SDX_FIN_BLOCK
+    // every wave takes a contiguous block of the protocol-sorted matches (all 8 waves busy, a wave's
+    // lanes on few protocols) instead of match i -> thread i (the first nm / 64 waves busy)
+    const int per = (nm + LANE_WAVES - 1) / LANE_WAVES;
+    const int i_end = (wave + 1) * per < nm ? (wave + 1) * per : nm;
+    for (int i = wave * per + lane; i < i_end; i += 64) {
+#else
     for (int i = tid; i < nm; i += blockDim.x) {
+#endif
       const MuMatch mm = i < MATCH_CAP ? L.mlist[sorted ? perm[i] : i] : spilled[i - MATCH_CAP];
       const int qm = mm.mi, qp = mm.p;
       const uint32_t rk = L.raise_key[qm];
@@ -2233,7 +2249,10 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       finish_mu_lane<NW>(L, out, wave, bv, bv.mu + qp, d, qp, qm, mm.j, mm.q, mm.k, d.width, (mm.flags & 1) != 0,
                          (uint8_t)((mm.flags >> 1) & 3), V1, VF);
     }
+    PROF_ADD(25, t_fl0);
+    PROF_T(t_fb);
     __syncthreads();
+    PROF_ADD(26, t_fb);
     PROF_ADD(16, t_fin);
   }
   PROF_T(t_fl);
@@ -2245,7 +2264,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   if (tid == 0 && blockIdx.x < 65536) g_wgt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
 #ifdef SDX_PROF
-  if (lane < 24) atomicAdd(&g_prof[lane], (unsigned long long)L.prof[wave][lane]);
+  if (lane < 28) atomicAdd(&g_prof[lane], (unsigned long long)L.prof[wave][lane]);
 #endif
 }
 

@@ -18,9 +18,9 @@ With the ``nccl`` backend (RCCL over xGMI on ROCm) the buffers stay in HBM and t
 its own HIP stream (:class:`Exchange`), overlapped with the next step's kernels:
   step k kernels ─ready_k─▶ [exchange stream] sdx_exchange_count_k ─ all-gather counts_k ─ D2H
   submit(k+1): host waits for counts_k (the GPU runs step k+1 meanwhile), sizes the sections (max
-               over ranks), enqueues sdx_exchange_pack_k ─released_k─ all-gather data_k, and only
-               then the wait on ready_{k+1} and step k+1's count: step k's pack and collective never
-               wait for step k+1's kernels.
+               over ranks), enqueues sdx_exchange_pack_into_k (this rank's chunk of the receive
+               buffer) ─released_k─ in-place all-gather data_k, and only then the wait on ready_{k+1}
+               and step k+1's count: step k's pack and collective never wait for step k+1's kernels.
 The same protocol runs synchronously on ``gloo`` (CPU tensors: numpy packing; CUDA tensors: the
 device kernels, the collective staged through host memory).
 """
@@ -158,10 +158,10 @@ def _part_tuple(p):
 
 
 class _Pending:
-    __slots__ = ("parts", "counts_host", "event", "enc")
+    __slots__ = ("parts", "counts_host", "event", "enc", "cnt")
 
-    def __init__(self, parts, counts_host, event, enc=None):
-        self.parts, self.counts_host, self.event, self.enc = parts, counts_host, event, enc
+    def __init__(self, parts, counts_host, event, enc=None, cnt=None):
+        self.parts, self.counts_host, self.event, self.enc, self.cnt = parts, counts_host, event, enc, cnt
 
 
 class Exchange:
@@ -172,9 +172,11 @@ class Exchange:
     = heap bytes, left on the device; the capacities are the buffers' sizes).  It first completes
     the PREVIOUS step's exchange (the data all-gather: its counts arrived while this step's kernels
     were running) and then enqueues this step's count + pack + count all-gather behind this step's
-    kernels.  It returns the event after which THIS step's output buffers may be overwritten (the
-    pack has read them; double-buffer the outputs so that the next step does not wait for it).
-    ``flush()`` completes the last step.  ``gathered()`` gives the last completed step's results as
+    kernels.  It returns the event after which the PREVIOUS step's output buffers may be overwritten
+    (its pack has read them; None on the first call): with the nccl backend a step is packed once its
+    counts are on the host, straight into this rank's chunk of the receive buffer, and all-gathered in
+    place (no send buffer, no local copy), so double-buffer the outputs.  ``flush()`` completes the
+    last step and returns the same event for it.  ``gathered()`` gives the last completed step's results as
     per launch (desc, rec, heap) byte tensors of the whole job in global message order.
 
     A launch with overflowed messages (the counts' "bad" column) makes every rank raise in the
@@ -215,6 +217,17 @@ class Exchange:
         w = self._buf(("work",) + tuple(ns), wb + 256, dev, zero=True)
         off = (-w.data_ptr()) % 256
         return w[off:], wb
+
+    def _count_device(self, parts, stream):
+        """sdx_exchange_count on `stream`: [K*4] int32 device counts (the pack follows once the host
+        has them: _complete, sdx_exchange_pack_into)."""
+        lib = runtime.load_library()
+        dev = parts[0][0].device
+        work, wb = self._work(parts, dev)
+        cnt = torch.empty(4 * len(parts), dtype=torch.int32, device=dev)
+        runtime._check(lib, lib.sdx_exchange_count(self._xparts(parts), len(parts), ctypes.c_void_p(work.data_ptr()), wb,
+                                                   ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
+        return cnt
 
     def _count_pack_device(self, parts, stream):
         """sdx_exchange_count + sdx_exchange_pack on `stream`: [K*4] int32 device counts; the wire
@@ -268,38 +281,42 @@ class Exchange:
         if self.stream is None:
             self.stream = torch.cuda.Stream(dev)
         stream = stream or torch.cuda.current_stream(dev)
-        # 1. the previous step's data collective: its counts are (about to be) on the host, and it is
-        #    enqueued ahead of anything that waits for this step's kernels
+        # 1. the previous step: its counts are (about to be) on the host -- pack it into its chunk of
+        #    the receive buffer and all-gather in place, ahead of anything that waits for this step
         prev, self.pending = self.pending, None
+        released = None
         if prev is not None:
             with torch.cuda.stream(self.stream):
-                self._complete(prev)
-        # 2. this step: count + pack + count all-gather, behind this step's kernels
+                released = self._complete(prev)
+        # 2. this step: count + count all-gather + counts to the host, behind this step's kernels
         ready = torch.cuda.Event()
         ready.record(stream)
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ready)
-            cnt = self._count_pack_device(parts, self.stream)
-            released = torch.cuda.Event()
-            released.record(self.stream)     # the launches' buffers have been read
+            cnt = self._count_device(parts, self.stream)
             allc = torch.empty(self.world * K * 4, dtype=torch.int32, device=dev)
             _all_gather_flat(allc, cnt, self.group)
             host = torch.empty(allc.numel(), dtype=torch.int32, pin_memory=True)
             host.copy_(allc, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
-        self.pending = _Pending(parts, host, ev)
+        self.pending = _Pending(parts, host, ev, cnt=cnt)
         return released
 
     def flush(self):
+        """Completes the last submitted step; returns the event after which its output buffers may
+        be overwritten (None when nothing was pending)."""
         prev, self.pending = self.pending, None
-        if prev is not None:
-            with torch.cuda.stream(self.stream):
-                self._complete(prev)
+        if prev is None:
+            return None
+        with torch.cuda.stream(self.stream):
+            return self._complete(prev)
 
     def _complete(self, p: _Pending):
         """The data collective of a step whose counts are on (or on their way to) the host; device
-        buffers: on the current stream."""
+        buffers: on the current stream.  nccl: the step is packed here (sdx_exchange_pack_into) into
+        this rank's chunk of the receive buffer and gathered in place; returns the event after which
+        the step's output buffers may be overwritten."""
         K = len(p.parts)
         if p.event is not None:
             p.event.synchronize()            # the counts (the GPU has moved on to the next step)
@@ -311,6 +328,7 @@ class Exchange:
         dev = p.parts[0][0].device
         self.bytes_sent.append(T)
         self.wire_bytes.append(int(nb[self.rank].sum()))
+        released = None
         if dev.type != "cuda":               # host packing (gloo, CPU tensors)
             send = torch.zeros(T, dtype=torch.uint8)
             sv = send.numpy()
@@ -320,11 +338,24 @@ class Exchange:
                 sv[o[1]: o[1] + 8 * len(w)] = w.view(np.uint8)
                 sv[o[2]: o[2] + len(pay)] = pay
             recv = torch.empty(self.world * T, dtype=torch.uint8)
+        elif p.cnt is not None:              # nccl: pack into the rank's chunk, all-gather in place
+            lib = runtime.load_library()
+            recv = self._buf("recv", self.world * T, dev)[: self.world * T]
+            send = recv[self.rank * T: (self.rank + 1) * T]
+            work, wb = self._work(p.parts, dev)
+            mine = np.ascontiguousarray(S[self.rank].reshape(-1).astype(np.uint32))
+            runtime._check(lib, lib.sdx_exchange_pack_into(
+                self._xparts(p.parts), K, ctypes.c_void_p(work.data_ptr()), wb, ctypes.c_void_p(p.cnt.data_ptr()),
+                mine.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(send.data_ptr()), T,
+                ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+            released = torch.cuda.Event()
+            released.record(torch.cuda.current_stream(dev))   # the launches' buffers have been read
         else:
             send = self._bufs["send"][:T]
             recv = self._buf("recv", self.world * T, dev)[: self.world * T]
         _all_gather_flat(recv, send, self.group)
         self.last = (recv, S, offs, nb, T)
+        return released
 
     def gathered(self) -> List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
         """Per launch (desc, rec, heap) byte tensors of the last completed exchange: the whole job in

@@ -41,7 +41,7 @@ RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u
 EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
             "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
-            "sdx_exchange_work_bytes", "sdx_exchange_send_bytes", "sdx_exchange_count", "sdx_exchange_pack", "sdx_exchange_unpack_work_bytes",
+            "sdx_exchange_work_bytes", "sdx_exchange_send_bytes", "sdx_exchange_count", "sdx_exchange_pack", "sdx_exchange_pack_into", "sdx_exchange_unpack_work_bytes",
             "sdx_exchange_unpack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
             "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general",
             "sdx_lines_general"]
@@ -199,12 +199,15 @@ def load_library(path: Optional[str] = None):
     lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
                                       ctypes.c_uint64, c_void_p]
     lib.sdx_exchange_pack.restype = c_int
+    lib.sdx_exchange_pack_into.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
+                                           c_void_p, ctypes.c_uint64, c_void_p]
+    lib.sdx_exchange_pack_into.restype = c_int
     lib.sdx_exchange_unpack_work_bytes.argtypes = [c_uint32, c_uint32]
     lib.sdx_exchange_unpack_work_bytes.restype = ctypes.c_uint64
     lib.sdx_exchange_unpack.argtypes = [POINTER(SdxXchgWire), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
                                         c_void_p, c_void_p]
     lib.sdx_exchange_unpack.restype = c_int
-    if lib.sdx_abi_version() != 9:
+    if lib.sdx_abi_version() != 10:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:

@@ -16,7 +16,8 @@ NAMES = {0: "stage bitmaps", 1: "MU normalise", 2: "MU pexists(start)", 3: "MU p
          8: "MU payload write", 9: "MU format+DFA", 10: "MS decode", 11: "MS finish", 12: "MU decode total",
          13: "flush", 14: "end barrier wait", 15: "kernel total", 16: "MU finish phase (lane = match)",
          17: "  stage: headers + pattern tables", 18: "  stage: id bitmaps", 19: "  stage: pairs + lengths", 20: "#results(MU)", 21: "#survivors(MU)",
-         22: "#matches(MU)", 23: "#survivors(MS)"}
+         22: "#matches(MU)", 23: "#survivors(MS)", 24: "  finish: tables + sort (to the loop)",
+         25: "  finish: match loop", 26: "  finish: end barrier"}
 
 
 def main():
@@ -51,7 +52,7 @@ def main():
         for i in sorted(NAMES):
             if v[i] == 0:
                 continue
-            if i >= 20:
+            if 20 <= i < 24:
                 print(f"  {NAMES[i]:28s} {v[i]:.0f}  ({v[i]/pb.n:.2f} per message)")
             else:
                 print(f"  {NAMES[i]:28s} {v[i]/tot*100:6.2f} %   {v[i]/pb.n:9.0f} wave-cycles/msg")
