@@ -2156,13 +2156,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     if (!L.ovf) {
       // survivors packed into the first waves (dealing them round-robin over all 8 measured
       // 0.73 vs 0.645 ms: more waves on the same divergent decode path)
-#ifdef SDX_MSDEC_BLOCK
-      const int per = (ns + LANE_WAVES - 1) / LANE_WAVES;
-      const int i_end = (wave + 1) * per < ns ? (wave + 1) * per : ns;
-      for (int i = wave * per + lane; i < i_end; i += 64) {
-#else
       for (int i = tid; i < ns; i += blockDim.x) {
-#endif
         const MsItem it = L.slist[i];
         const int qm = it.mi, qp = it.p;
         const uint32_t rk = L.raise_key[qm];
@@ -2227,15 +2221,10 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     }
     PROF_ADD(24, t_fin);
     PROF_T(t_fl0);
-#ifdef SDX_FIN_BLOCK
-    // every wave takes a contiguous block of the protocol-sorted matches (all 8 waves busy, a wave's
-    // lanes on few protocols) instead of match i -> thread i (the first nm / 64 waves busy)
-    const int per = (nm + LANE_WAVES - 1) / LANE_WAVES;
-    const int i_end = (wave + 1) * per < nm ? (wave + 1) * per : nm;
-    for (int i = wave * per + lane; i < i_end; i += 64) {
-#else
+    // match i -> thread i: the first nm / 64 waves work, the others leave their SIMDs' issue slots
+    // to the CU's other tile (contiguous blocks over all 8 waves measured slower: MU 1.144-1.159 vs
+    // 1.124-1.125 ms, profiles/r03/s2/blk_*)
     for (int i = tid; i < nm; i += blockDim.x) {
-#endif
       const MuMatch mm = i < MATCH_CAP ? L.mlist[sorted ? perm[i] : i] : spilled[i - MATCH_CAP];
       const int qm = mm.mi, qp = mm.p;
       const uint32_t rk = L.raise_key[qm];
