@@ -286,6 +286,26 @@ MU_COST_KCYC = {
     "0.5": 4.0, "69": 3.8, "0.4": 3.8, "49.1": 3.7, "32": 3.3, "62": 3.0, "0.2": 2.7, "0.1": 2.7, "3": 2.7,
     "4": 2.7, "3.1": 2.7, "17": 2.7, "0.3": 2.7, "0": 2.7, "24": 1.9
 }
+# the same, re-measured with one protocol per work item after the round-3 kernel changes
+# (SDX_MU_SPLIT=0.001 SDX_PROF build, profiles/r03/s2/phases_per_protocol.log; minus MU_NORM_KCYC)
+MU_COST_KCYC_R3 = {
+    "111": 30.2, "1": 23.7, "63": 23.0, "34": 22.2, "118.1": 21.7, "15": 21.5, "74": 19.6, "88": 18.6,
+    "25": 17.9, "42": 17.7, "87": 17.4, "121": 17.1, "82": 16.7, "72.1": 16.3, "8": 15.8, "70": 14.9,
+    "2": 14.7, "61": 14.4, "9": 14.3, "80": 14.2, "74.1": 14.1, "91.1": 13.9, "120": 13.8, "130": 12.8,
+    "73": 12.5, "19": 12.4, "13": 12.3, "27": 12.2, "20": 12.2, "71": 11.9, "90": 11.2, "39": 10.7,
+    "40": 10.3, "35": 10.2, "14": 10.0, "55": 9.7, "91": 9.5, "33.2": 9.3, "118": 9.2, "54": 8.9, "85": 8.9,
+    "38": 8.7, "64": 8.6, "89": 8.4, "54.1": 8.3, "75": 8.3, "20.1": 8.3, "99": 8.3, "72": 8.2, "41": 8.1,
+    "13.1": 8.1, "86": 8.0, "76": 7.9, "5": 7.8, "7.1": 7.7, "104": 7.5, "92": 7.4, "16": 7.3, "37": 7.3,
+    "45": 7.3, "22": 7.2, "23": 7.1, "127.1": 7.1, "135": 7.1, "128.1": 7.0, "50": 7.0, "49": 6.6, "93": 6.4,
+    "122": 6.3, "106": 6.3, "114": 6.3, "56": 6.2, "113": 6.2, "33": 6.1, "31": 6.1, "26": 6.1, "44.1": 6.0,
+    "53": 6.0, "28": 5.4, "21": 5.3, "51": 5.1, "84": 5.0, "68": 4.9, "110": 4.8, "60": 4.8, "95": 4.7,
+    "6": 4.4, "7": 4.4, "83": 4.2, "132": 4.0, "127": 3.9, "17.1": 3.9, "81": 3.7, "13.2": 3.7, "33.1": 3.7,
+    "78": 3.6, "48": 3.6, "77": 3.4, "79": 3.4, "46": 3.2, "65": 3.1, "49.1": 3.0, "0.5": 3.0, "29": 2.9,
+    "30": 2.9, "98": 2.9, "49.2": 2.7, "0.4": 2.7, "69": 2.7, "128": 2.4, "32": 2.3, "105": 2.3, "44": 2.3,
+    "94": 2.3, "36": 2.1, "59": 2.1, "97": 2.0, "62": 2.0, "66": 1.9, "67": 1.7, "0.2": 1.5, "0.1": 1.4,
+    "3": 1.4, "4": 1.3, "3.1": 1.2, "17": 1.1, "0.3": 0.9, "0": 0.5
+}
+
 
 # MS per-protocol cost of the filter loop in k_pulses<MS> (kcyc per tile and grab, tools/prof_phases.py
 # on the bench corpus, profiles/r03/s2/phases_split.log): the processing order is descending cost
@@ -627,8 +647,9 @@ class Bank:
         groups: Dict[float, List[int]] = {}
         for r in range(len(self.mu_pids)):
             groups.setdefault(float(mu[r]["clock"]), []).append(r)
-        med = float(np.median(list(MU_COST_KCYC.values())))
-        gcost = lambda g: MU_NORM_KCYC + sum(MU_COST_KCYC.get(str(self.mu_pids[r]), med) for r in g)  # noqa: E731
+        costs = MU_COST_KCYC_R3 if os.environ.get("SDX_MU_COSTS") == "r3" else MU_COST_KCYC
+        med = float(np.median(list(costs.values())))
+        gcost = lambda g: MU_NORM_KCYC + sum(costs.get(str(self.mu_pids[r]), med) for r in g)  # noqa: E731
         if os.environ.get("SDX_MU_ORDER") == "size":   # A/B: the round-2 order (largest group first)
             glist = sorted(groups.values(), key=lambda g: -len(g))
         else:
@@ -652,7 +673,7 @@ class Bank:
                 cum, cut, cur = 0.0, 1, []
                 for r in g:
                     cur.append(r)
-                    cum += MU_COST_KCYC.get(str(self.mu_pids[r]), med)
+                    cum += costs.get(str(self.mu_pids[r]), med)
                     if cum >= tot * cut / m and cut < m:
                         pieces.append(cur)
                         cur, cut = [], cut + 1

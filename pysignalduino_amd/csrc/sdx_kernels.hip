@@ -1921,8 +1921,14 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   int g_cur = -1;
   unsigned long long g_t0 = 0;
 #endif
+#ifdef SDX_PF
+  int p_next = -1;  // the work item's next protocol index, loaded one protocol ahead
+#endif
   while (true) {
     if (cur == cend) {
+#ifdef SDX_PF
+      p_next = -1;
+#endif
       int g = 0;
       if (lane == 0) g = atomicAdd(&L.next_p, 1);
       g = __builtin_amdgcn_readfirstlane(g);
@@ -1943,8 +1949,14 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         cend = g + 1;
       }
     }
+#ifdef SDX_PF
+    const int p = p_next >= 0 ? p_next : cld(&order[cur]);
+    ++cur;
+    p_next = cur < cend ? (int)cld(&order[cur]) : -1;
+#else
     const int p = cld(&order[cur]);
     ++cur;
+#endif
     if constexpr (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
       const sdx_mu_filt* fr = uniform_ptr(bv.mufilt + p);  // the filter's state: two 64-byte lines
