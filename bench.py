@@ -53,6 +53,12 @@ def parse():
     ap.add_argument("--mc-tail", action="store_true",
                     help="MC on a low-priority stream started with MU (the dispatcher gives its workgroups "
                          "the CUs MU's tail leaves idle) instead of beside MS")
+    ap.add_argument("--xchg", default="pack-after-mu", choices=("eager", "pack-after-mu", "defer"),
+                    help="exchange scheduling (N > 1 / --exchange): eager = count and pack as soon as possible "
+                         "(beside the next step's MU); pack-after-mu = the pack waits for the next step's MU; "
+                         "defer = count and pack both after the next step's MU (beside MS/MC)")
+    ap.add_argument("--raw-wire", action="store_true",
+                    help="exchange payloads raw (no nibble form: A/B of the wire size)")
     ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
                     help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
@@ -265,7 +271,11 @@ def main():
                 gdone[(k, par)] = e
             if si is not None:
                 gev[si][1].record(side)
-    exch = sdist.Exchange() if dist_on else None
+    # config 5's product entry: this rank's shard launches + the pipelined exchange with overflow re-runs
+    shd = (sdist.ShardedDemodulator(engine=eng, defer=args.xchg == "defer", nibble=not args.raw_wire)
+           if dist_on else None)
+    exch = shd.exchange if shd is not None else None
+    KIND = {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS, "MC": runtime.KIND_MC}
     done = [None] * nslot
     # one event pair per kernel and timed step: read after the closing synchronize
     ev = [{k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in kinds}
@@ -329,8 +339,8 @@ def main():
             u.record(stream)
             used[par] = u
         if exch is not None:  # RCCL all-gather of the decoded dmsg buffers (config 5), overlapped
-            rel = exch.submit([(outs[s_][k]["desc"], outs[s_][k]["rec"], outs[s_][k]["heap"], bds[k]["n"],
-                               outs[s_][k]["cursor"]) for k in kinds], stream)
+            parts = [sdist.Part.from_out(outs[s_][k], KIND[k], src=(KIND[k], bds[k], 0, -1)) for k in kinds]
+            rel = shd.submit(parts, stream, after=mu_done[0] if args.xchg != "eager" and "MU" in kinds else None)
             if rel is not None:             # the previous step's pack has read its slot
                 done[(j - 1) % nslot] = rel
 
@@ -426,10 +436,15 @@ def main():
     if exch is not None and exch.bytes_sent:
         nb = exch.bytes_sent[-args.steps:]
         wb = exch.wire_bytes[-args.steps:]
-        res["exchange"] = {"format": "wire (include/sdx.h): 4 B/message + 8 B/record + payload bytes",
+        res["exchange"] = {"format": "wire v3 (include/sdx.h): 4 B/message + 8 B/record + payloads "
+                                     + ("raw" if args.raw_wire else "(preamble + hex + postamble as packed digits)"),
+                           "scheduling": args.xchg,
                            "send_bytes_per_rank_per_step": float(np.mean(nb)),
                            "wire_bytes_per_rank_per_step": float(np.mean(wb)),
-                           "recv_bytes_per_rank_per_step": float(np.mean(nb)) * world}
+                           "payload_bytes_per_rank_per_step": float(np.mean(exch.payload_bytes[-args.steps:])),
+                           "payload_wire_bytes_per_rank_per_step": float(np.mean(exch.heap_wire_bytes[-args.steps:])),
+                           "recv_bytes_per_rank_per_step": float(np.mean(nb)) * world,
+                           "reruns": exch.reruns}
     if ovf:   # dense corpus: messages whose results did not fit the on-chip staging (the product re-runs them)
         res["overflow"] = {}
         for k in ovf:

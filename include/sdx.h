@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 10
+#define SDX_ABI_VERSION 11
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -41,7 +41,9 @@ enum sdx_status {
   SDX_ST_OK = 0,       /* results [rec_begin, rec_begin+n_rec) are the reference's list */
   SDX_ST_RAISED = 1,   /* the reference raises: raise_kind says which exception */
   SDX_ST_OVF_TILE = 2, /* on-chip result staging overflowed: re-run this message */
-  SDX_ST_OVF_OUT = 3   /* the caller's result/heap capacity overflowed: grow and re-run */
+  SDX_ST_OVF_OUT = 3,  /* the caller's result/heap capacity overflowed: grow and re-run */
+  SDX_ST_ABSENT = 0xFF /* ABI 11: an exchange overlay's descriptor that no re-run wrote (the caller fills an
+                        * overlay's descriptors with 0xFF bytes before its re-run launches) */
 };
 /* sdx_desc.raise_kind (Python exception class the reference raises) */
 enum sdx_raise { SDX_RAISE_NONE = 0, SDX_RAISE_INDEX = 1, SDX_RAISE_ATTRIBUTE = 2, SDX_RAISE_VALUE = 3,
@@ -151,6 +153,9 @@ typedef struct sdx_bank sdx_bank;
 
 int sdx_abi_version(void);
 const char* sdx_last_error(void);
+/* sha256 prefix of the sources and flags the library was built from (pysignalduino_amd/build.py
+ * source_hash): a caller can check that it loaded the library of the tree it runs in */
+const char* sdx_source_hash(void);
 /* sizeof() of the bank records, for host layout checks: 0 hdr, 1 patspec, 2 mu, 3 ms, 4 mc, 5 result, 6 desc,
  * 7 mu_desc */
 int sdx_layout_size(int which);
@@ -220,7 +225,8 @@ typedef struct {
   const int32_t* len_dev;      /* optional [n] lengths: message i = data[offsets[i], +len[i]) (slot layout) */
   int64_t work_stride;         /* > 0: the j-th message run takes its region at j * work_stride
                                 * (>= 5 * (max_len + 512)); 0: regions by offsets (5 * offsets[i] + 2560 * i) */
-  int32_t max_len;             /* the longest message run (characters): per-wave scratch and LDS sizing */
+  int32_t max_len;             /* HARD BOUND: the longest message run (characters); per-wave scratch, regions and LDS
+                                * are sized by it -- a message longer than max_len is not walked (SDX_RAISE_CONTRACT) */
   int32_t res;
 } sdx_general_batch;
 
@@ -414,19 +420,31 @@ int sdx_units(const sdx_unit_batch* batch, const sdx_out* out, void* hip_stream)
  * the stream ran sharded or not):
  *   msg section   uint32 per message: n_rec | status << 16 | raise_kind << 24  (sdx_desc minus rec_begin)
  *   rec section   sdx_wire_rec per record                                      (sdx_result minus payload_off, msg)
- *   heap section  the payloads concatenated in record order
- * rec_begin, payload_off and msg are prefix sums: sdx_exchange_unpack rebuilds them on the receiver.
+ *   heap section  the payloads in record order; a payload that is its protocol's preamble + uppercase
+ *                 hex digits + postamble (the bank's affixes; proto bit 15 = SDX_WIRE_NIB) travels as
+ *                 its digits packed two per byte (high nibble first, an odd last digit in a high
+ *                 nibble), any other payload as its bytes (ABI 11, wire v3)
+ * rec_begin, payload_off, msg and the affixes are rebuilt by the receiver (sdx_exchange_unpack).
  * A rank's send buffer holds, for launch 0, 1, ..., K-1 in turn, its msg, rec and heap sections, each
  * zero-padded to 16 bytes -- a layout that follows from the counts alone (dist.py _layout).
  * Sender: sdx_exchange_count (device counts per launch + the layout), then sdx_exchange_pack into the
  * send buffer, both without a host round trip; the host needs the counts only to size the collective.
- * A message whose status is an overflow, or whose descriptor / records lie outside what the launch
- * wrote (cursor clamped to the capacities), is counted in counts[3] ("bad") and shipped with n_rec 0
- * and status SDX_ST_OVF_OUT: the caller must re-run such a launch instead of exchanging it. */
+ * RE-RUNS (ABI 11): a launch part may name an OVERLAY part (alt = 1 + its index in the same array,
+ * aux = 1 on the overlay): the outputs of the launches that re-ran the launch's overflowed messages,
+ * over the same n_msgs, with every descriptor the re-runs did not write left at SDX_ST_ABSENT.  Message
+ * m is taken from the LAST overlay along the chain (an overlay may name the next) whose descriptor of m is
+ * present (at most 8 overlays per launch).
+ * An aux part has no sections of its own (its counts are 0).
+ * A message whose (resolved) status is an overflow, or whose descriptor / records lie outside what its
+ * launch wrote (cursor clamped to the capacities), is counted in counts[3] ("bad") and shipped with
+ * n_rec 0 and status SDX_ST_OVF_OUT: the caller re-runs it (into an overlay) before exchanging. */
 #define SDX_XCHG_MAX_RANKS 32
+#define SDX_XCHG_MAX_PARTS 16  /* launches + overlays per exchange */
+#define SDX_XCHG_COUNTS 8      /* u32 counts per part: messages, records, wire payload bytes, bad, payload bytes, 0, 0, 0 */
+#define SDX_WIRE_NIB 0x8000u   /* sdx_wire_rec.proto: the payload travels in the nibble form */
 typedef struct {
-  uint16_t proto;
-  uint16_t payload_len;
+  uint16_t proto;              /* record index in its class table | SDX_WIRE_NIB */
+  uint16_t payload_len;        /* the payload's length (not its wire length) */
   uint32_t bit_length;
 } sdx_wire_rec;
 
@@ -435,41 +453,49 @@ typedef struct {
   const uint8_t* rec_dev;      /* its sdx_result records */
   const uint8_t* heap_dev;     /* its payload heap */
   const uint32_t* cursor_dev;  /* its cursor: [0] records, [1] heap bytes written (clamped to rec_cap / heap_cap) */
-  uint32_t n_msgs, rec_cap, heap_cap, res;
+  uint32_t n_msgs, rec_cap, heap_cap;
+  uint8_t kind;                /* enum sdx_kind of the launch (its protocols' affixes); 0xFF: raw payloads only */
+  uint8_t alt;                 /* 0, or 1 + index (in the same array) of this launch's overlay part */
+  uint8_t aux;                 /* 1: this part is an overlay */
+  uint8_t res;
 } sdx_xchg_part;
 
-/* workspace of count + pack (kept between the two: 8 B per message + block sums + the layout);
- * 256-byte aligned and ZEROED once at allocation (the kernels leave their counters at zero) */
+/* workspace of count + pack (kept between the two: 12 B per message + block sums + a 256-byte head);
+ * 256-byte aligned and ZEROED once at allocation (the kernels leave their counters at zero; any layout
+ * of up to SDX_XCHG_MAX_PARTS parts may reuse one workspace of sufficient size) */
 uint64_t sdx_exchange_work_bytes(const uint32_t* n_msgs, int k);
-/* send buffer capacity for any outcome of the launches (from their capacities) */
+/* send buffer capacity for any outcome of the launches (from their and their overlays' capacities) */
 uint64_t sdx_exchange_send_bytes(const sdx_xchg_part* parts, int k);
-/* counts_dev[4*i + 0..3] = messages, records, payload bytes, bad messages of launch i */
-int sdx_exchange_count(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, uint32_t* counts_dev,
-                       void* hip_stream);
-/* after sdx_exchange_count on the same stream (reads its counts_dev and workspace) */
-int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap, const uint32_t* counts_dev,
-                      uint8_t* send_dev, uint64_t send_cap, void* hip_stream);
-/* ABI 10: the same pack after the counts have reached the host (counts_host = the same u32[4k]):
+/* counts_dev[SDX_XCHG_COUNTS * i + 0..4] = messages, records, wire payload bytes, bad messages, payload
+ * bytes of launch i.  bank: the uploaded bank (the affixes of the nibble form; NULL: raw payloads) */
+int sdx_exchange_count(const sdx_bank* bank, const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
+                       uint32_t* counts_dev, void* hip_stream);
+/* after sdx_exchange_count on the same stream (reads its counts_dev and workspace), the same bank */
+int sdx_exchange_pack(const sdx_bank* bank, const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
+                      const uint32_t* counts_dev, uint8_t* send_dev, uint64_t send_cap, void* hip_stream);
+/* ABI 10: the same pack after the counts have reached the host (counts_host = the same u32 counts):
  * dst_dev needs only the exact wire size (16-byte aligned), so the wire can be written straight into
  * this rank's chunk of an in-place all-gather's receive buffer (no send buffer, no local copy) */
-int sdx_exchange_pack_into(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
+int sdx_exchange_pack_into(const sdx_bank* bank, const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
                            const uint32_t* counts_dev, const uint32_t* counts_host, uint8_t* dst_dev, uint64_t dst_cap,
                            void* hip_stream);
 
 /* receiver: one launch's wire sections of every rank (rank order = global message order) -> the
- * whole job's sdx_desc[sum n_msgs], sdx_result[sum n_rec] and one contiguous heap (sum n_heap bytes,
- * heap_dev 4-byte aligned).  work_dev: sdx_exchange_unpack_work_bytes(total messages, total records),
- * 64-byte aligned, zeroed once. */
+ * whole job's sdx_desc[sum n_msgs], sdx_result[sum n_rec] and one contiguous heap (sum n_payload
+ * bytes <= heap_cap).  bank / kind: the sender's (the nibble form's affixes).  work_dev:
+ * sdx_exchange_unpack_work_bytes(total messages, total records), 64-byte aligned. */
 typedef struct {
   const uint8_t* msg_dev;
   const uint8_t* rec_dev;
   const uint8_t* heap_dev;
-  uint32_t n_msgs, n_rec, n_heap, res;     /* n_heap: payload bytes (without the padding) */
+  uint32_t n_msgs, n_rec, n_heap;  /* n_heap: wire payload bytes (without the padding) */
+  uint32_t n_payload;              /* payload bytes they expand to (the count's [4]) */
 } sdx_xchg_wire;
 
 uint64_t sdx_exchange_unpack_work_bytes(uint32_t n_msgs, uint32_t n_rec);
-int sdx_exchange_unpack(const sdx_xchg_wire* ranks, int nranks, void* work_dev, uint64_t work_cap, sdx_desc* desc_dev,
-                        sdx_result* rec_dev, uint8_t* heap_dev, void* hip_stream);
+int sdx_exchange_unpack(const sdx_bank* bank, int kind, const sdx_xchg_wire* ranks, int nranks, void* work_dev,
+                        uint64_t work_cap, sdx_desc* desc_dev, sdx_result* rec_dev, uint8_t* heap_dev,
+                        uint64_t heap_cap, void* hip_stream);
 
 #define SDX_SHORT_MAX 256   /* sdx_demod_pulses: messages of <= 256 pulses */
 #define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */

@@ -19,7 +19,7 @@ import json
 import os
 import math
 import struct
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -331,6 +331,22 @@ class Bank:
         set_defaults(self.protocols)
         self.pids: List[str] = list(self.protocols.keys())
         self.compile()
+
+    def affixes(self, kind: int) -> List[Tuple[bytes, bytes]]:
+        """Per record of a class table (kind 0 MU, 1 MS, 2 MC, 3 MN): the (preamble, postamble) bytes
+        its payloads carry -- the affixes of the exchange's nibble form (include/sdx.h, wire v3), the
+        same strings the compiler puts in the records' pre_off/post_off (message_unsynced.py:271-274,
+        message_synced.py:228-229, manchester.py:131-132, parser/mn.py:176-177)."""
+        P = self.protocols
+        enc = lambda v: f"{v}".encode("latin-1")  # noqa: E731
+        if kind in (0, 1):
+            pids = self.mu_pids if kind == 0 else self.ms_pids
+            return [(enc(P[p].get("preamble", "")), enc(P[p].get("postamble", ""))) for p in pids]
+        if kind == 2:
+            return [(enc(x), b"") for x in self.mc_preamble]
+        if kind == 3:
+            return [(enc(x), b"") for x in self.mn_preamble]
+        return []
 
     # -- helpers -------------------------------------------------------------------------------
     def _str(self, s: str):

@@ -20,19 +20,36 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
 
 
+DEPS = [*SRCS, os.path.join(HERE, "csrc", "sdx_device.h"), os.path.join(HERE, "csrc", "sdx_lane.h"),
+        os.path.join(HERE, "csrc", "sdx_mc.h"),
+        os.path.join(os.path.dirname(HERE), "include", "sdx.h"),
+        os.path.join(os.path.dirname(HERE), "include", "sdx_bank.h")]
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of every source and header libsdx.so is built from, plus the
+    flags: compiled into the library (sdx_source_hash()), so a run can prove it loaded a library
+    built from the tree it runs in (__graft_entry__.smoke checks it)."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for d in DEPS:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    deps = [*SRCS, os.path.join(HERE, "csrc", "sdx_device.h"), os.path.join(HERE, "csrc", "sdx_lane.h"),
-            os.path.join(HERE, "csrc", "sdx_mc.h"),
-            os.path.join(os.path.dirname(HERE), "include", "sdx.h"),
-            os.path.join(os.path.dirname(HERE), "include", "sdx_bank.h")]
+    deps = DEPS
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     # one object per translation unit, compiled in parallel, then one link
     objdir = os.path.join(os.path.dirname(OUT), "obj")
     os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, os.path.basename(src) + ".o") for src in SRCS]
-    cmds = [[HIPCC, *FLAGS[:-1], "-c", src, "-o", obj] for src, obj in zip(SRCS, objs)]
+    cmds = [[HIPCC, *FLAGS[:-1], f'-DSDX_SRC_HASH="{source_hash()}"', "-c", src, "-o", obj]
+            for src, obj in zip(SRCS, objs)]
     if verbose:
         for c in cmds:
             print(" ".join(c))

@@ -1,45 +1,54 @@
 // sdx_exchange.hip -- the device side of the multi-GPU exchange (BASELINE config 5).
 //
 // Every rank demodulates its contiguous shard of the stream; the one exchange step all-gathers the
-// decoded dmsg buffers of all ranks over RCCL.  What travels is the wire form of include/sdx.h:
-// per launch and rank, in message order, a 4-byte word per message (n_rec, status, raise_kind), an
-// 8-byte sdx_wire_rec per record (proto, payload_len, bit_length) and the payloads concatenated.
-// rec_begin, payload_off and msg are prefix sums and are not sent: 4 + 8 * records + payload bytes
-// per message instead of 8 + 16 * records + the (padded) heap.
+// decoded dmsg buffers of all ranks over RCCL.  What travels is the wire form of include/sdx.h (v3,
+// ABI 11): per launch and rank, in message order, a 4-byte word per message (n_rec, status,
+// raise_kind), an 8-byte sdx_wire_rec per record (proto, payload_len, bit_length) and the payloads.
+// A payload of the form preamble + uppercase hex digits + postamble of its protocol (the bank's
+// affixes: message_unsynced.py:271-274, message_synced.py:228-229, manchester.py:131-132) travels as
+// its hex digits packed two per byte (proto bit 15 = SDX_WIRE_NIB); any other payload travels raw.
+// rec_begin, payload_off, msg and the affixes are rebuilt by the receiver.
+//
+// Re-runs: a launch whose messages overflowed (SDX_ST_OVF_TILE / _OUT) is exchanged together with an
+// OVERLAY part (sdx_xchg_part.alt): the re-run's outputs, descriptors filled with SDX_ST_ABSENT except
+// for the re-run messages.  The sender takes message m from the deepest overlay whose descriptor of m
+// is present, so the wire is the same as for a launch that never overflowed.
 //
 // Sender, two launches around the host's count exchange:
-//   k_xw_count  lane = message: validate the descriptor and its records against the launch's
-//               cursor / capacities, count records and payload bytes, block-scan them (per-message
-//               local prefixes into the workspace), block totals;
+//   k_xw_count  lane = message: resolve the overlay chain, validate the descriptor and its records
+//               against the part's cursor / capacities, classify the payloads (raw / nibble), count
+//               records, wire payload bytes and payload bytes, block-scan them, block totals;
 //   k_xw_scan   one block per launch: exclusive block offsets, the launch's counts;
-//   k_xw_pack   block = the count block's 256 messages: wire words and wire records (lane =
-//               message), then the payloads as coalesced dwords (lane = output dword).  The source
+//   k_xw_pack   block = the count block's 256 messages: wire words and wire records (lane = message),
+//               then the payloads (lane = 32 output bytes, coalesced 16-byte stores).  The source
 //               records are in tile order (k_pulses places them per tile); the wire is in message
 //               order, so the pack is also the canonicalisation that makes sharded and un-sharded
 //               runs compare byte for byte.
 // Receiver:
-//   k_xu_sum / k_xu_scan / k_xu_write  rebuild sdx_desc / sdx_result / one contiguous heap of the whole
-//               job from the gathered wire sections of every rank (the same block-sum / scan / apply
-//               passes over the rank-concatenated messages and records).
+//   k_xu_sum / k_xu_scan / k_xu_write / k_xu_heap  rebuild sdx_desc / sdx_result / one contiguous heap
+//               of the whole job from the gathered wire sections of every rank.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <string>
 
 #include "../../include/sdx.h"
+#include "../../include/sdx_bank.h"
 
 namespace sdx {
 int set_error(int code, const std::string& msg);  // sdx_kernels.hip
+const void* bank_dev_ptr(const sdx_bank* b);
 }
 
 namespace sdxx {
 
 constexpr int XT = 256;       // threads per block; one message per thread in the scans
 constexpr int XB = XT;        // items per block
-constexpr int XMAX = 8;       // launches per exchange
+constexpr int XMAX = SDX_XCHG_MAX_PARTS;
 constexpr int XRANKS = SDX_XCHG_MAX_RANKS;
 constexpr int LREC = 2048;    // records of a pack block listed in LDS for the coalesced payload copy
 constexpr uint64_t BADBIT = 1ull << 63;
+constexpr int CHAIN = 8;      // overlays per launch (general-path rows, re-runs, re-runs of re-runs)
 
 // Inter-block results travel through kernel boundaries only (count -> scan -> pack): a grid-wide
 // "last block" protocol needs agent-scope release fences, and on a multi-XCD part each one writes
@@ -47,31 +56,37 @@ constexpr uint64_t BADBIT = 1ull << 63;
 
 __host__ __device__ inline uint32_t nblk_of(uint64_t n) { return n ? (uint32_t)((n + XB - 1) / XB) : 1u; }
 __host__ __device__ inline uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
-// per-launch workspace: [bad, records, bytes, -] (64 B) | loc u64[n] | blk u64[nblk]
+// workspace: a 256-byte head (bad-message counters of parts 0..XMAX-1 at fixed places, so one zeroed
+// workspace serves any layout), then per part: loc u64[n] | raw u32[n] | blk u64[nblk] | rawblk u32[nblk]
+constexpr uint64_t WHEAD = 256;
 __host__ __device__ inline uint64_t part_work_bytes(uint32_t n) {
-  return (64 + 8ull * n + 8ull * nblk_of(n) + 255) / 256 * 256;
+  return (12ull * n + 12ull * nblk_of(n) + 255) / 256 * 256;
 }
 
 struct Parts {
   sdx_xchg_part p[XMAX];
   uint64_t work_off[XMAX];
+  const uint8_t* bank;  // nullptr: raw payloads only
   int k;
 };
 
 struct PartWork {
   uint32_t* bad;   // bad messages (reset by k_xw_scan)
-  uint32_t* tot;   // [2]: records, payload bytes of the launch (written by k_xw_scan)
-  uint64_t* loc;   // per message: BADBIT | local record prefix << 32 | local byte prefix (in its block)
-  uint64_t* blk;   // block totals -> exclusive block offsets (records << 32 | bytes)
+  uint64_t* loc;   // per message: BADBIT | local record prefix << 32 | local wire byte prefix (in its block)
+  uint32_t* raw;   // per message: local payload byte prefix
+  uint64_t* blk;   // block totals -> exclusive block offsets (records << 32 | wire bytes)
+  uint32_t* rawblk;
 };
 
-__device__ inline PartWork part_work(uint8_t* work, uint64_t off, uint32_t n) {
+__device__ inline PartWork part_work(uint8_t* work, const Parts& P, int k) {
   PartWork w;
-  uint8_t* b = work + off;
-  w.bad = reinterpret_cast<uint32_t*>(b);
-  w.tot = w.bad + 1;
-  w.loc = reinterpret_cast<uint64_t*>(b + 64);
+  const uint32_t n = P.p[k].n_msgs;
+  uint8_t* b = work + WHEAD + P.work_off[k];
+  w.bad = reinterpret_cast<uint32_t*>(work) + k;
+  w.loc = reinterpret_cast<uint64_t*>(b);
   w.blk = w.loc + n;
+  w.raw = reinterpret_cast<uint32_t*>(w.blk + nblk_of(n));
+  w.rawblk = w.raw + n;
   return w;
 }
 
@@ -120,34 +135,131 @@ __device__ inline uint64_t block_scan_array(uint64_t* blk, uint32_t nb) {
   }
   return carry;
 }
+__device__ inline uint32_t block_scan_array32(uint32_t* blk, uint32_t nb) {
+  uint64_t carry = 0;
+  for (uint32_t c = 0; c < nb; c += XT) {
+    const uint32_t i = c + threadIdx.x;
+    const uint64_t v = i < nb ? blk[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl(v, &tot);
+    if (i < nb) blk[i] = (uint32_t)(carry + ex);
+    carry += tot;
+  }
+  return (uint32_t)carry;
+}
 
+// ---- payload affixes and the nibble form ----------------------------------------------------------
+struct Affix {
+  const uint8_t* pre;
+  const uint8_t* post;
+  uint32_t npre, npost;
+  bool ok;  // the bank knows the protocol: the nibble form applies
+};
+
+__device__ inline Affix affix_of(const uint8_t* bank, int kind, uint32_t proto) {
+  Affix a{nullptr, nullptr, 0, 0, false};
+  if (!bank) return a;
+  const sdx_bank_hdr* h = reinterpret_cast<const sdx_bank_hdr*>(bank);
+  const uint8_t* str = bank + h->off_str;
+  int32_t po = 0, pl = 0, qo = 0, ql = 0;
+  if (kind == SDX_KIND_MU && proto < h->n_mu) {
+    const sdx_mu_proto& p = reinterpret_cast<const sdx_mu_proto*>(bank + h->off_mu)[proto];
+    po = p.pre_off, pl = p.pre_len, qo = p.post_off, ql = p.post_len;
+  } else if (kind == SDX_KIND_MS && proto < h->n_ms) {
+    const sdx_ms_proto& p = reinterpret_cast<const sdx_ms_proto*>(bank + h->off_ms)[proto];
+    po = p.pre_off, pl = p.pre_len, qo = p.post_off, ql = p.post_len;
+  } else if (kind == SDX_KIND_MC && proto < h->n_mc) {
+    const sdx_mc_proto& p = reinterpret_cast<const sdx_mc_proto*>(bank + h->off_mc)[proto];
+    po = p.pre_off, pl = p.pre_len;
+  } else if (kind == SDX_KIND_MN && proto < h->n_mn) {
+    const sdx_mn_proto& p = reinterpret_cast<const sdx_mn_proto*>(bank + h->off_mn)[proto];
+    po = p.pre_off, pl = p.pre_len;
+  } else {
+    return a;
+  }
+  a.pre = str + po;
+  a.post = str + qo;
+  a.npre = (uint32_t)pl;
+  a.npost = (uint32_t)ql;
+  a.ok = pl >= 0 && ql >= 0;
+  return a;
+}
+
+__device__ inline bool is_uhex(uint8_t c) { return (uint8_t)(c - '0') < 10u || (uint8_t)(c - 'A') < 6u; }
+__device__ inline uint32_t hexval(uint8_t c) { return c <= '9' ? (uint32_t)(c - '0') : (uint32_t)(c - 'A' + 10); }
+
+// payload p[0, len) == pre + D uppercase hex digits + post?  Returns D, or -1 (raw form)
+__device__ inline int nib_digits(const Affix& a, const uint8_t* p, uint32_t len) {
+  if (!a.ok || len < a.npre + a.npost) return -1;
+  for (uint32_t i = 0; i < a.npre; ++i)
+    if (p[i] != a.pre[i]) return -1;
+  const uint32_t d = len - a.npre - a.npost;
+  for (uint32_t i = 0; i < a.npost; ++i)
+    if (p[a.npre + d + i] != a.post[i]) return -1;
+  for (uint32_t i = 0; i < d; ++i)
+    if (!is_uhex(p[a.npre + i])) return -1;
+  return (int)d;
+}
+
+__device__ inline uint32_t wire_bytes_of(int digits, uint32_t len) {
+  return digits >= 0 ? ((uint32_t)digits + 1) >> 1 : len;
+}
+
+// ---- sender ---------------------------------------------------------------------------------------
 __device__ inline void clamp_counts(const sdx_xchg_part& x, uint32_t* nrec_c, uint32_t* nheap_c) {
   const uint32_t c0 = x.cursor_dev[0], c1 = x.cursor_dev[1];
   *nrec_c = c0 < x.rec_cap ? c0 : x.rec_cap;
   *nheap_c = c1 < x.heap_cap ? c1 : x.heap_cap;
 }
 
-// the validated (records << 32 | payload bytes) of message m; *ok = false marks a message the
-// exchange cannot ship (an overflow status, or a descriptor / record outside what the launch wrote)
-__device__ inline uint64_t msg_counts(const sdx_xchg_part& x, uint32_t nrec_c, uint32_t nheap_c, uint32_t m,
-                                      bool* ok) {
-  const sdx_desc d = reinterpret_cast<const sdx_desc*>(x.desc_dev)[m];
+// message m of part k: the LAST overlay along the chain k -> alt -> alt ... whose descriptor of m is
+// present (later overlays take precedence: e.g. general-path rows, then the re-runs of overflows)
+__device__ inline int resolve(const Parts& P, int k, uint32_t m, sdx_desc* d) {
+  *d = reinterpret_cast<const sdx_desc*>(P.p[k].desc_dev)[m];
+  int res = k, c = k;
+  for (int hop = 0; hop < CHAIN; ++hop) {
+    const int a = (int)P.p[c].alt - 1;
+    if (a < 0 || a >= P.k) break;
+    const sdx_desc da = reinterpret_cast<const sdx_desc*>(P.p[a].desc_dev)[m];
+    if (da.status != SDX_ST_ABSENT) {
+      res = a;
+      *d = da;
+    }
+    c = a;
+  }
+  return res;
+}
+
+// the validated (records << 32 | wire payload bytes) of message m and its payload bytes; *ok = false
+// marks a message the exchange cannot ship (an overflow status, or a descriptor / record outside
+// what the launch wrote)
+__device__ inline uint64_t msg_counts(const Parts& P, int k0, uint32_t m, bool* ok, uint32_t* rawb) {
+  sdx_desc d;
+  const int k = resolve(P, k0, m, &d);
+  const sdx_xchg_part& x = P.p[k];
   *ok = true;
+  *rawb = 0;
   if (d.status == SDX_ST_RAISED) return 0;
+  uint32_t nrec_c, nheap_c;
+  clamp_counts(x, &nrec_c, &nheap_c);
   if (d.status != SDX_ST_OK || (d.n_rec && (uint64_t)d.rec_begin + d.n_rec > nrec_c)) {
     *ok = false;
     return 0;
   }
   const sdx_result* r = reinterpret_cast<const sdx_result*>(x.rec_dev) + d.rec_begin;
-  uint64_t bytes = 0;
+  uint64_t bytes = 0, raw = 0;
   bool good = true;
-#pragma unroll 4
   for (uint32_t j = 0; j < d.n_rec; ++j) {
     const sdx_result v = r[j];
-    good &= v.msg == m && (uint64_t)v.payload_off + v.payload_len <= nheap_c;
-    bytes += v.payload_len;
+    const bool in = v.msg == m && (uint64_t)v.payload_off + v.payload_len <= nheap_c;
+    good &= in;
+    if (!in) continue;
+    const int dg = nib_digits(affix_of(P.bank, x.kind, v.proto), x.heap_dev + v.payload_off, v.payload_len);
+    bytes += wire_bytes_of(dg, v.payload_len);
+    raw += v.payload_len;
   }
   *ok = good;
+  *rawb = good ? (uint32_t)raw : 0u;
   return good ? (((uint64_t)d.n_rec << 32) | bytes) : 0;
 }
 
@@ -155,34 +267,46 @@ __device__ inline uint64_t msg_counts(const sdx_xchg_part& x, uint32_t nrec_c, u
 __global__ __launch_bounds__(XT) void k_xw_count(Parts P, uint8_t* __restrict__ work) {
   const int k = blockIdx.y;
   const sdx_xchg_part& x = P.p[k];
-  if (blockIdx.x >= nblk_of(x.n_msgs)) return;
-  PartWork w = part_work(work, P.work_off[k], x.n_msgs);
-  uint32_t nrec_c, nheap_c;
-  clamp_counts(x, &nrec_c, &nheap_c);
+  if (x.aux || blockIdx.x >= nblk_of(x.n_msgs)) return;
+  PartWork w = part_work(work, P, k);
   const uint32_t m = blockIdx.x * XB + threadIdx.x;
   bool ok = true;
-  const uint64_t v = m < x.n_msgs ? msg_counts(x, nrec_c, nheap_c, m, &ok) : 0;
-  uint64_t tot;
+  uint32_t rawb = 0;
+  const uint64_t v = m < x.n_msgs ? msg_counts(P, k, m, &ok, &rawb) : 0;
+  uint64_t tot, rtot;
   const uint64_t pre = block_excl(v, &tot);
-  if (m < x.n_msgs) w.loc[m] = pre | (ok ? 0 : BADBIT);
+  const uint64_t rpre = block_excl(rawb, &rtot);
+  if (m < x.n_msgs) {
+    w.loc[m] = pre | (ok ? 0 : BADBIT);
+    w.raw[m] = (uint32_t)rpre;
+  }
   const uint64_t bad_wave = __ballot(!ok);
   if (lane_id() == 0 && bad_wave) atomicAdd(w.bad, (uint32_t)__popcll(bad_wave));
-  if (threadIdx.x == 0) w.blk[blockIdx.x] = tot;
+  if (threadIdx.x == 0) {
+    w.blk[blockIdx.x] = tot;
+    w.rawblk[blockIdx.x] = (uint32_t)rtot;
+  }
 }
 
 // one block per launch: block offsets, the launch's counts
 __global__ __launch_bounds__(XT) void k_xw_scan(Parts P, uint8_t* __restrict__ work, uint32_t* __restrict__ counts) {
   const int k = blockIdx.x;
   const sdx_xchg_part& x = P.p[k];
-  PartWork w = part_work(work, P.work_off[k], x.n_msgs);
+  uint32_t* c = counts + SDX_XCHG_COUNTS * k;
+  if (x.aux) {  // an overlay: its messages travel in the part it overlays
+    if (threadIdx.x < SDX_XCHG_COUNTS) c[threadIdx.x] = 0;
+    return;
+  }
+  PartWork w = part_work(work, P, k);
   const uint64_t all = block_scan_array(w.blk, nblk_of(x.n_msgs));
+  const uint32_t rall = block_scan_array32(w.rawblk, nblk_of(x.n_msgs));
   if (threadIdx.x == 0) {
-    w.tot[0] = (uint32_t)(all >> 32);
-    w.tot[1] = (uint32_t)all;
-    counts[4 * k + 0] = x.n_msgs;
-    counts[4 * k + 1] = (uint32_t)(all >> 32);
-    counts[4 * k + 2] = (uint32_t)all;
-    counts[4 * k + 3] = *w.bad;
+    c[0] = x.n_msgs;
+    c[1] = (uint32_t)(all >> 32);
+    c[2] = (uint32_t)all;
+    c[3] = *w.bad;
+    c[4] = rall;
+    c[5] = c[6] = c[7] = 0;
     *w.bad = 0;
   }
 }
@@ -191,13 +315,14 @@ __global__ __launch_bounds__(XT) void k_xw_scan(Parts P, uint8_t* __restrict__ w
 __device__ inline void section_offsets(const uint32_t* counts, int K, int k, uint64_t* o) {
   uint64_t off = 0;
   for (int i = 0; i < K; ++i) {
+    const uint32_t* c = counts + SDX_XCHG_COUNTS * i;
     if (i == k) {
       o[0] = off;
-      o[1] = off + r16(4ull * counts[4 * i]);
-      o[2] = o[1] + r16(8ull * counts[4 * i + 1]);
+      o[1] = off + r16(4ull * c[0]);
+      o[2] = o[1] + r16(8ull * c[1]);
       return;
     }
-    off += r16(4ull * counts[4 * i]) + r16(8ull * counts[4 * i + 1]) + r16(counts[4 * i + 2]);
+    off += r16(4ull * c[0]) + r16(8ull * c[1]) + r16(c[2]);
   }
 }
 
@@ -207,18 +332,22 @@ __device__ inline void zero_tail(uint8_t* sec, uint64_t used, uint32_t lane) {
 
 // block = 256 consecutive messages (the count blocks), grid.y = launch.
 // A (lane = message): the wire word, the wire records (contiguous per message) and the message's
-//   records' (source, destination, length) into an LDS list in output order;
+//   records' (source address, destination, digits) into an LDS list in output order;
 // B (lane = 32 consecutive output bytes of the block's payload range): one binary search for the
-//   first byte's record, a linear walk through the list, 32 independent source byte loads, two
-//   16-byte stores (byte stores only at the two ends of the range, which neighbouring blocks share).
+//   first byte's record, a linear walk through the list, the source byte loads (two digits per
+//   output byte in the nibble form), two 16-byte stores (byte stores only at the two ends of the
+//   range, which neighbouring blocks share).
 __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restrict__ counts,
                                                 uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
-  __shared__ uint32_t l_src[LREC], l_dst[LREC + 1];
+  __shared__ uint64_t l_src[LREC];
+  __shared__ uint32_t l_dst[LREC + 1];
+  __shared__ int32_t l_dig[LREC];   // nibble form: the digit count; raw: -1
   const int k = blockIdx.y;
   const sdx_xchg_part& x = P.p[k];
   const uint32_t nb = nblk_of(x.n_msgs);
-  if (blockIdx.x >= nb) return;
-  PartWork w = part_work(work, P.work_off[k], x.n_msgs);
+  if (x.aux || blockIdx.x >= nb) return;
+  PartWork w = part_work(work, P, k);
+  const uint32_t* ck = counts + SDX_XCHG_COUNTS * k;
   uint64_t so[3];
   section_offsets(counts, P.k, k, so);
   uint8_t* s_msg = send + so[0];
@@ -226,48 +355,53 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
   uint8_t* s_heap = send + so[2];
   if (blockIdx.x == 0) {  // deterministic section padding
     zero_tail(s_msg, 4ull * x.n_msgs, threadIdx.x);
-    zero_tail(reinterpret_cast<uint8_t*>(s_rec), 8ull * counts[4 * k + 1], threadIdx.x);
-    zero_tail(s_heap, counts[4 * k + 2], threadIdx.x);
+    zero_tail(reinterpret_cast<uint8_t*>(s_rec), 8ull * ck[1], threadIdx.x);
+    zero_tail(s_heap, ck[2], threadIdx.x);
   }
   const uint64_t boff = w.blk[blockIdx.x];
-  const uint64_t bnext = blockIdx.x + 1 < nb ? w.blk[blockIdx.x + 1]
-                                             : (((uint64_t)counts[4 * k + 1] << 32) | counts[4 * k + 2]);
+  const uint64_t bnext = blockIdx.x + 1 < nb ? w.blk[blockIdx.x + 1] : (((uint64_t)ck[1] << 32) | ck[2]);
   const uint32_t brec = (uint32_t)((bnext >> 32) - (boff >> 32));   // the block's records
   const uint32_t m = blockIdx.x * XB + threadIdx.x;
   if (m < x.n_msgs) {
-    const sdx_desc d = reinterpret_cast<const sdx_desc*>(x.desc_dev)[m];
+    sdx_desc d;
+    const sdx_xchg_part& y = P.p[resolve(P, k, m, &d)];
     const uint64_t loc = w.loc[m];
     const bool bad = (loc & BADBIT) != 0;
     const uint32_t nr = (bad || d.status != SDX_ST_OK) ? 0u : d.n_rec;
     reinterpret_cast<uint32_t*>(s_msg)[m] =
         nr | ((uint32_t)(bad ? SDX_ST_OVF_OUT : d.status) << 16) | ((uint32_t)d.raise_kind << 24);
-    const sdx_result* rec = reinterpret_cast<const sdx_result*>(x.rec_dev) + d.rec_begin;
+    const sdx_result* rec = reinterpret_cast<const sdx_result*>(y.rec_dev) + d.rec_begin;
     uint32_t lr = (uint32_t)((loc & ~BADBIT) >> 32), lb = (uint32_t)loc;   // block-local
-    for (uint32_t j = 0; j < nr; j += 4) {
-      sdx_result r4[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (j + i < nr) r4[i] = rec[j + i];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (j + i >= nr) break;
-        sdx_wire_rec o;
-        o.proto = r4[i].proto;
-        o.payload_len = r4[i].payload_len;
-        o.bit_length = r4[i].bit_length;
-        s_rec[(uint32_t)(boff >> 32) + lr] = o;
-        if (lr < LREC) {
-          l_src[lr] = r4[i].payload_off;
-          l_dst[lr] = lb;
-        } else {  // past the LDS list (a block of unusually many records): copy here, byte by byte
-          if (lr == LREC) l_dst[LREC] = lb;   // the list's end
-          uint8_t* dst = s_heap + (uint32_t)boff + lb;
-          const uint8_t* src = x.heap_dev + r4[i].payload_off;
-          for (uint32_t q = 0; q < r4[i].payload_len; ++q) dst[q] = src[q];
+    for (uint32_t j = 0; j < nr; ++j) {
+      const sdx_result r = rec[j];
+      const uint8_t* src = y.heap_dev + r.payload_off;
+      const Affix a = affix_of(P.bank, y.kind, r.proto);
+      const int dg = nib_digits(a, src, r.payload_len);
+      sdx_wire_rec o;
+      o.proto = (uint16_t)(r.proto | (dg >= 0 ? SDX_WIRE_NIB : 0u));
+      o.payload_len = r.payload_len;
+      o.bit_length = r.bit_length;
+      s_rec[(uint32_t)(boff >> 32) + lr] = o;
+      const uint8_t* s0 = dg >= 0 ? src + a.npre : src;
+      const uint32_t wl = wire_bytes_of(dg, r.payload_len);
+      if (lr < LREC) {
+        l_src[lr] = (uint64_t)(uintptr_t)s0;
+        l_dst[lr] = lb;
+        l_dig[lr] = dg;
+      } else {  // past the LDS list (a block of unusually many records): copy here, byte by byte
+        if (lr == LREC) l_dst[LREC] = lb;   // the list's end
+        uint8_t* dst = s_heap + (uint32_t)boff + lb;
+        for (uint32_t q = 0; q < wl; ++q) {
+          if (dg < 0) {
+            dst[q] = s0[q];
+          } else {
+            const uint32_t lo = 2 * q + 1 < (uint32_t)dg ? hexval(s0[2 * q + 1]) : 0u;
+            dst[q] = (uint8_t)((hexval(s0[2 * q]) << 4) | lo);
+          }
         }
-        ++lr;
-        lb += r4[i].payload_len;
       }
+      ++lr;
+      lb += wl;
     }
   }
   const uint32_t nl = brec < LREC ? brec : LREC;
@@ -275,13 +409,12 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
   if (threadIdx.x == 0 && nl == brec) l_dst[nl] = bbytes;   // the list's end (truncated lists: set above)
   __syncthreads();
   if (nl == 0) return;
-#ifdef SDX_XP_NOB
-  return;
-#endif
   // B: bytes [0, lim) of the block's range go through the list
   const uint32_t lim = l_dst[nl];
+  if (lim == 0) return;                         // only empty payloads: nothing to read
   const uint64_t G = so[2] + (uint32_t)boff;   // absolute offset of the block's first byte in send
   const uint64_t A0 = G & ~15ull;               // 16-byte aligned 32-byte pieces
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(counts);   // harmless in-bounds reads
   for (uint64_t a = A0 + 32ull * threadIdx.x; a < G + lim; a += 32ull * XT) {
     const int64_t p0 = (int64_t)(a - G);        // block-local position of the piece's first byte
     const uint32_t q = p0 < 0 ? 0u : (uint32_t)p0;
@@ -292,20 +425,37 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
       else hi = mid - 1;
     }
     uint32_t r = lo;
-    // source offsets first (LDS only), then 32 loads without control flow between them
-    uint32_t so32[32];
+    // source addresses first (LDS only), then the loads without control flow between them
+    const uint8_t* s0[32];
+    const uint8_t* s1[32];
+    uint8_t form[32];   // 0 raw byte, 1 two digits, 2 one digit (the odd last one)
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
       const int64_t p = p0 + i;
-      so32[i] = 0;  // heap[0]: a harmless in-bounds read for bytes outside the list's range
+      s0[i] = s1[i] = dummy;
+      form[i] = 0;
       if (p >= 0 && p < (int64_t)lim) {
         while (r + 1 < nl && (uint32_t)p >= l_dst[r + 1]) ++r;   // zero-length payloads are passed over
-        so32[i] = l_src[r] + ((uint32_t)p - l_dst[r]);
+        const uint32_t off = (uint32_t)p - l_dst[r];
+        const uint8_t* base = reinterpret_cast<const uint8_t*>((uintptr_t)l_src[r]);
+        const int dg = l_dig[r];
+        if (dg < 0) {
+          s0[i] = s1[i] = base + off;
+        } else {
+          s0[i] = base + 2 * off;
+          const bool two = 2 * off + 1 < (uint32_t)dg;
+          s1[i] = two ? base + 2 * off + 1 : s0[i];
+          form[i] = two ? 1 : 2;
+        }
       }
     }
     uint8_t bb[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) bb[i] = x.heap_dev[so32[i]];
+    for (int i = 0; i < 32; ++i) {
+      const uint8_t c0 = *s0[i];
+      const uint8_t c1 = *s1[i];
+      bb[i] = form[i] == 0 ? c0 : (uint8_t)((hexval(c0) << 4) | (form[i] == 1 ? hexval(c1) : 0u));
+    }
     uint32_t wv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -329,8 +479,9 @@ struct Wire {
   sdx_xchg_wire r[XRANKS];
   uint32_t msg0[XRANKS + 1];   // first global message of rank r
   uint32_t rec0[XRANKS + 1];   // first global record
-  uint32_t heap0[XRANKS + 1];  // first global payload byte
-  int nranks;
+  uint32_t wire0[XRANKS + 1];  // first global wire payload byte
+  const uint8_t* bank;
+  int nranks, kind;
 };
 
 __device__ inline int rank_of(const uint32_t* start, int nr, uint32_t g) {
@@ -343,8 +494,21 @@ __device__ inline int rank_of(const uint32_t* start, int nr, uint32_t g) {
   return lo;
 }
 
+__device__ inline sdx_wire_rec wrec_at(const Wire& W, uint32_t g) {
+  const int r = rank_of(W.rec0, W.nranks, g);
+  return reinterpret_cast<const sdx_wire_rec*>(W.r[r].rec_dev)[g - W.rec0[r]];
+}
+
+// digits of a nibble-form record (its payload minus the affixes)
+__device__ inline uint32_t wire_len(const Wire& W, const sdx_wire_rec& wr) {
+  if (!(wr.proto & SDX_WIRE_NIB)) return wr.payload_len;
+  const Affix a = affix_of(W.bank, W.kind, wr.proto & (SDX_WIRE_NIB - 1u));
+  const uint32_t dg = wr.payload_len - a.npre - a.npost;
+  return (dg + 1) >> 1;
+}
+
 // items: global messages [0, M) (value: records << 32) in blocks [0, nbm), global records [0, R)
-// (value: payload bytes) in blocks [nbm, nbm + nbr)
+// (value: payload bytes << 32 | wire bytes) in blocks [nbm, nbm + nbr)
 __device__ inline uint64_t xu_item(const Wire& W, bool is_msg, uint32_t g, uint32_t M, uint32_t R) {
   if (is_msg) {
     if (g >= M) return 0;
@@ -353,8 +517,8 @@ __device__ inline uint64_t xu_item(const Wire& W, bool is_msg, uint32_t g, uint3
     return (uint64_t)(word & 0xffffu) << 32;
   }
   if (g >= R) return 0;
-  const int r = rank_of(W.rec0, W.nranks, g);
-  return reinterpret_cast<const sdx_wire_rec*>(W.r[r].rec_dev)[g - W.rec0[r]].payload_len;
+  const sdx_wire_rec wr = wrec_at(W, g);
+  return ((uint64_t)wr.payload_len << 32) | wire_len(W, wr);
 }
 
 __global__ __launch_bounds__(XT) void k_xu_sum(Wire W, uint8_t* __restrict__ work) {
@@ -373,35 +537,18 @@ __global__ __launch_bounds__(XT) void k_xu_scan(Wire W, uint8_t* __restrict__ wo
   const uint32_t nbm = nblk_of(M), nbr = nblk_of(R);
   uint64_t* blk = reinterpret_cast<uint64_t*>(work + 64);
   block_scan_array(blk, nbm);
-  block_scan_array(blk + nbm, nbr);
+  const uint64_t all = block_scan_array(blk + nbm, nbr);
+  if (threadIdx.x == 0) reinterpret_cast<uint64_t*>(work)[0] = all;   // payload bytes << 32 | wire bytes
 }
 
-// blocks [0, nbm): descriptors (and each record's msg field); [nbm, nbm + nbr): records;
-// then heap blocks: one output dword per thread
-__global__ __launch_bounds__(XT) void k_xu_write(Wire W, const uint8_t* __restrict__ work, sdx_desc* __restrict__ desc,
-                                                 sdx_result* __restrict__ rec, uint8_t* __restrict__ heap) {
-  const uint32_t M = W.msg0[W.nranks], R = W.rec0[W.nranks], H = W.heap0[W.nranks];
+// blocks [0, nbm): descriptors (and each record's msg field); [nbm, nbm + nbr): records (and the
+// record's global wire byte offset into the workspace, for k_xu_heap)
+__global__ __launch_bounds__(XT) void k_xu_write(Wire W, uint8_t* __restrict__ work, sdx_desc* __restrict__ desc,
+                                                 sdx_result* __restrict__ rec) {
+  const uint32_t M = W.msg0[W.nranks], R = W.rec0[W.nranks];
   const uint32_t nbm = nblk_of(M), nbr = nblk_of(R);
   const uint64_t* blk = reinterpret_cast<const uint64_t*>(work + 64);
-  if (blockIdx.x >= nbm + nbr) {  // heap: output dword d = bytes [4d, 4d + 4)
-    const uint32_t d = (blockIdx.x - nbm - nbr) * XT + threadIdx.x;
-    if (4ull * d >= H) return;
-    uint32_t word = 0;
-    int r = rank_of(W.heap0, W.nranks, 4 * d);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t p = 4 * d + i;
-      if (p >= H) break;
-      while (p >= W.heap0[r + 1]) ++r;
-      word |= (uint32_t)W.r[r].heap_dev[p - W.heap0[r]] << (8 * i);
-    }
-    if (4ull * d + 4 <= H) {
-      reinterpret_cast<uint32_t*>(heap)[d] = word;
-    } else {
-      for (uint32_t i = 0; 4 * d + i < H; ++i) heap[4 * d + i] = (uint8_t)(word >> (8 * i));
-    }
-    return;
-  }
+  uint32_t* wsrc = reinterpret_cast<uint32_t*>(work + 64 + 8ull * (nbm + nbr));
   const bool is_msg = blockIdx.x < nbm;
   const uint32_t g = (is_msg ? blockIdx.x : blockIdx.x - nbm) * XB + threadIdx.x;
   const uint64_t v = xu_item(W, is_msg, g, M, R);
@@ -418,14 +565,42 @@ __global__ __launch_bounds__(XT) void k_xu_write(Wire W, const uint8_t* __restri
     desc[g] = o;
     for (uint32_t i = 0; i < o.n_rec; ++i) rec[o.rec_begin + i].msg = g;
   } else if (!is_msg && g < R) {
-    const int r = rank_of(W.rec0, W.nranks, g);
-    const sdx_wire_rec wr = reinterpret_cast<const sdx_wire_rec*>(W.r[r].rec_dev)[g - W.rec0[r]];
+    const sdx_wire_rec wr = wrec_at(W, g);
     sdx_result* o = rec + g;
-    o->payload_off = (uint32_t)pre;
+    o->payload_off = (uint32_t)(pre >> 32);
     o->payload_len = wr.payload_len;
-    o->proto = wr.proto;
+    o->proto = (uint16_t)(wr.proto & (SDX_WIRE_NIB - 1u));
     o->bit_length = wr.bit_length;
+    wsrc[g] = (uint32_t)pre | ((wr.proto & SDX_WIRE_NIB) ? 0x80000000u : 0u);
   }
+}
+
+// lane = record: its payload into the heap (raw copy, or preamble + the digits + postamble)
+__global__ __launch_bounds__(XT) void k_xu_heap(Wire W, const uint8_t* __restrict__ work,
+                                                const sdx_result* __restrict__ rec, uint8_t* __restrict__ heap) {
+  const uint32_t M = W.msg0[W.nranks], R = W.rec0[W.nranks];
+  const uint32_t nbm = nblk_of(M), nbr = nblk_of(R);
+  const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(work + 64 + 8ull * (nbm + nbr));
+  const uint32_t g = blockIdx.x * XT + threadIdx.x;
+  if (g >= R) return;
+  const sdx_result o = rec[g];
+  const uint32_t ws = wsrc[g] & 0x7fffffffu;
+  const bool nib = (wsrc[g] & 0x80000000u) != 0;
+  const int r = rank_of(W.wire0, W.nranks, ws);
+  const uint8_t* src = W.r[r].heap_dev + (ws - W.wire0[r]);
+  uint8_t* dst = heap + o.payload_off;
+  if (!nib) {
+    for (uint32_t i = 0; i < o.payload_len; ++i) dst[i] = src[i];
+    return;
+  }
+  const Affix a = affix_of(W.bank, W.kind, o.proto);
+  const uint32_t dg = o.payload_len - a.npre - a.npost;
+  for (uint32_t i = 0; i < a.npre; ++i) dst[i] = a.pre[i];
+  for (uint32_t i = 0; i < dg; ++i) {
+    const uint32_t v = (src[i >> 1] >> ((i & 1) ? 0 : 4)) & 15u;
+    dst[a.npre + i] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+  }
+  for (uint32_t i = 0; i < a.npost; ++i) dst[a.npre + dg + i] = a.post[i];
 }
 
 }  // namespace sdxx
@@ -433,31 +608,40 @@ __global__ __launch_bounds__(XT) void k_xu_write(Wire W, const uint8_t* __restri
 using namespace sdxx;
 
 extern "C" uint64_t sdx_exchange_work_bytes(const uint32_t* n_msgs, int k) {
-  uint64_t s = 0;
+  uint64_t s = WHEAD;
   for (int i = 0; i < k; ++i) s += part_work_bytes(n_msgs[i]);
   return s;
 }
 
 extern "C" uint64_t sdx_exchange_send_bytes(const sdx_xchg_part* parts, int k) {
   uint64_t s = 0;
-  for (int i = 0; i < k; ++i) s += r16(4ull * parts[i].n_msgs) + r16(8ull * parts[i].rec_cap) + r16(parts[i].heap_cap);
+  for (int i = 0; i < k; ++i)
+    if (!parts[i].aux) s += r16(4ull * parts[i].n_msgs) + r16(8ull * parts[i].rec_cap) + r16(parts[i].heap_cap);
+  // an overlaid launch may take its records from its overlays: their capacities bound its sections too
+  for (int i = 0; i < k; ++i)
+    if (parts[i].aux) s += r16(8ull * parts[i].rec_cap) + r16(parts[i].heap_cap);
   return s;
 }
 
 static int check_parts(const sdx_xchg_part* parts, int k, const char* who) {
-  if (!parts || k < 1 || k > XMAX) return sdx::set_error(SDX_EINVAL, std::string(who) + ": 1..8 launches");
+  if (!parts || k < 1 || k > XMAX) return sdx::set_error(SDX_EINVAL, std::string(who) + ": 1..SDX_XCHG_MAX_PARTS launches");
   for (int i = 0; i < k; ++i) {
     const sdx_xchg_part& x = parts[i];
-    if (!x.cursor_dev || (x.n_msgs && !x.desc_dev) || (x.rec_cap && !x.rec_dev) || (x.heap_cap && !x.heap_dev))
-      return sdx::set_error(SDX_EINVAL, std::string(who) + ": missing buffer");
+    if (!x.cursor_dev || (x.n_msgs && !x.desc_dev) || (x.rec_cap && !x.rec_dev) || (x.rec_cap && !x.heap_dev))
+      return sdx::set_error(SDX_EINVAL, std::string(who) + ": missing buffer (records need a heap)");
+    if (x.alt > k || x.alt == i + 1)
+      return sdx::set_error(SDX_EINVAL, std::string(who) + ": overlay index out of range");
+    if (x.alt && (!parts[x.alt - 1].aux || parts[x.alt - 1].n_msgs != x.n_msgs))
+      return sdx::set_error(SDX_EINVAL, std::string(who) + ": an overlay must be aux and cover the same messages");
   }
   return SDX_OK;
 }
 
-static Parts make_parts(const sdx_xchg_part* parts, int k) {
+static Parts make_parts(const sdx_bank* bank, const sdx_xchg_part* parts, int k) {
   Parts P;
   uint64_t off = 0;
   P.k = k;
+  P.bank = bank ? reinterpret_cast<const uint8_t*>(sdx::bank_dev_ptr(bank)) : nullptr;
   for (int i = 0; i < XMAX; ++i) {
     P.p[i] = i < k ? parts[i] : sdx_xchg_part{};
     P.work_off[i] = off;
@@ -484,12 +668,12 @@ static uint32_t max_blocks(const sdx_xchg_part* parts, int k) {
   return nb;
 }
 
-extern "C" int sdx_exchange_count(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
-                                  uint32_t* counts_dev, void* hip_stream) {
+extern "C" int sdx_exchange_count(const sdx_bank* bank, const sdx_xchg_part* parts, int k, void* work_dev,
+                                  uint64_t work_cap, uint32_t* counts_dev, void* hip_stream) {
   if (int rc = check_parts(parts, k, "sdx_exchange_count")) return rc;
   if (!counts_dev || !work_ok(parts, k, work_dev, work_cap))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_count: workspace too small / unaligned, or no counts buffer");
-  const Parts P = make_parts(parts, k);
+  const Parts P = make_parts(bank, parts, k);
   hipLaunchKernelGGL(k_xw_count, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream, P,
                      (uint8_t*)work_dev);
   if (int rc = launched("k_xw_count")) return rc;
@@ -497,82 +681,87 @@ extern "C" int sdx_exchange_count(const sdx_xchg_part* parts, int k, void* work_
   return launched("k_xw_scan");
 }
 
-extern "C" int sdx_exchange_pack(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
-                                 const uint32_t* counts_dev, uint8_t* send_dev, uint64_t send_cap, void* hip_stream) {
+extern "C" int sdx_exchange_pack(const sdx_bank* bank, const sdx_xchg_part* parts, int k, void* work_dev,
+                                 uint64_t work_cap, const uint32_t* counts_dev, uint8_t* send_dev, uint64_t send_cap,
+                                 void* hip_stream) {
   if (int rc = check_parts(parts, k, "sdx_exchange_pack")) return rc;
   if (!counts_dev || !send_dev || ((uintptr_t)send_dev & 15u) || send_cap < sdx_exchange_send_bytes(parts, k) ||
       !work_ok(parts, k, work_dev, work_cap))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack: workspace or send buffer too small / unaligned");
   hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream,
-                     make_parts(parts, k), counts_dev, (uint8_t*)work_dev, send_dev);
+                     make_parts(bank, parts, k), counts_dev, (uint8_t*)work_dev, send_dev);
   return launched("k_xw_pack");
 }
 
 // the pack into a buffer sized from the host's copy of the counts (the exact layout), e.g. the rank's
 // own chunk of an in-place all-gather's receive buffer
-extern "C" int sdx_exchange_pack_into(const sdx_xchg_part* parts, int k, void* work_dev, uint64_t work_cap,
-                                      const uint32_t* counts_dev, const uint32_t* counts_host, uint8_t* dst_dev,
-                                      uint64_t dst_cap, void* hip_stream) {
+extern "C" int sdx_exchange_pack_into(const sdx_bank* bank, const sdx_xchg_part* parts, int k, void* work_dev,
+                                      uint64_t work_cap, const uint32_t* counts_dev, const uint32_t* counts_host,
+                                      uint8_t* dst_dev, uint64_t dst_cap, void* hip_stream) {
   if (int rc = check_parts(parts, k, "sdx_exchange_pack_into")) return rc;
   if (!counts_dev || !counts_host || !dst_dev || ((uintptr_t)dst_dev & 15u) || !work_ok(parts, k, work_dev, work_cap))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: missing / unaligned buffer or workspace too small");
   uint64_t need = 0;
   for (int i = 0; i < k; ++i) {
-    if (counts_host[4 * i] != parts[i].n_msgs)
+    const uint32_t* c = counts_host + SDX_XCHG_COUNTS * i;
+    if (c[0] != (parts[i].aux ? 0u : parts[i].n_msgs))
       return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: counts_host are not this exchange's counts");
-    need += r16(4ull * counts_host[4 * i]) + r16(8ull * counts_host[4 * i + 1]) + r16(counts_host[4 * i + 2]);
+    need += r16(4ull * c[0]) + r16(8ull * c[1]) + r16(c[2]);
   }
   if (dst_cap < need) return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: destination smaller than the wire");
   hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream,
-                     make_parts(parts, k), counts_dev, (uint8_t*)work_dev, dst_dev);
+                     make_parts(bank, parts, k), counts_dev, (uint8_t*)work_dev, dst_dev);
   return launched("k_xw_pack");
 }
 
 extern "C" uint64_t sdx_exchange_unpack_work_bytes(uint32_t n_msgs, uint32_t n_rec) {
-  return 64 + 8ull * (nblk_of(n_msgs) + nblk_of(n_rec));
+  return 64 + 8ull * (nblk_of(n_msgs) + nblk_of(n_rec)) + 4ull * n_rec;
 }
 
-extern "C" int sdx_exchange_unpack(const sdx_xchg_wire* ranks, int nranks, void* work_dev, uint64_t work_cap,
-                                   sdx_desc* desc_dev, sdx_result* rec_dev, uint8_t* heap_dev, void* hip_stream) {
+extern "C" int sdx_exchange_unpack(const sdx_bank* bank, int kind, const sdx_xchg_wire* ranks, int nranks,
+                                   void* work_dev, uint64_t work_cap, sdx_desc* desc_dev, sdx_result* rec_dev,
+                                   uint8_t* heap_dev, uint64_t heap_cap, void* hip_stream) {
   if (!ranks || nranks < 1 || nranks > XRANKS)
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_unpack: 1..SDX_XCHG_MAX_RANKS ranks");
   Wire W;
   W.nranks = nranks;
-  uint64_t m = 0, r = 0, h = 0;
-  for (int i = 0; i < XRANKS; ++i) {
-    W.r[i] = i < nranks ? ranks[i] : sdx_xchg_wire{};
-    if (i <= nranks) {
-      W.msg0[i] = (uint32_t)m;
-      W.rec0[i] = (uint32_t)r;
-      W.heap0[i] = (uint32_t)h;
-    }
+  W.kind = kind;
+  W.bank = bank ? reinterpret_cast<const uint8_t*>(sdx::bank_dev_ptr(bank)) : nullptr;
+  uint64_t m = 0, r = 0, h = 0, pay = 0;
+  // every prefix entry [0, XRANKS] is written: the ranks' starts, then the end sentinel at [nranks]
+  // and beyond (the kernels read [nranks] as the job's totals, also when nranks == XRANKS)
+  for (int i = 0; i <= XRANKS; ++i) {
+    if (i < XRANKS) W.r[i] = i < nranks ? ranks[i] : sdx_xchg_wire{};
+    W.msg0[i] = (uint32_t)m;
+    W.rec0[i] = (uint32_t)r;
+    W.wire0[i] = (uint32_t)h;
     if (i < nranks) {
       m += ranks[i].n_msgs;
       r += ranks[i].n_rec;
       h += ranks[i].n_heap;
+      pay += ranks[i].n_payload;
       if ((ranks[i].n_msgs && !ranks[i].msg_dev) || (ranks[i].n_rec && !ranks[i].rec_dev) ||
           (ranks[i].n_heap && !ranks[i].heap_dev))
         return sdx::set_error(SDX_EINVAL, "sdx_exchange_unpack: missing section");
     }
   }
-  if (nranks < XRANKS) {
-    W.msg0[nranks] = (uint32_t)m;
-    W.rec0[nranks] = (uint32_t)r;
-    W.heap0[nranks] = (uint32_t)h;
-  }
-  if (m >= (1ull << 32) || r >= (1ull << 32) || h >= (1ull << 32))
+  if (m >= (1ull << 32) || r >= (1ull << 31) || h >= (1ull << 31) || pay >= (1ull << 32))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_unpack: the job exceeds 32-bit message / record / heap indices");
   if (!work_dev || work_cap < sdx_exchange_unpack_work_bytes((uint32_t)m, (uint32_t)r) || ((uintptr_t)work_dev & 63u) ||
-      (m && !desc_dev) || (r && !rec_dev) || (h && !heap_dev) || ((uintptr_t)heap_dev & 3u))
-    return sdx::set_error(SDX_EINVAL, "sdx_exchange_unpack: bad workspace or output buffers");
+      (m && !desc_dev) || (r && !rec_dev) || (pay && !heap_dev) || heap_cap < pay)
+    return sdx::set_error(SDX_EINVAL, "sdx_exchange_unpack: bad workspace or output buffers (heap_cap < payload bytes)");
   const uint32_t nb = nblk_of(m) + nblk_of(r);
-  const uint32_t nh = (uint32_t)((h + 4ull * XT - 1) / (4ull * XT));
   hipStream_t st = (hipStream_t)hip_stream;
   hipLaunchKernelGGL(k_xu_sum, dim3(nb), dim3(XT), 0, st, W, (uint8_t*)work_dev);
   if (int rc = launched("k_xu_sum")) return rc;
   hipLaunchKernelGGL(k_xu_scan, dim3(1), dim3(XT), 0, st, W, (uint8_t*)work_dev);
   if (int rc = launched("k_xu_scan")) return rc;
-  hipLaunchKernelGGL(k_xu_write, dim3(nb + nh), dim3(XT), 0, st, W, (const uint8_t*)work_dev, desc_dev, rec_dev,
-                     heap_dev);
-  return launched("k_xu_write");
+  hipLaunchKernelGGL(k_xu_write, dim3(nb), dim3(XT), 0, st, W, (uint8_t*)work_dev, desc_dev, rec_dev);
+  if (int rc = launched("k_xu_write")) return rc;
+  if (r) {
+    hipLaunchKernelGGL(k_xu_heap, dim3((uint32_t)((r + XT - 1) / XT)), dim3(XT), 0, st, W, (const uint8_t*)work_dev,
+                       rec_dev, heap_dev);
+    if (int rc = launched("k_xu_heap")) return rc;
+  }
+  return SDX_OK;
 }

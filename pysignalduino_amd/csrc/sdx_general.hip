@@ -807,6 +807,7 @@ __global__ __launch_bounds__(64) void k_gen_prep(sdx_general_batch b, sdx_out ou
   const int64_t off = b.offsets_dev[msg];
   const uint8_t* d = b.data_dev + off;
   const int n = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
+  if (n > g.max_len) return;  // outside the batch's max_len: k_gen_walk raises SDX_RAISE_CONTRACT for it
   const int nwp = ((n + 63) >> 6) + 1;
   uint64_t* bmw = reinterpret_cast<uint64_t*>(gen_region(b, out, g, i, msg));
   if (i == 0 && lane < 2) gen_ctr(out)[lane] = 0;  // the two walk passes' item counters
@@ -887,6 +888,14 @@ __global__ __launch_bounds__(64) void k_gen_walk(const void* __restrict__ bank, 
       }
     }
     GP_ADD(5, ti0);
+    if (m.n > g.max_len) {  // the per-slot scratch and regions are sized by max_len: never walk past them
+      if (PASS == 0 && lane == 0) {
+        e.nrec = 0;
+        e.nheap = 0;
+        e.raise = ((uint32_t)SDX_RAISE_CONTRACT << 16) | (uint32_t)p0;
+      }
+      continue;
+    }
     Sink sk{PASS == 1, 0, 0u, out.rec_dev, out.heap_dev, PASS == 1 ? e.rbase : 0u, PASS == 1 ? e.hbase : 0u,
             (uint32_t)msg};
     int rp = 0, raise;

@@ -1531,15 +1531,11 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   uint8_t* st_np = reinterpret_cast<uint8_t*>(st_clk + TM);                // [TM]
   int64_t pf_off = 0;
   int pf_n = 0;
-#ifdef SDX_STAGE_BALLOT
-  uint32_t pf_c[MPW][NW <= 4 ? NW : 1];
-#else
   // SWAR staging (short variants): 16 characters per lane, 4 messages per pass over the wave
   constexpr int SMSG = 64 / 16;                    // messages per pass
   constexpr int SPASS = (MPW + SMSG - 1) / SMSG;   // passes per wave
   static_assert(NW > 4 || NW == 4, "SWAR staging: 256-character rows, 16 lanes per message");
   uint32_t sx[NW <= 4 ? SPASS : 1][5];
-#endif
   if constexpr (NW <= 4) {
     // every header load of the tile is issued before any of them is used: the data offsets of the
     // wave's messages, and per (message, pattern) thread npat, P, the id and (MS) the message's
@@ -1620,19 +1616,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       }
     }
     PROF_ADD(17, t_stage);
-#ifdef SDX_STAGE_BALLOT
-#pragma unroll
-    for (int k = 0; k < MPW; ++k) {
-      const int lo = __shfl((int)(uint32_t)pf_off, k), hi = __shfl((int)(uint32_t)((uint64_t)pf_off >> 32), k);
-      const int64_t off = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-      const int n = __shfl(pf_n, k);
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const int pos = w * 64 + lane;
-        pf_c[k][w] = pos < n ? (uint32_t)b.data_dev[off + pos] : 0xFFu;
-      }
-    }
-#else
     // 16 characters per lane: lane group g = lane / 16 holds tile message 4 * pass + g, lane j = lane % 16
     // its characters [16 j, 16 j + 16) as five aligned dwords (realigned below; a dword that holds a
     // byte of the message cannot cross a page, so the loads past the message end stay in bounds)
@@ -1649,11 +1632,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
 #pragma unroll
       for (int i = 0; i < 5; ++i) sx[ps][i] = (on && a + 4 * i < off + n) ? src[i] : 0xFFFFFFFFu;
     }
-#endif
   }
   PROF_T(t_bm);
   if constexpr (NW <= 4) {
-#ifndef SDX_STAGE_BALLOT
   // per pass: the lane's 16 characters -> 10 id masks of 16 bits (SWAR on 4 characters per dword),
   // written as 16-bit pieces of the per-id bitmaps; non-digit characters per message by ballot
   uint32_t ndmsg = 0;  // bit k: tile message k of the wave holds a non-digit character
@@ -1704,7 +1685,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     }
   }
   wave_sync();
-#endif
   PROF_ADD(18, t_bm);
   PROF_T(t_pairs);
 #pragma unroll
@@ -1713,28 +1693,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     if (mi >= nvalid) break;
     const int n = __shfl(pf_n, k);
     const int nwu = (n + 63) >> 6;  // words holding pulses (wave-uniform); the rest are empty
-#ifdef SDX_STAGE_BALLOT
-    bool nondigit = false;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const int pos = w * 64 + lane;
-      const uint8_t c = (uint8_t)pf_c[k][w];
-      nondigit |= pos < n && !((c >= '0' && c <= '9') || c == 0xFE);
-      uint64_t mine = 0;
-      if (KIND != SDX_KIND_MS || w < nwu) {  // short MS messages (sync + bits, mostly < 128 pulses)
-        // skip the ballots of empty words (MU: the uniform branch measured 1.8 % slower)
-#pragma unroll
-        for (int id = 0; id < 10; ++id) {
-          const uint64_t bb = ballot(c == (uint8_t)('0' + id));
-          if (lane == id) mine = bb;
-        }
-      }
-      if (lane < 10) L.bm[mi * T::MSTRIDE + lane * T::WS + w] = mine;
-    }
-    const uint64_t nd = ballot(nondigit);
-#else
     const uint64_t nd = (ndmsg >> k) & 1u;
-#endif
     if constexpr (NW <= 4) {  // pair presence: lane = id pair (a, b), a = q / 10, b = q % 10
       wave_sync();
       uint64_t pr[2];
@@ -1921,14 +1880,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   int g_cur = -1;
   unsigned long long g_t0 = 0;
 #endif
-#ifdef SDX_PF
-  int p_next = -1;  // the work item's next protocol index, loaded one protocol ahead
-#endif
   while (true) {
     if (cur == cend) {
-#ifdef SDX_PF
-      p_next = -1;
-#endif
       int g = 0;
       if (lane == 0) g = atomicAdd(&L.next_p, 1);
       g = __builtin_amdgcn_readfirstlane(g);
@@ -1949,14 +1902,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         cend = g + 1;
       }
     }
-#ifdef SDX_PF
-    const int p = p_next >= 0 ? p_next : cld(&order[cur]);
-    ++cur;
-    p_next = cur < cend ? (int)cld(&order[cur]) : -1;
-#else
     const int p = cld(&order[cur]);
     ++cur;
-#endif
     if constexpr (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
       const sdx_mu_filt* fr = uniform_ptr(bv.mufilt + p);  // the filter's state: two 64-byte lines
@@ -2618,6 +2565,11 @@ int sdx_wgtime_read(unsigned long long* out, int n) {
 }
 #endif
 const char* sdx_last_error(void) { return g_err.c_str(); }
+
+#ifndef SDX_SRC_HASH
+#define SDX_SRC_HASH "unknown"
+#endif
+const char* sdx_source_hash(void) { return SDX_SRC_HASH; }
 
 int sdx_layout_size(int which) {
   switch (which) {

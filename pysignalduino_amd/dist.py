@@ -4,42 +4,52 @@ Messages are independent: each rank demodulates its contiguou
 communication during compute.  The one exchange step gathers every rank's results so that every
 rank holds the whole stream's results in global message order (BASELINE config 5).
 
-What travels is the WIRE form of include/sdx.h, per launch and rank, in message order:
+What travels is the WIRE form of include/sdx.h (v3), per launch and rank, in message order:
   msg  section  u32 per message = n_rec | status << 16 | raise_kind << 24
-  rec  section  8 B per record  = proto, payload_len, bit_length
-  heap section  the payloads concatenated in record order, zero-padded to 16 bytes
+  rec  section  8 B per record  = proto (| WIRE_NIB), payload_len, bit_length
+  heap section  the payloads in record order, zero-padded to 16 bytes; a payload that is its
+                protocol's preamble + uppercase hex digits + postamble travels as the digits packed
+                two per byte (the receiver has the same bank and rebuilds the affixes)
 rec_begin, payload_off and msg are prefix sums and are rebuilt by the receiver
-(``sdx_exchange_unpack``), so a message costs 4 + 8 * records + payload bytes on the wire instead of
-8 + 16 * records + the launch's padded heap.  The wire is also canonical: the bytes do not depend
-on the order in which tiles wrote their records, so a sharded run and an un-sharded run compare
-byte for byte (tests/test_dist.py).
+(``sdx_exchange_unpack``).  The wire is canonical: the bytes do not depend on the order in which
+tiles wrote their records, so a sharded run and an un-sharded run compare byte for byte.
+
+Overflow re-runs (ABI 11): a launch whose messages overflowed (ST_OVF_TILE / ST_OVF_OUT) is never
+exchanged as such.  Its messages are re-run into an OVERLAY (:class:`Part` ``overlays``: outputs over
+the same messages, descriptors left at ST_ABSENT where no re-run wrote) and the sender takes each
+message from the last overlay that has it.  :class:`Exchange` drives the re-runs itself when the
+count exchange reports overflowed messages on any rank (``rerun`` callback, all ranks recount), and
+:class:`ShardedDemodulator` is the product entry that shards a batch, demodulates, re-runs and
+exchanges.
 
 With the ``nccl`` backend (RCCL over xGMI on ROCm) the buffers stay in HBM and the exchange runs on
 its own HIP stream (:class:`Exchange`), overlapped with the next step's kernels:
   step k kernels ─ready_k─▶ [exchange stream] sdx_exchange_count_k ─ all-gather counts_k ─ D2H
-  submit(k+1): host waits for counts_k (the GPU runs step k+1 meanwhile), sizes the sections (max
-               over ranks), enqueues sdx_exchange_pack_into_k (this rank's chunk of the receive
-               buffer) ─released_k─ in-place all-gather data_k, and only then the wait on ready_{k+1}
-               and step k+1's count: step k's pack and collective never wait for step k+1's kernels.
+  submit(k+1): host waits for counts_k (the GPU runs step k+1 meanwhile), re-runs overflowed
+               messages (rare), sizes the sections (max over ranks), enqueues
+               sdx_exchange_pack_into_k (this rank's chunk of the receive buffer) ─released_k─
+               in-place all-gather data_k, and only then the wait on ready_{k+1} and step k+1's count.
 The same protocol runs synchronously on ``gloo`` (CPU tensors: numpy packing; CUDA tensors: the
 device kernels, the collective staged through host memory).
 """
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import runtime
-from .runtime import DESC_DT, RES_DT, WIRE_REC_DT
+from .runtime import DESC_DT, KIND_RAW, RES_DT, ST_ABSENT, WIRE_NIB, WIRE_REC_DT, XCHG_COUNTS
 
 DESC_BYTES = 8
 REC_BYTES = 16
 WIRE_MSG_BYTES = 4
 WIRE_REC_BYTES = 8
+RAISE_HOST = 0xFE   # raise_kind of a host overlay row: the host packing raised for this message
+OVF = (runtime.ST_OVF_TILE, runtime.ST_OVF_OUT)
 
 
 def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -54,26 +64,73 @@ def _r16(x):
 
 
 # ---- host (numpy) form of the wire: CPU tensors on gloo, and the checker of the device kernels ----
+def _nib_digits(affix, proto: int, p: bytes) -> int:
+    """The nibble form's test (sdx_exchange.hip nib_digits): payload == pre + D uppercase hex digits +
+    post of the protocol -> D, else -1."""
+    if affix is None or proto >= len(affix):
+        return -1
+    pre, post = affix[proto]
+    if len(p) < len(pre) + len(post) or not p.startswith(pre) or not p.endswith(post):
+        return -1
+    mid = p[len(pre): len(p) - len(post)]
+    return len(mid) if all(c in b"0123456789ABCDEF" for c in mid) else -1
+
+
+def _nib_pack(digits: bytes) -> bytes:
+    v = [int(chr(c), 16) for c in digits]
+    if len(v) % 2:
+        v.append(0)
+    return bytes((v[i] << 4) | v[i + 1] for i in range(0, len(v), 2))
+
+
+def _nib_unpack(b: bytes, nd: int) -> bytes:
+    out = bytearray()
+    for i in range(nd):
+        x = (b[i >> 1] >> (0 if i & 1 else 4)) & 15
+        out.append(ord("0123456789ABCDEF"[x]))
+    return bytes(out)
+
+
+def resolve_host(levels) -> Tuple[np.ndarray, np.ndarray]:
+    """levels: [(desc, ...)] of a launch and its overlays in chain order -> (per message the level
+    its results come from, the resolved descriptors): the last level whose descriptor is present."""
+    desc = levels[0][0].copy()
+    lev = np.zeros(len(desc), np.int64)
+    for j, lv in enumerate(levels[1:], 1):
+        d = lv[0]
+        here = d["status"] != ST_ABSENT
+        desc[here] = d[here]
+        lev[here] = j
+    return lev, desc
+
+
 def wire_encode(desc: np.ndarray, rec: np.ndarray, heap: np.ndarray, nrec_written: Optional[int] = None,
-                nheap_written: Optional[int] = None):
-    """One launch's host (desc, rec, heap) -> (msg u32[n], wire records, payload bytes, bad count),
-    with the validation rules of k_xw_count (a record or payload outside what the launch wrote makes
-    its message "bad": shipped with n_rec 0 and status ST_OVF_OUT)."""
-    nrec_c = len(rec) if nrec_written is None else min(nrec_written, len(rec))
-    nheap_c = len(heap) if nheap_written is None else min(nheap_written, len(heap))
+                nheap_written: Optional[int] = None, affix=None, overlays=()):
+    """One launch's host (desc, rec, heap) (plus its overlays: (desc, rec, heap, nrec_written,
+    nheap_written) in chain order) -> (msg u32[n], wire records, wire payload bytes, bad count), with
+    the validation rules of k_xw_count (a record or payload outside what its launch wrote makes the
+    message "bad": shipped with n_rec 0 and status ST_OVF_OUT) and the nibble form where ``affix``
+    (Bank.affixes(kind)) is given."""
+    def clamp(r, h, nr, nh):
+        return (len(r) if nr is None else min(nr, len(r))), (len(h) if nh is None else min(nh, len(h)))
+
+    levels = [(desc, rec, np.asarray(heap, np.uint8), *clamp(rec, heap, nrec_written, nheap_written))]
+    for d2, r2, h2, nr2, nh2 in overlays:
+        levels.append((d2, r2, np.asarray(h2, np.uint8), *clamp(r2, h2, nr2, nh2)))
+    lev, rdesc = resolve_host(levels)
     n = len(desc)
     msg = np.zeros(n, np.uint32)
     recs, pays, bad = [], [], 0
-    hb = np.asarray(heap, np.uint8)
     for m in range(n):
-        d = desc[m]
+        d = rdesc[m]
+        _, rr, hb, nrec_c, nheap_c = levels[int(lev[m])]
         st, nr, rb = int(d["status"]), int(d["n_rec"]), int(d["rec_begin"])
         if st == runtime.ST_RAISED:
             msg[m] = (st << 16) | (int(d["raise_kind"]) << 24)
             continue
         ok = st == runtime.ST_OK and (nr == 0 or rb + nr <= nrec_c)
         if ok:
-            rs = rec[rb: rb + nr]
+            rs = rr[rb: rb + nr]
             ok = bool(np.all(rs["msg"] == m)) and bool(np.all(rs["payload_off"].astype(np.int64)
                                                               + rs["payload_len"] <= nheap_c))
         if not ok:
@@ -82,19 +139,27 @@ def wire_encode(desc: np.ndarray, rec: np.ndarray, heap: np.ndarray, nrec_writte
             continue
         msg[m] = nr | (st << 16) | (int(d["raise_kind"]) << 24)
         for r in rs:
-            recs.append((int(r["proto"]), int(r["payload_len"]), int(r["bit_length"])))
-            pays.append(hb[int(r["payload_off"]): int(r["payload_off"]) + int(r["payload_len"])])
+            p = hb[int(r["payload_off"]): int(r["payload_off"]) + int(r["payload_len"])].tobytes()
+            pr = int(r["proto"])
+            dg = _nib_digits(affix, pr, p)
+            if dg >= 0:
+                pre = affix[pr][0]
+                pays.append(np.frombuffer(_nib_pack(p[len(pre): len(pre) + dg]), np.uint8))
+                pr |= WIRE_NIB
+            else:
+                pays.append(np.frombuffer(p, np.uint8))
+            recs.append((pr, int(r["payload_len"]), int(r["bit_length"])))
     wrec = np.array(recs, WIRE_REC_DT) if recs else np.zeros(0, WIRE_REC_DT)
     pay = np.concatenate(pays) if pays else np.zeros(0, np.uint8)
     return msg, wrec, pay.astype(np.uint8), bad
 
 
-def wire_decode(ranks: Sequence[Tuple[np.ndarray, np.ndarray, np.ndarray]]):
+def wire_decode(ranks: Sequence[Tuple[np.ndarray, np.ndarray, np.ndarray]], affix=None):
     """Wire sections of every rank (rank order) -> the whole job's (desc, rec, heap), as
-    sdx_exchange_unpack builds them."""
+    sdx_exchange_unpack builds them (nibble-form payloads rebuilt with the protocols' affixes)."""
     msg = np.concatenate([np.asarray(m, np.uint32) for m, _, _ in ranks]) if ranks else np.zeros(0, np.uint32)
     wrec = np.concatenate([w for _, w, _ in ranks]) if ranks else np.zeros(0, WIRE_REC_DT)
-    heap = np.concatenate([np.asarray(p, np.uint8) for _, _, p in ranks]) if ranks else np.zeros(0, np.uint8)
+    wheap = b"".join(np.asarray(p, np.uint8).tobytes() for _, _, p in ranks)
     n = len(msg)
     desc = np.zeros(n, DESC_DT)
     nrec = (msg & 0xFFFF).astype(np.int64)
@@ -103,13 +168,27 @@ def wire_decode(ranks: Sequence[Tuple[np.ndarray, np.ndarray, np.ndarray]]):
     desc["raise_kind"] = msg >> 24
     desc["rec_begin"] = np.concatenate([[0], np.cumsum(nrec)[:-1]]) if n else np.zeros(0, np.int64)
     rec = np.zeros(len(wrec), RES_DT)
-    rec["proto"] = wrec["proto"]
+    proto = wrec["proto"].astype(np.int64)
+    rec["proto"] = proto & (WIRE_NIB - 1)
     rec["payload_len"] = wrec["payload_len"]
     rec["bit_length"] = wrec["bit_length"]
     pl = wrec["payload_len"].astype(np.int64)
     rec["payload_off"] = np.concatenate([[0], np.cumsum(pl)[:-1]]) if len(pl) else np.zeros(0, np.int64)
     rec["msg"] = np.repeat(np.arange(n, dtype=np.int64), nrec)
-    return desc, rec, heap
+    out = bytearray()
+    o = 0
+    for i in range(len(wrec)):
+        ln = int(pl[i])
+        if proto[i] & WIRE_NIB:
+            pre, post = affix[int(proto[i] & (WIRE_NIB - 1))]
+            nd = ln - len(pre) - len(post)
+            nb = (nd + 1) // 2
+            out += pre + _nib_unpack(wheap[o: o + nb], nd) + post
+            o += nb
+        else:
+            out += wheap[o: o + ln]
+            o += ln
+    return desc, rec, np.frombuffer(bytes(out), np.uint8).copy()
 
 
 def canonical(desc: np.ndarray, rec: np.ndarray, heap: np.ndarray):
@@ -119,6 +198,64 @@ def canonical(desc: np.ndarray, rec: np.ndarray, heap: np.ndarray):
     if bad:
         raise ValueError(f"{bad} messages overflowed: re-run before comparing")
     return wire_decode([(m, w, p)])
+
+
+# ---- launches as the exchange sees them ------------------------------------------------------------
+class Part:
+    """One demodulation launch's outputs as the exchange reads them: byte tensors ``desc`` /
+    ``rec`` / ``heap`` of ``n`` messages, the launch's ``cursor`` (records, heap bytes written),
+    ``kind`` (runtime.KIND_*: its protocols' affixes for the nibble form; KIND_RAW: raw payloads), the
+    ``overlays`` (Parts over the same messages holding re-run / general-path results, in precedence
+    order) and ``src`` = (kind, device batch) for re-running its overflowed messages."""
+
+    __slots__ = ("desc", "rec", "heap", "n", "cursor", "kind", "overlays", "src", "keep")
+
+    def __init__(self, desc, rec, heap, n, cursor, kind=KIND_RAW, overlays=(), src=None, keep=None):
+        self.desc, self.rec, self.heap, self.n, self.cursor = desc, rec, heap, int(n), cursor
+        self.kind, self.overlays, self.src, self.keep = kind, list(overlays), src, keep
+
+    @staticmethod
+    def of(p) -> "Part":
+        """A Part, or a (desc, rec, heap, n, cursor[, kind]) tuple."""
+        return p if isinstance(p, Part) else Part(*p)
+
+    @staticmethod
+    def from_out(out, kind=KIND_RAW, src=None) -> "Part":
+        """An Engine.alloc_out dict."""
+        return Part(out["desc"], out["rec"], out["heap"], out["n"], out["cursor"], kind, src=src, keep=out)
+
+    def caps(self):
+        return self.rec.numel() // REC_BYTES, self.heap.numel()
+
+
+def _flatten(parts: Sequence[Part]):
+    """Primary launches first, then each launch's overlays (chained in order): the sdx_xchg_part
+    array with its alt / aux fields, as (Part, alt, aux) triples."""
+    flat = [(p, 0, 0) for p in parts]
+    for i, p in enumerate(parts):
+        prev = i
+        for ov in p.overlays:
+            flat.append((ov, 0, 1))
+            j = len(flat) - 1
+            q, _, aux = flat[prev]
+            flat[prev] = (q, j + 1, aux)
+            prev = j
+    if len(flat) > runtime.XCHG_MAX_PARTS:
+        raise RuntimeError(f"exchange: {len(flat)} launches + overlays exceed SDX_XCHG_MAX_PARTS")
+    return flat
+
+
+def _layout(S: np.ndarray):
+    """S[world, K, >=3] = (messages, records, wire payload bytes, ...) -> per rank the section offsets
+    [world, K, 3] of its send buffer (launch 0, 1, ...: msg, rec, heap sections, each padded to 16
+    bytes -- the layout k_xw_pack computes on the device), the section byte counts [world, K, 3]
+    and the collective's per-rank size T (the largest rank's buffer)."""
+    S = np.asarray(S, np.int64)
+    nb = np.stack([S[..., 0] * WIRE_MSG_BYTES, S[..., 1] * WIRE_REC_BYTES, S[..., 2]], axis=-1)
+    sizes = _r16(nb).reshape(S.shape[0], -1)                                     # [world, K*3]
+    offs = np.concatenate([np.zeros((S.shape[0], 1), np.int64), np.cumsum(sizes, axis=1)[:, :-1]], axis=1)
+    T = int(max(16, sizes.sum(axis=1).max()))
+    return offs.reshape(S.shape[0], S.shape[1], 3), nb, T
 
 
 # ---- collectives -------------------------------------------------------------------------------------
@@ -138,60 +275,64 @@ def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
         dist.all_gather(list(out.chunk(w)), inp, group=group)
 
 
-def _layout(S: np.ndarray):
-    """S[world, K, 4] = (messages, records, payload bytes, bad) -> per rank the section offsets
-    [world, K, 3] of its send buffer (launch 0, 1, ...: msg, rec, heap sections, each padded to 16
-    bytes -- the layout k_xw_count computes on the device), the section byte counts [world, K, 3]
-    and the collective's per-rank size T (the largest rank's buffer)."""
-    S = np.asarray(S, np.int64)
-    nb = np.stack([S[..., 0] * WIRE_MSG_BYTES, S[..., 1] * WIRE_REC_BYTES, S[..., 2]], axis=-1)
-    sizes = _r16(nb).reshape(S.shape[0], -1)                                     # [world, K*3]
-    offs = np.concatenate([np.zeros((S.shape[0], 1), np.int64), np.cumsum(sizes, axis=1)[:, :-1]], axis=1)
-    T = int(max(16, sizes.sum(axis=1).max()))
-    return offs.reshape(S.shape[0], S.shape[1], 3), nb, T
-
-
-def _part_tuple(p):
-    """(desc u8, rec u8, heap u8, n_msgs, cursor) -> the same plus rec_cap / heap_cap from the sizes."""
-    desc, rec, heap, n, cur = p
-    return desc, rec, heap, int(n), cur, rec.numel() // REC_BYTES, heap.numel()
-
-
 class _Pending:
-    __slots__ = ("parts", "counts_host", "event", "enc", "cnt")
+    __slots__ = ("parts", "counts_host", "event", "enc", "cnt", "rerun", "ready")
 
-    def __init__(self, parts, counts_host, event, enc=None, cnt=None):
-        self.parts, self.counts_host, self.event, self.enc, self.cnt = parts, counts_host, event, enc, cnt
+    def __init__(self, parts, counts_host, event, enc=None, cnt=None, rerun=None, ready=None):
+        self.parts, self.counts_host, self.event, self.enc, self.cnt, self.rerun, self.ready = \
+            parts, counts_host, event, enc, cnt, rerun, ready
 
 
 class Exchange:
     """All-gather of the decoded dmsg buffers of K launches per step, pipelined.
 
-    ``submit(parts, stream)`` is called after the step's kernels are enqueued on ``stream``
-    (``parts``: per launch (desc u8, rec u8, heap u8, n_msgs, cursor), cursor[0] = records, cursor[1]
-    = heap bytes, left on the device; the capacities are the buffers' sizes).  It first completes
-    the PREVIOUS step's exchange (the data all-gather: its counts arrived while this step's kernels
-    were running) and then enqueues this step's count + pack + count all-gather behind this step's
-    kernels.  It returns the event after which the PREVIOUS step's output buffers may be overwritten
-    (its pack has read them; None on the first call): with the nccl backend a step is packed once its
-    counts are on the host, straight into this rank's chunk of the receive buffer, and all-gathered in
-    place (no send buffer, no local copy), so double-buffer the outputs.  ``flush()`` completes the
-    last step and returns the same event for it.  ``gathered()`` gives the last completed step's results as
-    per launch (desc, rec, heap) byte tensors of the whole job in global message order.
+    ``submit(parts, stream, rerun)`` is called after the step's kernels are enqueued on ``stream``
+    (``parts``: :class:`Part` objects or (desc u8, rec u8, heap u8, n_msgs, cursor[, kind]) tuples;
+    cursor[0] = records, cursor[1] = heap bytes, left on the device; the capacities are the buffers'
+    sizes).  It first completes the PREVIOUS step's exchange (the data all-gather: its counts arrived
+    while this step's kernels were running) and then enqueues this step's count + count all-gather
+    behind this step's kernels.  It returns the event after which the PREVIOUS step's output buffers
+    may be overwritten (its pack has read them; None on the first call): with the nccl backend a step
+    is packed once its counts are on the host, straight into this rank's chunk of the receive buffer,
+    and all-gathered in place (no send buffer, no local copy), so double-buffer the outputs.
+    ``flush()`` completes the last step and returns the same event for it.  ``gathered()`` gives the
+    last completed step's results as per launch (desc, rec, heap) byte tensors of the whole job in
+    global message order.
 
-    A launch with overflowed messages (the counts' "bad" column) makes every rank raise in the
-    completing call: overflowed results are re-run, never exchanged."""
+    Overflowed messages (the counts' "bad" column, seen by every rank): each rank whose launch k has
+    some calls ``rerun(part)`` -> the Part with one more overlay holding their re-run results, then
+    every rank recounts; without a ``rerun`` the completing call raises.  ``engine``: the Engine whose
+    bank gives the nibble form's affixes (None: raw payloads)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, engine=None, defer: bool = False):
         self.group = group
+        # defer: a step's count AND pack run only in the NEXT submit, behind its ``after`` event (e.g.
+        # the end of the next step's first launch), so the exchange kernels share the GPU with the
+        # next step's later launches instead of its first one
+        self.defer = defer
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.engine = engine
         self.pending: Optional[_Pending] = None
         self.stream = None
         self._bufs = {}
-        self.last = None        # (recv, S, offs, nb, T) of the last completed exchange
+        self.last = None        # (recv, S, offs, nb, T, K, kinds) of the last completed exchange
         self.bytes_sent = []    # per completed step: the collective's bytes per rank (T)
         self.wire_bytes = []    # per completed step: this rank's wire bytes before padding
+        self.payload_bytes = []  # per completed step: this rank's payload bytes (before the nibble form)
+        self.heap_wire_bytes = []  # per completed step: this rank's payload bytes on the wire (nibble form)
+        self.reruns = 0         # launches re-run before exchanging
+
+    def _bank(self):
+        return None if self.engine is None else self.engine.handle
+
+    def _affix(self, kind):
+        if self.engine is None or kind == KIND_RAW:
+            return None
+        c = self.__dict__.setdefault("_affix_cache", {})
+        if kind not in c:
+            c[kind] = self.engine.bank.affixes(kind)
+        return c[kind]
 
     def _buf(self, name, n, dev, zero=False):
         b = self._bufs.get(name)
@@ -201,107 +342,145 @@ class Exchange:
         return b
 
     # -- device path ----------------------------------------------------------------------------------
-    @staticmethod
-    def _xparts(parts):
-        arr = (runtime.SdxXchgPart * len(parts))()
-        for k, (desc, rec, heap, n, cur, rcap, hcap) in enumerate(parts):
-            arr[k] = runtime.SdxXchgPart(desc.data_ptr(), rec.data_ptr(), heap.data_ptr(), cur.data_ptr(), n, rcap,
-                                         hcap, 0)
+    def _xparts(self, flat):
+        arr = (runtime.SdxXchgPart * len(flat))()
+        for k, (p, alt, aux) in enumerate(flat):
+            rcap, hcap = p.caps()
+            arr[k] = runtime.SdxXchgPart(p.desc.data_ptr(), p.rec.data_ptr(), p.heap.data_ptr(), p.cursor.data_ptr(),
+                                         p.n, rcap, hcap, p.kind if self.engine is not None else KIND_RAW, alt, aux, 0)
         return arr
 
-    def _work(self, parts, dev):
+    def _work(self, flat, dev):
+        """ONE zeroed workspace, grown to the largest layout (the bad counters sit at fixed places in
+        its head and the kernels leave them at zero, so any layout may reuse it)."""
         lib = runtime.load_library()
-        ns = (ctypes.c_uint32 * len(parts))(*[p[3] for p in parts])
-        wb = int(lib.sdx_exchange_work_bytes(ns, len(parts)))
-        # one zeroed workspace per launch layout: the kernels keep its counters at zero between uses
-        w = self._buf(("work",) + tuple(ns), wb + 256, dev, zero=True)
+        ns = (ctypes.c_uint32 * len(flat))(*[p.n for p, _, _ in flat])
+        wb = int(lib.sdx_exchange_work_bytes(ns, len(flat)))
+        w = self._buf("work", wb + 256, dev, zero=True)
         off = (-w.data_ptr()) % 256
         return w[off:], wb
 
-    def _count_device(self, parts, stream):
-        """sdx_exchange_count on `stream`: [K*4] int32 device counts (the pack follows once the host
-        has them: _complete, sdx_exchange_pack_into)."""
+    def _count_device(self, flat, stream):
+        """sdx_exchange_count on `stream`: [K * XCHG_COUNTS] int32 device counts (the pack follows once
+        the host has them: _complete, sdx_exchange_pack_into)."""
         lib = runtime.load_library()
-        dev = parts[0][0].device
-        work, wb = self._work(parts, dev)
-        cnt = torch.empty(4 * len(parts), dtype=torch.int32, device=dev)
-        runtime._check(lib, lib.sdx_exchange_count(self._xparts(parts), len(parts), ctypes.c_void_p(work.data_ptr()), wb,
+        dev = flat[0][0].desc.device
+        work, wb = self._work(flat, dev)
+        cnt = torch.empty(XCHG_COUNTS * len(flat), dtype=torch.int32, device=dev)
+        runtime._check(lib, lib.sdx_exchange_count(self._bank(), self._xparts(flat), len(flat),
+                                                   ctypes.c_void_p(work.data_ptr()), wb,
                                                    ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
         return cnt
 
-    def _count_pack_device(self, parts, stream):
-        """sdx_exchange_count + sdx_exchange_pack on `stream`: [K*4] int32 device counts; the wire
-        form of this rank is in the "send" buffer (layout: _layout)."""
+    def _count_pack_device(self, flat, stream):
+        """sdx_exchange_count + sdx_exchange_pack on `stream`: [K * XCHG_COUNTS] int32 device counts;
+        the wire form of this rank is in the "send" buffer (layout: _layout)."""
         lib = runtime.load_library()
-        dev = parts[0][0].device
-        work, wb = self._work(parts, dev)
-        xp = self._xparts(parts)
-        cnt = torch.empty(4 * len(parts), dtype=torch.int32, device=dev)
+        dev = flat[0][0].desc.device
+        work, wb = self._work(flat, dev)
+        xp = self._xparts(flat)
+        cnt = torch.empty(XCHG_COUNTS * len(flat), dtype=torch.int32, device=dev)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        runtime._check(lib, lib.sdx_exchange_count(xp, len(parts), ctypes.c_void_p(work.data_ptr()), wb,
+        runtime._check(lib, lib.sdx_exchange_count(self._bank(), xp, len(flat), ctypes.c_void_p(work.data_ptr()), wb,
                                                    ctypes.c_void_p(cnt.data_ptr()), sp))
-        cap = int(lib.sdx_exchange_send_bytes(xp, len(parts)))
+        cap = int(lib.sdx_exchange_send_bytes(xp, len(flat)))
         send = self._buf("send", cap, dev)
-        runtime._check(lib, lib.sdx_exchange_pack(xp, len(parts), ctypes.c_void_p(work.data_ptr()), wb,
+        runtime._check(lib, lib.sdx_exchange_pack(self._bank(), xp, len(flat), ctypes.c_void_p(work.data_ptr()), wb,
                                                   ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(send.data_ptr()),
                                                   send.numel(), sp))
         return cnt
 
     # -- host path (CPU tensors) ------------------------------------------------------------------------
-    @staticmethod
-    def _encode_host(parts):
+    def _encode_host(self, parts):
         out = []
-        for desc, rec, heap, n, cur, rcap, hcap in parts:
-            d = desc[: n * DESC_BYTES].numpy().view(DESC_DT)
-            r = rec[: rcap * REC_BYTES].numpy().view(RES_DT)
-            out.append(wire_encode(d, r, heap.numpy(), int(cur[0]), int(cur[1])))
+        for p in parts:
+            def arrs(q):
+                rcap, _ = q.caps()
+                return (q.desc[: q.n * DESC_BYTES].numpy().view(DESC_DT), q.rec[: rcap * REC_BYTES].numpy().view(RES_DT),
+                        q.heap.numpy(), int(q.cursor[0]), int(q.cursor[1]))
+            d, r, h, nr, nh = arrs(p)
+            enc = wire_encode(d, r, h, nr, nh, affix=self._affix(p.kind), overlays=[arrs(o) for o in p.overlays])
+            out.append(enc + (int(enc[1]["payload_len"].astype(np.int64).sum()),))
         return out
 
+    def _counts_host(self, enc):
+        """K primary launches' counts (messages, records, wire bytes, bad, payload bytes, 0, 0, 0)."""
+        return torch.tensor([[len(m), len(w), len(p), b, pb, 0, 0, 0] for m, w, p, b, pb in enc],
+                            dtype=torch.int32).reshape(-1)
+
     # -- protocol ----------------------------------------------------------------------------------------
-    def submit(self, parts, stream=None):
-        parts = [_part_tuple(p) for p in parts]
-        K = len(parts)
-        dev = parts[0][0].device
+    def submit(self, parts, stream=None, rerun: Optional[Callable[[Part], Part]] = None, after=None):
+        parts = [Part.of(p) for p in parts]
+        dev = parts[0].desc.device
         overlap = dev.type == "cuda" and dist.get_backend(self.group) == "nccl"
         if not overlap:   # synchronous form: gloo (CPU tensors, or CUDA tensors staged through the host)
             if dev.type == "cuda":
                 stream = stream or torch.cuda.current_stream(dev)
                 with torch.cuda.stream(stream):
-                    cnt = self._count_pack_device(parts, stream)
-                    allc = torch.empty(self.world * K * 4, dtype=torch.int32, device=dev)
+                    flat = _flatten(parts)
+                    cnt = self._count_pack_device(flat, stream)
+                    allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
                     _all_gather_flat(allc, cnt, self.group)
-                    self._complete(_Pending(parts, allc.cpu(), None))
+                    self._complete(_Pending(parts, allc.cpu(), None, rerun=rerun))
             else:
                 enc = self._encode_host(parts)
-                cnt = torch.tensor([[len(m), len(w), len(p), b] for m, w, p, b in enc], dtype=torch.int32).reshape(-1)
-                allc = torch.empty(self.world * K * 4, dtype=torch.int32)
+                cnt = self._counts_host(enc)
+                allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32)
                 _all_gather_flat(allc, cnt, self.group)
-                self._complete(_Pending(parts, allc, None, enc))
+                self._complete(_Pending(parts, allc, None, enc, rerun=rerun))
             return None
         if self.stream is None:
             self.stream = torch.cuda.Stream(dev)
         stream = stream or torch.cuda.current_stream(dev)
+        if self.defer:
+            return self._submit_deferred(parts, stream, rerun, after)
         # 1. the previous step: its counts are (about to be) on the host -- pack it into its chunk of
         #    the receive buffer and all-gather in place, ahead of anything that waits for this step
         prev, self.pending = self.pending, None
         released = None
         if prev is not None:
             with torch.cuda.stream(self.stream):
+                if after is not None:   # the previous step's pack behind this step's ``after`` event
+                    self.stream.wait_event(after)
                 released = self._complete(prev)
         # 2. this step: count + count all-gather + counts to the host, behind this step's kernels
         ready = torch.cuda.Event()
         ready.record(stream)
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ready)
-            cnt = self._count_device(parts, self.stream)
-            allc = torch.empty(self.world * K * 4, dtype=torch.int32, device=dev)
-            _all_gather_flat(allc, cnt, self.group)
-            host = torch.empty(allc.numel(), dtype=torch.int32, pin_memory=True)
-            host.copy_(allc, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        self.pending = _Pending(parts, host, ev, cnt=cnt)
+            host, ev, cnt = self._count_to_host(_flatten(parts), dev)
+        self.pending = _Pending(parts, host, ev, cnt=cnt, rerun=rerun)
         return released
+
+    def _submit_deferred(self, parts, stream, rerun, after):
+        """defer mode: behind ``after`` (default: now on ``stream``) the previous step is counted,
+        its counts gathered and brought to the host (this call waits for them), re-run if needed,
+        packed into its chunk and all-gathered; this step is only recorded."""
+        dev = parts[0].desc.device
+        released = None
+        prev, self.pending = self.pending, None
+        if prev is not None:
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(prev.ready)
+                if after is not None:
+                    self.stream.wait_event(after)
+                prev.counts_host, prev.event, prev.cnt = self._count_to_host(_flatten(prev.parts), dev)
+                released = self._complete(prev)
+        ready = torch.cuda.Event()
+        ready.record(stream)
+        self.pending = _Pending(parts, None, None, rerun=rerun, ready=ready)
+        return released
+
+    def _count_to_host(self, flat, dev):
+        """count + count all-gather + pinned D2H on the current stream: (host counts, event, device counts)."""
+        cnt = self._count_device(flat, torch.cuda.current_stream(dev))
+        allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
+        _all_gather_flat(allc, cnt, self.group)
+        host = torch.empty(allc.numel(), dtype=torch.int32, pin_memory=True)
+        host.copy_(allc, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        return host, ev, cnt
 
     def flush(self):
         """Completes the last submitted step; returns the event after which its output buffers may
@@ -310,7 +489,42 @@ class Exchange:
         if prev is None:
             return None
         with torch.cuda.stream(self.stream):
+            if prev.counts_host is None:    # defer mode: not counted yet
+                self.stream.wait_event(prev.ready)
+                prev.counts_host, prev.event, prev.cnt = self._count_to_host(_flatten(prev.parts), prev.parts[0].desc.device)
             return self._complete(prev)
+
+    def _rerun_bad(self, p: _Pending, S: np.ndarray, K: int) -> np.ndarray:
+        """Every rank: re-run the launches with overflowed messages on this rank (p.rerun), then
+        recount all launches (a collective every rank takes part in) -> the new counts."""
+        for attempt in range(4):
+            if not S[:, :K, 3].any():
+                return S
+            if p.rerun is None:
+                bad = {(r, k): int(S[r, k, 3]) for r in range(self.world) for k in range(K) if S[r, k, 3]}
+                raise RuntimeError(f"exchange: overflowed messages in (rank, launch) {bad} and no re-run given")
+            for k in range(K):
+                if S[self.rank, k, 3]:
+                    p.parts[k] = p.rerun(p.parts[k])
+                    self.reruns += 1
+            dev = p.parts[0].desc.device
+            if dev.type != "cuda":
+                p.enc = self._encode_host(p.parts)
+                cnt = self._counts_host(p.enc)
+                allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32)
+                _all_gather_flat(allc, cnt, self.group)
+                host = allc
+            elif p.cnt is None:        # gloo with device tensors: count + pack again
+                flat = _flatten(p.parts)
+                cnt = self._count_pack_device(flat, torch.cuda.current_stream(dev))
+                allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
+                _all_gather_flat(allc, cnt, self.group)
+                host = allc.cpu()
+            else:
+                host, ev, p.cnt = self._count_to_host(_flatten(p.parts), dev)
+                ev.synchronize()
+            S = host.numpy().astype(np.int64).reshape(self.world, -1, XCHG_COUNTS)
+        raise RuntimeError("exchange: overflow persists after 4 re-runs (pathological message)")
 
     def _complete(self, p: _Pending):
         """The data collective of a step whose counts are on (or on their way to) the host; device
@@ -320,19 +534,20 @@ class Exchange:
         K = len(p.parts)
         if p.event is not None:
             p.event.synchronize()            # the counts (the GPU has moved on to the next step)
-        S = p.counts_host.numpy().astype(np.int64).reshape(self.world, K, 4)
-        if S[..., 3].any():
-            bad = {(r, k): int(S[r, k, 3]) for r in range(self.world) for k in range(K) if S[r, k, 3]}
-            raise RuntimeError(f"exchange: overflowed messages in (rank, launch) {bad}; re-run them before exchanging")
+        S = p.counts_host.numpy().astype(np.int64).reshape(self.world, -1, XCHG_COUNTS)
+        S = self._rerun_bad(p, S, K)
+        flat = _flatten(p.parts) if p.enc is None else None
         offs, nb, T = _layout(S)
-        dev = p.parts[0][0].device
+        dev = p.parts[0].desc.device
         self.bytes_sent.append(T)
         self.wire_bytes.append(int(nb[self.rank].sum()))
+        self.payload_bytes.append(int(S[self.rank, :, 4].sum()))
+        self.heap_wire_bytes.append(int(S[self.rank, :, 2].sum()))
         released = None
         if dev.type != "cuda":               # host packing (gloo, CPU tensors)
             send = torch.zeros(T, dtype=torch.uint8)
             sv = send.numpy()
-            for k, (m, w, pay, _) in enumerate(p.enc):
+            for k, (m, w, pay, _, _) in enumerate(p.enc):
                 o = offs[self.rank, k]
                 sv[o[0]: o[0] + 4 * len(m)] = np.asarray(m, np.uint32).view(np.uint8)
                 sv[o[1]: o[1] + 8 * len(w)] = w.view(np.uint8)
@@ -342,77 +557,81 @@ class Exchange:
             lib = runtime.load_library()
             recv = self._buf("recv", self.world * T, dev)[: self.world * T]
             send = recv[self.rank * T: (self.rank + 1) * T]
-            work, wb = self._work(p.parts, dev)
+            work, wb = self._work(flat, dev)
             mine = np.ascontiguousarray(S[self.rank].reshape(-1).astype(np.uint32))
             runtime._check(lib, lib.sdx_exchange_pack_into(
-                self._xparts(p.parts), K, ctypes.c_void_p(work.data_ptr()), wb, ctypes.c_void_p(p.cnt.data_ptr()),
-                mine.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(send.data_ptr()), T,
-                ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+                self._bank(), self._xparts(flat), len(flat), ctypes.c_void_p(work.data_ptr()), wb,
+                ctypes.c_void_p(p.cnt.data_ptr()), mine.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(send.data_ptr()),
+                T, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
             released = torch.cuda.Event()
             released.record(torch.cuda.current_stream(dev))   # the launches' buffers have been read
         else:
             send = self._bufs["send"][:T]
             recv = self._buf("recv", self.world * T, dev)[: self.world * T]
         _all_gather_flat(recv, send, self.group)
-        self.last = (recv, S, offs, nb, T)
+        self.last = (recv, S, offs, nb, T, K, [q.kind for q in p.parts])
         return released
 
     def gathered(self) -> List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
         """Per launch (desc, rec, heap) byte tensors of the last completed exchange: the whole job in
         global message order (canonical form; sdx_exchange_unpack on the device)."""
-        recv, S, offs, nb, T = self.last
+        recv, S, offs, nb, T, K, kinds = self.last
         out = []
         if recv.device.type != "cuda":
             rv = recv.numpy()
-            for k in range(S.shape[1]):
+            for k in range(K):
                 ranks = []
                 for r in range(self.world):
                     o = r * T + offs[r, k]
                     ranks.append((rv[o[0]: o[0] + nb[r, k, 0]].view(np.uint32),
                                   rv[o[1]: o[1] + nb[r, k, 1]].view(WIRE_REC_DT), rv[o[2]: o[2] + nb[r, k, 2]]))
-                d, rc, h = wire_decode(ranks)
+                d, rc, h = wire_decode(ranks, self._affix(kinds[k]))
                 out.append(tuple(torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()) for a in (d, rc, h)))
             return out
         if self.stream is not None:
             torch.cuda.current_stream(recv.device).wait_stream(self.stream)
-        for k in range(S.shape[1]):
-            out.append(unpack_device(recv, S[:, k, :3], [r * T + offs[r, k] for r in range(self.world)]))
+        for k in range(K):
+            out.append(unpack_device(recv, S[:, k, :], [r * T + offs[r, k] for r in range(self.world)],
+                                     self.engine, kinds[k]))
         return out
 
 
-def unpack_device(recv: torch.Tensor, S: np.ndarray, offs) -> Tuple[torch.Tensor, ...]:
+def unpack_device(recv: torch.Tensor, S: np.ndarray, offs, engine=None, kind: int = KIND_RAW) -> Tuple[torch.Tensor, ...]:
     """sdx_exchange_unpack of one launch: the wire sections of every rank inside ``recv`` (per rank
-    r: offsets offs[r] of its msg / rec / heap sections, counts S[r] = (messages, records, bytes))
-    -> (desc, rec, heap) byte tensors of the whole job, on the current stream."""
+    r: offsets offs[r] of its msg / rec / heap sections, counts S[r] = (messages, records, wire bytes,
+    bad, payload bytes)) -> (desc, rec, heap) byte tensors of the whole job, on the current stream.
+    ``engine`` / ``kind``: the sender's bank and launch kind (the nibble form's affixes)."""
     lib = runtime.load_library()
     dev = recv.device
     world = len(offs)
+    S = np.asarray(S, np.int64)
     arr = (runtime.SdxXchgWire * world)()
     base = recv.data_ptr()
     for r in range(world):
         o = [int(x) for x in offs[r]]
         arr[r] = runtime.SdxXchgWire(base + o[0], base + o[1], base + o[2], int(S[r, 0]), int(S[r, 1]),
-                                     int(S[r, 2]), 0)
-    M, R, H = (int(S[:, j].sum()) for j in range(3))
+                                     int(S[r, 2]), int(S[r, 4]) if S.shape[1] > 4 else int(S[r, 2]))
+    M, R = int(S[:, 0].sum()), int(S[:, 1].sum())
+    H = int(S[:, 4].sum()) if S.shape[1] > 4 else int(S[:, 2].sum())
     desc = torch.empty(max(M, 1) * DESC_BYTES, dtype=torch.uint8, device=dev)
     rec = torch.empty(max(R, 1) * REC_BYTES, dtype=torch.uint8, device=dev)
     heap = torch.empty(_r16(max(H, 1)), dtype=torch.uint8, device=dev)
     wb = int(lib.sdx_exchange_unpack_work_bytes(M, R))
     work = torch.zeros(wb + 64, dtype=torch.uint8, device=dev)
-    runtime._check(lib, lib.sdx_exchange_unpack(arr, world, ctypes.c_void_p(work.data_ptr()), wb,
+    runtime._check(lib, lib.sdx_exchange_unpack(None if engine is None else engine.handle, kind, arr, world,
+                                                ctypes.c_void_p(work.data_ptr()), wb,
                                                 ctypes.c_void_p(desc.data_ptr()), ctypes.c_void_p(rec.data_ptr()),
-                                                ctypes.c_void_p(heap.data_ptr()),
+                                                ctypes.c_void_p(heap.data_ptr()), heap.numel(),
                                                 ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
     torch.cuda.current_stream(dev).synchronize()
     return desc[: M * DESC_BYTES], rec[: R * REC_BYTES], heap[:H]
 
 
-def allgather_streams(parts: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, int, torch.Tensor]],
-                      group=None) -> List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+def allgather_streams(parts: Sequence[Any], group=None, engine=None, rerun=None) -> List[Tuple[torch.Tensor, ...]]:
     """One exchange of several launches (e.g. MU, MS, MC), completed at once: per launch (desc,
     rec, heap) of the whole job in global message order (canonical form)."""
-    ex = Exchange(group)
-    ex.submit(parts)
+    ex = Exchange(group, engine)
+    ex.submit(parts, rerun=rerun)
     ex.flush()
     return ex.gathered()
 
@@ -422,3 +641,212 @@ def allgather_results(desc: torch.Tensor, rec: torch.Tensor, heap: torch.Tensor,
     """One launch's (desc[n_msgs], rec[n_rec], heap[n_heap]) of every rank (host-known counts)."""
     cur = torch.tensor([n_rec, n_heap, 0, 0], dtype=torch.int32, device=desc.device)
     return allgather_streams([(desc, rec, heap, n_msgs, cur)], group)[0]
+
+
+# ---- the product entry -------------------------------------------------------------------------------
+class _ShardMeta:
+    """meta.rssi / MS meta.clock of the whole job's messages for SDProtocols._decode_pulses (each rank
+    packed only its own shard): rssi = msg_data.get('R') (message_unsynced.py:287,
+    message_synced.py:238), the MS clock = abs(float(P[CP])) (message_synced.py:66-72) derived with the
+    packer's own conversions, only for the messages that have results."""
+
+    def __init__(self, messages, kind):
+        self.messages, self.kind = messages, kind
+        self.rssi = _Lazy(lambda i: messages[i].get("R"))
+        self.clock_abs = _Lazy(self._clock)
+
+    def _clock(self, i):
+        from . import packing
+        pk = packing.PulsePacker(self.kind)
+        try:
+            pk.add(self.messages[i])
+        except packing.GeneralPathMessage:
+            pk = packing.GeneralPacker(self.kind)
+            pk.add(self.messages[i])
+        return pk.clock_abs[0]
+
+
+class _Lazy:
+    __slots__ = ("f",)
+
+    def __init__(self, f):
+        self.f = f
+
+    def __getitem__(self, i):
+        return self.f(i)
+
+
+class ShardedDemodulator:
+    """BASELINE config 5 as a product entry: a batch is split into contiguous shards,
+    one per rank (one process per GPU); every rank demodulates its shard with the launches and the
+    GPU re-runs of ``Engine.run`` (overflowed messages re-run into overlays, never dropped), and one
+    all-gather of the decoded dmsg buffers (:class:`Exchange`, RCCL over xGMI with the ``nccl``
+    backend) gives every rank the whole job's results in global message order.  The reference runs
+    one process over one stream (signalduino/controller.py:252); this entry adds the sharding.
+
+    Batch level (synchronous): ``demodulate_batch(messages, msg_type)`` -- the
+    ``SDProtocols.demodulate_batch`` contract (one result list, or the exception instance, per
+    message) for the WHOLE batch on every rank, each rank demodulating only its shard.
+
+    Device level (pipelined; the bench's step):  ``part = launch(kind, bd, out)`` for this rank's
+    device batch, ``submit(parts, stream)`` per step (re-runs happen inside the exchange when any rank
+    reports overflowed messages), ``flush()``, ``gathered()``."""
+
+    def __init__(self, protocols=None, group=None, engine=None, defer: bool = False, nibble: bool = True):
+        from .sd_protocols import SDProtocols
+        self.protocols = protocols if protocols is not None else SDProtocols(mc_mode="fixed")
+        self.group = group
+        self.defer = defer      # Exchange(defer=...): count + pack behind the next step's ``after`` event
+        self.nibble = nibble    # the wire's nibble form (False: raw payloads)
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self._eng = engine
+        self._ex = None
+
+    @property
+    def eng(self):
+        return self._eng if self._eng is not None else self.protocols._ensure()
+
+    @property
+    def exchange(self) -> Exchange:
+        want = self.eng if self.nibble else None
+        if self._ex is None or self._ex.engine is not want:
+            self._ex = Exchange(self.group, want, defer=self.defer)
+        return self._ex
+
+    def shard(self, n: int) -> Tuple[int, int]:
+        return shard_bounds(n, self.rank, self.world)
+
+    # -- device level -------------------------------------------------------------------------------------
+    def launch(self, kind: int, bd, out=None, mn_elig: int = 0, mn_method: int = -1, grouped_sel=None,
+               mrec=None) -> Part:
+        """The first pass over this rank's device batch (Engine.launch_routed; ``grouped_sel``: a
+        grouping computed ahead, as the bench does) into ``out`` (default: Engine.first_pass's
+        capacities); no host synchronisation."""
+        eng = self.eng
+        if out is None:
+            out = eng.first_pass(kind, bd, mn_elig=mn_elig, mn_method=mn_method)
+        elif grouped_sel is not None:
+            eng.launch_pulses(kind, bd, out, sel=grouped_sel, group=False, mrec=mrec)
+        else:
+            eng.launch_routed(kind, bd, out, mn_elig=mn_elig, mn_method=mn_method)
+        return Part.from_out(out, kind, src=(kind, bd, mn_elig, mn_method))
+
+    def rerun(self, part: Part) -> Part:
+        """The exchange's re-run callback: this rank's overflowed messages of ``part`` (resolved over
+        its overlays) re-run on the GPU into one more overlay (Engine.rerun_overlay: the long MU/MS
+        variant, the general MC kernel for long frames, grown capacities)."""
+        if part.src is None:
+            raise RuntimeError("exchange: a launch with overflowed messages and no source batch to re-run")
+        kind, bd, mn_elig, mn_method = part.src
+        dev = part.desc.device
+        torch.cuda.current_stream(dev).synchronize()
+        levels = [part] + part.overlays
+        _, rd = resolve_host([(q.desc[: q.n * DESC_BYTES].cpu().numpy().view(DESC_DT),) for q in levels])
+        redo = np.nonzero(np.isin(rd["status"], OVF))[0].astype(np.int32)
+        if not len(redo):
+            return part
+        lvl = len(part.overlays)
+        rcap = max(4096, 256 * len(redo)) << lvl
+        hcap = max(1 << 20, 16384 * len(redo)) << lvl
+        out2 = self.eng.rerun_overlay(kind, bd, redo, rcap, hcap, mn_elig=mn_elig, mn_method=mn_method)
+        part.overlays.append(Part.from_out(out2, kind))
+        return part
+
+    def submit(self, parts: Sequence[Part], stream=None, after=None):
+        return self.exchange.submit(parts, stream, rerun=self.rerun, after=after)
+
+    def flush(self):
+        return self.exchange.flush()
+
+    def gathered(self):
+        return self.exchange.gathered()
+
+    def run_device(self, launches: Sequence[Tuple[int, Any]]) -> List[Tuple[np.ndarray, np.ndarray, np.ndarray]]:
+        """[(kind, this rank's device batch)] -> per launch the whole job's host (desc, rec, heap) in
+        canonical form (synchronous: launch, exchange with re-runs, unpack)."""
+        parts = [self.launch(k, bd) for k, bd in launches]
+        return self._exchange_host(parts)
+
+    def _exchange_host(self, parts):
+        ex = self.exchange
+        ex.submit(parts, rerun=self.rerun)
+        ex.flush()
+        out = []
+        for d, r, h in ex.gathered():
+            out.append((d.cpu().numpy().view(DESC_DT).copy(), r.cpu().numpy().view(RES_DT).copy(),
+                        h.cpu().numpy().copy()))
+        return out
+
+    def _host_overlay(self, n: int, rows, kind: int) -> Part:
+        """An overlay that marks ``rows`` as RAISED by the host packing (raise_kind RAISE_HOST): the
+        receiving ranks re-derive the exception from the message itself."""
+        eng = self.eng
+        d = np.zeros(max(n, 1), DESC_DT)
+        d["status"] = ST_ABSENT
+        rows = np.asarray(sorted(rows), np.int64)
+        d["status"][rows] = runtime.ST_RAISED
+        d["raise_kind"][rows] = RAISE_HOST
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(eng.dev)  # noqa: E731
+        return Part(t(d), torch.zeros(REC_BYTES, dtype=torch.uint8, device=eng.dev),
+                    torch.zeros(16, dtype=torch.uint8, device=eng.dev), n,
+                    torch.zeros(4, dtype=torch.int32, device=eng.dev), kind)
+
+    # -- batch level ----------------------------------------------------------------------------------------
+    def demodulate_batch(self, messages: Sequence[Dict[str, Any]], msg_type: str, raise_errors: bool = False):
+        """SDProtocols.demodulate_batch over the whole batch on every rank, each rank demodulating its
+        contiguous shard (MU, MS; MC in the 'fixed' chain -- the 'strict' chain reaches no device
+        launch and runs unsharded)."""
+        P = self.protocols
+        messages = list(messages)
+        if msg_type == "MC":
+            if P.mc_mode == "strict":
+                return P.demodulate_batch(messages, "MC", raise_errors=raise_errors)
+            return self._demodulate_mc(messages, raise_errors)
+        if msg_type not in ("MU", "MS"):
+            return P.demodulate_batch(messages, msg_type, raise_errors=raise_errors)
+        from . import packing
+        eng = self.eng
+        kind = runtime.KIND_MU if msg_type == "MU" else runtime.KIND_MS
+        lo, hi = self.shard(len(messages))
+        mine = messages[lo:hi]
+        packer, gen, gen_rows, pack_err = P._pack_pulses(mine, msg_type, raise_errors=False)
+        bd = eng.to_device_pulses(packer.batch())
+        part = self.launch(kind, bd)
+        if gen_rows:   # the general path's results as an overlay indexed like the launch
+            genall = packing.GeneralPacker(msg_type)
+            gset = set(gen_rows)
+            for i, m in enumerate(mine):
+                genall.add(m if i in gset else {"data": ""})
+            ov = eng.general_overlay(kind, eng.to_device_general(genall.arrays()), np.asarray(gen_rows, np.int32))
+            part.overlays.append(Part.from_out(ov, kind))
+        if pack_err:
+            part.overlays.append(self._host_overlay(len(mine), pack_err.keys(), kind))
+        desc, rec, heap = self._exchange_host([part])[0]
+        errs = self._host_errors(messages, desc, lambda m: P._pack_error(m, msg_type))
+        return P._decode_pulses(msg_type, desc, rec, heap, _ShardMeta(messages, msg_type), errs, raise_errors)
+
+    @staticmethod
+    def _host_errors(messages, desc, derive):
+        rows = np.nonzero((desc["status"] == runtime.ST_RAISED) & (desc["raise_kind"] == RAISE_HOST))[0]
+        return {int(i): derive(messages[int(i)]) for i in rows}
+
+    def _demodulate_mc(self, messages, raise_errors):
+        P = self.protocols
+        eng = self.eng
+        lo, hi = self.shard(len(messages))
+        frames, slot_err, only = P._mc_frames(messages[lo:hi], "MC", None, raise_errors=False)
+        bd = eng.to_device_mc(packing_mc(frames))
+        if any(only):
+            bd["only"] = P._mc_only(only, eng)
+        part = self.launch(runtime.KIND_MC, bd)
+        if slot_err:
+            part.overlays.append(self._host_overlay(hi - lo, slot_err.keys(), runtime.KIND_MC))
+        desc, rec, heap = self._exchange_host([part])[0]
+        errs = self._host_errors(messages, desc, lambda m: P._mc_frame_error(m, "MC"))
+        return P._decode_mc(desc, rec, heap, errs, raise_errors)
+
+
+def packing_mc(frames):
+    from . import packing
+    return packing.mc_batch_from_frames(frames)

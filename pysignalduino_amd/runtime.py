@@ -19,6 +19,7 @@ from . import bank as bankmod
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libsdx.so")
+ABI_VERSION = 11   # include/sdx.h SDX_ABI_VERSION
 
 KIND_MU, KIND_MS, KIND_MC = 0, 1, 2
 KIND_MN = 3        # host-side tag for Engine.run (sdx_demod_mn)
@@ -38,7 +39,7 @@ MREC_BYTES = 128
 RES_DT = np.dtype([("payload_off", "<u4"), ("payload_len", "<u2"), ("proto", "<u2"), ("bit_length", "<u4"),
                    ("msg", "<u4")])
 
-EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
+EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_source_hash", "sdx_layout_size", "sdx_bank_create", "sdx_bank_destroy",
             "sdx_bank_device_ptr", "sdx_demod_pulses", "sdx_demod_pulses_long", "sdx_demod_mc", "sdx_demod_mn",
             "sdx_parse_lines", "sdx_select_lines", "sdx_serialize_json", "sdx_units",
             "sdx_exchange_work_bytes", "sdx_exchange_send_bytes", "sdx_exchange_count", "sdx_exchange_pack", "sdx_exchange_pack_into", "sdx_exchange_unpack_work_bytes",
@@ -96,17 +97,24 @@ class SdxUnitBatch(Structure):
 
 class SdxXchgPart(Structure):
     _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("cursor_dev", c_void_p),
-                ("n_msgs", c_uint32), ("rec_cap", c_uint32), ("heap_cap", c_uint32), ("res", c_uint32)]
+                ("n_msgs", c_uint32), ("rec_cap", c_uint32), ("heap_cap", c_uint32), ("kind", ctypes.c_uint8),
+                ("alt", ctypes.c_uint8), ("aux", ctypes.c_uint8), ("res", ctypes.c_uint8)]
 
 
 class SdxXchgWire(Structure):
     _fields_ = [("msg_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("n_msgs", c_uint32),
-                ("n_rec", c_uint32), ("n_heap", c_uint32), ("res", c_uint32)]
+                ("n_rec", c_uint32), ("n_heap", c_uint32), ("n_payload", c_uint32)]
 
 
-# the exchange's wire form (include/sdx.h): one word per message, 8 bytes per record, packed payloads
+# the exchange's wire form (include/sdx.h, v3): one word per message, 8 bytes per record, payloads raw or
+# as packed hex digits (proto bit 15 = WIRE_NIB: preamble + digits + postamble of the protocol)
 WIRE_REC_DT = np.dtype([("proto", "<u2"), ("payload_len", "<u2"), ("bit_length", "<u4")])
+WIRE_NIB = 0x8000
 XCHG_MAX_RANKS = 32
+XCHG_MAX_PARTS = 16
+XCHG_COUNTS = 8     # u32 counts per part: messages, records, wire payload bytes, bad, payload bytes, 0, 0, 0
+ST_ABSENT = 0xFF    # an exchange overlay's descriptor no re-run wrote
+KIND_RAW = 0xFF     # sdx_xchg_part.kind: no affixes (raw payloads only)
 
 
 class SdxOut(Structure):
@@ -148,6 +156,7 @@ def load_library(path: Optional[str] = None):
     lib = ctypes.CDLL(p)
     lib.sdx_abi_version.restype = c_int
     lib.sdx_last_error.restype = c_char_p
+    lib.sdx_source_hash.restype = c_char_p
     lib.sdx_layout_size.argtypes = [c_int]
     lib.sdx_layout_size.restype = c_int
     lib.sdx_bank_create.argtypes = [c_void_p, c_size_t, c_int, POINTER(c_void_p)]
@@ -194,20 +203,21 @@ def load_library(path: Optional[str] = None):
     lib.sdx_exchange_work_bytes.restype = ctypes.c_uint64
     lib.sdx_exchange_send_bytes.argtypes = [POINTER(SdxXchgPart), c_int]
     lib.sdx_exchange_send_bytes.restype = ctypes.c_uint64
-    lib.sdx_exchange_count.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p]
+    lib.sdx_exchange_count.argtypes = [c_void_p, POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p,
+                                       c_void_p]
     lib.sdx_exchange_count.restype = c_int
-    lib.sdx_exchange_pack.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
-                                      ctypes.c_uint64, c_void_p]
+    lib.sdx_exchange_pack.argtypes = [c_void_p, POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p,
+                                      c_void_p, ctypes.c_uint64, c_void_p]
     lib.sdx_exchange_pack.restype = c_int
-    lib.sdx_exchange_pack_into.argtypes = [POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
-                                           c_void_p, ctypes.c_uint64, c_void_p]
+    lib.sdx_exchange_pack_into.argtypes = [c_void_p, POINTER(SdxXchgPart), c_int, c_void_p, ctypes.c_uint64, c_void_p,
+                                           c_void_p, c_void_p, ctypes.c_uint64, c_void_p]
     lib.sdx_exchange_pack_into.restype = c_int
     lib.sdx_exchange_unpack_work_bytes.argtypes = [c_uint32, c_uint32]
     lib.sdx_exchange_unpack_work_bytes.restype = ctypes.c_uint64
-    lib.sdx_exchange_unpack.argtypes = [POINTER(SdxXchgWire), c_int, c_void_p, ctypes.c_uint64, c_void_p, c_void_p,
-                                        c_void_p, c_void_p]
+    lib.sdx_exchange_unpack.argtypes = [c_void_p, c_int, POINTER(SdxXchgWire), c_int, c_void_p, ctypes.c_uint64,
+                                        c_void_p, c_void_p, c_void_p, ctypes.c_uint64, c_void_p]
     lib.sdx_exchange_unpack.restype = c_int
-    if lib.sdx_abi_version() != 10:
+    if lib.sdx_abi_version() != ABI_VERSION:
         raise RuntimeError("libsdx ABI version mismatch")
     check_layout(lib)
     if path is None:
@@ -442,6 +452,39 @@ class Engine:
             rec_cap, heap_cap = 4 * rec_cap, 4 * heap_cap   # whole-batch re-run with grown outputs
         raise RuntimeError("general path: result capacity overflow persists")
 
+    def general_overlay(self, kind: int, gd, rows: np.ndarray, work_stride: int = 0):
+        """The general path over the messages ``rows`` of a general batch ``gd`` that holds every
+        message of a launch (placeholders elsewhere), into an exchange overlay indexed like that
+        launch (descriptors of the other messages stay ST_ABSENT).  Capacity overflows re-run the
+        launch with grown outputs until none is left (host checks; the general path is rare)."""
+        rows = np.asarray(rows, np.int32)
+        n = gd["n"]
+        lens = np.asarray(gd["lengths"])[rows]
+        rec_cap = 16 * len(rows) + 1024
+        heap_cap = int(2 * int(lens.sum()) + 256 * len(rows) + 65536)
+        max_len = int(lens.max(initial=0))
+        wb = int(self.lib.sdx_general_work_bytes(self.handle, kind, int(gd["total"]), n, max_len, int(work_stride)))
+        work = self.torch.empty(max(wb, 1), dtype=self.torch.uint8, device=self.dev)
+        # the longest messages first: the device's work queue then ends on short ones
+        order = rows[np.argsort(-lens, kind="stable")].astype(np.int32)
+        sel = self.torch.from_numpy(order).to(self.dev)
+        for attempt in range(6):
+            out = self.overlay_out(n, rec_cap, heap_cap)
+            o = self._out_struct(out)
+            o.work_dev, o.work_cap = _ptr(work), int(work.numel())
+            b = SdxGeneralBatch(_ptr(gd["data"]), _ptr(gd["offsets"]), _ptr(gd["npat"]), _ptr(gd["pat_ids"]),
+                                _ptr(gd["pat_val"]), _ptr(gd["cp_slot"]), _ptr(gd["ms_ok"]), _ptr(sel), n,
+                                len(order), _ptr(gd.get("len")), int(work_stride), max_len, 0)
+            _check(self.lib, self.lib.sdx_demod_pulses_general(self.handle, kind, ctypes.byref(b), ctypes.byref(o),
+                                                               self.stream_ptr()))
+            self.torch.cuda.current_stream(self.dev).synchronize()
+            st = out["desc"][: n * DESC_DT.itemsize].view(-1, DESC_DT.itemsize)[:, 6].cpu().numpy()[rows]
+            if not (st == ST_OVF_OUT).any():
+                out["_keep"] = (work, sel)
+                return out
+            rec_cap, heap_cap = 4 * rec_cap, 4 * heap_cap
+        raise RuntimeError("general path: result capacity overflow persists")
+
     def to_device_mn(self, hexes) -> Dict[str, "object"]:
         """MN frames (hex strings / bytes) -> device batch.  Contract: [0-9A-Fa-f]* and at most
         MN_HEX_MAX characters (checked here; ContractError-free callers check before)."""
@@ -480,7 +523,8 @@ class Engine:
     # -- full run with contract routing and overflow re-runs (all on the GPU) --------------------
     def run(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None,
             sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1, workspace: bool = True):
-        """Demodulate a device batch; returns host numpy (desc, rec, heap).
+        """Demodulate a device batch; returns host numpy (desc, rec, heap).  The first pass
+        (first_pass) then GPU re-runs of overflowed messages (rerun_overlay) merged on the host.
 
         ``workspace``: MU/MS launches run in the grouped message order with spill regions for
         result-heavy tiles (sdx_group_pulses, sdx_demod_pulses); False runs the messages in batch
@@ -490,7 +534,37 @@ class Engine:
         long variant (MC: ``sel_short`` only), as sdx_select_lines builds them; the other
         messages keep an empty OK descriptor.  Without them every message runs, routed by length.
         """
-        t = self.torch
+        out = self.first_pass(kind, bd, rec_cap, heap_cap, sel_short, sel_long, mn_elig, mn_method, workspace)
+        rec_cap, heap_cap = out["rec_cap"], out["heap_cap"]
+        desc, rec, heap = self.fetch(out)
+        # re-runs on the GPU: grown output buffers / the long variant's larger per-message staging
+        for attempt in range(4):
+            st = desc["status"]
+            redo = np.nonzero((st == ST_OVF_OUT) | (st == ST_OVF_TILE))[0].astype(np.int32)
+            if not len(redo):
+                break
+            if attempt == 3:
+                raise RuntimeError("result staging overflow persists (pathological message)")
+            rec_cap, heap_cap = 2 * rec_cap + 64 * len(redo), 2 * heap_cap + 8192 * len(redo)
+            out2 = self.rerun_overlay(kind, bd, redo, rec_cap, heap_cap, mn_elig=mn_elig, mn_method=mn_method)
+            d2, r2, h2 = self.fetch(out2)
+            # merge: re-based records appended after the first pass
+            base_r, base_h = len(rec), len(heap)
+            r2 = r2.copy()
+            r2["payload_off"] += base_h
+            rec = np.concatenate([rec, r2])
+            heap = np.concatenate([heap, h2])
+            for i in redo:
+                d = d2[i].copy()
+                d["rec_begin"] += base_r
+                desc[i] = d
+        return desc, rec, heap
+
+    def first_pass(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None,
+                   sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1, workspace: bool = True):
+        """Output buffers sized for a device batch (default capacities: 8 records and 200 payload
+        bytes per message) and the first pass's launches into them (launch_routed), enqueued on the
+        current stream; returns the output dict (run() re-runs what overflowed)."""
         n = bd["n"]
         selected = sel_short is not None or sel_long is not None
         if selected:
@@ -513,15 +587,27 @@ class Engine:
             heap_cap = max(heap_cap, int(4 * int(np.sum(bd["lengths"])) + 160 * n_work + 65536))
         out = self.alloc_out(n, rec_cap, heap_cap,
                              self.pulses_work_bytes(n_work) if workspace and kind in (KIND_MU, KIND_MS) else 0)
+        self.launch_routed(kind, bd, out, sel_short=sel_short, sel_long=sel_long, mn_elig=mn_elig, mn_method=mn_method,
+                           workspace=workspace)
+        return out
+
+    def launch_routed(self, kind: int, bd, out, sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1,
+                      workspace: bool = True) -> None:
+        """The first pass of run(): every message (or the given selection lists) to the launch that
+        takes it -- MU/MS: the short variant (grouped order, spill regions) for <= SHORT_MAX pulses,
+        the long one above; MC: k_mc, frames of more than MC_HEX_MAX characters on the general MC
+        kernel; MN: k_mn.  Enqueued on the current stream, no host synchronisation."""
+        t = self.torch
         if kind == KIND_MN:
             self.launch_mn(bd, out, elig=mn_elig, method=mn_method, sel=sel_short)
-        elif selected:
+        elif sel_short is not None or sel_long is not None:
             if sel_short is not None and sel_short.numel():
                 (self.launch_mc(bd, out, sel=sel_short) if kind == KIND_MC else
                  self.launch_pulses(kind, bd, out, sel=sel_short, group=workspace))
             if sel_long is not None and sel_long.numel():
                 self.launch_pulses(kind, bd, out, sel=sel_long, long_variant=True)
         elif kind == KIND_MC:
+            lengths = bd["lengths"]
             longf = lengths > MC_HEX_MAX
             if not longf.any():
                 self.launch_mc(bd, out)
@@ -531,6 +617,7 @@ class Engine:
                 self.launch_mc_general(bd, out, t.from_numpy(np.nonzero(longf)[0].astype(np.int32)).to(self.dev),
                                        int(lengths.max()))
         else:
+            lengths = bd["lengths"]
             short = lengths <= SHORT_MAX
             if short.all():
                 self.launch_pulses(kind, bd, out, group=workspace)
@@ -540,45 +627,40 @@ class Engine:
                                        group=workspace)
                 self.launch_pulses(kind, bd, out, sel=t.from_numpy(np.nonzero(~short)[0].astype(np.int32)).to(self.dev),
                                    long_variant=True)
-        desc, rec, heap = self.fetch(out)
-        # re-runs on the GPU: grown output buffers / the long variant's larger per-message staging
-        for attempt in range(4):
-            st = desc["status"]
-            redo_out = np.nonzero(st == ST_OVF_OUT)[0]
-            redo_tile = np.nonzero(st == ST_OVF_TILE)[0]
-            if not len(redo_out) and not len(redo_tile):
-                break
-            if attempt == 3:
-                raise RuntimeError("result staging overflow persists (pathological message)")
-            redo = np.concatenate([redo_out, redo_tile]).astype(np.int32)
-            out2 = self.alloc_out(n, 2 * rec_cap + 64 * len(redo), 2 * heap_cap + 8192 * len(redo))
-            sel = t.from_numpy(redo).to(self.dev)
-            if kind == KIND_MN:
-                self.launch_mn(bd, out2, elig=mn_elig, method=mn_method, sel=sel)
-            elif kind == KIND_MC:   # k_mc hands frames of > MC_HEX_MAX characters over as ST_OVF_TILE
-                if "lengths" in bd:
-                    rl = np.asarray(bd["lengths"])[redo]
-                else:                # a line batch: the frames' lengths are on the device
-                    rl = bd["len"][t.from_numpy(redo.astype(np.int64)).to(self.dev)].cpu().numpy()
-                lr = rl > MC_HEX_MAX
-                if (~lr).any():
-                    self.launch_mc(bd, out2, sel=t.from_numpy(redo[~lr]).to(self.dev))
-                if lr.any():
-                    self.launch_mc_general(bd, out2, t.from_numpy(redo[lr]).to(self.dev), int(rl.max()))
-            else:
-                self.launch_pulses(kind, bd, out2, sel=sel, long_variant=True)
-            d2, r2, h2 = self.fetch(out2)
-            # merge: re-based records appended after the first pass
-            base_r, base_h = len(rec), len(heap)
-            r2 = r2.copy()
-            r2["payload_off"] += base_h
-            rec = np.concatenate([rec, r2])
-            heap = np.concatenate([heap, h2])
-            for i in redo:
-                d = d2[i].copy()
-                d["rec_begin"] += base_r
-                desc[i] = d
-        return desc, rec, heap
+
+    def overlay_out(self, n: int, rec_cap: int, heap_cap: int):
+        """Output buffers of an exchange overlay (include/sdx.h ABI 11): every descriptor at
+        ST_ABSENT until a launch writes it."""
+        o = self.alloc_out(n, rec_cap, heap_cap)
+        o["desc"].fill_(ST_ABSENT)
+        return o
+
+    def rerun_overlay(self, kind: int, bd, redo: np.ndarray, rec_cap: int, heap_cap: int, mn_elig: int = 0,
+                      mn_method: int = -1):
+        """Re-run the messages ``redo`` (host int array of batch indices whose first pass overflowed)
+        into a fresh overlay: MU/MS on the long variant (larger per-message staging), MC on k_mc or,
+        for frames of more than MC_HEX_MAX characters (k_mc hands them over as ST_OVF_TILE), on
+        sdx_demod_mc_general, MN on k_mn; grown output capacities.  Enqueued on the current stream."""
+        t = self.torch
+        redo = np.asarray(redo, np.int32)
+        out2 = self.overlay_out(bd["n"], rec_cap, heap_cap)
+        sel = t.from_numpy(redo).to(self.dev)
+        if kind == KIND_MN:
+            self.launch_mn(bd, out2, elig=mn_elig, method=mn_method, sel=sel)
+        elif kind == KIND_MC:
+            if "lengths" in bd:
+                rl = np.asarray(bd["lengths"])[redo]
+            else:                # a line batch: the frames' lengths are on the device
+                rl = bd["len"][t.from_numpy(redo.astype(np.int64)).to(self.dev)].cpu().numpy()
+            lr = rl > MC_HEX_MAX
+            if (~lr).any():
+                self.launch_mc(bd, out2, sel=t.from_numpy(redo[~lr]).to(self.dev))
+            if lr.any():
+                self.launch_mc_general(bd, out2, t.from_numpy(redo[lr]).to(self.dev), int(rl.max()))
+        else:
+            self.launch_pulses(kind, bd, out2, sel=sel, long_variant=True)
+        out2["_sel"] = sel          # alive until the launches have run
+        return out2
 
     def fetch(self, out):
         self.torch.cuda.current_stream(self.dev).synchronize()

@@ -318,6 +318,23 @@ class SDProtocols(UnitsMixin):
                 if self.mc_mode == "strict" else self.demodulate_mc_batch(messages, raise_errors=raise_errors)
         if msg_type not in ("MU", "MS"):
             return [self.demodulate(m, msg_type) for m in messages]
+        packer, gen, gen_rows, pack_err = self._pack_pulses(messages, msg_type, raise_errors)
+        pb = packer.batch()
+        eng = self._ensure()
+        kind = runtime.KIND_MU if msg_type == "MU" else runtime.KIND_MS
+        desc, rec, heap = eng.run(kind, eng.to_device_pulses(pb))
+        out = self._decode_pulses(msg_type, desc, rec, heap, packer, pack_err, raise_errors)
+        if gen_rows:
+            gd, gr, gh = eng.run_general(kind, eng.to_device_general(gen.arrays()))
+            res = self._decode_pulses(msg_type, gd, gr, gh, gen, {}, raise_errors)
+            for j, i in enumerate(gen_rows):
+                out[i] = res[j]
+        return out
+
+    @staticmethod
+    def _pack_pulses(messages, msg_type, raise_errors=False):
+        """messages -> (PulsePacker with one entry per message, GeneralPacker of the general-path
+        messages, their rows, {row: exception} of the messages whose host conversion raised)."""
         packer = packing.PulsePacker(msg_type)
         gen = packing.GeneralPacker(msg_type)   # multi-digit pattern ids / more than LONG_MAX pulses
         gen_rows: List[int] = []
@@ -338,17 +355,13 @@ class SDProtocols(UnitsMixin):
                     raise
                 pack_err[i] = e
                 packer.add({"data": ""})
-        pb = packer.batch()
-        eng = self._ensure()
-        kind = runtime.KIND_MU if msg_type == "MU" else runtime.KIND_MS
-        desc, rec, heap = eng.run(kind, eng.to_device_pulses(pb))
-        out = self._decode_pulses(msg_type, desc, rec, heap, packer, pack_err, raise_errors)
-        if gen_rows:
-            gd, gr, gh = eng.run_general(kind, eng.to_device_general(gen.arrays()))
-            res = self._decode_pulses(msg_type, gd, gr, gh, gen, {}, raise_errors)
-            for j, i in enumerate(gen_rows):
-                out[i] = res[j]
-        return out
+        return packer, gen, gen_rows, pack_err
+
+    @classmethod
+    def _pack_error(cls, msg, msg_type) -> BaseException:
+        """The exception the host conversion of one message raises (the same steps as _pack_pulses)."""
+        err = cls._pack_pulses([msg], msg_type)[3]
+        return err.get(0, RuntimeError("host packing of this message raised on another rank only"))
 
     @staticmethod
     def _catch(fn, m, t, raise_errors):
@@ -433,6 +446,21 @@ class SDProtocols(UnitsMixin):
                             version: Optional[str] = None, raise_errors: bool = False):
         """'fixed' MC chain on the GPU; accepts MCParser dicts (raw_hex/clock/mcbitnum/messagetype)
         or demodulate_mc dicts (data/clock/bit_length)."""
+        frames, slot_err, only = self._mc_frames(messages, msg_type, version, raise_errors)
+        mb = packing.mc_batch_from_frames(frames)
+        eng = self._ensure()
+        bd = eng.to_device_mc(mb)
+        # demodulate_mc(msg_data) with a protocol_id evaluates that protocol only (sd_protocols.py:
+        # 79-99): a raise of another id must not surface for it, so the device skips the others
+        if any(only):
+            bd["only"] = self._mc_only(only, eng)
+        desc, rec, heap = eng.run(runtime.KIND_MC, bd)
+        return self._decode_mc(desc, rec, heap, slot_err, raise_errors)
+
+    @staticmethod
+    def _mc_frames(messages, msg_type="MC", version=None, raise_errors=False):
+        """MC dicts -> (frames (raw_hex, clock, mcbitnum, messagetype, version), {row: exception},
+        per message its protocol_id or None)."""
         frames, slot_err = [], {}
         for i, m in enumerate(messages):
             try:
@@ -448,18 +476,20 @@ class SDProtocols(UnitsMixin):
                     raise
                 slot_err[i] = e
                 frames.append(("", 0, 0, "MC", None))
-        mb = packing.mc_batch_from_frames(frames)
-        eng = self._ensure()
+        return frames, slot_err, [m.get("protocol_id") for m in messages]
+
+    @classmethod
+    def _mc_frame_error(cls, msg, msg_type="MC") -> BaseException:
+        err = cls._mc_frames([msg], msg_type)[1]
+        return err.get(0, RuntimeError("host conversion of this MC frame raised on another rank only"))
+
+    def _mc_only(self, only, eng):
+        idx = {str(p): i for i, p in enumerate(self._bank.mc_pids)}
+        sel_only = np.array([-1 if not o else idx.get(str(o), len(self._bank.mc_pids)) for o in only], np.int16)
+        return eng.torch.from_numpy(sel_only).to(eng.dev)
+
+    def _decode_mc(self, desc, rec, heap, slot_err, raise_errors):
         bk = self._bank
-        bd = eng.to_device_mc(mb)
-        # demodulate_mc(msg_data) with a protocol_id evaluates that protocol only (sd_protocols.py:
-        # 79-99): a raise of another id must not surface for it, so the device skips the others
-        only = [m.get("protocol_id") for m in messages]
-        if any(only):
-            idx = {str(p): i for i, p in enumerate(bk.mc_pids)}
-            sel_only = np.array([-1 if not o else idx.get(str(o), len(bk.mc_pids)) for o in only], np.int16)
-            bd["only"] = eng.torch.from_numpy(sel_only).to(eng.dev)
-        desc, rec, heap = eng.run(runtime.KIND_MC, bd)
         hs = heap.tobytes().decode("latin-1")
         d_st, d_rk, d_rb, d_nr = (desc["status"].tolist(), desc["raise_kind"].tolist(), desc["rec_begin"].tolist(),
                                   desc["n_rec"].tolist())

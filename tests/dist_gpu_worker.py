@@ -1,10 +1,21 @@
-"""Rank process of tests/test_dist.py::test_world2_real_kernels_match_unsharded (GPU box only).
+"""Rank process of tests/test_dist.py's world-2 GPU tests (GPU box only).
 
-World size 2 over gloo with both ranks on cuda:0 (the one-GPU rehearsal of config 5): each rank
-demodulates its contiguous shard of one global MU + MS + MC batch with the product launches
-(grouped order + spill regions for MU/MS), runs two pipelined Exchange steps (double-buffered
-outputs), and checks the gathered (desc, rec, heap) of every launch against an un-sharded device
-run of the whole batch in canonical form, byte for byte.  Prints "OK" on success.
+World size 2 over gloo with both ranks on cuda:0 (the one-GPU rehearsal of config 5).  Modes
+(SDX_WORKER_MODE):
+  pipelined  each rank demodulates its contiguous shard of one global MU + MS + MC batch with the
+             product launches (ShardedDemodulator.launch: grouped order + spill regions for MU/MS),
+             runs two pipelined exchange steps (double-buffered outputs, nibble wire form) and checks
+             the gathered (desc, rec, heap) of every launch against an un-sharded device run of the
+             whole batch in canonical form, byte for byte;
+  overflow   the same with capacities and inputs that force overflows: MU on the dense corpus with a
+             record capacity of one record per message (ST_OVF_OUT) and no spill workspace
+             (ST_OVF_TILE), MC frames longer than 128 hex characters (k_mc hands them over as
+             ST_OVF_TILE) -- the exchange re-runs them into overlays on each rank before it ships, and
+             the gathered results equal the un-sharded Engine.run (its own re-runs) byte for byte;
+  dict       ShardedDemodulator.demodulate_batch on msg_data dicts (general-path messages with
+             multi-digit ids, messages whose host conversion raises) == SDProtocols.demodulate_batch of
+             the whole list, on every rank.
+Prints "OK" on success.
 """
 import os
 import sys
@@ -18,57 +29,86 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pysignalduino_amd import bank as bankmod, dist as sdist, runtime, synth  # noqa: E402
 
 N = 12000   # per kind: shards of 6000 >= GROUP_MIN, so MU/MS run grouped with spill regions
+KIND = {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS, "MC": runtime.KIND_MC}
 
 
 def subset(pb, lo, hi):
     return pb.subset(np.arange(lo, hi))
 
 
+def long_mc(P, mb, n_long, seed):
+    """mb with n_long frames replaced by frames of 129..800 hex characters (synth.general_mc_frames)."""
+    from pysignalduino_amd import packing
+    frames = [(mb.hex(i), int(mb.clock[i]), int(mb.mcbitnum[i]), "Mc" if mb.mtype[i] else "MC", None)
+              for i in range(mb.n)]
+    rng = np.random.default_rng(seed)
+    for j, f in zip(rng.choice(mb.n, n_long, replace=False), synth.general_mc_frames(P, n_long, seed=seed)):
+        frames[int(j)] = f
+    return packing.mc_batch_from_frames(frames)
+
+
+def canon_full(eng, kind, bd):
+    d, r, h = eng.run(KIND[kind], bd)
+    assert not np.isin(d["status"], (runtime.ST_OVF_OUT, runtime.ST_OVF_TILE)).any(), kind
+    return sdist.canonical(d, r, h)
+
+
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    mode = os.environ.get("SDX_WORKER_MODE", "pipelined")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     bk = bankmod.Bank()
     eng = runtime.Engine(bk, 0)
     P = bk.protocols
-    full = {"MU": synth.mu_corpus(P, N, seed=81), "MS": synth.ms_corpus(P, N, seed=82),
+    sd = sdist.ShardedDemodulator(group=None, engine=eng)
+    assert sd.world == 2
+    if mode == "dict":
+        return dict_mode(sd, P, rank)
+    dense = mode == "overflow"
+    full = {"MU": synth.mu_corpus(P, N, seed=81, noise_frac=0.0 if dense else 0.15), "MS": synth.ms_corpus(P, N, seed=82),
             "MC": synth.mc_corpus(P, N, seed=83)}
+    if dense:
+        full["MC"] = long_mc(P, full["MC"], 40, seed=84)
     kinds = ("MU", "MS", "MC")
-    lo, hi = sdist.shard_bounds(N, rank, world)
+    lo, hi = sd.shard(N)
     shard = {k: subset(full[k], lo, hi) for k in kinds}
     bds = {k: (eng.to_device_mc(c) if k == "MC" else eng.to_device_pulses(c)) for k, c in shard.items()}
 
     def alloc(n, k):
+        if dense and k == "MU":   # one record per message, no spill regions: ST_OVF_OUT and ST_OVF_TILE
+            return eng.alloc_out(n, n, 40 * n, 0)
         return eng.alloc_out(n, 12 * n + 4096, 320 * n + 65536, eng.pulses_work_bytes(n) if k != "MC" else 0)
 
-    def launch(k, bd, o):
-        if k == "MC":
-            eng.launch_mc(bd, o)
-        else:
-            eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, o)
-
     outs = [{k: alloc(hi - lo, k) for k in kinds} for _ in range(2)]
-    ex = sdist.Exchange()
     stream = torch.cuda.current_stream(dev)
     snaps = []
     for j in range(2):
         o = outs[j % 2]
+        parts = []
         for k in kinds:
             o[k]["cursor"].zero_()
-            launch(k, bds[k], o[k])
-        ex.submit([(o[k]["desc"], o[k]["rec"], o[k]["heap"], bds[k]["n"], o[k]["cursor"]) for k in kinds], stream)
-        snaps.append([tuple(t.cpu().numpy() for t in g) for g in ex.gathered()])
-    ex.flush()
-    assert ex.world == 2 and dist.get_world_size() == 2
-    # the un-sharded device run of the whole batch, canonicalised on the host
+            parts.append(sd.launch(KIND[k], bds[k], o[k]))
+        if dense and j == 0:   # the first pass really overflowed on this rank
+            torch.cuda.synchronize()
+            st = {k: o[k]["desc"][: (hi - lo) * 8].view(-1, 8)[:, 6].cpu().numpy() for k in kinds}
+            assert (st["MU"] == runtime.ST_OVF_OUT).any(), rank
+            print("first-pass MU overflows: OUT", int((st["MU"] == runtime.ST_OVF_OUT).sum()), "TILE",
+                  int((st["MU"] == runtime.ST_OVF_TILE).sum()), flush=True)
+            assert (st["MC"] == runtime.ST_OVF_TILE).any(), rank
+        sd.submit(parts, stream)
+        snaps.append([tuple(t.cpu().numpy() for t in g) for g in sd.gathered()])
+    sd.flush()
+    if dense:
+        assert sd.exchange.reruns >= 4, sd.exchange.reruns
+    # the nibble form is on: the wire carries fewer payload bytes than it delivers
+    assert sd.exchange.heap_wire_bytes[-1] < 0.8 * sd.exchange.payload_bytes[-1], (sd.exchange.heap_wire_bytes,
+                                                                                  sd.exchange.payload_bytes)
+    # the un-sharded device run of the whole batch (Engine.run: its own re-runs), canonicalised on the host
     for k in kinds:
         bd = eng.to_device_mc(full[k]) if k == "MC" else eng.to_device_pulses(full[k])
-        o = alloc(N, k)
-        launch(k, bd, o)
-        d, r, h = eng.fetch(o)
-        assert not np.isin(d["status"], (runtime.ST_OVF_OUT, runtime.ST_OVF_TILE)).any(), k
-        cd, cr, ch = sdist.canonical(d, r, h)
+        cd, cr, ch = canon_full(eng, k, bd)
         i = kinds.index(k)
         for j, snap in enumerate(snaps):
             gd, gr, gh = snap[i]
@@ -76,6 +116,45 @@ def main():
             assert gr.tobytes() == cr.tobytes(), (rank, j, k, "rec")
             assert gh.tobytes() == ch.tobytes(), (rank, j, k, "heap")
         assert len(cr) > N // 4, (k, len(cr))
+    dist.barrier()
+    dist.destroy_process_group()
+    print("OK", flush=True)
+
+
+def dict_mode(sd, P, rank):
+    """ShardedDemodulator.demodulate_batch == SDProtocols.demodulate_batch on the whole list."""
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    ref = SDProtocols(mc_mode="fixed")
+    sd.protocols, sd._eng = ref, None     # the entry on the reference-shaped object's own engine
+    for kind in ("MU", "MS"):
+        pb = synth.mu_corpus(P, 5000, seed=91) if kind == "MU" else synth.ms_corpus(P, 5000, seed=92)
+        msgs = [pb.to_msg_dict(i) for i in range(pb.n)]
+        gen = synth.general_pulse_messages(P, kind, 60, seed=93)
+        for j, g in enumerate(gen):                      # general-path messages on both ranks' shards
+            msgs.insert(37 * j + 11, g)
+        msgs[5] = dict(msgs[5], data=12345)              # host conversion raises (TypeError) on rank 0
+        msgs[len(msgs) - 3] = dict(msgs[-3], data=None)  # and on rank 1
+        got = sd.demodulate_batch(msgs, kind)
+        want = ref.demodulate_batch(msgs, kind)
+        assert len(got) == len(want) == len(msgs)
+        for i, (g, w) in enumerate(zip(got, want)):
+            if isinstance(w, BaseException):
+                assert type(g) is type(w), (kind, i, g, w)
+            else:
+                assert g == w, (kind, i, g, w)
+        assert sum(isinstance(w, list) and len(w) > 0 for w in want) > 500, kind
+    mb = synth.mc_corpus(P, 4000, seed=94)
+    frames = [mb.to_msg_dict(i) for i in range(mb.n)]
+    for j, (h, c, L, t, v) in enumerate(synth.general_mc_frames(P, 30, seed=95)):
+        frames.insert(100 * j + 7, {"raw_hex": h, "clock": c, "mcbitnum": L, "messagetype": t})
+    frames[9] = {"raw_hex": 17, "clock": "1", "mcbitnum": "4"}   # not a str: ContractError on the host
+    got = sd.demodulate_batch(frames, "MC")
+    want = ref.demodulate_batch(frames, "MC")
+    for i, (g, w) in enumerate(zip(got, want)):
+        if isinstance(w, BaseException):
+            assert type(g) is type(w), ("MC", i, g, w)
+        else:
+            assert g == w, ("MC", i, g, w)
     dist.barrier()
     dist.destroy_process_group()
     print("OK", flush=True)

@@ -98,7 +98,27 @@ def _worker(rank, world, port, msgs, pids, q):
         steps.append([decode(a.numpy().view(runtime.DESC_DT), b.numpy().view(runtime.RES_DT), c.numpy(), pids)
                       for a, b, c in ex.gathered()])
     ex.flush()
-    q.put((rank, got, got_multi, got_half, steps))
+    # overflow + re-run: rank 1's launch has overflowed messages; the re-run callback adds an overlay
+    # with their results, every rank recounts, and the gathered stream is the un-sharded one
+    n = hi - lo
+    ovf = (np.arange(n) % 5 == 0) & (rank == 1)
+    d3 = d.copy()
+    d3["status"][ovf] = runtime.ST_OVF_OUT
+    d3["n_rec"][ovf] = 0
+    td3 = torch.from_numpy(d3.view(np.uint8).copy())
+
+    def rerun(part):
+        od = d.copy()
+        od["status"][~ovf] = runtime.ST_ABSENT
+        part.overlays.append(sdist.Part(torch.from_numpy(od.view(np.uint8).copy()), tr, th, n, cur))
+        return part
+
+    ex2 = sdist.Exchange()
+    ex2.submit([sdist.Part(td3, tr, th, n, cur)], rerun=rerun)
+    ex2.flush()
+    a3, b3, c3 = ex2.gathered()[0]
+    got_rerun = decode(a3.numpy().view(runtime.DESC_DT), b3.numpy().view(runtime.RES_DT), c3.numpy(), pids)
+    q.put((rank, got, got_multi, got_half, steps, got_rerun, ex2.reruns))
     dist.destroy_process_group()
 
 
@@ -131,17 +151,46 @@ def test_gloo_world2_allgather_matches_unsharded():
     for r in range(2):
         lo, hi = sdist.shard_bounds(len(msgs), r, 2)
         halves += full[lo: lo + (hi - lo) // 2]
-    for rank, got, got_multi, got_half, steps in outs:
+    for rank, got, got_multi, got_half, steps, got_rerun, reruns in outs:
+        assert got_rerun == full, f"rank {rank}: the re-run exchange differs"
+        assert reruns == (1 if rank == 1 else 0), (rank, reruns)
         assert got == full, f"rank {rank} gathered stream differs"
         assert got_multi == full, f"rank {rank}: allgather_streams differs"
         assert got_half == halves, f"rank {rank}: second launch of allgather_streams differs"
         assert steps == [[full], [halves, full]], f"rank {rank}: Exchange steps differ"
 
 
-def synth_launch(rng, n, spill=True):
+def synth_affix(rng, nproto=129):
+    """A per-protocol (preamble, postamble) table shaped like Bank.affixes (preambles such as 'W54#',
+    's', '', postambles mostly empty)."""
+    out = []
+    for _ in range(nproto):
+        pre = bytes(rng.choice(list(b"WPsiu0123456789#"), size=int(rng.integers(0, 6))).astype(np.uint8))
+        post = bytes(rng.choice(list(b"#;x"), size=int(rng.integers(0, 3)) * int(rng.random() < 0.3)).astype(np.uint8))
+        out.append((pre, post))
+    return out
+
+
+def synth_payload(rng, affix, proto):
+    """Payloads of every form: pre + uppercase hex + post (the nibble form; odd and even digit counts,
+    none), lowercase hex, a broken affix, arbitrary bytes."""
+    pre, post = affix[proto] if affix is not None else (b"", b"")
+    u = rng.random()
+    nd = int(rng.integers(0, 40))
+    if u < 0.6:
+        return pre + bytes(rng.choice(list(b"0123456789ABCDEF"), size=nd).astype(np.uint8)) + post
+    if u < 0.7:
+        return pre + bytes(rng.choice(list(b"0123456789abcdef"), size=nd + 1).astype(np.uint8)) + post
+    if u < 0.8:
+        return pre[:-1] + b"Z" + bytes(rng.choice(list(b"0123456789ABCDEF"), size=nd).astype(np.uint8)) + post
+    return bytes(rng.integers(32, 127, size=nd, dtype=np.uint8))
+
+
+def synth_launch(rng, n, spill=True, affix=None, status_absent=0.0):
     """Launch outputs shaped like k_pulses writes them: records per tile of 64 messages in a shuffled
     tile order, tile pieces of the heap 16-byte aligned with gaps, RAISED and empty messages, and
-    (``spill``) records past the used range that no message owns."""
+    (``spill``) records past the used range that no message owns.  ``status_absent``: the fraction of
+    descriptors left at ST_ABSENT (an overlay's)."""
     nrec = rng.integers(0, 7, size=n) * (rng.random(n) < 0.8)
     status = np.where(rng.random(n) < 0.1, runtime.ST_RAISED, runtime.ST_OK)
     nrec[status == runtime.ST_RAISED] = 0
@@ -155,15 +204,81 @@ def synth_launch(rng, n, spill=True):
         for m in rng.permutation(np.arange(64 * t, min(n, 64 * t + 64))):
             desc[m]["rec_begin"] = len(recs) if nrec[m] else rng.integers(0, 1000)
             for _ in range(nrec[m]):
-                ln = int(rng.integers(0, 40))
-                heap += bytes(rng.integers(32, 127, size=ln, dtype=np.uint8))
-                recs.append((len(heap) - ln, ln, int(rng.integers(0, 129)), int(rng.integers(0, 300)), int(m)))
+                pr = int(rng.integers(0, 129))
+                pay = synth_payload(rng, affix, pr)
+                heap += pay
+                recs.append((len(heap) - len(pay), len(pay), pr, int(rng.integers(0, 300)), int(m)))
         heap += b"\0" * ((-len(heap)) % 16 + 16 * int(rng.integers(0, 2)))
     if spill:   # written but unowned records (an abandoned tile region)
         for _ in range(5):
             recs.append((0, 3, 1, 1, int(rng.integers(0, n))))
+    if status_absent:
+        absent = rng.random(n) < status_absent
+        desc["status"][absent] = runtime.ST_ABSENT
     rec = np.array(recs, runtime.RES_DT) if recs else np.zeros(0, runtime.RES_DT)
     return desc, rec, np.frombuffer(bytes(heap), np.uint8).copy()
+
+
+def test_wire_nibble_form_round_trip():
+    """wire v3: payloads of the form preamble + uppercase hex + postamble travel as packed digits
+    (proto | WIRE_NIB), everything else raw; decode(encode(x)) == canonical(x) with the affixes, and
+    the wire payload bytes shrink by about half for the nibble records."""
+    rng = np.random.default_rng(21)
+    affix = synth_affix(rng)
+    d, r, h = synth_launch(rng, 800, spill=False, affix=affix)
+    m, w, p, bad = sdist.wire_encode(d, r, h, affix=affix)
+    assert bad == 0
+    nib = (w["proto"] & runtime.WIRE_NIB) != 0
+    assert 0.3 < nib.mean() < 0.9, nib.mean()
+    raw_bytes = int(w["payload_len"].astype(np.int64).sum())
+    assert len(p) < raw_bytes
+    got = sdist.wire_decode([(m, w, p)], affix)
+    want = sdist.canonical(d, r, h)
+    for a, b in zip(got, want):
+        assert a.tobytes() == b.tobytes()
+    # every nibble record really is pre + uppercase hex + post, every raw one is not
+    hb = want[2].tobytes()
+    for x, isnib in zip(want[1], nib):
+        pay = hb[int(x["payload_off"]): int(x["payload_off"]) + int(x["payload_len"])]
+        assert (sdist._nib_digits(affix, int(x["proto"]), pay) >= 0) == bool(isnib)
+
+
+def test_wire_overlays_last_present_wins():
+    """A launch with two overlays (host form of sdx_xchg_part.alt): message m comes from the last level
+    whose descriptor is not ST_ABSENT; the primary's overflowed messages are then shipped from the
+    overlays, and an overflow no overlay covers stays "bad"."""
+    rng = np.random.default_rng(22)
+    n = 600
+    d0, r0, h0 = synth_launch(rng, n, spill=False)
+    ovf = rng.random(n) < 0.2
+    d0["status"][ovf] = runtime.ST_OVF_OUT
+    d0["n_rec"][ovf] = 0
+    d1, r1, h1 = synth_launch(rng, n, spill=False, status_absent=0.5)
+    d2, r2, h2 = synth_launch(rng, n, spill=False, status_absent=0.8)
+    d1["status"][ovf & (d1["status"] == runtime.ST_ABSENT) & (d2["status"] == runtime.ST_ABSENT)] = runtime.ST_OK
+    m, w, p, bad = sdist.wire_encode(d0, r0, h0, overlays=[(d1, r1, h1, None, None), (d2, r2, h2, None, None)])
+    assert bad == 0
+    lev, rd = sdist.resolve_host([(d0,), (d1,), (d2,)])
+    assert (lev[d2["status"] != runtime.ST_ABSENT] == 2).all()
+    assert (lev[(d2["status"] == runtime.ST_ABSENT) & (d1["status"] != runtime.ST_ABSENT)] == 1).all()
+    # the same results as one launch holding each message's resolved records
+    cd, cr, ch = sdist.wire_decode([(m, w, p)])
+    for i in rng.choice(n, 60, replace=False):
+        src = [(d0, r0, h0), (d1, r1, h1), (d2, r2, h2)][int(lev[i])]
+        dd = src[0][i]
+        assert int(cd[i]["status"]) == int(dd["status"]) and int(cd[i]["n_rec"]) == (
+            int(dd["n_rec"]) if dd["status"] == runtime.ST_OK else 0)
+        for j in range(int(cd[i]["n_rec"])):
+            a = cr[int(cd[i]["rec_begin"]) + j]
+            b = src[1][int(dd["rec_begin"]) + j]
+            assert (int(a["proto"]), int(a["bit_length"])) == (int(b["proto"]), int(b["bit_length"]))
+            assert ch[int(a["payload_off"]): int(a["payload_off"]) + int(a["payload_len"])].tobytes() == \
+                src[2][int(b["payload_off"]): int(b["payload_off"]) + int(b["payload_len"])].tobytes()
+    # an overflow that no overlay covers is shipped as bad
+    d0b = d0.copy()
+    hole = np.nonzero((d1["status"] == runtime.ST_ABSENT) & (d2["status"] == runtime.ST_ABSENT))[0][0]
+    d0b["status"][hole] = runtime.ST_OVF_TILE
+    assert sdist.wire_encode(d0b, r0, h0, overlays=[(d1, r1, h1, None, None), (d2, r2, h2, None, None)])[3] == 1
 
 
 def test_wire_canonical_is_order_free():
@@ -199,55 +314,174 @@ def test_wire_canonical_is_order_free():
     assert bad[3] >= 1
 
 
-def _dev_launch(desc, rec, heap, dev, cursor=None):
+def _dev_launch(desc, rec, heap, dev, cursor=None, kind=runtime.KIND_RAW):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy() if len(a) else  # noqa: E731
                                    np.zeros(16, np.uint8)).to(dev)
     cur = torch.tensor(cursor if cursor is not None else [len(rec), len(heap), 0, 0], dtype=torch.int32, device=dev)
-    return (t(desc), t(rec), t(heap), len(desc), cur)
+    return sdist.Part(t(desc), t(rec), t(heap), len(desc), cur, kind)
+
+
+def _kernel_exchange(eng=None):
+    ex = sdist.Exchange.__new__(sdist.Exchange)
+    ex._bufs, ex.engine = {}, eng
+    return ex
 
 
 @pytest.mark.gpu
 def test_exchange_kernels_match_host_wire():
     """sdx_exchange_count / sdx_exchange_pack (HIP) == the numpy wire form for K = 3 launches laid
-    out like k_pulses output (shuffled tiles, padded heap, RAISED / empty / unowned records), and
-    sdx_exchange_unpack over 3 ranks' sections == wire_decode; an out-of-range message is counted bad."""
+    out like k_pulses output (shuffled tiles, padded heap, RAISED / empty / unowned records), raw and
+    in the nibble form (the real bank's MU affixes), and sdx_exchange_unpack over 3 ranks' sections ==
+    wire_decode; an out-of-range message is counted bad."""
+    from pysignalduino_amd import bank as bankmod
     dev = torch.device("cuda", 0)
-    rng = np.random.default_rng(3)
-    launches = [synth_launch(rng, n) for n in (1, 3000, 20000)]
-    parts = [_dev_launch(d, r, h, dev) for d, r, h in launches]
-    ex = sdist.Exchange.__new__(sdist.Exchange)
-    ex._bufs = {}
-    pt = [sdist._part_tuple(p) for p in parts]
+    eng = runtime.Engine(bankmod.Bank(), 0)
+    affix = eng.bank.affixes(runtime.KIND_MU)
     s = torch.cuda.current_stream(dev)
-    cnt = ex._count_pack_device(pt, s).cpu().numpy().reshape(3, 4)
-    want = [sdist.wire_encode(d, r, h) for d, r, h in launches]
-    for k, (m, w, p, bad) in enumerate(want):
-        assert list(cnt[k]) == [len(m), len(w), len(p), bad], (k, cnt[k])
+    for nib in (False, True):
+        rng = np.random.default_rng(3)
+        launches = [synth_launch(rng, n, affix=affix) for n in (1, 3000, 20000)]
+        kind = runtime.KIND_MU if nib else runtime.KIND_RAW
+        parts = [_dev_launch(d, r, h, dev, kind=kind) for d, r, h in launches]
+        ex = _kernel_exchange(eng if nib else None)
+        flat = sdist._flatten(parts)
+        cnt = ex._count_pack_device(flat, s).cpu().numpy().reshape(3, runtime.XCHG_COUNTS)
+        want = [sdist.wire_encode(d, r, h, affix=affix if nib else None) for d, r, h in launches]
+        for k, (m, w, p, bad) in enumerate(want):
+            pb = int(w["payload_len"].astype(np.int64).sum())
+            assert list(cnt[k]) == [len(m), len(w), len(p), bad, pb, 0, 0, 0], (nib, k, cnt[k])
+        if nib:
+            assert cnt[:, 2].sum() < 0.8 * cnt[:, 4].sum()
+        offs, nb, T = sdist._layout(cnt[None])
+        sv = ex._bufs["send"].cpu().numpy()
+        for k, (m, w, p, _) in enumerate(want):
+            o = offs[0, k]
+            assert sv[o[0]: o[0] + 4 * len(m)].tobytes() == m.tobytes(), k
+            assert sv[o[1]: o[1] + 8 * len(w)].tobytes() == w.tobytes(), k
+            assert sv[o[2]: o[2] + len(p)].tobytes() == p.tobytes(), k
+            for j, ln in enumerate((4 * len(m), 8 * len(w), len(p))):   # zero padding to 16 bytes
+                assert not sv[o[j] + ln: o[j] + sdist._r16(ln)].any(), (k, j)
+        # the same layout twice (counters reset by the kernels themselves)
+        cnt2 = ex._count_pack_device(flat, s).cpu().numpy().reshape(3, runtime.XCHG_COUNTS)
+        assert (cnt2 == cnt).all()
+        assert (ex._bufs["send"].cpu().numpy()[:T] == sv[:T]).all()
+        # unpack: three "ranks" = the three launches' wire sections of one buffer
+        Su = np.array([[len(m), len(w), len(p), 0, int(w["payload_len"].astype(np.int64).sum())]
+                       for m, w, p, _ in want], np.int64)
+        gd, gr, gh = sdist.unpack_device(ex._bufs["send"], Su, [offs[0, k] for k in range(3)], ex.engine, kind)
+        ed, er, eh = sdist.wire_decode([(m, w, p) for m, w, p, _ in want], affix if nib else None)
+        assert gd.cpu().numpy().tobytes() == ed.tobytes()
+        assert gr.cpu().numpy().tobytes() == er.tobytes()
+        assert gh.cpu().numpy().tobytes() == eh.tobytes()
+    # a cursor short of the records written: the owning messages are "bad"
+    d, r, h = launches[1]
+    bad_parts = sdist._flatten([_dev_launch(d, r, h, dev, [len(r) - 10, len(h), 0, 0])])
+    cb = _kernel_exchange().\
+        _count_pack_device(bad_parts, s).cpu().numpy()
+    assert cb[3] == sdist.wire_encode(d, r, h, nrec_written=len(r) - 10)[3] > 0
+
+
+@pytest.mark.gpu
+def test_exchange_overlays_on_device():
+    """sdx_xchg_part.alt / aux (ABI 11): a launch with overflowed messages and two overlays -> the
+    device wire equals the host wire_encode with the same overlays (last present level wins, nibble
+    form), the aux parts have zero counts, and an overflow no overlay covers is counted bad."""
+    from pysignalduino_amd import bank as bankmod
+    dev = torch.device("cuda", 0)
+    eng = runtime.Engine(bankmod.Bank(), 0)
+    affix = eng.bank.affixes(runtime.KIND_MU)
+    rng = np.random.default_rng(23)
+    n = 5000
+    d0, r0, h0 = synth_launch(rng, n, affix=affix)
+    ovf = rng.random(n) < 0.2
+    d0["status"][ovf] = runtime.ST_OVF_TILE
+    d0["n_rec"][ovf] = 0
+    d1, r1, h1 = synth_launch(rng, n, affix=affix, status_absent=0.5)
+    d2, r2, h2 = synth_launch(rng, n, affix=affix, status_absent=0.8)
+    d1["status"][ovf & (d1["status"] == runtime.ST_ABSENT) & (d2["status"] == runtime.ST_ABSENT)] = runtime.ST_OK
+    p0 = _dev_launch(d0, r0, h0, dev, kind=runtime.KIND_MU)
+    p0.overlays = [_dev_launch(d1, r1, h1, dev, kind=runtime.KIND_MU), _dev_launch(d2, r2, h2, dev, kind=runtime.KIND_MU)]
+    q = _dev_launch(*synth_launch(rng, 700, affix=affix), dev, kind=runtime.KIND_MU)   # a second launch, no overlays
+    flat = sdist._flatten([p0, q])
+    assert [(a, x) for _, a, x in flat] == [(3, 0), (0, 0), (4, 1), (0, 1)]
+    ex = _kernel_exchange(eng)
+    s = torch.cuda.current_stream(dev)
+    cnt = ex._count_pack_device(flat, s).cpu().numpy().reshape(4, runtime.XCHG_COUNTS)
+    m, w, p, bad = sdist.wire_encode(d0, r0, h0, affix=affix, overlays=[(d1, r1, h1, None, None), (d2, r2, h2, None, None)])
+    assert bad == 0 and list(cnt[0][:4]) == [n, len(w), len(p), 0], cnt[0]
+    assert not cnt[2:].any()
     offs, nb, T = sdist._layout(cnt[None])
     sv = ex._bufs["send"].cpu().numpy()
-    for k, (m, w, p, _) in enumerate(want):
-        o = offs[0, k]
-        assert sv[o[0]: o[0] + 4 * len(m)].tobytes() == m.tobytes(), k
-        assert sv[o[1]: o[1] + 8 * len(w)].tobytes() == w.tobytes(), k
-        assert sv[o[2]: o[2] + len(p)].tobytes() == p.tobytes(), k
-        for j, ln in enumerate((4 * len(m), 8 * len(w), len(p))):   # zero padding to 16 bytes
-            assert not sv[o[j] + ln: o[j] + sdist._r16(ln)].any(), (k, j)
-    # the same layout twice (counters reset by the kernels themselves)
-    cnt2 = ex._count_pack_device(pt, s).cpu().numpy().reshape(3, 4)
-    assert (cnt2 == cnt).all()
-    assert (ex._bufs["send"].cpu().numpy()[:T] == sv[:T]).all()
-    # unpack: three "ranks" = the three launches' wire sections of one buffer
-    Su = np.array([[len(m), len(w), len(p)] for m, w, p, _ in want], np.int64)
-    gd, gr, gh = sdist.unpack_device(ex._bufs["send"], Su, [offs[0, k] for k in range(3)])
-    ed, er, eh = sdist.wire_decode([(m, w, p) for m, w, p, _ in want])
+    o = offs[0, 0]
+    assert sv[o[0]: o[0] + 4 * n].tobytes() == m.tobytes()
+    assert sv[o[1]: o[1] + 8 * len(w)].tobytes() == w.tobytes()
+    assert sv[o[2]: o[2] + len(p)].tobytes() == p.tobytes()
+    # an overflow no overlay covers
+    hole = np.nonzero((d1["status"] == runtime.ST_ABSENT) & (d2["status"] == runtime.ST_ABSENT) & ~ovf)[0][:3]
+    d0b = d0.copy()
+    d0b["status"][hole] = runtime.ST_OVF_OUT
+    p0b = _dev_launch(d0b, r0, h0, dev, kind=runtime.KIND_MU)
+    p0b.overlays = p0.overlays
+    cb = ex._count_pack_device(sdist._flatten([p0b]), s).cpu().numpy()
+    assert cb[3] == 3
+
+
+@pytest.mark.gpu
+def test_exchange_pack_into_rank1_chunk_and_32_rank_unpack():
+    """sdx_exchange_pack_into at a rank > 0 chunk of an in-place receive buffer gives the
+    same bytes as the canonical wire, and sdx_exchange_unpack over SDX_XCHG_MAX_RANKS (32) ranks of
+    fake wire sections rebuilds the concatenated job (the end sentinels at [32])."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    launches = [synth_launch(rng, n, spill=False) for n in (2500, 900)]
+    parts = [_dev_launch(d, r, h, dev) for d, r, h in launches]
+    ex = _kernel_exchange()
+    flat = sdist._flatten(parts)
+    s = torch.cuda.current_stream(dev)
+    cnt_dev = ex._count_device(flat, s)
+    mine = cnt_dev.cpu().numpy().astype(np.int64).reshape(2, runtime.XCHG_COUNTS)
+    # rank 1 of 2: a rank 0 with other counts makes the chunk size T the larger one
+    S = np.stack([mine + np.array([0, 7, 100, 0, 100, 0, 0, 0]), mine])
+    offs, nb, T = sdist._layout(S)
+    recv = torch.full((2 * T + 64,), 0xAB, dtype=torch.uint8, device=dev)
+    work, wb = ex._work(flat, dev)
+    lib = runtime.load_library()
+    import ctypes
+    hc = np.ascontiguousarray(mine.reshape(-1).astype(np.uint32))
+    runtime._check(lib, lib.sdx_exchange_pack_into(None, ex._xparts(flat), len(flat), ctypes.c_void_p(work.data_ptr()), wb,
+                                                   ctypes.c_void_p(cnt_dev.data_ptr()), hc.ctypes.data_as(ctypes.c_void_p),
+                                                   ctypes.c_void_p(recv[T:].data_ptr()), T, ctypes.c_void_p(s.cuda_stream)))
+    rv = recv.cpu().numpy()
+    assert (rv[:T] == 0xAB).all() and (rv[2 * T:] == 0xAB).all()   # nothing outside the chunk
+    for k, (d, r, h) in enumerate(launches):
+        m, w, p, _ = sdist.wire_encode(d, r, h)
+        o = T + offs[1, k]
+        assert rv[o[0]: o[0] + 4 * len(m)].tobytes() == m.tobytes()
+        assert rv[o[1]: o[1] + 8 * len(w)].tobytes() == w.tobytes()
+        assert rv[o[2]: o[2] + len(p)].tobytes() == p.tobytes()
+    # 32 ranks: launch 1's wire sections, each rank a different slice of messages
+    m, w, p, _ = sdist.wire_encode(*launches[1])
+    nrec = (m & 0xFFFF).astype(np.int64)
+    rb = np.concatenate([[0], np.cumsum(nrec)])
+    pb = np.concatenate([[0], np.cumsum(w["payload_len"].astype(np.int64))])
+    cuts = np.linspace(0, len(m), 33).astype(np.int64)
+    buf, sec, Sr = bytearray(), [], []
+    for i in range(32):
+        a, b = cuts[i], cuts[i + 1]
+        ra, rb_ = rb[a], rb[b]
+        parts_i = (m[a:b].tobytes(), w[ra:rb_].tobytes(), p[pb[ra]: pb[rb_]].tobytes())
+        o = []
+        for x in parts_i:
+            o.append(len(buf))
+            buf += x + b"\0" * ((-len(x)) % 16)
+        sec.append(o)
+        Sr.append([b - a, rb_ - ra, pb[rb_] - pb[ra], 0, pb[rb_] - pb[ra]])
+    tb = torch.from_numpy(np.frombuffer(bytes(buf), np.uint8).copy()).to(dev)
+    gd, gr, gh = sdist.unpack_device(tb, np.array(Sr, np.int64), sec)
+    ed, er, eh = sdist.wire_decode([(m, w, p)])
     assert gd.cpu().numpy().tobytes() == ed.tobytes()
     assert gr.cpu().numpy().tobytes() == er.tobytes()
     assert gh.cpu().numpy().tobytes() == eh.tobytes()
-    # a cursor short of the records written: the owning messages are "bad"
-    d, r, h = launches[1]
-    bad_parts = [sdist._part_tuple(_dev_launch(d, r, h, dev, [len(r) - 10, len(h), 0, 0]))]
-    cb = ex._count_pack_device(bad_parts, s).cpu().numpy()
-    assert cb[3] == sdist.wire_encode(d, r, h, nrec_written=len(r) - 10)[3] > 0
 
 
 def _run_worker(name, env_extra, timeout=240):
@@ -268,23 +502,18 @@ def test_exchange_rccl_world1():
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
-@pytest.mark.gpu
-def test_world2_real_kernels_match_unsharded():
-    """Config 5's path at world size 2 on the one GPU (gloo, both ranks on cuda:0): each rank
-    demodulates its contiguous shard of a real MU + MS + MC batch with the product kernels (grouped
-    order, spill regions), the pipelined Exchange gathers two steps, and the gathered descriptors,
-    records and heap equal an un-sharded device run (canonical form) byte for byte."""
+def _world2(mode, timeout=300):
     import subprocess
     import sys
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_gpu_worker.py")
     port = str(_free_port())
     procs = [subprocess.Popen([sys.executable, worker], env=dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
-                                                                 RANK=str(r), WORLD_SIZE="2"),
+                                                                 RANK=str(r), WORLD_SIZE="2", SDX_WORKER_MODE=mode),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
     outs = []
     for p in procs:
         try:
-            o, e = p.communicate(timeout=240)
+            o, e = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
@@ -292,6 +521,33 @@ def test_world2_real_kernels_match_unsharded():
         outs.append((p.returncode, o, e))
     for rank, (rc, o, e) in enumerate(outs):
         assert rc == 0 and o.strip().endswith("OK"), (rank, rc, o[-2000:], e[-4000:])
+
+
+@pytest.mark.gpu
+def test_world2_real_kernels_match_unsharded():
+    """Config 5's path at world size 2 on the one GPU (gloo, both ranks on cuda:0): each rank
+    demodulates its contiguous shard of a real MU + MS + MC batch with the product launches
+    (ShardedDemodulator: grouped order, spill regions), the pipelined exchange (nibble wire form)
+    gathers two steps, and the gathered descriptors, records and heap equal an un-sharded device run
+    (canonical form) byte for byte."""
+    _world2("pipelined")
+
+
+@pytest.mark.gpu
+def test_world2_overflow_reruns_match_unsharded():
+    """a corpus and capacities that force ST_OVF_OUT / ST_OVF_TILE (dense MU corpus,
+    one record per message, no spill workspace; MC frames of 129..800 hex characters): the ranks
+    re-run their overflowed messages into overlays inside the exchange (no RuntimeError) and the
+    gathered results equal the un-sharded Engine.run byte for byte."""
+    _world2("overflow")
+
+
+@pytest.mark.gpu
+def test_world2_sharded_demodulate_batch_dicts():
+    """ShardedDemodulator.demodulate_batch (the product's sharded dict API) == SDProtocols.
+    demodulate_batch of the whole list on both ranks: MU / MS with general-path messages and host
+    conversion errors on both shards, MC fixed with long frames and a non-str frame."""
+    _world2("dict")
 
 
 @pytest.mark.gpu

@@ -79,11 +79,11 @@ def main():
     sers = []
     for s in range(2):   # one serialiser (exchange sender kernels) per slot
         ex = sdist.Exchange.__new__(sdist.Exchange)
-        ex._bufs = {}
+        ex._bufs, ex.engine = {}, eng     # the wire's nibble form with the engine's bank
         sers.append(ex)
     cin, sp, sd, cout = (torch.cuda.Stream(dev) for _ in range(4))
     host_counts = [torch.empty(8, dtype=torch.int32).pin_memory() for _ in range(2)]
-    host_wc = [torch.empty(12, dtype=torch.int32).pin_memory() for _ in range(2)]
+    host_wc = [torch.empty(3 * runtime.XCHG_COUNTS, dtype=torch.int32).pin_memory() for _ in range(2)]
     host_out = [torch.empty(sum(caps[k][0] * C * 8 + caps[k][1] * C + 4 * C for k in caps) + 2 * C + 65536,
                             dtype=torch.uint8).pin_memory() for _ in range(2)]
     ev = lambda: torch.cuda.Event()  # noqa: E731
@@ -98,7 +98,7 @@ def main():
         nonlocal d2h_bytes
         s = j % 2
         wc_ev[s].synchronize()
-        S = host_wc[s].numpy().astype(np.int64).reshape(1, 3, 4)
+        S = host_wc[s].numpy().astype(np.int64).reshape(1, 3, runtime.XCHG_COUNTS)
         if S[..., 3].any():
             raise SystemExit(f"chunk {j}: overflowed messages {S[..., 3]}")
         offs, nb, T = sdist._layout(S)
@@ -190,8 +190,9 @@ def main():
                         eng.launch_pulses(kind, pb, o[kk], sel=sels[short])
                     if cnt[long_]:
                         eng.launch_pulses(kind, pb, o[kk], sel=sels[long_], long_variant=True)
-            wc = sers[s]._count_pack_device([sdist._part_tuple((o[kk]["desc"], o[kk]["rec"], o[kk]["heap"], C,
-                                                                o[kk]["cursor"])) for kk in kinds], sd)
+            KIND = {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS, "MC": runtime.KIND_MC}
+            wc = sers[s]._count_pack_device(sdist._flatten([sdist.Part(o[kk]["desc"], o[kk]["rec"], o[kk]["heap"], C,
+                                                                       o[kk]["cursor"], KIND[kk]) for kk in kinds]), sd)
             e1.record(sd)
             host_wc[s].copy_(wc, non_blocking=True)
             we = ev()
@@ -229,7 +230,7 @@ def main():
             m = buf[o[0]: o[0] + nb[0, i, 0]].view(np.uint32)
             w = buf[o[1]: o[1] + nb[0, i, 1]].view(runtime.WIRE_REC_DT)
             p = buf[o[2]: o[2] + nb[0, i, 2]]
-            dec[kk] = sdist.wire_decode([(m, w, p)])
+            dec[kk] = sdist.wire_decode([(m, w, p)], bk.affixes(i))
         lines = [data[offsets[i]: offsets[i + 1]].tobytes() for i in range(C)]
         from pysignalduino_amd.sd_protocols import SDProtocols
         sp_ = frontend.SignalParser(SDProtocols(mc_mode="fixed"))

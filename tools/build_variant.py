@@ -1,7 +1,7 @@
 """Build a variant of libsdx.so for A/B timing: sdx_kernels.hip from a given file (default the
 working tree) with extra -D flags, linked with the other translation units' objects of the
 in-tree build.  usage: python tools/build_variant.py NAME [--unit FILE.hip] [--src FILE] [-DFLAG ...]
--> pysignalduino_amd/_lib/variants/libsdx_NAME.so (time with SDX_LIB=... tools/time_mu.py)"""
+-> pysignalduino_amd/_lib/ab/libsdx_NAME.so (time with SDX_LIB=... tools/time_mu.py)"""
 import os
 import subprocess
 import sys
@@ -25,7 +25,7 @@ def main():
         src = os.path.abspath(args[i + 1])
         del args[i:i + 2]
     B.build()
-    out_dir = os.path.join(REPO, "pysignalduino_amd", "_lib", "variants")
+    out_dir = os.path.join(REPO, "pysignalduino_amd", "_lib", "ab")
     os.makedirs(out_dir, exist_ok=True)
     obj = os.path.join(out_dir, f"{unit}_{name}.o")
     inc = ["-I", os.path.join(REPO, "pysignalduino_amd", "csrc")]

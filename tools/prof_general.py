@@ -1,7 +1,7 @@
 """Where the general MU path's time goes (SDX_GPROF variant of sdx_general.hip): cycles per phase
 summed over items, and the slowest (message, protocol) items of pass 0.
 usage: python tools/build_variant.py gprof --unit sdx_general.hip -DSDX_GPROF
-       SDX_LIB=pysignalduino_amd/_lib/variants/libsdx_gprof.so python tools/prof_general.py"""
+       SDX_LIB=pysignalduino_amd/_lib/ab/libsdx_gprof.so python tools/prof_general.py"""
 import ctypes
 import gzip
 import json

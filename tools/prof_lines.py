@@ -1,6 +1,6 @@
 """Phase breakdown of k_parse_comp from the SDX_LPROF build (s_memtime cycles per wave: for each
 phase the max over the wave's lanes, summed over waves).
-usage: SDX_LIB=pysignalduino_amd/_lib/variants/libsdx_lprof.so python tools/prof_lines.py [lines]"""
+usage: SDX_LIB=pysignalduino_amd/_lib/ab/libsdx_lprof.so python tools/prof_lines.py [lines]"""
 import ctypes
 import os
 import sys

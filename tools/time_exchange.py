@@ -1,6 +1,7 @@
 """Standalone time of the exchange's sender kernels (sdx_exchange_count + sdx_exchange_pack) on the
 bench step's outputs (1M messages: MU/MS/MC 1/3 each), and of the receiver rebuild
-(sdx_exchange_unpack) at world 1.  usage: python tools/time_exchange.py [msgs] [reps]"""
+(sdx_exchange_unpack) at world 1.  usage: python tools/time_exchange.py [msgs] [reps] [raw]
+(raw: payloads without the nibble form)"""
 import os
 import sys
 
@@ -14,6 +15,7 @@ from pysignalduino_amd import bank as bankmod, dist as sdist, runtime, synth
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    nib = not (len(sys.argv) > 3 and sys.argv[3] == "raw")
     bk = bankmod.Bank()
     eng = runtime.Engine(bk, 0)
     P = bk.protocols
@@ -28,11 +30,12 @@ def main():
             eng.launch_mc(bd, o)
         else:
             eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bd, o)
-        parts.append((o["desc"], o["rec"], o["heap"], c.n, o["cursor"]))
+        parts.append(sdist.Part.from_out(o, {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS, "MC": runtime.KIND_MC}[k]
+                                         if nib else runtime.KIND_RAW))
     torch.cuda.synchronize()
     ex = sdist.Exchange.__new__(sdist.Exchange)
-    ex._bufs = {}
-    pt = [sdist._part_tuple(p) for p in parts]
+    ex._bufs, ex.engine = {}, eng if nib else None
+    pt = sdist._flatten(parts)
     s = torch.cuda.current_stream()
     cnt = ex._count_pack_device(pt, s)
     torch.cuda.synchronize()
@@ -44,16 +47,16 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
-    S = cnt.cpu().numpy().astype(np.int64).reshape(1, 3, 4)
+    S = cnt.cpu().numpy().astype(np.int64).reshape(1, 3, runtime.XCHG_COUNTS)
     offs, nb, T = sdist._layout(S)
     wire = int(nb.sum())
-    src = sum(int(p[4][0]) * 16 + int(p[4][1]) + 8 * p[3] for p in parts)
+    src = sum(int(p.cursor[0]) * 16 + int(p.cursor[1]) + 8 * p.n for p in parts)
     tu = []
     for _ in range(3):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for k in range(3):
-            sdist.unpack_device(ex._bufs["send"], S[:, k, :3], [offs[0, k]])
+            sdist.unpack_device(ex._bufs["send"], S[:, k, :], [offs[0, k]], ex.engine, parts[k].kind)
         e1.record()
         torch.cuda.synchronize()
         tu.append(e0.elapsed_time(e1))

@@ -1,6 +1,6 @@
 """Workgroup timeline of k_pulses<MU>/<MS> from the SDX_WGTIME diagnostic build: per-tile start / end
 stamps -> tile durations, average concurrency and the tail (time at < 90 % of peak concurrency).
-usage: SDX_LIB=pysignalduino_amd/_lib/variants/libsdx_wgt.so python tools/wg_timeline.py [n]"""
+usage: SDX_LIB=pysignalduino_amd/_lib/ab/libsdx_wgt.so python tools/wg_timeline.py [n]"""
 import ctypes
 import os
 import sys
