@@ -337,7 +337,9 @@ int sdx_lines_general(const sdx_lines* lines, const sdx_lines_out* out, const in
  * (meta.rssi = the raw R string for MU/MS, meta.clock = float(clockabs) / abs(P[CP]); MC: protocol_id,
  * rssi/freq_afc null; MN: calc_rssi(R), round(26000000/16384*A/1000, 0), modulation, rfmode).
  * first_only = 1 gives the one message per line the controller publishes (decoded[0],
- * signalduino/controller.py:254-257); 0 gives one JSON text per result record. */
+ * signalduino/controller.py:254-257); 0 gives one JSON text per result record; 2 (ABI 11) is 1 but
+ * SPARSE: off/len are written only for the lines that get a text, so the launches of all kinds can
+ * share one json_dev / off_dev / len_dev / cursor (a line belongs to one kind; the caller zeroes len). */
 typedef struct {
   int32_t kind;                /* enum sdx_kind of the demodulation launch */
   int32_t first_only;

@@ -18,22 +18,33 @@ performs the reference's per-line side effects in line order: the first decoded 
 A line outside the device contract (``ContractError`` in its slot) is logged and publishes
 nothing -- like a line whose parser raised in the reference.
 
-``publish="json"`` publishes the device-built texts instead (``SignalParser.parse_lines_json``,
-sdx_serialize_json): ``mqtt_publisher.client.publish(f"{base_topic}/state/messages", text)``, the
-call MqttPublisher.publish makes (signalduino/mqtt.py:260-272) with the text its
-``_message_to_json`` would build.  ``message_callback`` needs the objects, so it is only allowed
-with the default ``publish="objects"``.
+``publish="json"`` publishes the device-built texts instead (sdx_serialize_json):
+``mqtt_publisher.client.publish(f"{base_topic}/state/messages", text)``, the call
+MqttPublisher.publish makes (signalduino/mqtt.py:260-272) with the text its ``_message_to_json``
+would build.  Its batches go through a pipelined :class:`~pysignalduino_amd.stream.LineStream`
+(``stream=True``, the default): the upload, parse, demodulation and serialisation of batch k+1..k+3
+run while the texts of batch k are published; when the queue runs dry for ``max_delay`` the stream
+is drained, so a line's publication waits at most ``max_delay`` plus the GPU time of its batch.
+``message_callback`` needs the objects, so it is only allowed with the default
+``publish="objects"``.
+
+Per-line overheads of the reference loop that have no observable effect are skipped exactly when
+they have none: ``_handle_as_command_response(line)`` (controller.py:360-387) only matches pending
+command responses and logs at DEBUG, so it is awaited for a line only while the controller has
+pending responses or its logger is enabled for DEBUG (a controller without ``_pending_responses``
+gets it for every line); an unbounded ``asyncio.Queue`` is drained in bulk.
 """
 from __future__ import annotations
 
 import asyncio
+import collections
 import logging
-from typing import Any, List, Optional
+from typing import Any, Deque, List, Optional
 
 
 class BatchingParserTask:
     def __init__(self, controller: Any, max_batch: int = 4096, max_delay: float = 0.005, publish: str = "objects",
-                 logger: Optional[logging.Logger] = None):
+                 logger: Optional[logging.Logger] = None, stream: bool = True, lag: int = 3):
         if publish not in ("objects", "json"):
             raise ValueError("publish must be 'objects' or 'json'")
         if publish == "json" and getattr(controller, "message_callback", None):
@@ -47,23 +58,49 @@ class BatchingParserTask:
         self.logger = logger or getattr(controller, "logger", None) or logging.getLogger(__name__)
         self.batches = 0
         self.lines = 0
+        self.use_stream = stream and publish == "json"
+        self.lag = lag
+        self._stream = None
 
     def install(self) -> "BatchingParserTask":
         """Replace the controller's per-line loop (the attribute its run() schedules)."""
         self.c._parser_task = self.run
         return self
 
-    async def _next_batch(self) -> List[Any]:
+    def _take(self, q: asyncio.Queue, batch: List[Any]) -> None:
+        """Move up to max_batch - len(batch) queued lines into batch without waiting: an unbounded
+        asyncio.Queue is drained straight from its deque (no putter can be waiting on it, and the
+        reference loop never calls task_done), any other queue with get_nowait()."""
+        k = self.max_batch - len(batch)
+        dq = getattr(q, "_queue", None)
+        if type(q) is asyncio.Queue and q.maxsize <= 0 and isinstance(dq, collections.deque):
+            k = min(k, len(dq))
+            batch.extend([dq.popleft() for _ in range(k)])
+            return
+        for _ in range(k):
+            try:
+                batch.append(q.get_nowait())
+            except asyncio.QueueEmpty:
+                return
+
+    async def _next_batch(self, first_timeout: Optional[float] = None) -> List[Any]:
+        """Up to max_batch lines, waiting at most max_delay after the first; with ``first_timeout``
+        [] when no line arrives within it."""
         q: asyncio.Queue = self.c._raw_message_queue
-        batch = [await q.get()]
+        if first_timeout is None:
+            batch = [await q.get()]
+        else:
+            try:
+                batch = [await asyncio.wait_for(q.get(), first_timeout)]
+            except asyncio.TimeoutError:
+                return []
         loop = asyncio.get_running_loop()
         deadline = loop.time() + self.max_delay
         while len(batch) < self.max_batch:
-            try:
-                batch.append(q.get_nowait())
+            n0 = len(batch)
+            self._take(q, batch)
+            if len(batch) > n0:
                 continue
-            except asyncio.QueueEmpty:
-                pass
             remaining = deadline - loop.time()
             if remaining <= 0:
                 break
@@ -84,8 +121,62 @@ class BatchingParserTask:
         except Exception:  # noqa: BLE001  (mqtt.py:271-272)
             self.logger.error("Failed to publish message", exc_info=True)
 
+    def _cmd_check(self) -> bool:
+        """Whether _handle_as_command_response can have an effect now (see the module docstring)."""
+        c = self.c
+        pend = getattr(c, "_pending_responses", None)
+        if pend is None:
+            return True
+        lg = getattr(c, "logger", None)
+        return bool(pend) or (lg is not None and lg.isEnabledFor(logging.DEBUG))
+
+    async def _publish_texts(self, lines: List[Any], texts: List[Any]) -> None:
+        c = self.c
+        pub = c.mqtt_publisher
+        for line, res in zip(lines, texts):
+            if res is not None:
+                if isinstance(res, Exception):   # parse_line raised for this line
+                    self.logger.error("Parser error for line %r: %s", line, res)
+                elif pub:
+                    await self._publish_json(res)
+            if self._cmd_check():
+                await c._handle_as_command_response(line)
+
+    async def _run_stream(self) -> None:
+        """publish='json' through a pipelined LineStream (chunks = micro-batches)."""
+        c = self.c
+        if self._stream is None:
+            self._stream = c.parser.stream(chunk_lines=self.max_batch, output="json", lag=self.lag)
+        ls = self._stream
+        pending: Deque[List[Any]] = collections.deque()
+        while not c._stop_event.is_set():
+            try:
+                batch = await self._next_batch(self.max_delay if pending else None)
+                lines = [ln for ln in batch if ln]
+                if lines:
+                    await asyncio.to_thread(ls.submit, lines)
+                    pending.append(lines)
+                    self.batches += 1
+                    done = ls.poll()
+                elif pending:           # the queue ran dry: publish everything in flight
+                    done = await asyncio.to_thread(ls.drain)
+                else:
+                    done = []
+                for r in done:
+                    blines = pending.popleft()
+                    await self._publish_texts(blines, r.texts())
+                    self.lines += len(blines)
+                await asyncio.sleep(0)
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001  (controller.py:262-264)
+                self.logger.error(f"Parser task error: {e}")
+                break
+
     async def run(self) -> None:
         c = self.c
+        if self.use_stream:
+            return await self._run_stream()
         while not c._stop_event.is_set():
             try:
                 batch = await self._next_batch()
@@ -94,7 +185,6 @@ class BatchingParserTask:
                     parse = c.parser.parse_lines_json if self.publish == "json" else c.parser.parse_lines
                     results = await asyncio.to_thread(parse, lines)
                     self.batches += 1
-                    self.lines += len(lines)
                     for line, res in zip(lines, results):
                         if isinstance(res, Exception):  # parse_line raised for this line
                             self.logger.error("Parser error for line %r: %s", line, res)
@@ -107,7 +197,9 @@ class BatchingParserTask:
                                 await c.message_callback(res[0])
                             if c.mqtt_publisher and res:
                                 await c.mqtt_publisher.publish(res[0])
-                        await c._handle_as_command_response(line)
+                        if self._cmd_check():
+                            await c._handle_as_command_response(line)
+                    self.lines += len(lines)
                 await asyncio.sleep(0)
             except asyncio.CancelledError:
                 raise

@@ -265,6 +265,7 @@ __global__ __launch_bounds__(JT) void k_json(const void* __restrict__ bank, sdx_
   base = (uint32_t)__shfl((int)base, 0);
   ovf = __shfl(ovf, 0);
   if (g >= nitems) return;
+  if (in.first_only == 2 && !have) return;   // sparse: only the lines with a text (kinds share the outputs)
   const uint32_t off = base + incl - len;
   out.off_dev[g] = off;
   out.len_dev[g] = ovf ? 0u : len;

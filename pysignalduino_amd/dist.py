@@ -323,6 +323,16 @@ class Exchange:
         self.heap_wire_bytes = []  # per completed step: this rank's payload bytes on the wire (nibble form)
         self.reruns = 0         # launches re-run before exchanging
 
+    @classmethod
+    def sender(cls, engine=None) -> "Exchange":
+        """The wire serialiser alone (sdx_exchange_count / _pack on one device, no process group): e.g.
+        the streaming front end's compact results (stream.LineStream output='wire')."""
+        ex = cls.__new__(cls)
+        ex.group, ex.world, ex.rank, ex.engine, ex.defer = None, 1, 0, engine, False
+        ex.pending, ex.stream, ex._bufs, ex.last = None, None, {}, None
+        ex.bytes_sent, ex.wire_bytes, ex.payload_bytes, ex.heap_wire_bytes, ex.reruns = [], [], [], [], 0
+        return ex
+
     def _bank(self):
         return None if self.engine is None else self.engine.handle
 

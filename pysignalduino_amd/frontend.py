@@ -417,6 +417,15 @@ class SignalParser:
         return msgs
 
     # ------------------------------------------------------------------------------------------
+    def stream(self, chunk_lines: int = 250_000, chunk_bytes: Optional[int] = None, output: str = "json",
+               lag: int = 3):
+        """A pipelined LineStream over this parser (pysignalduino_amd/stream.py): chunks of raw lines
+        in, the controller's JSON texts (or the wire form) out, the PCIe copies, parse, demodulation
+        and serialisation of successive chunks overlapping; the same per-line results as
+        parse_lines_json / parse_lines."""
+        from .stream import LineStream
+        return LineStream(self, chunk_lines=chunk_lines, chunk_bytes=chunk_bytes, output=output, lag=lag)
+
     def parse_lines_json(self, lines: Sequence[Union[str, bytes]]) -> List[Union[Optional[str], Exception]]:
         """Per line, the MQTT message text the reference controller publishes for it:
         ``MqttPublisher._message_to_json(parse_line(line)[0])`` (signalduino/controller.py:254-257,

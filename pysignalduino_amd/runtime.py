@@ -504,8 +504,10 @@ class Engine:
         _check(self.lib, self.lib.sdx_demod_mn(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 
     def launch_json(self, kind: int, demod_out, lines_out, n: int, jout, first_only: bool = True) -> None:
-        """sdx_serialize_json over a demodulation launch's device outputs (no host sync)."""
-        ji = SdxJsonIn(kind, 1 if first_only else 0, _ptr(demod_out["desc"]), _ptr(demod_out["rec"]),
+        """sdx_serialize_json over a demodulation launch's device outputs (no host sync).  first_only:
+        True / 1 one text per line, 2 the same sparse (only lines with a text are written: launches of
+        several kinds share one output), False / 0 one text per record."""
+        ji = SdxJsonIn(kind, int(first_only), _ptr(demod_out["desc"]), _ptr(demod_out["rec"]),
                        _ptr(demod_out["cursor"]), _ptr(demod_out["heap"]), _ptr(lines_out["meta"]),
                        _ptr(lines_out.get("pat_val")), _ptr(lines_out.get("cp_slot")), n,
                        0 if first_only else demod_out["rec_cap"])

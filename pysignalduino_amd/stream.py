@@ -1,0 +1,400 @@
+"""Streaming front end: raw firmware lines -> decoded results, chunk after chunk, over PCIe.
+
+The reference decodes one line at a time in its controller's parser task
+(signalduino/controller.py:245-264: ``parser.parse_line(line)`` in a worker thread, then the first
+decoded message to the callback and the MQTT publisher, signalduino/mqtt.py:227-272).
+:class:`LineStream` is the device-rate form of that loop: chunks of raw lines in
+pinned host memory go to HBM, are parsed, demodulated and serialised there, and only the results
+come back -- with every stage of chunk k overlapping other chunks' stages on four HIP streams:
+
+  copy-in   chunk k's line bytes + offsets H2D                    (stage A, at submit(k))
+  parse     sdx_parse_lines + sdx_select_lines, class counts D2H  (stage A)
+  demod     the MU / MS short+long, MC ('fixed'), MN launches over the selection lists, then either
+            the publish-ready JSON texts (sdx_serialize_json, sparse: all kinds into one buffer)
+            or the exchange's wire form (sdx_exchange_count/pack), their sizes D2H   (stage B)
+  copy-out  the texts (or wire) + per-line kind/status D2H, sized from the device sizes  (stage C)
+
+The host only waits for events of chunks enqueued ``lag`` submits earlier (stage B of chunk k-1
+waits for k-1's class counts, stage C of k-2 for its sizes, the collection of k-3 for its copy),
+so the GPU always has a chunk queued behind the one it runs.  Lines the fast path does not finish
+-- the general path (multi-digit pattern ids, > 4096 pulses), lines outside the device contract,
+messages whose results overflowed their buffers (MC frames of > 128 hex characters, ST_OVF_*) --
+are taken by ``SignalParser.parse_lines_json`` / ``parse_lines`` on those lines only, so every
+line's result is exactly the batch API's.
+"""
+from __future__ import annotations
+
+import collections
+from typing import Any, Deque, List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import runtime
+from .packing import ContractError
+
+_KINDS = (("MU", runtime.KIND_MU, runtime.SEL_MU_SHORT, runtime.SEL_MU_LONG),
+          ("MS", runtime.KIND_MS, runtime.SEL_MS_SHORT, runtime.SEL_MS_LONG),
+          ("MC", runtime.KIND_MC, runtime.SEL_MC, None),
+          ("MN", runtime.KIND_MN, runtime.SEL_MN, None))
+
+
+class ChunkResult:
+    """One chunk's results in host memory.  json output: ``texts()`` -> per line the MQTT text the
+    reference publishes for it (``_message_to_json(parse_line(line)[0])``), None (nothing decoded) or
+    the line's ContractError.  wire output: ``sections(kind)`` -> the (msg, wire records, wire heap)
+    of that kind's launch (include/sdx.h wire v3, per line), ``decode(kind)`` -> (desc, rec, heap);
+    ``host`` holds the lines the batch API took (line index -> its parse_lines result).
+
+    The arrays are views of the stream's pinned buffers (no host copy on the critical path): they
+    stay valid until the stream's next submit(); ``detach()`` copies them out."""
+
+    def __init__(self, cid: int, n: int, kind: np.ndarray, status: np.ndarray):
+        self.id, self.n, self.kind, self.status = cid, n, kind, status
+        self.json = self.off = self.len = None
+        self.wire = self.layout = None
+        self.host = {}            # line -> result of the batch API (fallback lines)
+        self.affix = {}
+
+    def detach(self) -> "ChunkResult":
+        for f in ("kind", "status", "off", "len", "wire"):
+            v = getattr(self, f)
+            if isinstance(v, np.ndarray):
+                setattr(self, f, v.copy())
+        if isinstance(self.json, memoryview):
+            self.json = self.json.tobytes()
+        return self
+
+    def texts(self) -> List[Union[Optional[str], Exception]]:
+        out: List[Any] = [None] * self.n
+        blob = bytes(self.json)
+        rows = np.nonzero(self.len)[0]
+        for i, o, ln in zip(rows.tolist(), self.off[rows].tolist(), self.len[rows].tolist()):
+            out[i] = blob[o: o + ln].decode("ascii")
+        for i, r in self.host.items():
+            out[i] = r
+        return out
+
+    def sections(self, k: int):
+        offs, nb, T = self.layout
+        o = offs[0, k]
+        b = self.wire
+        return (b[o[0]: o[0] + nb[0, k, 0]].view(np.uint32), b[o[1]: o[1] + nb[0, k, 1]].view(runtime.WIRE_REC_DT),
+                b[o[2]: o[2] + nb[0, k, 2]])
+
+    def decode(self, k: int):
+        from . import dist as sdist
+        return sdist.wire_decode([self.sections(k)], self.affix.get(k))
+
+
+class _Slot:
+    """Device + pinned host buffers of one chunk in flight."""
+
+    def __init__(self, ls: "LineStream"):
+        from .frontend import LineBatch
+        t, eng = ls.torch, ls.eng
+        C, B = ls.C, ls.B
+        self.lb = LineBatch(eng, np.zeros(B, np.uint8), np.linspace(0, B, C + 1).astype(np.int64))
+        self.h_bytes = t.empty(B + 16, dtype=t.uint8).pin_memory()
+        self.h_offs = t.empty(C + 1, dtype=t.int64).pin_memory()
+        self.h_cnt = t.zeros(8, dtype=t.int32).pin_memory()
+        self.outs = {}
+        nmn = max(1, len(ls.bank.mn_pids))
+        caps = {"MU": (8 * C + 4096, 200 * C + 65536), "MS": (4 * C + 4096, 64 * C + 65536),
+                "MC": (4 * C + 4096, 96 * C + 65536), "MN": (nmn * C + 4096, 4 * B + 64 * C + 65536)}
+        for name, kd, _, _ in _KINDS:
+            if name == "MC" and not ls.mc:
+                continue
+            rc, hc = caps[name]
+            self.outs[name] = eng.alloc_out(C, rc, hc, eng.pulses_work_bytes(C) if name in ("MU", "MS") else 0)
+        self.gbufs = {name: eng.group_buffers(C) for name in ("MU", "MS")}
+        self.cursors = t.zeros((len(self.outs), 4), dtype=t.int32, device=eng.dev)
+        for j, o in enumerate(self.outs.values()):
+            o["cursor"] = self.cursors[j]
+        if ls.output == "json":
+            self.jcap = 600 * C + 65536
+            self.jout = eng.alloc_json(C, self.jcap)
+            self.h_sizes = t.zeros(2 + 4 * len(self.outs), dtype=t.int32).pin_memory()
+            self.h_out = t.empty(self.jcap + 10 * C + 64, dtype=t.uint8).pin_memory()
+        else:
+            from . import dist as sdist
+            self.ser = sdist.Exchange.sender(eng)
+            self.h_sizes = t.zeros(runtime.XCHG_COUNTS * len(self.outs) + 4 * len(self.outs), dtype=t.int32).pin_memory()
+            cap = sum(16 * C + 8 * o["rec_cap"] + o["heap_cap"] + 64 for o in self.outs.values())
+            self.h_out = t.empty(cap + 2 * C + 64, dtype=t.uint8).pin_memory()
+        self.reset()
+
+    def reset(self):
+        self.cid = -1
+        self.stage = 0
+        self.n = 0
+        self.lines = None
+        self.ev = None
+
+
+class LineStream:
+    """See the module docstring.  ``parser``: a frontend.SignalParser; ``chunk_lines`` /
+    ``chunk_bytes``: the capacity of one chunk; ``output``: "json" (the controller's publication) or
+    "wire" (per line and kind the exchange's wire form); ``lag``: chunks the host stays behind the
+    GPU (slots = lag + 1).
+
+    submit(lines) -> chunk id; ``submit_packed(data, offsets)`` the same for lines already packed as
+    (uint8 bytes, int64 offsets[n + 1]); poll() -> the finished chunks' ChunkResults in submission
+    order (never blocks on a chunk newer than ``lag`` submits); drain() -> all of them (blocks)."""
+
+    def __init__(self, parser, chunk_lines: int = 250_000, chunk_bytes: Optional[int] = None, output: str = "json",
+                 lag: int = 3):
+        if output not in ("json", "wire"):
+            raise ValueError("output must be 'json' or 'wire'")
+        import torch
+        self.torch = torch
+        self.parser = parser
+        self.eng = parser.protocols._ensure()
+        self.bank = parser.protocols._bank
+        self.mc = parser.protocols.mc_mode == "fixed"   # 'strict' MC reaches no device launch
+        self.output = output
+        self.C = int(chunk_lines)
+        self.B = int(chunk_bytes or 256 * self.C)
+        self.lag = max(1, int(lag))
+        self.slots = [_Slot(self) for _ in range(self.lag + 1)]
+        dev = self.eng.dev
+        self.cin, self.sp, self.sd, self.cout = (torch.cuda.Stream(dev) for _ in range(4))
+        self.inflight: Deque[_Slot] = collections.deque()
+        self.done: Deque[ChunkResult] = collections.deque()
+        self.next_id = 0
+        self.elig = parser.protocols.mn_eligibility(parser.rfmode)
+        self.h2d_bytes = self.d2h_bytes = 0
+        self.kernel_events = []   # (parse start, parse end, demod start, demod end) per chunk
+
+    # -- public ------------------------------------------------------------------------------------------
+    def submit(self, lines: Sequence[Union[str, bytes]]) -> int:
+        from .frontend import pack_lines
+        data, offsets, bad = pack_lines(lines)
+        return self.submit_packed(data, offsets, lines=lines, bad=bad)
+
+    def submit_packed(self, data: np.ndarray, offsets: np.ndarray, lines=None, bad=None) -> int:
+        n = len(offsets) - 1
+        if n > self.C or int(offsets[-1] - offsets[0]) > self.B:
+            raise ValueError(f"chunk of {n} lines / {int(offsets[-1] - offsets[0])} bytes exceeds the stream's "
+                             f"capacity ({self.C} lines, {self.B} bytes)")
+        while len(self.inflight) >= len(self.slots):     # every slot busy: finish the oldest chunk
+            self._advance(self.inflight[0], 4)
+        s = next(x for x in self.slots if x.stage == 0)
+        s.cid, s.n = self.next_id, n
+        s.lines, s.bad = lines, bad or {}
+        s.data, s.offsets = data, offsets
+        self.next_id += 1
+        self._stage_a(s, data, offsets)
+        self.inflight.append(s)
+        # the chunks behind: stage B for the previous one, C for the one before, collect the oldest
+        for age, want in ((1, 2), (2, 3), (3, 4)):
+            if len(self.inflight) > age and self.lag >= age:
+                self._advance(self.inflight[-1 - age], want)
+        return s.cid
+
+    def poll(self) -> List[ChunkResult]:
+        for s in list(self.inflight):      # stages B and C of any chunk whose previous stage is done
+            while s.stage in (1, 2) and s.ev.query():
+                self._advance(s, s.stage + 1)
+        while self.inflight and self.inflight[0].stage == 3 and self.inflight[0].ev.query():
+            self._advance(self.inflight[0], 4)     # results leave in submission order
+        return self._pop_done()
+
+    def drain(self) -> List[ChunkResult]:
+        while self.inflight:
+            self._advance(self.inflight[0], 4)
+        return self._pop_done()
+
+    # -- stages --------------------------------------------------------------------------------------------
+    def _pop_done(self):
+        out = []
+        while self.done:
+            out.append(self.done.popleft())
+        return out
+
+    def _advance(self, s: _Slot, want: int) -> bool:
+        if want >= 4:
+            while self.inflight and self.inflight[0] is not s:   # results leave in submission order
+                self._advance(self.inflight[0], 4)
+        while s.stage < want:
+            if s.stage == 1:
+                self._stage_b(s)
+            elif s.stage == 2:
+                self._stage_c(s)
+            elif s.stage == 3:
+                self._collect(s)
+        return True
+
+    def _stage_a(self, s: _Slot, data, offsets):
+        t = self.torch
+        n, nb = s.n, int(offsets[-1] - offsets[0])
+        s.h_bytes.numpy()[:nb] = data[int(offsets[0]): int(offsets[-1])]
+        s.h_bytes.numpy()[nb: nb + 16] = 0
+        s.h_offs.numpy()[: n + 1] = offsets - offsets[0]
+        lb = s.lb
+        with t.cuda.stream(self.cin):
+            lb.bytes[: nb + 16].copy_(s.h_bytes[: nb + 16], non_blocking=True)
+            lb.offsets[: n + 1].copy_(s.h_offs[: n + 1], non_blocking=True)
+            h2d = t.cuda.Event()
+            h2d.record(self.cin)
+        self.h2d_bytes += nb + 8 * (n + 1)
+        lb.n = n
+        lb.c_lines.n = n
+        with t.cuda.stream(self.sp):
+            self.sp.wait_event(h2d)
+            e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+            e0.record(self.sp)
+            lb.launch()
+            e1.record(self.sp)
+            s.h_cnt.copy_(lb.counts, non_blocking=True)
+            ev = t.cuda.Event()
+            ev.record(self.sp)
+        s.parse_ev, s.ev, s.kt = e1, ev, [e0, e1]
+        s.stage = 1
+
+    def _stage_b(self, s: _Slot):
+        """The demodulation + serialisation launches, sized by the class counts (on the host by now)."""
+        t, eng = self.torch, self.eng
+        s.ev.synchronize()
+        cnt = s.h_cnt.numpy()[: runtime.SEL_NCLASS].astype(np.int64)
+        start = np.concatenate([[0], np.cumsum(cnt)])
+        lb, n = s.lb, s.n
+        sels = [lb.sel[int(start[i]): int(start[i + 1])] for i in range(runtime.SEL_NCLASS)]
+        with t.cuda.stream(self.sd):
+            self.sd.wait_event(s.parse_ev)
+            e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+            e0.record(self.sd)
+            s.cursors.zero_()
+            pb = lb.pulse_batch()
+            for name, kd, short, long_ in _KINDS:
+                o = s.outs.get(name)
+                if o is None:
+                    continue
+                o["n"] = n
+                o["desc"][: 8 * n].zero_()          # lines of other classes keep an empty descriptor
+                if kd == runtime.KIND_MN:
+                    if cnt[short]:
+                        eng.launch_mn(lb.mn_batch(), o, elig=self.elig, sel=sels[short])
+                elif kd == runtime.KIND_MC:
+                    if cnt[short]:
+                        eng.launch_mc(lb.mc_batch(), o, sel=sels[short])
+                else:
+                    if cnt[short]:   # the grouped order (the slot's own grouping buffers: no shared cache)
+                        sel = (eng.group(kd, pb, sels[short], bufs=s.gbufs[name]) if cnt[short] >= runtime.GROUP_MIN
+                               else sels[short])
+                        eng.launch_pulses(kd, pb, o, sel=sel, group=False)
+                    if cnt[long_]:
+                        eng.launch_pulses(kd, pb, o, sel=sels[long_], long_variant=True)
+            s.cnt = cnt
+            if self.output == "json":
+                jo = s.jout
+                jo["cursor"].zero_()
+                jo["len"][:n].zero_()
+                lo = {"meta": lb.meta, "pat_val": lb.pat_val, "cp_slot": lb.cp_slot}
+                for name, kd, short, long_ in _KINDS:
+                    o = s.outs.get(name)
+                    if o is not None and (cnt[short] or (long_ is not None and cnt[long_])):
+                        eng.launch_json(kd, o, lo, n, jo, first_only=2)
+                s.h_sizes[:2].copy_(jo["cursor"], non_blocking=True)
+                s.h_sizes[2:].copy_(s.cursors.reshape(-1), non_blocking=True)
+            else:
+                from . import dist as sdist
+                parts = [sdist.Part(o["desc"], o["rec"], o["heap"], n, o["cursor"], kd)
+                         for name, kd, _, _ in _KINDS for o in [s.outs.get(name)] if o is not None]
+                wc = s.ser._count_pack_device(sdist._flatten(parts), self.sd)
+                k = len(parts)
+                s.h_sizes[: runtime.XCHG_COUNTS * k].copy_(wc, non_blocking=True)
+                s.h_sizes[runtime.XCHG_COUNTS * k:].copy_(s.cursors.reshape(-1), non_blocking=True)
+            e1.record(self.sd)
+            ev = t.cuda.Event()
+            ev.record(self.sd)
+        s.demod_ev, s.ev = e1, ev
+        s.kt += [e0, e1]
+        s.stage = 2
+
+    def _stage_c(self, s: _Slot):
+        """The results D2H, sized by the device sizes (on the host by now)."""
+        t = self.torch
+        s.ev.synchronize()
+        n, lb = s.n, s.lb
+        hs = s.h_sizes.numpy().astype(np.int64)
+        k = len(s.outs)
+        with t.cuda.stream(self.cout):
+            self.cout.wait_event(s.demod_ev)
+            ho = s.h_out
+            if self.output == "json":
+                T = int(min(hs[0], s.jcap))
+                s.ovf_json = bool(hs[1])
+                s.dcur = hs[2:].reshape(k, 4)
+                ho[:T].copy_(s.jout["json"][:T], non_blocking=True)
+                a = (T + 3) & ~3
+                ho[a: a + 4 * n].view(t.int32).copy_(s.jout["off"][:n].view(t.int32), non_blocking=True)
+                ho[a + 4 * n: a + 8 * n].view(t.int32).copy_(s.jout["len"][:n].view(t.int32), non_blocking=True)
+                b = a + 8 * n
+                s.lay = (T, a)
+            else:
+                from . import dist as sdist
+                S = hs[: runtime.XCHG_COUNTS * k].reshape(1, k, runtime.XCHG_COUNTS)
+                s.dcur = hs[runtime.XCHG_COUNTS * k:].reshape(k, 4)
+                s.S = S
+                offs, nb, T = sdist._layout(S)
+                ho[:T].copy_(s.ser._bufs["send"][:T], non_blocking=True)
+                b = T
+                s.lay = (offs, nb, T)
+            ho[b: b + n].copy_(lb.kind[:n], non_blocking=True)
+            ho[b + n: b + 2 * n].copy_(lb.status[:n], non_blocking=True)
+            s.kb = b
+            ev = t.cuda.Event()
+            ev.record(self.cout)
+        self.d2h_bytes += b + 2 * n
+        s.ev = ev
+        s.stage = 3
+
+    def _collect(self, s: _Slot):
+        s.ev.synchronize()
+        n, b = s.n, s.kb
+        ho = s.h_out.numpy()
+        kind = ho[b: b + n]
+        status = ho[b + n: b + 2 * n]
+        r = ChunkResult(s.cid, n, kind, status)
+        self.kernel_events.append(tuple(s.kt))
+        names = list(s.outs)
+        redo_kinds = {names[j] for j in range(len(names)) if s.dcur[j, 2]}   # ST_OVF_* in that launch
+        if self.output == "json":
+            T, a = s.lay
+            r.json = memoryview(ho[:T])
+            r.off = ho[a: a + 4 * n].view(np.uint32)
+            r.len = ho[a + 4 * n: a + 8 * n].view(np.uint32)
+            if s.ovf_json:
+                redo_kinds = set(names)            # the text buffer overflowed: the batch API for all
+        else:
+            r.wire = ho[: s.lay[2]]
+            r.layout = s.lay
+            r.affix = {j: self.bank.affixes(kd) for j, (name, kd, _, _) in
+                       enumerate(x for x in _KINDS if x[0] in s.outs)}
+            r.names = names
+            if s.S[0, :, 3].any():
+                redo_kinds |= {names[j] for j in range(len(names)) if s.S[0, j, 3]}
+        # the lines the fast path does not finish: the batch API on those lines only
+        kname = {runtime.LINE_MU: "MU", runtime.LINE_MS: "MS", runtime.LINE_MC: "MC", runtime.LINE_MN: "MN"}
+        rows = set(np.nonzero((status == runtime.LS_GENERAL) | (status == runtime.LS_UNSUPPORTED))[0].tolist())
+        rows |= set(s.bad)
+        if redo_kinds:
+            for kk, name in kname.items():
+                if name in redo_kinds:
+                    rows |= set(np.nonzero((kind == kk) & (status == runtime.LS_OK))[0].tolist())
+        if rows:
+            rows = sorted(rows)
+            lines = [self._line(s, i) for i in rows]
+            res = (self.parser.parse_lines_json(lines) if self.output == "json" else self.parser.parse_lines(lines))
+            for i, x in zip(rows, res):
+                r.host[i] = s.bad[i] if i in s.bad else x
+        self.done.append(r)
+        self.inflight.remove(s)
+        s.reset()
+        s.stage = 0
+
+    @staticmethod
+    def _line(s: _Slot, i: int):
+        if s.lines is not None:
+            return s.lines[i]
+        return bytes(s.data[int(s.offsets[i]): int(s.offsets[i + 1])])

@@ -39,6 +39,40 @@ class FakeParser:
         return [(json.dumps(r[0]) if r else None) if not isinstance(r, Exception) else r
                 for r in self.parse_lines(lines)]
 
+    def stream(self, chunk_lines, output="json", lag=3):
+        assert output == "json"
+        return FakeStream(self, lag)
+
+
+class _Chunk:
+    def __init__(self, texts):
+        self._t = texts
+
+    def texts(self):
+        return self._t
+
+
+class FakeStream:
+    """stream.LineStream's contract on the host: submit / poll (finished chunks in order, chunks
+    finish ``lag`` submits later) / drain."""
+
+    def __init__(self, parser, lag):
+        self.parser, self.lag, self.q, self.submitted = parser, lag, [], 0
+
+    def submit(self, lines):
+        self.q.append(_Chunk(self.parser.parse_lines_json(lines)))
+        self.submitted += 1
+        return self.submitted - 1
+
+    def poll(self):
+        k = max(0, len(self.q) - self.lag)
+        out, self.q = self.q[:k], self.q[k:]
+        return out
+
+    def drain(self):
+        out, self.q = self.q, []
+        return out
+
 
 class Pub:
     def __init__(self):
@@ -110,17 +144,50 @@ def test_batched_loop_matches_reference_loop():
     assert task.lines == 801
 
 
-def test_batched_loop_json_mode():
-    lines = [f"MC;D={i};" for i in range(200)]
+@pytest.mark.parametrize("stream", [True, False])
+def test_batched_loop_json_mode(stream):
+    """publish='json', through the pipelined stream (chunks finish 3 submits later, the rest when the
+    queue runs dry) and through parse_lines_json: the same publications in line order."""
+    lines = [f"MC;D={i};" for i in range(2000)] + ["boom", ""] + [f"MC;D=x{i};" for i in range(77)]
     parser = FakeParser()
     ctl = Ctl(parser, callback=False)
-    task = BatchingParserTask(ctl, publish="json").install()
+    task = BatchingParserTask(ctl, publish="json", max_batch=50, max_delay=0.005, stream=stream).install()
     assert ctl._parser_task == task.run
     asyncio.run(_drive(ctl, task, lines))
-    _, sent, _ = reference_side_effects(FakeParser(), lines)
+    _, sent, cmd = reference_side_effects(FakeParser(), lines)
     assert ctl.mqtt_publisher.sent == [("t/v1/state/messages", json.dumps(s[0])) for s in sent]
+    assert ctl.cmd == cmd and task.lines == len(cmd)
     with pytest.raises(ValueError):
         BatchingParserTask(Ctl(parser), publish="json")
+
+
+def test_command_response_skipped_only_without_effect():
+    """_handle_as_command_response (controller.py:360-387) is skipped only while the controller has
+    no pending responses and does not log at DEBUG; otherwise it runs for every line."""
+    lines = [f"MS;P0={i};D=01;" for i in range(300)]
+    for pending, level, want in (([], logging.WARNING, 0), (["cmd"], logging.WARNING, 300),
+                                 ([], logging.DEBUG, 300)):
+        parser = FakeParser()
+        ctl = Ctl(parser)
+        ctl._pending_responses = pending
+        ctl.logger = logging.getLogger(f"test.skip.{level}.{len(pending)}")
+        ctl.logger.setLevel(level)
+        task = BatchingParserTask(ctl, max_batch=64, max_delay=0.01)
+
+        async def go():
+            runner = asyncio.create_task(task.run())
+            for ln in lines:
+                ctl._raw_message_queue.put_nowait(ln)
+            while task.lines < len(lines):
+                await asyncio.sleep(0.01)
+            ctl._stop_event.set()
+            runner.cancel()
+            await asyncio.gather(runner, return_exceptions=True)
+
+        asyncio.run(go())
+        assert len(ctl.cmd) == want, (pending, level, len(ctl.cmd))
+        cb, _, _ = reference_side_effects(FakeParser(), lines)
+        assert ctl.cb == cb
 
 
 @pytest.mark.gpu

@@ -1,0 +1,100 @@
+"""The streaming front end (pysignalduino_amd/stream.py): LineStream's per-line results
+equal the batch API's (SignalParser.parse_lines_json / parse_lines) on mixed lines in many small
+chunks -- MU/MS/MC/MN, compressed lines, general-path lines (multi-digit ids), lines outside the
+device contract, MC frames of > 128 hex characters (ST_OVF_TILE re-runs) -- in submission order,
+with polls interleaved and a drain at the end."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _mixed_lines(golden, seed=7):
+    from pysignalduino_amd import bank as B, synth
+    P = B.Bank().protocols
+    rng = np.random.default_rng(seed)
+    raw, _ = synth.line_corpus(P, 9000, seed=seed, mix=(1, 1, 1), compress_frac=0.3)
+    raw += [synth.frame(synth.mn_payload(*f)) for f in synth.mn_frames(2000, seed=seed + 1)]
+    # general-path MU/MS lines (reference-recorded: multi-digit ids, > 4096 pulses) and long MC frames
+    raw += [c["line"].encode("latin-1") if isinstance(c["line"], str) else bytes(c["line"])
+            for c in golden("lines_general_golden.json.gz")][:200]
+    for h, c, L, t, v in synth.general_mc_frames(P, 30, seed=seed + 4):
+        c = max(int(c), 1)
+        raw.append(synth.frame(("%s;LL=%d;LH=%d;SL=%d;SH=%d;D=%s;C=%d;L=%d;R=10;"
+                                % (t, -2 * c, 2 * c, -c, c, h, c, L)).encode("latin-1")))
+    raw += [synth.mutate_line(rng, raw[int(rng.integers(0, len(raw)))]) for _ in range(500)]
+    idx = rng.permutation(len(raw))
+    return [raw[i] for i in idx]
+
+
+@pytest.mark.parametrize("output", ["json", "wire"])
+def test_stream_matches_batch_api(output, golden):
+    from pysignalduino_amd import runtime
+    from pysignalduino_amd.frontend import SignalParser
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    lines = _mixed_lines(golden)
+    sp = SignalParser(SDProtocols(mc_mode="fixed"))
+    ls = sp.stream(chunk_lines=1500, chunk_bytes=1500 * 4200, output=output, lag=3)
+    chunks = []
+    i = 0
+    rng = np.random.default_rng(3)
+    while i < len(lines):
+        k = int(rng.integers(200, 1501))
+        chunks.append(lines[i: i + k])
+        i += k
+    got = []
+    for j, ch in enumerate(chunks):
+        ls.submit(ch)
+        if j % 2:
+            got += [r.detach() for r in ls.poll()]
+    got += [r.detach() for r in ls.drain()]
+    assert [r.id for r in got] == list(range(len(chunks)))
+    bk = sp.protocols._bank
+    pid = {"MU": bk.mu_pids, "MS": bk.ms_pids, "MC": bk.mc_pids, "MN": bk.mn_pids}
+    lk = {runtime.LINE_MU: "MU", runtime.LINE_MS: "MS", runtime.LINE_MC: "MC", runtime.LINE_MN: "MN"}
+    nres = nhost = 0
+    for ch, r in zip(chunks, got):
+        assert r.n == len(ch)
+        nhost += len(r.host)
+        if output == "json":
+            exp = sp.parse_lines_json(ch)
+            for i, (e, g) in enumerate(zip(exp, r.texts())):
+                if isinstance(e, Exception):
+                    assert isinstance(g, type(e)), (i, e, g)
+                else:
+                    assert e == g, (i, e, g)
+                    nres += e is not None
+            continue
+        exp = sp.parse_lines(ch)
+        dec = {nm: r.decode(j) for j, nm in enumerate(r.names)}
+        for i, e in enumerate(exp):
+            if i in r.host:
+                g = r.host[i]
+                if isinstance(e, Exception):
+                    assert isinstance(g, type(e))
+                else:
+                    assert [(m.protocol_id, m.payload, m.metadata) for m in g] == \
+                        [(m.protocol_id, m.payload, m.metadata) for m in e]
+                continue
+            nm = lk.get(int(r.kind[i]))
+            if int(r.status[i]) != runtime.LS_OK or nm not in dec:
+                assert e == [], (i, e)
+                continue
+            d, rc, h = dec[nm]
+            got_i = [(str(pid[nm][int(x["proto"])]),
+                      h[int(x["payload_off"]): int(x["payload_off"]) + int(x["payload_len"])].tobytes().decode("latin-1"))
+                     for x in rc[int(d[i]["rec_begin"]): int(d[i]["rec_begin"]) + int(d[i]["n_rec"])]]
+            assert got_i == [(m.protocol_id, m.payload) for m in e], (i, got_i, e)
+            nres += bool(e)
+    assert nres > 3000 and nhost > 50, (nres, nhost)
+
+
+def test_stream_capacity_and_empty_chunk():
+    from pysignalduino_amd.frontend import SignalParser
+    sp = SignalParser()
+    ls = sp.stream(chunk_lines=100, chunk_bytes=100 * 300, output="json", lag=2)
+    with pytest.raises(ValueError):
+        ls.submit([b"\x02MU;P0=1;D=0;\x03"] * 101)
+    ls.submit([])
+    out = ls.drain()
+    assert len(out) == 1 and out[0].n == 0 and out[0].texts() == []
