@@ -668,6 +668,8 @@ class Bank:
         gcost = lambda g: MU_NORM_KCYC + sum(costs.get(str(self.mu_pids[r]), med) for r in g)  # noqa: E731
         if os.environ.get("SDX_MU_ORDER") == "size":   # A/B: the round-2 order (largest group first)
             glist = sorted(groups.values(), key=lambda g: -len(g))
+        elif os.environ.get("SDX_MU_ORDER") == "clock":  # A/B: no cost model (groups by clock)
+            glist = [groups[c] for c in sorted(groups)]
         else:
             glist = sorted(groups.values(), key=lambda g: (-gcost(g), -len(g)))
         # work items of at most ~MU_SPLIT_KCYC: a clock group whose cost exceeds it is cut at protocol

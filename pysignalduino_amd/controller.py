@@ -130,17 +130,60 @@ class BatchingParserTask:
         lg = getattr(c, "logger", None)
         return bool(pend) or (lg is not None and lg.isEnabledFor(logging.DEBUG))
 
-    async def _publish_texts(self, lines: List[Any], texts: List[Any]) -> None:
+    async def _publish_items(self, lines: List[Any], items: List[Any]) -> None:
+        """The reference's per-line effects for one chunk, from its sparse results ``items`` =
+        [(line index, text or exception)] in line order: per line, the publication of its text, then
+        its _handle_as_command_response turn if _cmd_check() holds at that point.  The check can only
+        change across an await, so after a false check the lines up to the next result (nothing is
+        awaited for them) are skipped without re-checking."""
         c = self.c
-        pub = c.mqtt_publisher
-        for line, res in zip(lines, texts):
-            if res is not None:
-                if isinstance(res, Exception):   # parse_line raised for this line
-                    self.logger.error("Parser error for line %r: %s", line, res)
-                elif pub:
-                    await self._publish_json(res)
-            if self._cmd_check():
+        pend = getattr(c, "_pending_responses", None)
+        if pend is None:        # no pending-response list: every line gets its turn
+            res_at = dict(items)
+            for i, line in enumerate(lines):
+                res = res_at.get(i)
+                if res is not None:
+                    await self._publish_one(line, res)
                 await c._handle_as_command_response(line)
+            return
+        lg = getattr(c, "logger", None)
+        dbg = lg.isEnabledFor if lg is not None else (lambda _lv: False)
+        handle = c._handle_as_command_response
+        pub = c.mqtt_publisher
+        client = getattr(pub, "client", None) if pub else None
+        topic = f"{pub.base_topic}/state/messages" if client else None
+        log = self.logger
+        D = logging.DEBUG
+        quiet = not (pend or dbg(D))    # the check for the next line
+        j = 0                           # the next line whose turn is still open
+        for i, res in items + [(len(lines), None)]:
+            while not quiet and j < i:  # lines without a result: their command-response turns
+                await handle(lines[j])
+                j += 1
+                quiet = not (pend or dbg(D))
+            if i == len(lines):
+                break
+            if isinstance(res, Exception):   # parse_line raised for this line
+                log.error("Parser error for line %r: %s", lines[i], res)
+            elif pub:
+                if not client:
+                    log.warning("Attempted to publish without an active MQTT client.")
+                else:
+                    try:
+                        await client.publish(topic, res)
+                    except Exception:  # noqa: BLE001  (mqtt.py:271-272)
+                        log.error("Failed to publish message", exc_info=True)
+                    quiet = not (pend or dbg(D))
+            if not quiet:
+                await handle(lines[i])
+                quiet = not (pend or dbg(D))
+            j = i + 1
+
+    async def _publish_one(self, line: Any, res: Any) -> None:
+        if isinstance(res, Exception):   # parse_line raised for this line
+            self.logger.error("Parser error for line %r: %s", line, res)
+        elif self.c.mqtt_publisher:
+            await self._publish_json(res)
 
     async def _run_stream(self) -> None:
         """publish='json' through a pipelined LineStream (chunks = micro-batches)."""
@@ -164,7 +207,9 @@ class BatchingParserTask:
                     done = []
                 for r in done:
                     blines = pending.popleft()
-                    await self._publish_texts(blines, r.texts())
+                    items = r.items() if hasattr(r, "items") else [(i, t) for i, t in enumerate(r.texts())
+                                                                  if t is not None]
+                    await self._publish_items(blines, items)
                     self.lines += len(blines)
                 await asyncio.sleep(0)
             except asyncio.CancelledError:

@@ -25,7 +25,7 @@ line's result is exactly the batch API's.
 from __future__ import annotations
 
 import collections
-from typing import Any, Deque, List, Optional, Sequence, Union
+from typing import Any, Deque, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -66,13 +66,21 @@ class ChunkResult:
 
     def texts(self) -> List[Union[Optional[str], Exception]]:
         out: List[Any] = [None] * self.n
-        blob = bytes(self.json)
-        rows = np.nonzero(self.len)[0]
-        for i, o, ln in zip(rows.tolist(), self.off[rows].tolist(), self.len[rows].tolist()):
-            out[i] = blob[o: o + ln].decode("ascii")
-        for i, r in self.host.items():
+        for i, r in self.items():
             out[i] = r
         return out
+
+    def items(self) -> List[Tuple[int, Union[str, Exception]]]:
+        """(line, text or ContractError) for the lines that publish something, in line order: the
+        sparse form of texts() (one ASCII decode of the chunk's text buffer, one slice per text)."""
+        rows = np.nonzero(self.len)[0]
+        blob = bytes(self.json).decode("ascii")
+        dev = zip(rows.tolist(), [blob[o: o + ln] for o, ln in zip(self.off[rows].tolist(), self.len[rows].tolist())])
+        if not self.host:
+            return list(dev)
+        d = dict(dev)
+        d.update(self.host)
+        return [(i, d[i]) for i in sorted(d) if d[i] is not None]
 
     def sections(self, k: int):
         offs, nb, T = self.layout

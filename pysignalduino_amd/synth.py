@@ -161,11 +161,17 @@ def _templates(protocols: Dict[str, dict], key_start: str):
 
 
 def _assemble(rng, n, tpls, npulse_fn, repeat: bool, clock_sweep, noise_frac: float, kind: str,
-              fixed_len: Optional[int]):
-    """Shared vectorised MU/MS message assembly (padded [n, Tmax] then packed ragged)."""
+              fixed_len: Optional[int], skew: float = 0.0):
+    """Shared vectorised MU/MS message assembly (padded [n, Tmax] then packed ragged).  skew > 0:
+    templates drawn with Zipf weights 1 / rank^skew over a seeded ranking (a capture dominated by a
+    few protocols) instead of uniformly."""
     ntpl = len(tpls)
     Tmax = fixed_len if fixed_len else 256
-    choice = rng.integers(0, ntpl, size=n)
+    if skew > 0:
+        w = 1.0 / np.arange(1, ntpl + 1, dtype=np.float64) ** skew
+        choice = rng.permutation(ntpl)[rng.choice(ntpl, size=n, p=w / w.sum())]
+    else:
+        choice = rng.integers(0, ntpl, size=n)
     is_noise = rng.random(n) < noise_frac
     npat = np.zeros(n, np.uint8)
     pat_id = np.zeros((n, MAXPAT), np.uint8)
@@ -249,14 +255,15 @@ def _assemble(rng, n, tpls, npulse_fn, repeat: bool, clock_sweep, noise_frac: fl
 
 
 def mu_corpus(protocols: Dict[str, dict], n: int, seed: int = 42, npulse: int = 256,
-              noise_frac: float = 0.15) -> PulseBatch:
+              noise_frac: float = 0.15, skew: float = 0.0) -> PulseBatch:
     """Config 2: MU messages of exactly ``npulse`` pulses, frames repeated."""
     rng = np.random.default_rng(seed)
     tpls = _templates(protocols, "start")
-    return _assemble(rng, n, tpls, None, True, lambda r, m: np.ones(m), noise_frac, "MU", npulse)
+    return _assemble(rng, n, tpls, None, True, lambda r, m: np.ones(m), noise_frac, "MU", npulse, skew)
 
 
-def ms_corpus(protocols: Dict[str, dict], n: int, seed: int = 43, noise_frac: float = 0.1) -> PulseBatch:
+def ms_corpus(protocols: Dict[str, dict], n: int, seed: int = 43, noise_frac: float = 0.1,
+              skew: float = 0.0) -> PulseBatch:
     """Config 3: one sync+bits frame per message, clock swept x U(0.6,1.4) over the ±30 % gate."""
     rng = np.random.default_rng(seed)
     tpls = _templates(protocols, "sync")
@@ -267,7 +274,7 @@ def ms_corpus(protocols: Dict[str, dict], n: int, seed: int = 43, noise_frac: fl
         return np.minimum(frame_len + extra, 256)
 
     return _assemble(rng, n, tpls, npulse_fn, True, lambda r, m: r.uniform(0.6, 1.4, size=m),
-                     noise_frac, "MS", None)
+                     noise_frac, "MS", None, skew)
 
 
 def mc_protocols(protocols: Dict[str, dict]) -> List[int]:

@@ -212,12 +212,12 @@ def test_mu_clock_divider_is_exact():
     """The MU integer normalisation (sdx_mu_filt clk_c/clk_m/clk_sh, bank.clock_divider): for every
     MU clock, floor(x / c) == (x * m) >> sh over the device's input range (x = 10|P| < 2^30), at
     every multiple of c +- 1 on a grid and on random x; and the rounding built on it (half-even on
-    the exact remainder, ties to the fp64 path) equals Python's round(P / clockabs, 1) * 10."""
+    the exact remainder, exact ties by fl((2q + 1) / 20)) equals Python's round(P / clockabs, 1) * 10."""
     import numpy as np
     bk = bankmod.Bank()
     rng = np.random.default_rng(3)
     clocks = sorted({float(c) for c in bk.mu_clock})
-    checked = 0
+    checked = ties = 0
     for clock in clocks:
         c, m, shf = bankmod.clock_divider(clock)
         if not (shf >> 8) & 1:
@@ -228,16 +228,21 @@ def test_mu_clock_divider_is_exact():
         x = np.concatenate([q * c, q * c + 1, np.maximum(q * c, 1) - 1, rng.integers(0, 1 << 30, 20000).astype(np.uint64)])
         x = x[x < (1 << 30)].astype(np.uint64)
         assert np.array_equal((x * np.uint64(m)) >> np.uint64(sh), x // np.uint64(c)), clock
-        # integral P: k from the integer remainder vs round(P / clock, 1) (exact ties excluded:
-        # the device sends those to the fp64 path)
-        P = rng.integers(-(1 << 20), 1 << 20, 3000)
-        for p in P.tolist():
+        # integral P: k from the integer remainder vs round(P / clock, 1); exact rational ties
+        # (2r == c) round like fl((2q + 1) / 20), the same correctly rounded quotient
+        P = rng.integers(-(1 << 20), 1 << 20, 3000).tolist()
+        if c % 2 == 0:   # planted ties: 10|P| = q c + c / 2
+            P += [s * (qq * c + c // 2) // 10 for qq in rng.integers(0, (1 << 20) // c, 3000).tolist()
+                  for s in (1, -1) if (qq * c + c // 2) % 10 == 0]
+        for p in P:
             xx = 10 * abs(p)
             qq, r = divmod(xx, c)
             if 2 * r == c:
-                continue
-            k = qq + (1 if 2 * r > c else 0)
+                k = round(round((2 * qq + 1) / 20, 1) * 10)
+                ties += 1
+            else:
+                k = qq + (1 if 2 * r > c else 0)
             k = -k if (p < 0) != (clock < 0) else k
             assert k == round(round(p / clock, 1) * 10), (p, clock)
         checked += 1
-    assert checked >= 10
+    assert checked >= 10 and ties > 1000, (checked, ties)

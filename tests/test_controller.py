@@ -215,3 +215,57 @@ def test_batched_loop_with_the_gpu_parser():
     ctl2 = Ctl(sp, callback=False)
     asyncio.run(_drive(ctl2, BatchingParserTask(ctl2, max_batch=512, publish="json"), lines, chunk=200))
     assert [t for _, t in ctl2.mqtt_publisher.sent] == [J.published([d]) for d in exp]
+
+
+def test_json_stream_command_turns_follow_state_changes():
+    """publish='json' through the stream: a publisher that adds / clears pending responses while
+    publishing (as another task could during the await) -- every line gets its command-response turn
+    exactly when the reference loop would check true for it (controller.py:245-264, 360-387)."""
+    lines = [f"MC;D={i};" for i in range(3000)]
+    parser = FakeParser()
+    texts = parser.parse_lines_json(lines)
+
+    class TogglePub(Pub):
+        def __init__(self, ctl):
+            super().__init__()
+            self.ctl = ctl
+
+        async def publish(self, *a):
+            self.sent.append(a)
+            n = len(self.sent)
+            if n % 97 == 0:
+                self.ctl._pending_responses.append("cmd")
+            elif n % 97 == 5:
+                self.ctl._pending_responses.clear()
+
+    ctl = Ctl(parser, callback=False)
+    ctl._pending_responses = []
+    ctl.logger = logging.getLogger("test.toggle")
+    ctl.logger.setLevel(logging.WARNING)
+    ctl.mqtt_publisher = TogglePub(ctl)
+    # the reference loop's turns under the same state changes
+    exp_cmd, pend, nsent = [], [], 0
+    for ln, t in zip(lines, texts):
+        if t is not None:
+            nsent += 1
+            if nsent % 97 == 0:
+                pend.append("cmd")
+            elif nsent % 97 == 5:
+                pend.clear()
+        if pend:
+            exp_cmd.append(ln)
+    task = BatchingParserTask(ctl, publish="json", max_batch=200, max_delay=0.005)
+
+    async def go():
+        runner = asyncio.create_task(task.run())
+        for ln in lines:
+            ctl._raw_message_queue.put_nowait(ln)
+        while task.lines < len(lines):
+            await asyncio.sleep(0.01)
+        ctl._stop_event.set()
+        runner.cancel()
+        await asyncio.gather(runner, return_exceptions=True)
+
+    asyncio.run(go())
+    assert [t for _, t in ctl.mqtt_publisher.sent] == [t for t in texts if t is not None]
+    assert ctl.cmd == exp_cmd and 0 < len(exp_cmd) < len(lines)

@@ -89,6 +89,37 @@ def test_synthetic_vs_oracle(proto, obank, kind, seed, n):
     assert not bad, f"{len(bad)}/{n} mismatches; first: {bad[:2]}"
 
 
+def test_mu_exact_rational_ties_vs_oracle(proto, obank):
+    """MU pattern values planted on exact rational ties of the bank's clocks (10|P| = q c + c / 2):
+    the device rounds those by fl((2q + 1) / 20) instead of reloading P (round 4); every message
+    must still equal the oracle's round(P / clock, 1) result."""
+    from pysignalduino_amd import synth
+    rng = np.random.default_rng(77)
+    P = proto.get_protocol_list()
+    clocks = sorted({int(float(p["clockabs"])) for p in P.values()
+                     if "clockabs" in p and "sync" not in p and float(p["clockabs"]).is_integer()
+                     and int(float(p["clockabs"])) % 2 == 0})
+    pb = synth.mu_corpus(P, 1500, seed=78)
+    msgs = [pb.to_msg_dict(i) for i in range(pb.n)] + synth.planted_pulse_messages(P, "MU", 500, seed=79)
+    ties = 0
+    for m in msgs:
+        c = clocks[int(rng.integers(0, len(clocks)))]
+        for key in [k for k in m if k[:1] == "P" and k[1:].isdigit()]:
+            v = int(float(m[key]))
+            q0 = 10 * abs(v) // c
+            for q in sorted(range(max(0, q0 - 12), q0 + 12), key=lambda q: abs(q - q0)):
+                if (q * c + c // 2) % 10 == 0:
+                    m[key] = str((-1 if v < 0 else 1) * ((q * c + c // 2) // 10))
+                    ties += 1
+                    break
+    assert ties > 4000, ties
+    got = proto.demodulate_batch(msgs, "MU")
+    exp = [_oracle(obank, m, "MU") for m in msgs]
+    bad = [(i, m, e, _flat(g)) for i, (m, e, g) in enumerate(zip(msgs, exp, got)) if _flat(g) != e]
+    assert not bad, f"{len(bad)}/{len(msgs)} mismatches; first: {bad[:2]}"
+    assert sum(bool(_flat(g).get("results")) for g in got) > 200
+
+
 def test_long_messages_vs_oracle(proto, obank):
     """Messages beyond 256 pulses run through the long-message kernel variant."""
     from pysignalduino_amd import synth

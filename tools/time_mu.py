@@ -16,8 +16,13 @@ def main():
     bk = bankmod.Bank()
     eng = runtime.Engine(bk, 0)
     res = []
+    # SDX_CORPUS: bench (default) | dense (no noise messages) | zipf (templates drawn with Zipf
+    # weights, skew 1.2: a capture dominated by a few protocols) -- the A/B corpora of the
+    # profile-guided processing order (bank.py MU_COST_KCYC / MS_COST_KCYC)
+    corpus = os.environ.get("SDX_CORPUS", "bench")
+    kw = {"dense": {"noise_frac": 0.0}, "zipf": {"skew": 1.2}}.get(corpus, {})
     for kind, gen in (("MU", synth.mu_corpus), ("MS", synth.ms_corpus)):
-        pb = gen(bk.protocols, n, seed=42)
+        pb = gen(bk.protocols, n, seed=42, **kw)
         bd = eng.to_device_pulses(pb)
         out = eng.alloc_out(pb.n, 12 * pb.n + 4096, 320 * pb.n + 65536, eng.pulses_work_bytes(pb.n))
         k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
@@ -34,7 +39,7 @@ def main():
             ts.append(e0.elapsed_time(e1))
         cur = out["cursor"].cpu().numpy()
         res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) * 112 >> 10} MB)")
-    tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped") + (" order=" + os.environ.get("SDX_MU_ORDER", "lpt"))
+    tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped") + (" order=" + os.environ.get("SDX_MU_ORDER", "lpt")) + " corpus=" + corpus
     print(tag, " | ".join(res), flush=True)
 
 
