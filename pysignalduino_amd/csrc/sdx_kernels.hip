@@ -65,59 +65,6 @@ constexpr int POOL_HEAP = 16384; // MU/MS: staged payload bytes per tile
 constexpr int POOL_REC_MS = 256;   // short MS tiles: ~1 result per message; smaller LDS -> more tiles/CU
 constexpr int POOL_HEAP_MS = 8192;
 
-// A protocol's 128-byte lane-filter record (sdx_mu_filt / sdx_ms_filt) held in ONE vector register
-// of the wave: lane l (< 32) holds dword l, loaded with a single coalesced global load one protocol
-// ahead of its use; fields are read with v_readlane (wave-uniform results in SGPRs).  A scalar load
-// of the record would be waited for by the first LDS access after it (both count in lgkmcnt),
-// so a scalar prefetch hides nothing; the vector load is waited for (vmcnt) only where the next
-// iteration first reads it.
-struct FiltReg {
-  uint32_t v;
-  SDX_DEV uint32_t u(int k) const { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
-  SDX_DEV uint64_t q(int k) const { return (uint64_t)u(k) | ((uint64_t)u(k + 1) << 32); }
-  SDX_DEV double d(int k) const { return __longlong_as_double((long long)q(k)); }
-  // the compact search list whose sdx_fspec starts at dword k0 (upk: the list's position pack)
-  SDX_DEV SpecV spec(int k0, uint64_t upk) const {
-    SpecV s;
-    const uint32_t w = u(k0 + 4), rk01 = u(k0 + 3);
-    s.nu = (int)(w >> 24);
-    s.slen = (int)((w >> 16) & 0xFF);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const uint32_t lh = u(k0 + i);
-      s.klo[i] = (int)(int16_t)(lh & 0xFFFF);
-      s.khi[i] = (int)(int16_t)(lh >> 16);
-    }
-    s.klo[3] = 0;
-    s.khi[3] = -1;
-    s.rk_off[0] = rk01 & 0xFFFF;
-    s.rk_off[1] = rk01 >> 16;
-    s.rk_off[2] = w & 0xFFFF;
-    s.rk_off[3] = 0;
-    s.upk = upk;
-    return s;
-  }
-  SDX_DEV int klen(int k0) const { return (int)((u(k0 + 4) >> 16) & 0xFF); }
-};
-template <class F>
-SDX_DEV uint32_t filt_load(const F* rec, int lane) {
-  return lane < 32 ? reinterpret_cast<const uint32_t*>(rec)[lane] : 0u;
-}
-// dword offsets of the fields FiltReg reads (include/sdx_bank.h)
-constexpr int MUF_CLOCK = 0, MUF_START_UPK = 2, MUF_FLAGS = 4, MUF_SPEC = 5, MUF_CLK_C = 29, MUF_CLK_M = 30,
-              MUF_CLK_SH = 31;
-constexpr int MSF_PCLOCK = 0, MSF_SYNC_UPK = 2, MSF_FLAGS = 4, MSF_WIDTH = 5, MSF_LMIN = 6, MSF_SPEC = 7;
-static_assert(offsetof(sdx_mu_filt, clock) == 4 * MUF_CLOCK && offsetof(sdx_mu_filt, start_upk) == 4 * MUF_START_UPK &&
-                  offsetof(sdx_mu_filt, flags) == 4 * MUF_FLAGS && offsetof(sdx_mu_filt, spec) == 4 * MUF_SPEC &&
-                  offsetof(sdx_mu_filt, clk_c) == 4 * MUF_CLK_C && offsetof(sdx_mu_filt, clk_m) == 4 * MUF_CLK_M &&
-                  offsetof(sdx_mu_filt, clk_sh) == 4 * MUF_CLK_SH && sizeof(sdx_fspec) == 24 &&
-                  offsetof(sdx_fspec, rk01) == 12 && offsetof(sdx_fspec, rk2_len_nu) == 16 && offsetof(sdx_fspec, upk) == 20,
-              "sdx_mu_filt dword map");
-static_assert(offsetof(sdx_ms_filt, pclock) == 4 * MSF_PCLOCK && offsetof(sdx_ms_filt, sync_upk) == 4 * MSF_SYNC_UPK &&
-                  offsetof(sdx_ms_filt, flags) == 4 * MSF_FLAGS && offsetof(sdx_ms_filt, width) == 4 * MSF_WIDTH &&
-                  offsetof(sdx_ms_filt, lmin_sync) == 4 * MSF_LMIN && offsetof(sdx_ms_filt, spec) == 4 * MSF_SPEC,
-              "sdx_ms_filt dword map");
-
 struct StageRec {
   uint32_t off;
   uint16_t len, proto;
@@ -1933,9 +1880,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   int g_cur = -1;
   unsigned long long g_t0 = 0;
 #endif
-  // the next protocol in this wave's processing order (-1: no work left); a new work item is
-  // grabbed when the current one is used up, i.e. while its last protocol is still to run
-  auto next_proto = [&]() -> int {
+  while (true) {
     if (cur == cend) {
       int g = 0;
       if (lane == 0) g = atomicAdd(&L.next_p, 1);
@@ -1948,7 +1893,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       g_cur = g;
       g_t0 = __builtin_amdgcn_s_memtime();
 #endif
-      if (g >= ngrab) return -1;
+      if (g >= ngrab) break;
       if (KIND == SDX_KIND_MU) {
         cur = cld(&gstart[g]);
         cend = cld(&gstart[g + 1]);
@@ -1957,23 +1902,12 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         cend = g + 1;
       }
     }
-    return cld(&order[cur++]);
-  };
-  auto filt_of = [&](int p) -> uint32_t {
-    if constexpr (KIND == SDX_KIND_MU) return filt_load(bv.mufilt + p, lane);
-    else return filt_load(bv.msfilt + p, lane);
-  };
-  // the filter record of protocol p_next is in flight while protocol p runs
-  int p_next = next_proto();
-  uint32_t f_next = p_next >= 0 ? filt_of(p_next) : 0u;
-  while (p_next >= 0) {
-    const int p = p_next;
-    const FiltReg F{f_next};
-    p_next = next_proto();
-    if (p_next >= 0) f_next = filt_of(p_next);
+    const int p = cld(&order[cur]);
+    ++cur;
     if constexpr (KIND == SDX_KIND_MU) {
       const sdx_mu_proto* rec = uniform_ptr(bv.mu + p);
-      const uint32_t ff = F.u(MUF_FLAGS);
+      const sdx_mu_filt* fr = uniform_ptr(bv.mufilt + p);  // the filter's state: two 64-byte lines
+      const uint32_t ff = cld(&fr->flags);
       if ((ff & 2u) || !(ff & 4u)) continue;  // never / not active
       const bool full = (ff & 8u) != 0;
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
@@ -1981,7 +1915,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       uint64_t st_tgt = 0, ut0 = 0, ut1 = 0, ut2 = 0;
       int fmask = 0;
       PROF_T(t_norm);
-      const double pclk = F.d(MUF_CLOCK);
+      const double pclk = cld(&fr->clock);
       if (pclk != last_clock) {  // wave-uniform: consecutive protocols often share a clock
         last_clock = pclk;
         if constexpr (LANE_MU) {
@@ -1990,11 +1924,11 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           // fl(P / clock) differs from the rational by < 2^-23 while a non-tie is >= 1 / (2 |clock|)
           // from a rounding boundary.  An exact rational tie |P| / |clock| == (2q + 1) / 20 rounds
           // like fl((2q + 1) / 20): both are the correctly rounded quotient of the same rational,
-          // so py_round1_k of it needs no pattern value (the tie used to reload P from HBM,
-          // a divergent global load in ~every wave's normalisation).  Non-integral P and clocks
-          // outside the divider's range use py_round1_k on fl(P / clock).
-          const uint32_t csh = F.u(MUF_CLK_SH);
-          const uint32_t cc = F.u(MUF_CLK_C), cm = F.u(MUF_CLK_M), sh = csh & 0xFFu;
+          // so py_round1_k of it needs no pattern value (it used to reload P from HBM: MU 1.119-1.128
+          // -> 1.111-1.114 ms, profiles/r04/ab_tie.log).  Non-integral P and clocks outside the
+          // divider's range use py_round1_k on fl(P / clock).
+          const uint32_t csh = cld(&fr->clk_sh);
+          const uint32_t cc = cld(&fr->clk_c), cm = cld(&fr->clk_m), sh = csh & 0xFFu;
           const bool ivalid = (csh & 0x100u) != 0, cneg = (csh & 0x200u) != 0;
 #pragma unroll
           for (int k = 0; k < SDX_MAXPAT; ++k) {
@@ -2022,7 +1956,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       PROF_ADD(1, t_norm);
       auto SV = [&](int key, const sdx_patspec* sp) -> SpecV {
         if constexpr (NW <= 4) {
-          if (!full) return F.spec(MUF_SPEC + 6 * key, key == 0 ? F.q(MUF_START_UPK) : (uint64_t)F.u(MUF_SPEC + 6 * key + 5));
+          if (!full) return spec_compact(&fr->spec[key], key == 0 ? cld(&fr->start_upk) : (uint64_t)cld(&fr->spec[key].upk));
           return spec_full(sp);
         } else {
           return SpecV{};
@@ -2039,7 +1973,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       }
       PROF_ADD(2, t_st);
       PROF_T(t_ozf);
-      auto klen = [&](int key) -> int { return F.klen(MUF_SPEC + 6 * key); };
+      auto klen = [&](int key) -> int { return (int)((cld(&fr->spec[key].rk2_len_nu) >> 16) & 0xFF); };
       if (alive && klen(1)) {
         const PexRes r = PEXV(SV(1, &rec->one), &rec->one, idx, false);
         if (r.found) { ut0 = r.tgt; fmask |= 1; } else alive = false;
@@ -2090,11 +2024,12 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       PROF_ADD(12, t_dec);
     } else {
       const sdx_ms_proto* rec = uniform_ptr(bv.ms + p);
-      const uint32_t ff = F.u(MSF_FLAGS);
+      const sdx_ms_filt* fr = uniform_ptr(bv.msfilt + p);  // the filter's state: two 64-byte lines
+      const uint32_t ff = cld(&fr->flags);
       if (ff & 2u) continue;  // never
       const bool full = (ff & 8u) != 0;
       bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
-      const double pclk = F.d(MSF_PCLOCK);
+      const double pclk = cld(&fr->pclock);
       if (alive && pclk > 0.0)  // clock tolerance gate (:83-88)
         alive = !(fabs(pclk - clock) > clock * 0.3);
       int start = 0;
@@ -2102,22 +2037,22 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       int fmask = 0;
       auto SV = [&](int key) -> SpecV {
         if constexpr (NW <= 4) {
-          if (!full) return F.spec(MSF_SPEC + 6 * key, key == 0 ? F.q(MSF_SYNC_UPK) : (uint64_t)F.u(MSF_SPEC + 6 * key + 5));
+          if (!full) return spec_compact(&fr->spec[key], key == 0 ? cld(&fr->sync_upk) : (uint64_t)cld(&fr->spec[key].upk));
           return spec_full(&rec->key[key]);
         } else {
           return SpecV{};
         }
       };
-      auto klen = [&](int key) -> int { return F.klen(MSF_SPEC + 6 * key); };
+      auto klen = [&](int key) -> int { return (int)((cld(&fr->spec[key].rk2_len_nu) >> 16) & 0xFF); };
       if (alive && klen(0)) {  // sync (:140-158)
         const PexRes r = PEXV(SV(0), &rec->key[0], 0, true);
         if (r.found) {
           kt0 = r.tgt;
           fmask |= 1;
           start = r.pos + klen(0);
-          const int width = (int)F.u(MSF_WIDTH);
+          const int width = cld(&fr->width);
           const double avail = width > 0 ? (double)(n - start) / (double)width : 0.0;
-          if ((double)(int)F.u(MSF_LMIN) > avail) alive = false;
+          if ((double)cld(&fr->lmin_sync) > avail) alive = false;
         } else alive = false;
       }
       if (alive && klen(1)) {

@@ -223,7 +223,7 @@ class LineStream:
         if want >= 4:
             while self.inflight and self.inflight[0] is not s:   # results leave in submission order
                 self._advance(self.inflight[0], 4)
-        while s.stage < want:
+        while 0 < s.stage < want:      # _collect frees the slot (stage 0): nothing left to advance
             if s.stage == 1:
                 self._stage_b(s)
             elif s.stage == 2:

@@ -5,7 +5,7 @@
   clock  no cost model: MU groups in clock order, unsplit; MS in bank order
   size   the round-2 order: MU largest group first, unsplit; MS in bank order
 Each (corpus, order) runs in its own process (the order is fixed when the bank is compiled),
-twice, interleaved.  usage: python tools/ab_order.py [n]"""
+``reps`` times, interleaved.  usage: python tools/ab_order.py [n] [reps]"""
 import os
 import subprocess
 import sys
@@ -17,8 +17,9 @@ ORDERS = {"lpt": {}, "clock": {"SDX_MU_ORDER": "clock", "SDX_MU_SPLIT": "0", "SD
 
 def main():
     n = sys.argv[1] if len(sys.argv) > 1 else "333333"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     for corpus in ("bench", "dense", "zipf"):
-        for rep in (1, 2):
+        for rep in range(1, reps + 1):
             for name, env in ORDERS.items():
                 e = dict(os.environ, SDX_CORPUS=corpus, **env)
                 r = subprocess.run([sys.executable, os.path.join(HERE, "time_mu.py"), n, "5"], env=e,

@@ -3,6 +3,7 @@
 #   tools/gpu.sh OUT STEP [STEP ...]        (run from the repo root, e.g. through gpurun)
 # Every step has its own time limit; the script stops at the first failure (no retries).
 # Steps:
+#   warm                 import torch + device name (a fresh box pages torch in: 1-2 min)  -> OUT/warm.log
 #   tests[=PYTEST_K]     the whole -m gpu suite (or -k PYTEST_K)            -> OUT/tests*.txt
 #   smoke                __graft_entry__.smoke()                           -> OUT/smoke.log
 #   bench[=ARGS]         python bench.py ARGS (',' separates arguments)    -> OUT/bench_<n>.log
@@ -36,9 +37,11 @@ for st in "$@"; do
   n=$((n+1)); name=${st%%=*}; arg=""; [ "$name" != "$st" ] && arg=${st#*=}
   args=${arg//,/ }
   case $name in
+    warm) run 240 "$O/warm.log" python -u -c "print('importing torch', flush=True); import torch; print(torch.cuda.get_device_name(0), flush=True)"
+      tail -1 "$O/warm.log" ;;
     tests)
-      if [ -n "$arg" ]; then run 900 "$O/tests_$n.txt" python -u -m pytest tests -m gpu -x -v -k "$arg" --timeout 280 --timeout-method thread
-      else run 900 "$O/tests.txt" python -u -m pytest tests -m gpu -x -v --timeout 280 --timeout-method thread; fi
+      if [ -n "$arg" ]; then run 900 "$O/tests_$n.txt" python -u -m pytest tests -m gpu -x -v -k "$arg" --timeout 150 --timeout-method thread
+      else run 900 "$O/tests.txt" python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread; fi
       tail -1 "$O"/tests*.txt | tail -1 ;;
     smoke) run 240 "$O/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$O/smoke.log" ;;
     bench) run 240 "$O/bench_$n.log" python bench.py --no-cpu $args; echo "bench $arg: $(tail -1 "$O/bench_$n.log" | summ)" ;;
