@@ -9,8 +9,8 @@ World size 2 over gloo with both ranks on cuda:0 (the one-GPU rehearsal of confi
              whole batch in canonical form, byte for byte;
   overflow   the same with capacities and inputs that force overflows: MU on the dense corpus with a
              record capacity of one record per message (ST_OVF_OUT) and no spill workspace
-             (ST_OVF_TILE), MC frames longer than 128 hex characters (k_mc hands them over as
-             ST_OVF_TILE) -- the exchange re-runs them into overlays on each rank before it ships, and
+             (ST_OVF_TILE), MC frames longer than 128 hex characters launched on k_mc alone (which hands
+             them over as ST_OVF_TILE; the routed launch sends them to the general kernel) -- the exchange re-runs them into overlays on each rank before it ships, and
              the gathered results equal the un-sharded Engine.run (its own re-runs) byte for byte;
   dict       ShardedDemodulator.demodulate_batch on msg_data dicts (general-path messages with
              multi-digit ids, messages whose host conversion raises) == SDProtocols.demodulate_batch of
@@ -89,7 +89,11 @@ def main():
         parts = []
         for k in kinds:
             o[k]["cursor"].zero_()
-            parts.append(sd.launch(KIND[k], bds[k], o[k]))
+            if dense and k == "MC":   # k_mc alone (no routing): it hands the > 128-character frames over
+                eng.launch_mc(bds[k], o[k])   # as ST_OVF_TILE, and the exchange re-runs them
+                parts.append(sdist.Part.from_out(o[k], KIND[k], src=(KIND[k], bds[k], 0, -1)))
+            else:
+                parts.append(sd.launch(KIND[k], bds[k], o[k]))
         if dense and j == 0:   # the first pass really overflowed on this rank
             torch.cuda.synchronize()
             st = {k: o[k]["desc"][: (hi - lo) * 8].view(-1, 8)[:, 6].cpu().numpy() for k in kinds}
