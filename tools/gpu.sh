@@ -3,6 +3,8 @@
 #   tools/gpu.sh OUT STEP [STEP ...]        (run from the repo root, e.g. through gpurun)
 # Every step has its own time limit; the script stops at the first failure (no retries).
 # Steps:
+#   testc[=PYTEST_K]     like tests but without -x, and the script goes on after test FAILURES
+#                        (not after a timeout, abort or crash: exit status 124/134/137/139 stops it)
 #   warm                 import torch + device name (a fresh box pages torch in: 1-2 min)  -> OUT/warm.log
 #   tests[=PYTEST_K]     the whole -m gpu suite (or -k PYTEST_K)            -> OUT/tests*.txt
 #   smoke                __graft_entry__.smoke()                           -> OUT/smoke.log
@@ -12,6 +14,8 @@
 #   e2e[=ARGS]           tools/bench_lines_e2e.py --check ARGS             -> OUT/e2e_<n>.log
 #   kt                   rocprofv3 --kernel-trace --stats of bench.py      -> OUT/kt_bench/
 #   ktlines              the same for tools/bench_lines.py                 -> OUT/kt_lines/
+#   ktpy=SCRIPT[,ARGS]   the same for python3 SCRIPT ARGS                  -> OUT/kt_<n>/
+#   ktx[=ARGS]           the same for bench.py --no-cpu ARGS (',' separates) -> OUT/ktx_<n>/
 #   pmc[=PASSES]         tools/pmc.sh (default sq1,sq2,fetch,write)        -> OUT/pmc/, OUT/pmc_traffic.json
 #   time=V1,V2           tools/time_mu.py for in-tree libsdx + variants V (pysignalduino_amd/_lib/ab/libsdx_V.so), 2 rounds
 #   env=E1,E2            bench.py --no-cpu under env settings E (VAR=value), 2 rounds
@@ -39,6 +43,12 @@ for st in "$@"; do
   case $name in
     warm) run 240 "$O/warm.log" python -u -c "print('importing torch', flush=True); import torch; print(torch.cuda.get_device_name(0), flush=True)"
       tail -1 "$O/warm.log" ;;
+    testc)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v ${arg:+-k "$arg"} --timeout 150 --timeout-method thread > "$O/testc_$n.txt" 2>&1
+      rc=$?
+      tail -1 "$O/testc_$n.txt"
+      grep -E "^(FAILED|ERROR)" "$O/testc_$n.txt" | head -20 || true
+      case $rc in 124|134|137|139) echo "tests stopped ($rc): no further GPU steps"; exit 1 ;; esac ;;
     tests)
       if [ -n "$arg" ]; then run 900 "$O/tests_$n.txt" python -u -m pytest tests -m gpu -x -v -k "$arg" --timeout 150 --timeout-method thread
       else run 900 "$O/tests.txt" python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread; fi
@@ -50,6 +60,10 @@ for st in "$@"; do
     e2e) run 400 "$O/e2e_$n.log" python -u tools/bench_lines_e2e.py --check $args; echo "e2e $arg: $(tail -1 "$O/e2e_$n.log" | cut -c1-400)" ;;
     kt) run 300 "$O/kt_bench.log" rocprofv3 --kernel-trace --stats -d "$O/kt_bench" -o b --output-format csv -- python3 bench.py --no-cpu
         echo "kt: $(tail -1 "$O/kt_bench.log" | summ)" ;;
+    ktpy) run 300 "$O/ktpy_$n.log" rocprofv3 --kernel-trace --stats -d "$O/kt_$n" -o k --output-format csv -- python3 $args
+        echo "ktpy $arg: $(tail -1 "$O/ktpy_$n.log" | cut -c1-300)" ;;
+    ktx) run 300 "$O/ktx_$n.log" rocprofv3 --kernel-trace --stats -d "$O/ktx_$n" -o b --output-format csv -- python3 bench.py --no-cpu $args
+        echo "ktx $arg: $(tail -1 "$O/ktx_$n.log" | summ)" ;;
     ktlines) run 300 "$O/kt_lines.log" rocprofv3 --kernel-trace --stats -d "$O/kt_lines" -o l --output-format csv -- python3 tools/bench_lines.py --no-cpu
         echo "ktlines: $(tail -1 "$O/kt_lines.log" | cut -c1-200)" ;;
     pmc) PMC_OUT=$O/pmc PMC_TRAFFIC=$O/pmc_traffic.json run 1200 "$O/pmc.log" bash tools/pmc.sh ${args:-sq1 sq2 fetch write}
