@@ -59,6 +59,8 @@ def parse():
                          "defer = count and pack both after the next step's MU (beside MS/MC)")
     ap.add_argument("--raw-wire", action="store_true",
                     help="exchange payloads raw (no nibble form: A/B of the wire size)")
+    ap.add_argument("--scan-wire", action="store_true",
+                    help="the exchange classifies every payload itself (no kernel-written counts, ABI 12: A/B)")
     ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
                     help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
@@ -239,7 +241,7 @@ def main():
         for i, k in enumerate(kinds):
             n = corp[k].n
             o[k] = eng.alloc_out(n, caps[k][0] * n + 4096, caps[k][1] * n + 65536,
-                                 eng.pulses_work_bytes(n) if k != "MC" else 0)
+                                 eng.pulses_work_bytes(n) if k != "MC" else 0, wire=dist_on and not args.scan_wire)
             o[k]["cursor"] = cursors[s_, i]   # one fill per step resets a slot's cursors
         outs.append(o)
     # the launch stream at high priority, the grouping's side stream at low priority: the hardware

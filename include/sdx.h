@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 11
+#define SDX_ABI_VERSION 12
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -147,7 +147,18 @@ typedef struct {
                                 * sdx_pulses_work_bytes); without it a tile whose results overflow
                                 * LDS is re-run (ST_OVF_TILE) */
   uint64_t work_cap;           /* bytes at work_dev (< 4 GiB - 112 KB: spill offsets are 32-bit) */
+  /* ABI 12, optional (NULL = none): the exchange's view of the results, written by the flushes of
+   * sdx_demod_pulses / _long and sdx_demod_mc while the payloads are still on chip, so that
+   * sdx_exchange_count / _pack need not classify every payload again:
+   *   wire_dev[n]        per message: (payload bytes << 32) | wire payload bytes of its records (0 for
+   *                      a message without results; written with its descriptor)
+   *   xrec_dev[rec_cap]  per record (same index as rec_dev): SDX_XREC_NIB | preamble length << 16 |
+   *                      hex digit count when the payload is preamble + uppercase hex + postamble of
+   *                      its protocol (the nibble form), 0 otherwise */
+  uint64_t* wire_dev;
+  uint32_t* xrec_dev;
 } sdx_out;
+#define SDX_XREC_NIB 0x80000000u
 
 typedef struct sdx_bank sdx_bank;
 
@@ -460,6 +471,9 @@ typedef struct {
   uint8_t alt;                 /* 0, or 1 + index (in the same array) of this launch's overlay part */
   uint8_t aux;                 /* 1: this part is an overlay */
   uint8_t res;
+  const uint64_t* wire_dev;    /* ABI 12, optional: the launch's sdx_out.wire_dev / xrec_dev (written by its
+                                * kernels): messages with status OK are counted and packed from them */
+  const uint32_t* xrec_dev;
 } sdx_xchg_part;
 
 /* workspace of count + pack (kept between the two: 12 B per message + block sums + a 256-byte head);

@@ -190,7 +190,7 @@ __device__ inline uint32_t hexval(uint8_t c) { return c <= '9' ? (uint32_t)(c - 
 
 // payload p[0, len) == pre + D uppercase hex digits + post?  Returns D, or -1 (raw form)
 __device__ inline int nib_digits(const Affix& a, const uint8_t* p, uint32_t len) {
-  if (!a.ok || len < a.npre + a.npost) return -1;
+  if (!a.ok || a.npre > 255u || len < a.npre + a.npost) return -1;   // npre > 255: raw (as the xrec word)
   for (uint32_t i = 0; i < a.npre; ++i)
     if (p[i] != a.pre[i]) return -1;
   const uint32_t d = len - a.npre - a.npost;
@@ -203,6 +203,11 @@ __device__ inline int nib_digits(const Affix& a, const uint8_t* p, uint32_t len)
 
 __device__ inline uint32_t wire_bytes_of(int digits, uint32_t len) {
   return digits >= 0 ? ((uint32_t)digits + 1) >> 1 : len;
+}
+
+// the nibble form applies to a part's payloads at all (a bank and the part's protocol kind)
+__device__ inline bool nibble_on(const Parts& P, const sdx_xchg_part& x) {
+  return P.bank != nullptr && x.kind <= SDX_KIND_MN;
 }
 
 // ---- sender ---------------------------------------------------------------------------------------
@@ -245,6 +250,12 @@ __device__ inline uint64_t msg_counts(const Parts& P, int k0, uint32_t m, bool* 
   if (d.status != SDX_ST_OK || (d.n_rec && (uint64_t)d.rec_begin + d.n_rec > nrec_c)) {
     *ok = false;
     return 0;
+  }
+  if (x.wire_dev) {  // ABI 12: the launch's kernel counted the message while its payloads were on chip
+    const uint64_t w = x.wire_dev[m];
+    const uint32_t rb = (uint32_t)(w >> 32);
+    *rawb = rb;
+    return ((uint64_t)d.n_rec << 32) | (nibble_on(P, x) ? (uint32_t)w : rb);
   }
   const sdx_result* r = reinterpret_cast<const sdx_result*>(x.rec_dev) + d.rec_begin;
   uint64_t bytes = 0, raw = 0;
@@ -372,17 +383,27 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
         nr | ((uint32_t)(bad ? SDX_ST_OVF_OUT : d.status) << 16) | ((uint32_t)d.raise_kind << 24);
     const sdx_result* rec = reinterpret_cast<const sdx_result*>(y.rec_dev) + d.rec_begin;
     uint32_t lr = (uint32_t)((loc & ~BADBIT) >> 32), lb = (uint32_t)loc;   // block-local
+    const bool xr_on = y.xrec_dev != nullptr && nibble_on(P, y);
     for (uint32_t j = 0; j < nr; ++j) {
       const sdx_result r = rec[j];
       const uint8_t* src = y.heap_dev + r.payload_off;
-      const Affix a = affix_of(P.bank, y.kind, r.proto);
-      const int dg = nib_digits(a, src, r.payload_len);
+      int dg;
+      uint32_t npre = 0;
+      if (y.xrec_dev) {  // ABI 12: classified by the launch's kernel
+        const uint32_t xr = xr_on ? y.xrec_dev[d.rec_begin + j] : 0u;
+        dg = (xr & SDX_XREC_NIB) ? (int)(xr & 0xFFFFu) : -1;
+        npre = (xr >> 16) & 0xFFu;
+      } else {
+        const Affix a = affix_of(P.bank, y.kind, r.proto);
+        dg = nib_digits(a, src, r.payload_len);
+        npre = a.npre;
+      }
       sdx_wire_rec o;
       o.proto = (uint16_t)(r.proto | (dg >= 0 ? SDX_WIRE_NIB : 0u));
       o.payload_len = r.payload_len;
       o.bit_length = r.bit_length;
       s_rec[(uint32_t)(boff >> 32) + lr] = o;
-      const uint8_t* s0 = dg >= 0 ? src + a.npre : src;
+      const uint8_t* s0 = dg >= 0 ? src + npre : src;
       const uint32_t wl = wire_bytes_of(dg, r.payload_len);
       if (lr < LREC) {
         l_src[lr] = (uint64_t)(uintptr_t)s0;

@@ -1314,21 +1314,55 @@ SDX_DEV void decode_ms_lane(T& L, const sdx_out& out, const BankView& bv, const 
 // message with a smaller (protocol, rank) key -- rank is the per-message atomic counter, which
 // increases monotonically along one (message, protocol) pair's finditer loop.
 // ---------------------------------------------------------------------------------------------
+// The exchange's wire form of one payload (include/sdx.h ABI 12, sdx_out.xrec_dev): preamble + D
+// uppercase hex digits + postamble of its protocol (message_unsynced.py:271-274,
+// message_synced.py:228-229, manchester.py:131-132) -> the xrec word SDX_XREC_NIB | npre << 16 | D,
+// else 0 (raw).  The same rule as sdx_exchange.hip nib_digits; run by the flushes on the staged
+// payloads (LDS or spill region), so the exchange never re-reads a payload to classify it.
+SDX_DEV bool uhex_c(uint8_t c) { return (uint8_t)(c - '0') < 10u || (uint8_t)(c - 'A') < 6u; }
+SDX_DEV uint32_t wire_class(const BankView& bv, int kind, int proto, const uint8_t* p, int len) {
+  int po, pl, qo = 0, ql = 0;
+  if (kind == SDX_KIND_MU) {
+    const sdx_mu_proto* r = bv.mu + proto;
+    po = r->pre_off, pl = r->pre_len, qo = r->post_off, ql = r->post_len;
+  } else if (kind == SDX_KIND_MS) {
+    const sdx_ms_proto* r = bv.ms + proto;
+    po = r->pre_off, pl = r->pre_len, qo = r->post_off, ql = r->post_len;
+  } else {
+    const sdx_mc_proto* r = bv.mc + proto;
+    po = r->pre_off, pl = r->pre_len;
+  }
+  if (pl < 0 || ql < 0 || pl > 255 || len < pl + ql) return 0u;
+  const int d = len - pl - ql;
+  bool ok = true;
+  for (int i = 0; i < pl; ++i) ok &= p[i] == bv.str[po + i];
+  for (int i = 0; i < ql; ++i) ok &= p[pl + d + i] == bv.str[qo + i];
+  for (int i = 0; i < d; ++i) ok &= uhex_c(p[pl + i]);
+  return ok ? (SDX_XREC_NIB | ((uint32_t)pl << 16) | (uint32_t)d) : 0u;
+}
+SDX_DEV uint32_t wire_bytes_x(uint32_t xr, int len) {
+  return (xr & SDX_XREC_NIB) ? ((xr & 0xFFFFu) + 1u) >> 1 : (uint32_t)len;
+}
+
 template <int NW, int TM, int LM>
-SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, const sdx_out& out) {
+SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, const sdx_out& out, const BankView& bv,
+                        int kind) {
   using T = TileLds<NW, TM, LM>;
   const int tid = threadIdx.x;
   // staged records: the LDS pool [0, nr_l), then (lane writers of heavy tiles) the spill region
   // [nr_l, nr); payload bytes likewise (StageRec.off with HEAP_SPILLED: spill region)
   constexpr int RMAX = T::PREC + (LM != 0 ? (int)SPILL_R : 0);
   // flush scratch aliases the id bitmaps (dead once every wave has left the protocol loop)
-  static_assert(sizeof(L.bm) >= TM * 8 + RMAX * 2, "flush scratch does not fit the bitmaps");
-  uint32_t* fill = reinterpret_cast<uint32_t*>(L.bm);       // bucket fill per message
+  static_assert(sizeof(L.bm) >= TM * 16 + RMAX * 2, "flush scratch does not fit the bitmaps");
+  uint64_t* wsum = reinterpret_cast<uint64_t*>(L.bm);       // per message: payload << 32 | wire bytes
+  uint32_t* fill = reinterpret_cast<uint32_t*>(wsum + TM);  // bucket fill per message
   uint32_t* cntm = fill + TM;                               // staged records per message
   uint16_t* bidx = reinterpret_cast<uint16_t*>(cntm + TM);  // record indices bucketed by message
+  const bool wx = out.wire_dev != nullptr;                  // the exchange's counts (ABI 12)
   if (tid < TM) {
     fill[tid] = 0;
     cntm[tid] = 0;
+    wsum[tid] = 0;
   }
   __syncthreads();
   const int nr_l = (int)(uint32_t)L.pool_ctr < T::PREC ? (int)(uint32_t)L.pool_ctr : T::PREC;
@@ -1411,6 +1445,16 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       o.bit_length = sr.bitlen;
       o.msg = (uint32_t)msg_of[sr.msg];
       out.rec_dev[L.rec_base + b0 + rk] = o;
+      if (wx) {
+        uint32_t xr;   // two call sites: one pointer per address space (a selected generic pointer
+        if (sr.off & HEAP_SPILLED)   // here crashed the ROCm 7.2 compiler)
+          xr = wire_class(bv, kind, sr.proto, sreg + SPILL_OFF_H + (sr.off & ~HEAP_SPILLED), sr.len);
+        else
+          xr = wire_class(bv, kind, sr.proto, L.heap + sr.off, sr.len);
+        if (out.xrec_dev) out.xrec_dev[L.rec_base + b0 + rk] = xr;
+        atomicAdd(reinterpret_cast<unsigned long long*>(&wsum[sr.msg]),
+                  (unsigned long long)(((uint64_t)sr.len << 32) | wire_bytes_x(xr, sr.len)));
+      }
     }
     uint8_t* hd = out.heap_dev + L.heap_base;
     if ((((uintptr_t)hd) & 15u) == 0) {  // 16-B stores (every tile reserves a multiple of 16 B)
@@ -1429,6 +1473,7 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       for (int i = tid; i < nh_s; i += blockDim.x) hd[nh_l16 + i] = sreg[SPILL_OFF_H + i];
     }
   }
+  if (wx) __syncthreads();  // wsum complete (block-uniform)
   for (int m = tid; m < nvalid; m += blockDim.x) {
     sdx_desc d;
     d.rec_begin = L.rec_base + L.mbase[m];
@@ -1447,6 +1492,7 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       d.n_rec = (uint16_t)cntm[m];
     }
     out.desc_dev[msg_of[m]] = d;
+    if (wx) out.wire_dev[msg_of[m]] = d.status == SDX_ST_OK ? wsum[m] : 0ull;
   }
 }
 
@@ -2208,7 +2254,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     PROF_ADD(16, t_fin);
   }
   PROF_T(t_fl);
-  flush_tile(L, msg_of, nvalid, out);
+  flush_tile(L, msg_of, nvalid, out, bv, KIND);
   PROF_ADD(13, t_fl);
   PROF_ADD(15, t_kernel);
 #ifdef SDX_WGTIME
@@ -2471,6 +2517,14 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   rbase = (uint32_t)__shfl((int)rbase, 0);
   hbase = (uint32_t)__shfl((int)hbase, 0);
   st = __shfl(st, 0);
+  // the exchange's counts (ABI 12): per frame payload << 32 | wire bytes, in this wave's slice of
+  // the (now dead) bit rows
+  const bool wx = out.wire_dev != nullptr;
+  unsigned long long* wsum = reinterpret_cast<unsigned long long*>(&L.bn[64 * wave]);
+  if (wx) {
+    wsum[lane] = 0ull;
+    wave_sync();
+  }
   if (st == 0) {
     const int excl = incl - mycnt;
     for (int i0 = 0; i0 < nr; i0 += WAVE) {  // wave-uniform trip count (the shuffles below)
@@ -2487,6 +2541,11 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
         o.bit_length = 0;
         o.msg = (uint32_t)fmsg;
         out.rec_dev[rbase + fbase + sr.rank] = o;
+        if (wx) {
+          const uint32_t xr = wire_class(bv, SDX_KIND_MC, sr.proto, &L.heap[wave][sr.off], sr.len);
+          if (out.xrec_dev) out.xrec_dev[rbase + fbase + sr.rank] = xr;
+          atomicAdd(&wsum[fl], (unsigned long long)(((uint64_t)sr.len << 32) | wire_bytes_x(xr, sr.len)));
+        }
       }
     }
     uint4* hd = reinterpret_cast<uint4*>(out.heap_dev + hbase);
@@ -2504,6 +2563,10 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     else if (st) { d.status = st == 2 ? SDX_ST_OVF_TILE : SDX_ST_OVF_OUT; d.raise_kind = 0; d.n_rec = 0; }
     else { d.status = SDX_ST_OK; d.raise_kind = 0; d.n_rec = (uint16_t)mycnt; }
     out.desc_dev[msg] = d;
+  }
+  if (wx) {
+    wave_sync();
+    if (valid) out.wire_dev[msg] = (!raise && st == 0) ? (uint64_t)wsum[lane] : 0ull;
   }
 }
 
@@ -2594,6 +2657,7 @@ int sdx_layout_size(int which) {
     case 14: return (int)sizeof(sdx_wire_rec);
     case 15: static_assert(sizeof(sdx_msg_rec) == 128, "sdx_msg_rec is one 128-byte line"); return (int)sizeof(sdx_msg_rec);
     case 16: return (int)sizeof(sdx_pulse_batch);
+    case 17: return (int)sizeof(sdx_out);
   }
   return -1;
 }

@@ -70,8 +70,8 @@ def _nib_digits(affix, proto: int, p: bytes) -> int:
     if affix is None or proto >= len(affix):
         return -1
     pre, post = affix[proto]
-    if len(p) < len(pre) + len(post) or not p.startswith(pre) or not p.endswith(post):
-        return -1
+    if len(pre) > 255 or len(p) < len(pre) + len(post) or not p.startswith(pre) or not p.endswith(post):
+        return -1   # (a preamble of > 255 bytes does not fit the xrec word: raw)
     mid = p[len(pre): len(p) - len(post)]
     return len(mid) if all(c in b"0123456789ABCDEF" for c in mid) else -1
 
@@ -208,11 +208,13 @@ class Part:
     ``overlays`` (Parts over the same messages holding re-run / general-path results, in precedence
     order) and ``src`` = (kind, device batch) for re-running its overflowed messages."""
 
-    __slots__ = ("desc", "rec", "heap", "n", "cursor", "kind", "overlays", "src", "keep")
+    __slots__ = ("desc", "rec", "heap", "n", "cursor", "kind", "overlays", "src", "keep", "wire", "xrec")
 
-    def __init__(self, desc, rec, heap, n, cursor, kind=KIND_RAW, overlays=(), src=None, keep=None):
+    def __init__(self, desc, rec, heap, n, cursor, kind=KIND_RAW, overlays=(), src=None, keep=None, wire=None,
+                 xrec=None):
         self.desc, self.rec, self.heap, self.n, self.cursor = desc, rec, heap, int(n), cursor
         self.kind, self.overlays, self.src, self.keep = kind, list(overlays), src, keep
+        self.wire, self.xrec = wire, xrec   # the kernels' exchange counts / record classes (ABI 12), or None
 
     @staticmethod
     def of(p) -> "Part":
@@ -222,7 +224,8 @@ class Part:
     @staticmethod
     def from_out(out, kind=KIND_RAW, src=None) -> "Part":
         """An Engine.alloc_out dict."""
-        return Part(out["desc"], out["rec"], out["heap"], out["n"], out["cursor"], kind, src=src, keep=out)
+        return Part(out["desc"], out["rec"], out["heap"], out["n"], out["cursor"], kind, src=src, keep=out,
+                    wire=out.get("wire"), xrec=out.get("xrec"))
 
     def caps(self):
         return self.rec.numel() // REC_BYTES, self.heap.numel()
@@ -243,6 +246,11 @@ def _flatten(parts: Sequence[Part]):
     if len(flat) > runtime.XCHG_MAX_PARTS:
         raise RuntimeError(f"exchange: {len(flat)} launches + overlays exceed SDX_XCHG_MAX_PARTS")
     return flat
+
+
+def _nprimary(flat) -> int:
+    """The primary launches of a _flatten() array (they come first; overlays follow)."""
+    return sum(1 for _, _, aux in flat if not aux)
 
 
 def _layout(S: np.ndarray):
@@ -357,7 +365,8 @@ class Exchange:
         for k, (p, alt, aux) in enumerate(flat):
             rcap, hcap = p.caps()
             arr[k] = runtime.SdxXchgPart(p.desc.data_ptr(), p.rec.data_ptr(), p.heap.data_ptr(), p.cursor.data_ptr(),
-                                         p.n, rcap, hcap, p.kind if self.engine is not None else KIND_RAW, alt, aux, 0)
+                                         p.n, rcap, hcap, p.kind if self.engine is not None else KIND_RAW, alt, aux, 0,
+                                         runtime._ptr(p.wire), runtime._ptr(p.xrec))
         return arr
 
     def _work(self, flat, dev):
@@ -428,7 +437,7 @@ class Exchange:
                 stream = stream or torch.cuda.current_stream(dev)
                 with torch.cuda.stream(stream):
                     flat = _flatten(parts)
-                    cnt = self._count_pack_device(flat, stream)
+                    cnt = self._count_pack_device(flat, stream)[: XCHG_COUNTS * len(parts)]
                     allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
                     _all_gather_flat(allc, cnt, self.group)
                     self._complete(_Pending(parts, allc.cpu(), None, rerun=rerun))
@@ -482,10 +491,13 @@ class Exchange:
         return released
 
     def _count_to_host(self, flat, dev):
-        """count + count all-gather + pinned D2H on the current stream: (host counts, event, device counts)."""
+        """count + count all-gather + pinned D2H on the current stream: (host counts, event, device counts).
+        Only the primary launches' counts travel: the ranks' overlay parts differ in number (an overlay
+        has no sections of its own), so the collective's size must not depend on them."""
         cnt = self._count_device(flat, torch.cuda.current_stream(dev))
-        allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
-        _all_gather_flat(allc, cnt, self.group)
+        kp = _nprimary(flat)
+        allc = torch.empty(self.world * XCHG_COUNTS * kp, dtype=torch.int32, device=dev)
+        _all_gather_flat(allc, cnt[: XCHG_COUNTS * kp], self.group)
         host = torch.empty(allc.numel(), dtype=torch.int32, pin_memory=True)
         host.copy_(allc, non_blocking=True)
         ev = torch.cuda.Event()
@@ -526,7 +538,7 @@ class Exchange:
                 host = allc
             elif p.cnt is None:        # gloo with device tensors: count + pack again
                 flat = _flatten(p.parts)
-                cnt = self._count_pack_device(flat, torch.cuda.current_stream(dev))
+                cnt = self._count_pack_device(flat, torch.cuda.current_stream(dev))[: XCHG_COUNTS * K]
                 allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
                 _all_gather_flat(allc, cnt, self.group)
                 host = allc.cpu()
@@ -568,7 +580,9 @@ class Exchange:
             recv = self._buf("recv", self.world * T, dev)[: self.world * T]
             send = recv[self.rank * T: (self.rank + 1) * T]
             work, wb = self._work(flat, dev)
-            mine = np.ascontiguousarray(S[self.rank].reshape(-1).astype(np.uint32))
+            mine = np.zeros((len(flat), XCHG_COUNTS), np.uint32)   # overlay parts: no sections (zeros)
+            mine[:K] = S[self.rank, :K]
+            mine = mine.reshape(-1)
             runtime._check(lib, lib.sdx_exchange_pack_into(
                 self._bank(), self._xparts(flat), len(flat), ctypes.c_void_p(work.data_ptr()), wb,
                 ctypes.c_void_p(p.cnt.data_ptr()), mine.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(send.data_ptr()),
@@ -735,7 +749,7 @@ class ShardedDemodulator:
         capacities); no host synchronisation."""
         eng = self.eng
         if out is None:
-            out = eng.first_pass(kind, bd, mn_elig=mn_elig, mn_method=mn_method)
+            out = eng.first_pass(kind, bd, mn_elig=mn_elig, mn_method=mn_method, wire=True)
         elif grouped_sel is not None:
             eng.launch_pulses(kind, bd, out, sel=grouped_sel, group=False, mrec=mrec)
         else:

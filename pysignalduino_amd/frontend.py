@@ -183,9 +183,10 @@ def _contract(i: int, name) -> ContractError:
                          "(include/sdx.h SDX_GEN_*, payloads > 65535 bytes)")
 
 
-def pack_lines(lines: Sequence[Union[str, bytes]]):
+def pack_lines(lines: Sequence[Union[str, bytes]], copy: bool = True):
     """Concatenate lines into (data uint8, offsets int64[n+1]); per-line ContractError where a line
-    cannot be represented (returned in ``bad``; such lines are replaced by an empty line)."""
+    cannot be represented (returned in ``bad``; such lines are replaced by an empty line).
+    ``copy=False``: data is a read-only view of the joined bytes (one host copy fewer)."""
     bs, bad = [], {}
     for i, ln in enumerate(lines):
         try:
@@ -196,8 +197,8 @@ def pack_lines(lines: Sequence[Union[str, bytes]]):
     lens = np.fromiter((len(b) for b in bs), np.int64, len(bs))
     offsets = np.zeros(len(bs) + 1, np.int64)
     np.cumsum(lens, out=offsets[1:])
-    data = np.frombuffer(b"".join(bs), np.uint8).copy()
-    return data, offsets, bad
+    data = np.frombuffer(b"".join(bs), np.uint8)
+    return (data.copy() if copy else data), offsets, bad
 
 
 class SignalParser:

@@ -19,7 +19,7 @@ from . import bank as bankmod
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libsdx.so")
-ABI_VERSION = 11   # include/sdx.h SDX_ABI_VERSION
+ABI_VERSION = 12   # include/sdx.h SDX_ABI_VERSION
 
 KIND_MU, KIND_MS, KIND_MC = 0, 1, 2
 KIND_MN = 3        # host-side tag for Engine.run (sdx_demod_mn)
@@ -98,7 +98,8 @@ class SdxUnitBatch(Structure):
 class SdxXchgPart(Structure):
     _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("cursor_dev", c_void_p),
                 ("n_msgs", c_uint32), ("rec_cap", c_uint32), ("heap_cap", c_uint32), ("kind", ctypes.c_uint8),
-                ("alt", ctypes.c_uint8), ("aux", ctypes.c_uint8), ("res", ctypes.c_uint8)]
+                ("alt", ctypes.c_uint8), ("aux", ctypes.c_uint8), ("res", ctypes.c_uint8),
+                ("wire_dev", c_void_p), ("xrec_dev", c_void_p)]
 
 
 class SdxXchgWire(Structure):
@@ -119,7 +120,8 @@ KIND_RAW = 0xFF     # sdx_xchg_part.kind: no affixes (raw payloads only)
 
 class SdxOut(Structure):
     _fields_ = [("desc_dev", c_void_p), ("rec_dev", c_void_p), ("heap_dev", c_void_p), ("cursor_dev", c_void_p),
-                ("rec_cap", c_uint32), ("heap_cap", c_uint32), ("work_dev", c_void_p), ("work_cap", ctypes.c_uint64)]
+                ("rec_cap", c_uint32), ("heap_cap", c_uint32), ("work_dev", c_void_p), ("work_cap", ctypes.c_uint64),
+                ("wire_dev", c_void_p), ("xrec_dev", c_void_p)]
 
 
 class SdxLines(Structure):
@@ -231,7 +233,7 @@ def check_layout(lib) -> None:
             4: bankmod.MC_REC.itemsize, 5: RES_DT.itemsize, 6: DESC_DT.itemsize, 7: bankmod.MU_DESC.itemsize,
             8: bankmod.MN_REC.itemsize, 9: bankmod.JSON_REC.itemsize, 10: bankmod.MU_FILT.itemsize,
             11: bankmod.MS_FILT.itemsize, 12: ctypes.sizeof(SdxXchgPart), 13: ctypes.sizeof(SdxXchgWire),
-            14: WIRE_REC_DT.itemsize, 15: MREC_DT.itemsize, 16: ctypes.sizeof(SdxPulseBatch)}
+            14: WIRE_REC_DT.itemsize, 15: MREC_DT.itemsize, 16: ctypes.sizeof(SdxPulseBatch), 17: ctypes.sizeof(SdxOut)}
     for k, v in want.items():
         got = lib.sdx_layout_size(k)
         if got != v:
@@ -350,7 +352,10 @@ class Engine:
                                                    int(work.numel()), self.stream_ptr()))
         return order[:n]
 
-    def alloc_out(self, n: int, rec_cap: int, heap_cap: int, work_bytes: int = 0):
+    def alloc_out(self, n: int, rec_cap: int, heap_cap: int, work_bytes: int = 0, wire: bool = False):
+        """Output buffers of one launch.  ``wire``: also the exchange's per-message counts and
+        per-record classes (sdx_out.wire_dev / xrec_dev, ABI 12), written by the kernels' flushes so
+        that sdx_exchange_count / _pack need not re-read the payloads."""
         t = self.torch
         d = self.dev
         return {
@@ -359,6 +364,8 @@ class Engine:
             "heap": t.empty(max(heap_cap, 1), dtype=t.uint8, device=d),
             "cursor": t.zeros(4, dtype=t.int32, device=d),
             "work": t.empty(work_bytes, dtype=t.uint8, device=d) if work_bytes else None,
+            "wire": t.zeros(max(n, 1), dtype=t.int64, device=d) if wire else None,
+            "xrec": t.empty(max(rec_cap, 1), dtype=t.int32, device=d) if wire else None,
             "rec_cap": rec_cap, "heap_cap": heap_cap, "n": n,
         }
 
@@ -366,7 +373,8 @@ class Engine:
     def _out_struct(o) -> SdxOut:
         w = o.get("work")
         return SdxOut(_ptr(o["desc"]), _ptr(o["rec"]), _ptr(o["heap"]), _ptr(o["cursor"]), o["rec_cap"],
-                      o["heap_cap"], _ptr(w), 0 if w is None else int(w.numel()))
+                      o["heap_cap"], _ptr(w), 0 if w is None else int(w.numel()), _ptr(o.get("wire")),
+                      _ptr(o.get("xrec")))
 
     def stream_ptr(self):
         return c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
@@ -563,10 +571,14 @@ class Engine:
         return desc, rec, heap
 
     def first_pass(self, kind: int, bd, rec_cap: Optional[int] = None, heap_cap: Optional[int] = None,
-                   sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1, workspace: bool = True):
+                   sel_short=None, sel_long=None, mn_elig: int = 0, mn_method: int = -1, workspace: bool = True,
+                   wire: bool = False):
         """Output buffers sized for a device batch (default capacities: 8 records and 200 payload
         bytes per message) and the first pass's launches into them (launch_routed), enqueued on the
-        current stream; returns the output dict (run() re-runs what overflowed)."""
+        current stream; returns the output dict (run() re-runs what overflowed).  ``wire``: the
+        kernels also write the exchange's counts (alloc_out), where every message of the launch goes
+        to a kernel that writes them (k_pulses, k_mc: not MN, not MC batches with frames for the
+        general MC kernel)."""
         n = bd["n"]
         selected = sel_short is not None or sel_long is not None
         if selected:
@@ -587,8 +599,10 @@ class Engine:
         if kind == KIND_MN and not selected:   # parser mode: <= n_mn results of <= preamble + frame bytes
             rec_cap = max(rec_cap, 4 * n_work + 1024)
             heap_cap = max(heap_cap, int(4 * int(np.sum(bd["lengths"])) + 160 * n_work + 65536))
+        if wire and (kind == KIND_MN or (kind == KIND_MC and not selected and bool((bd["lengths"] > MC_HEX_MAX).any()))):
+            wire = False
         out = self.alloc_out(n, rec_cap, heap_cap,
-                             self.pulses_work_bytes(n_work) if workspace and kind in (KIND_MU, KIND_MS) else 0)
+                             self.pulses_work_bytes(n_work) if workspace and kind in (KIND_MU, KIND_MS) else 0, wire=wire)
         self.launch_routed(kind, bd, out, sel_short=sel_short, sel_long=sel_long, mn_elig=mn_elig, mn_method=mn_method,
                            workspace=workspace)
         return out
@@ -630,10 +644,10 @@ class Engine:
                 self.launch_pulses(kind, bd, out, sel=t.from_numpy(np.nonzero(~short)[0].astype(np.int32)).to(self.dev),
                                    long_variant=True)
 
-    def overlay_out(self, n: int, rec_cap: int, heap_cap: int):
+    def overlay_out(self, n: int, rec_cap: int, heap_cap: int, wire: bool = False):
         """Output buffers of an exchange overlay (include/sdx.h ABI 11): every descriptor at
         ST_ABSENT until a launch writes it."""
-        o = self.alloc_out(n, rec_cap, heap_cap)
+        o = self.alloc_out(n, rec_cap, heap_cap, wire=wire)
         o["desc"].fill_(ST_ABSENT)
         return o
 
@@ -645,7 +659,8 @@ class Engine:
         sdx_demod_mc_general, MN on k_mn; grown output capacities.  Enqueued on the current stream."""
         t = self.torch
         redo = np.asarray(redo, np.int32)
-        out2 = self.overlay_out(bd["n"], rec_cap, heap_cap)
+        # MU/MS re-run on the long k_pulses variant, which writes the exchange's counts (ABI 12)
+        out2 = self.overlay_out(bd["n"], rec_cap, heap_cap, wire=kind in (KIND_MU, KIND_MS))
         sel = t.from_numpy(redo).to(self.dev)
         if kind == KIND_MN:
             self.launch_mn(bd, out2, elig=mn_elig, method=mn_method, sel=sel)

@@ -113,7 +113,9 @@ class _Slot:
             if name == "MC" and not ls.mc:
                 continue
             rc, hc = caps[name]
-            self.outs[name] = eng.alloc_out(C, rc, hc, eng.pulses_work_bytes(C) if name in ("MU", "MS") else 0)
+            # wire output: k_pulses / k_mc write the exchange's counts (k_mn does not)
+            self.outs[name] = eng.alloc_out(C, rc, hc, eng.pulses_work_bytes(C) if name in ("MU", "MS") else 0,
+                                            wire=ls.output == "wire" and name != "MN")
         self.gbufs = {name: eng.group_buffers(C) for name in ("MU", "MS")}
         self.cursors = t.zeros((len(self.outs), 4), dtype=t.int32, device=eng.dev)
         for j, o in enumerate(self.outs.values()):
@@ -176,10 +178,13 @@ class LineStream:
     # -- public ------------------------------------------------------------------------------------------
     def submit(self, lines: Sequence[Union[str, bytes]]) -> int:
         from .frontend import pack_lines
-        data, offsets, bad = pack_lines(lines)
+        data, offsets, bad = pack_lines(lines, copy=False)   # read once, into the slot's pinned buffer
         return self.submit_packed(data, offsets, lines=lines, bad=bad)
 
-    def submit_packed(self, data: np.ndarray, offsets: np.ndarray, lines=None, bad=None) -> int:
+    def submit_packed(self, data, offsets: np.ndarray, lines=None, bad=None) -> int:
+        """``data``: the lines' bytes as a numpy uint8 array (copied into the slot's pinned buffer) or
+        a PINNED torch uint8 tensor (uploaded from where it is, no host copy: keep it unchanged until
+        the chunk has been collected); ``offsets``: int64[n + 1] into it."""
         n = len(offsets) - 1
         if n > self.C or int(offsets[-1] - offsets[0]) > self.B:
             raise ValueError(f"chunk of {n} lines / {int(offsets[-1] - offsets[0])} bytes exceeds the stream's "
@@ -234,13 +239,19 @@ class LineStream:
 
     def _stage_a(self, s: _Slot, data, offsets):
         t = self.torch
-        n, nb = s.n, int(offsets[-1] - offsets[0])
-        s.h_bytes.numpy()[:nb] = data[int(offsets[0]): int(offsets[-1])]
-        s.h_bytes.numpy()[nb: nb + 16] = 0
-        s.h_offs.numpy()[: n + 1] = offsets - offsets[0]
+        n, o0, nb = s.n, int(offsets[0]), int(offsets[-1] - offsets[0])
+        s.h_offs.numpy()[: n + 1] = offsets - o0
         lb = s.lb
+        pinned = isinstance(data, t.Tensor) and data.is_pinned()
+        if not pinned:
+            s.h_bytes.numpy()[:nb] = data[o0: o0 + nb]
         with t.cuda.stream(self.cin):
-            lb.bytes[: nb + 16].copy_(s.h_bytes[: nb + 16], non_blocking=True)
+            if pinned:   # straight from the caller's pinned buffer; the 16 pad bytes zeroed on the device
+                lb.bytes[:nb].copy_(data[o0: o0 + nb], non_blocking=True)
+                lb.bytes[nb: nb + 16].zero_()
+            else:
+                s.h_bytes.numpy()[nb: nb + 16] = 0
+                lb.bytes[: nb + 16].copy_(s.h_bytes[: nb + 16], non_blocking=True)
             lb.offsets[: n + 1].copy_(s.h_offs[: n + 1], non_blocking=True)
             h2d = t.cuda.Event()
             h2d.record(self.cin)
@@ -279,6 +290,8 @@ class LineStream:
                     continue
                 o["n"] = n
                 o["desc"][: 8 * n].zero_()          # lines of other classes keep an empty descriptor
+                if o.get("wire") is not None:
+                    o["wire"][:n].zero_()           # ... and no exchange counts
                 if kd == runtime.KIND_MN:
                     if cnt[short]:
                         eng.launch_mn(lb.mn_batch(), o, elig=self.elig, sel=sels[short])
@@ -306,7 +319,8 @@ class LineStream:
                 s.h_sizes[2:].copy_(s.cursors.reshape(-1), non_blocking=True)
             else:
                 from . import dist as sdist
-                parts = [sdist.Part(o["desc"], o["rec"], o["heap"], n, o["cursor"], kd)
+                parts = [sdist.Part(o["desc"], o["rec"], o["heap"], n, o["cursor"], kd, wire=o.get("wire"),
+                                    xrec=o.get("xrec"))
                          for name, kd, _, _ in _KINDS for o in [s.outs.get(name)] if o is not None]
                 wc = s.ser._count_pack_device(sdist._flatten(parts), self.sd)
                 k = len(parts)
@@ -405,4 +419,5 @@ class LineStream:
     def _line(s: _Slot, i: int):
         if s.lines is not None:
             return s.lines[i]
-        return bytes(s.data[int(s.offsets[i]): int(s.offsets[i + 1])])
+        d = s.data.numpy() if hasattr(s.data, "numpy") else s.data   # a pinned torch tensor or numpy
+        return d[int(s.offsets[i]): int(s.offsets[i + 1])].tobytes()

@@ -78,8 +78,11 @@ def main():
 
     def alloc(n, k):
         if dense and k == "MU":   # one record per message, no spill regions: ST_OVF_OUT and ST_OVF_TILE
-            return eng.alloc_out(n, n, 40 * n, 0)
-        return eng.alloc_out(n, 12 * n + 4096, 320 * n + 65536, eng.pulses_work_bytes(n) if k != "MC" else 0)
+            return eng.alloc_out(n, n, 40 * n, 0, wire=True)
+        # the kernels write the exchange's counts (ABI 12) in the pipelined mode; the overflow mode's
+        # MS / MC launches leave the classification to the exchange kernels
+        return eng.alloc_out(n, 12 * n + 4096, 320 * n + 65536, eng.pulses_work_bytes(n) if k != "MC" else 0,
+                             wire=not dense)
 
     outs = [{k: alloc(hi - lo, k) for k in kinds} for _ in range(2)]
     stream = torch.cuda.current_stream(dev)

@@ -382,6 +382,57 @@ def test_exchange_kernels_match_host_wire():
 
 
 @pytest.mark.gpu
+def test_kernel_written_wire_counts_match_the_scan():
+    """ABI 12: the MU / MS (short and long k_pulses, spill regions) and MC (k_mc) flushes write the
+    exchange's per-message counts and per-record classes (sdx_out.wire_dev / xrec_dev); the wire
+    packed from them is byte-identical to the wire of the same launches classified by the exchange
+    kernels themselves (parts without them), nibble form on and off, and equals the host
+    wire_encode of the fetched outputs."""
+    from pysignalduino_amd import bank as bankmod, synth
+    dev = torch.device("cuda", 0)
+    eng = runtime.Engine(bankmod.Bank(), 0)
+    P = eng.bank.protocols
+    s = torch.cuda.current_stream(dev)
+    n = 20000
+    launches = []
+    for kind, c in ((runtime.KIND_MU, synth.mu_corpus(P, n, seed=31, noise_frac=0.0)),   # heavy tiles spill
+                    (runtime.KIND_MS, synth.ms_corpus(P, n, seed=32)),
+                    (runtime.KIND_MU, synth.mu_corpus(P, 400, seed=33, npulse=700)),       # long variant
+                    (runtime.KIND_MC, synth.mc_corpus(P, n, seed=34))):
+        bd = eng.to_device_mc(c) if kind == runtime.KIND_MC else eng.to_device_pulses(c)
+        o = eng.alloc_out(c.n, 16 * c.n + 4096, 400 * c.n + 65536,
+                          eng.pulses_work_bytes(c.n) if kind != runtime.KIND_MC else 0, wire=True)
+        if kind == runtime.KIND_MC:
+            eng.launch_mc(bd, o)
+        else:
+            eng.launch_pulses(kind, bd, o, long_variant=c.n == 400)
+        launches.append((kind, o))
+    torch.cuda.synchronize()
+    for _, o in launches:
+        assert int(o["cursor"][2]) == 0
+    spilled = int(launches[0][1]["cursor"][3])
+    for nib in (True, False):
+        sends = []
+        for use in (True, False):
+            parts = [sdist.Part.from_out(o, kind if nib else runtime.KIND_RAW) for kind, o in launches]
+            if not use:
+                for p in parts:
+                    p.wire = p.xrec = None
+            ex = _kernel_exchange(eng if nib else None)
+            cnt = ex._count_pack_device(sdist._flatten(parts), s).cpu().numpy().reshape(len(parts), runtime.XCHG_COUNTS)
+            offs, nb, T = sdist._layout(cnt[None])
+            sends.append((cnt, ex._bufs["send"][:T].cpu().numpy().copy()))
+        assert (sends[0][0] == sends[1][0]).all(), (nib, sends[0][0], sends[1][0])
+        assert sends[0][1].tobytes() == sends[1][1].tobytes(), nib
+        assert sends[0][0][:, 3].sum() == 0 and sends[0][0][:, 1].sum() > 3 * n
+        for k, (kind, o) in enumerate(launches):   # and the host's wire of the same outputs
+            d, r, h = eng.fetch(o)
+            m, w, p, bad = sdist.wire_encode(d, r, h, affix=eng.bank.affixes(kind) if nib else None)
+            assert list(sends[0][0][k][:4]) == [len(m), len(w), len(p), bad], (nib, k)
+    assert spilled > 0   # the dense MU launch used spill regions (payloads classified in HBM too)
+
+
+@pytest.mark.gpu
 def test_exchange_overlays_on_device():
     """sdx_xchg_part.alt / aux (ABI 11): a launch with overflowed messages and two overlays -> the
     device wire equals the host wire_encode with the same overlays (last present level wins, nibble

@@ -98,3 +98,35 @@ def test_stream_capacity_and_empty_chunk():
     ls.submit([])
     out = ls.drain()
     assert len(out) == 1 and out[0].n == 0 and out[0].texts() == []
+
+
+def test_stream_pinned_submit_matches_batch_api(golden):
+    """submit_packed from PINNED torch tensors (uploaded in place, no host copy): the same texts as
+    the batch API, fallback lines (general path, contract) taken from the tensor."""
+    import torch
+    from pysignalduino_amd.frontend import SignalParser, pack_lines
+    from pysignalduino_amd.sd_protocols import SDProtocols
+    lines = _mixed_lines(golden, seed=11)[:6000]
+    sp = SignalParser(SDProtocols(mc_mode="fixed"))
+    ls = sp.stream(chunk_lines=2000, chunk_bytes=2000 * 4200, output="json", lag=2)
+    chunks, got = [], []
+    for i in range(0, len(lines), 2000):
+        ch = lines[i: i + 2000]
+        data, offs, bad = pack_lines(ch)
+        assert not bad
+        t = torch.from_numpy(data.copy()).pin_memory()
+        chunks.append((ch, t))                      # kept alive until collected
+        ls.submit_packed(t, offs)
+        got += [r.detach() for r in ls.poll()]
+    got += [r.detach() for r in ls.drain()]
+    assert len(got) == len(chunks)
+    nres = 0
+    for (ch, _), r in zip(chunks, got):
+        exp = sp.parse_lines_json(ch)
+        for i, (e, g) in enumerate(zip(exp, r.texts())):
+            if isinstance(e, Exception):
+                assert isinstance(g, type(e)), (i, e, g)
+            else:
+                assert e == g, (i, e, g)
+                nres += e is not None
+    assert nres > 1000

@@ -77,8 +77,8 @@ def main():
     for k in range(nck):
         o = offsets[k * C: (k + 1) * C + 1].astype(np.int64)
         b = torch.from_numpy(data[o[0]: o[-1]].copy()).pin_memory()
-        chunks.append((b.numpy(), o - o[0]))
-    maxb = max(len(b) for b, _ in chunks)
+        chunks.append((b, o - o[0]))
+    maxb = max(b.numel() for b, _ in chunks)
     ls = sp.stream(chunk_lines=C, chunk_bytes=maxb, output=args.output, lag=args.lag)
     # warm-up: one pass through every stage (kernels loaded, buffers touched)
     for b, o in chunks[:2]:
@@ -109,7 +109,7 @@ def main():
     k_demod = float(np.median([c.elapsed_time(d) * 1e-3 for _, _, c, d in ke]))
     span = [ke[i][0].elapsed_time(ke[i][3]) * 1e-3 for i in range(len(ke))]
     per_chunk = dt / nsteps
-    h2d_rate, d2h_rate = copy_rates(torch, chunks[0][0])
+    h2d_rate, d2h_rate = copy_rates(torch, chunks[0][0].numpy())
     stages = {"kernels (parse + demod + serialise)": k_parse + k_demod,
               "H2D": ls.h2d_bytes / nsteps / h2d_rate, "D2H": ls.d2h_bytes / nsteps / d2h_rate,
               "host (submit + poll)": host_t / nsteps}
@@ -131,6 +131,7 @@ def main():
     res["bound"] = max(stages, key=stages.get)
     if args.check:
         b, o = chunks[0]
+        b = b.numpy()
         lines = [b[o[i]: o[i + 1]].tobytes() for i in range(C)]
         bad = 0
         if args.output == "json":

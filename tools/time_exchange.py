@@ -1,7 +1,8 @@
 """Standalone time of the exchange's sender kernels (sdx_exchange_count + sdx_exchange_pack) on the
 bench step's outputs (1M messages: MU/MS/MC 1/3 each), and of the receiver rebuild
-(sdx_exchange_unpack) at world 1.  usage: python tools/time_exchange.py [msgs] [reps] [raw]
-(raw: payloads without the nibble form)"""
+(sdx_exchange_unpack) at world 1.  usage: python tools/time_exchange.py [msgs] [reps] [raw|scan]
+(raw: payloads without the nibble form; scan: the exchange classifies every payload itself instead of
+reading the counts the kernels wrote, ABI 12)"""
 import os
 import sys
 
@@ -15,7 +16,8 @@ from pysignalduino_amd import bank as bankmod, dist as sdist, runtime, synth
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    nib = not (len(sys.argv) > 3 and sys.argv[3] == "raw")
+    mode = sys.argv[3] if len(sys.argv) > 3 else ""
+    nib = mode != "raw"
     bk = bankmod.Bank()
     eng = runtime.Engine(bk, 0)
     P = bk.protocols
@@ -25,7 +27,8 @@ def main():
         c = (synth.mu_corpus if k == "MU" else synth.ms_corpus if k == "MS" else synth.mc_corpus)(P, per[k], seed=s)
         bd = eng.to_device_mc(c) if k == "MC" else eng.to_device_pulses(c)
         caps = {"MU": (12, 320), "MS": (4, 64), "MC": (4, 96)}[k]
-        o = eng.alloc_out(c.n, caps[0] * c.n + 4096, caps[1] * c.n + 65536, eng.pulses_work_bytes(c.n) if k != "MC" else 0)
+        o = eng.alloc_out(c.n, caps[0] * c.n + 4096, caps[1] * c.n + 65536, eng.pulses_work_bytes(c.n) if k != "MC" else 0,
+                          wire=mode != "scan")
         if k == "MC":
             eng.launch_mc(bd, o)
         else:
@@ -60,7 +63,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         tu.append(e0.elapsed_time(e1))
-    print(f"count+pack {np.median(ts) * 1e3:.1f} us (min {min(ts) * 1e3:.1f}); wire {wire / 1e6:.2f} MB "
+    print(f"[{mode or 'nibble'}] count+pack {np.median(ts) * 1e3:.1f} us (min {min(ts) * 1e3:.1f}); wire {wire / 1e6:.2f} MB "
           f"(source desc+rec+heap {src / 1e6:.2f} MB); {wire / (min(ts) * 1e-3) / 1e9:.0f} GB/s of wire; "
           f"unpack x3 (world 1, incl. host sync) {min(tu) * 1e3:.0f} us; counts {S[0].tolist()}", flush=True)
 
