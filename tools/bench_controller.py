@@ -42,6 +42,7 @@ class _Ctl:
         self.mqtt_publisher = _Pub()
         self.message_callback = None
         self.logger = logging.getLogger("bench")
+        self._pending_responses = []    # as SignalduinoController.__init__ (controller.py:65)
         self.ncmd = 0
 
     async def _handle_as_command_response(self, line):
@@ -53,6 +54,7 @@ def main():
     ap.add_argument("--lines", type=int, default=200_000)
     ap.add_argument("--max-batch", type=int, default=16384)
     ap.add_argument("--publish", default="json", choices=("json", "objects"))
+    ap.add_argument("--profile", action="store_true", help="cProfile the timed loop (top 30 by own time, stderr)")
     args = ap.parse_args()
     from pysignalduino_amd import bank as B, synth
     from pysignalduino_amd.controller import BatchingParserTask
@@ -70,11 +72,20 @@ def main():
         for ln in lines:
             ctl._raw_message_queue.put_nowait(ln)
         task = BatchingParserTask(ctl, max_batch=args.max_batch, max_delay=0.002, publish=args.publish)
+        prof = None
+        if args.profile:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         runner = asyncio.create_task(task.run())
-        while ctl.ncmd < len(lines):
+        while task.lines < len(lines):      # every line taken through its effects
             await asyncio.sleep(0.001)
         dt = time.perf_counter() - t0
+        if prof is not None:
+            import pstats
+            prof.disable()
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
         ctl._stop_event.set()
         runner.cancel()
         await asyncio.gather(runner, return_exceptions=True)

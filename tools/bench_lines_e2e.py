@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--lag", type=int, default=3)
     ap.add_argument("--output", default="wire", choices=("wire", "json"))
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="cProfile the timed loop (top 30 by own time, stderr)")
     args = ap.parse_args()
     import torch
     from pysignalduino_amd import frontend, runtime, synth
@@ -90,6 +91,11 @@ def main():
     first = None
     host_t = 0.0
     torch.cuda.synchronize()
+    prof = None
+    if args.profile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for k in range(nsteps):
         b, o = chunks[k % nck]
@@ -103,6 +109,10 @@ def main():
         if first is None and args.check:
             first = r.detach()
     dt = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
     total = nsteps * C
     ke = ls.kernel_events
     k_parse = float(np.median([a.elapsed_time(b) * 1e-3 for a, b, _, _ in ke]))
