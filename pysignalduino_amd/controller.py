@@ -74,8 +74,11 @@ class BatchingParserTask:
         k = self.max_batch - len(batch)
         dq = getattr(q, "_queue", None)
         if type(q) is asyncio.Queue and q.maxsize <= 0 and isinstance(dq, collections.deque):
-            k = min(k, len(dq))
-            batch.extend([dq.popleft() for _ in range(k)])
+            if k >= len(dq):          # the whole queue fits: one bulk move
+                batch.extend(dq)
+                dq.clear()
+            else:
+                batch.extend([dq.popleft() for _ in range(k)])
             return
         for _ in range(k):
             try:

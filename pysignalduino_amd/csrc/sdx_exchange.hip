@@ -341,13 +341,49 @@ __device__ inline void zero_tail(uint8_t* sec, uint64_t used, uint32_t lane) {
   if (lane < 16 && used + lane < r16(used)) sec[used + lane] = 0;
 }
 
+// the bytes [p, p + n) (n <= 8) of a payload as a little-endian word: aligned dword loads, only of
+// dwords that hold one of those bytes (each lies inside the payload's allocation), realigned
+__device__ inline uint64_t load_le(const uint8_t* p, uint32_t n) {
+  const uint32_t sh = (uint32_t)(uintptr_t)p & 3u;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(p - sh);
+  const uint32_t w0 = a[0];
+  const uint32_t w1 = sh + n > 4 ? a[1] : 0u;
+  const uint32_t w2 = sh + n > 8 ? a[2] : 0u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  const uint64_t x = ((uint64_t)hi << 32) | lo;
+  return n >= 8 ? x : x & ((1ull << (8 * n)) - 1);
+}
+
+// one record's wire bytes: dg < 0 copies its n payload bytes; dg >= 0 packs its dg uppercase hex
+// digits two per byte (high nibble first; an odd last digit in a high nibble), n = (dg + 1) / 2
+__device__ inline void wire_copy(uint8_t* dst, const uint8_t* src, int dg, uint32_t n) {
+  for (uint32_t q = 0; q < n; q += 4) {
+    const uint32_t cnt = n - q < 4 ? n - q : 4;
+    uint32_t out;
+    if (dg < 0) {
+      out = (uint32_t)load_le(src + q, cnt);
+    } else {
+      const uint32_t nd = (uint32_t)dg - 2 * q < 8 ? (uint32_t)dg - 2 * q : 8;   // digits of this step (>= 1)
+      const uint64_t x = load_le(src + 2 * q, nd);
+      // '0'-'9' -> 0-9, 'A'-'F' -> 10-15 (bit 6 set); the bytes past the digits are zero
+      const uint64_t v = (x & 0x0F0F0F0F0F0F0F0Full) + 9ull * ((x >> 6) & 0x0101010101010101ull);
+      uint64_t y = ((v & 0x00FF00FF00FF00FFull) << 4) | ((v >> 8) & 0x00FF00FF00FF00FFull);  // digit pairs
+      y = (y | (y >> 8)) & 0x0000FFFF0000FFFFull;
+      out = (uint32_t)(y | (y >> 16));
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if ((uint32_t)b < cnt) dst[q + b] = (uint8_t)(out >> (8 * b));
+  }
+}
+
 // block = 256 consecutive messages (the count blocks), grid.y = launch.
 // A (lane = message): the wire word, the wire records (contiguous per message) and the message's
 //   records' (source address, destination, digits) into an LDS list in output order;
-// B (lane = 32 consecutive output bytes of the block's payload range): one binary search for the
-//   first byte's record, a linear walk through the list, the source byte loads (two digits per
-//   output byte in the nibble form), two 16-byte stores (byte stores only at the two ends of the
-//   range, which neighbouring blocks share).
+// B (lane = record of the list): its wire bytes (wire_copy).  One lane per record instead of one
+//   per 32 output bytes (round 3): no per-byte LDS walk and no 64 pointer registers -- the piece
+//   form took 182 VGPRs (2 waves/SIMD) and 200 us for the bench step's 1M messages in the nibble
+//   form.
 __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restrict__ counts,
                                                 uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
   __shared__ uint64_t l_src[LREC];
@@ -409,17 +445,9 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
         l_src[lr] = (uint64_t)(uintptr_t)s0;
         l_dst[lr] = lb;
         l_dig[lr] = dg;
-      } else {  // past the LDS list (a block of unusually many records): copy here, byte by byte
+      } else {  // past the LDS list (a block of unusually many records): copy here
         if (lr == LREC) l_dst[LREC] = lb;   // the list's end
-        uint8_t* dst = s_heap + (uint32_t)boff + lb;
-        for (uint32_t q = 0; q < wl; ++q) {
-          if (dg < 0) {
-            dst[q] = s0[q];
-          } else {
-            const uint32_t lo = 2 * q + 1 < (uint32_t)dg ? hexval(s0[2 * q + 1]) : 0u;
-            dst[q] = (uint8_t)((hexval(s0[2 * q]) << 4) | lo);
-          }
-        }
+        wire_copy(s_heap + (uint32_t)boff + lb, s0, dg, wl);
       }
       ++lr;
       lb += wl;
@@ -429,69 +457,13 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
   const uint32_t bbytes = (uint32_t)bnext - (uint32_t)boff;
   if (threadIdx.x == 0 && nl == brec) l_dst[nl] = bbytes;   // the list's end (truncated lists: set above)
   __syncthreads();
-  if (nl == 0) return;
-  // B: bytes [0, lim) of the block's range go through the list
-  const uint32_t lim = l_dst[nl];
-  if (lim == 0) return;                         // only empty payloads: nothing to read
-  const uint64_t G = so[2] + (uint32_t)boff;   // absolute offset of the block's first byte in send
-  const uint64_t A0 = G & ~15ull;               // 16-byte aligned 32-byte pieces
-  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(counts);   // harmless in-bounds reads
-  for (uint64_t a = A0 + 32ull * threadIdx.x; a < G + lim; a += 32ull * XT) {
-    const int64_t p0 = (int64_t)(a - G);        // block-local position of the piece's first byte
-    const uint32_t q = p0 < 0 ? 0u : (uint32_t)p0;
-    uint32_t lo = 0, hi = nl - 1;               // the last record with l_dst <= q
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (l_dst[mid] <= q) lo = mid;
-      else hi = mid - 1;
-    }
-    uint32_t r = lo;
-    // source addresses first (LDS only), then the loads without control flow between them
-    const uint8_t* s0[32];
-    const uint8_t* s1[32];
-    uint8_t form[32];   // 0 raw byte, 1 two digits, 2 one digit (the odd last one)
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const int64_t p = p0 + i;
-      s0[i] = s1[i] = dummy;
-      form[i] = 0;
-      if (p >= 0 && p < (int64_t)lim) {
-        while (r + 1 < nl && (uint32_t)p >= l_dst[r + 1]) ++r;   // zero-length payloads are passed over
-        const uint32_t off = (uint32_t)p - l_dst[r];
-        const uint8_t* base = reinterpret_cast<const uint8_t*>((uintptr_t)l_src[r]);
-        const int dg = l_dig[r];
-        if (dg < 0) {
-          s0[i] = s1[i] = base + off;
-        } else {
-          s0[i] = base + 2 * off;
-          const bool two = 2 * off + 1 < (uint32_t)dg;
-          s1[i] = two ? base + 2 * off + 1 : s0[i];
-          form[i] = two ? 1 : 2;
-        }
-      }
-    }
-    uint8_t bb[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const uint8_t c0 = *s0[i];
-      const uint8_t c1 = *s1[i];
-      bb[i] = form[i] == 0 ? c0 : (uint8_t)((hexval(c0) << 4) | (form[i] == 1 ? hexval(c1) : 0u));
-    }
-    uint32_t wv[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      wv[i] = (uint32_t)bb[4 * i] | ((uint32_t)bb[4 * i + 1] << 8) | ((uint32_t)bb[4 * i + 2] << 16) |
-              ((uint32_t)bb[4 * i + 3] << 24);
-    if (p0 >= 0 && p0 + 32 <= (int64_t)lim) {
-      reinterpret_cast<uint4*>(send + a)[0] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-      reinterpret_cast<uint4*>(send + a)[1] = make_uint4(wv[4], wv[5], wv[6], wv[7]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const int64_t p = p0 + i;
-        if (p >= 0 && p < (int64_t)lim) send[a + i] = bb[i];
-      }
-    }
+  // B (lane = record of the list): its wire bytes from aligned dword loads (raw copy, or 8 digits ->
+  // 4 bytes with SWAR), byte stores into its range of the block's heap section
+  uint8_t* bh = s_heap + (uint32_t)boff;
+  for (uint32_t i = threadIdx.x; i < nl; i += XT) {
+    const uint8_t* src = reinterpret_cast<const uint8_t*>((uintptr_t)l_src[i]);
+    const uint32_t d0 = l_dst[i];
+    wire_copy(bh + d0, src, l_dig[i], l_dst[i + 1] - d0);
   }
 }
 

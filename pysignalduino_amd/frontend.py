@@ -187,6 +187,19 @@ def pack_lines(lines: Sequence[Union[str, bytes]], copy: bool = True):
     """Concatenate lines into (data uint8, offsets int64[n+1]); per-line ContractError where a line
     cannot be represented (returned in ``bad``; such lines are replaced by an empty line).
     ``copy=False``: data is a read-only view of the joined bytes (one host copy fewer)."""
+    if lines and set(map(type, lines)) == {str}:
+        # all str (what the transports deliver): one join and one latin-1 encode for the whole batch
+        # (a str's latin-1 bytes are as many as its characters); any character above U+00FF sends
+        # the batch to the per-line path below, which marks just those lines
+        try:
+            blob = "".join(lines).encode("latin-1")
+        except UnicodeEncodeError:
+            blob = None
+        if blob is not None:
+            offsets = np.zeros(len(lines) + 1, np.int64)
+            np.cumsum(np.fromiter(map(len, lines), np.int64, len(lines)), out=offsets[1:])
+            data = np.frombuffer(blob, np.uint8)
+            return (data.copy() if copy else data), offsets, {}
     bs, bad = [], {}
     for i, ln in enumerate(lines):
         try:

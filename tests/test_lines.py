@@ -81,6 +81,27 @@ def test_synth_lines_roundtrip():
     assert ok[LO.MU] > 150 and ok[LO.MS] > 150 and ok[LO.MC] > 80, ok
 
 
+def test_pack_lines_bulk_and_per_line_forms_agree():
+    """frontend.pack_lines: the bulk form for all-str batches (one join + one latin-1 encode) gives the
+    bytes and offsets of the per-line form; a character above U+00FF marks exactly its own line
+    (ContractError, replaced by an empty line) and leaves the others' bytes."""
+    from pysignalduino_amd.frontend import pack_lines
+    from pysignalduino_amd.packing import ContractError
+    lines = ["\x02MU;P0=-1000;P1=500;D=0101;CP=1;\x03", "", "MS;P0=1;D=\xb5\xff;", "x" * 300]
+    d, o, bad = pack_lines(lines)
+    mixed = [ln.encode("latin-1") for ln in lines[:2]] + lines[2:]            # bytes + str: per-line form
+    d2, o2, bad2 = pack_lines(mixed)
+    assert not bad and not bad2 and d.tobytes() == d2.tobytes() and o.tolist() == o2.tolist()
+    cum = [0]
+    for ln in lines:
+        cum.append(cum[-1] + len(ln))
+    assert d.tobytes() == "".join(lines).encode("latin-1") and o.tolist() == cum
+    d3, o3, bad3 = pack_lines(lines[:2] + ["P\u0100"] + lines[2:], copy=False)
+    assert list(bad3) == [2] and isinstance(bad3[2], ContractError)
+    assert d3.tobytes() == "".join(lines).encode("latin-1") and o3.tolist() == cum[:3] + cum[2:]
+    assert pack_lines([])[1].tolist() == [0]
+
+
 def test_compressed_payload_decompresses_to_the_plain_one():
     P = B.Bank().protocols
     pb = synth.ms_corpus(P, 200, seed=3)
