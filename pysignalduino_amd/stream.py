@@ -240,7 +240,7 @@ class LineStream:
     def _stage_a(self, s: _Slot, data, offsets):
         t = self.torch
         n, o0, nb = s.n, int(offsets[0]), int(offsets[-1] - offsets[0])
-        s.h_offs.numpy()[: n + 1] = offsets - o0
+        np.subtract(offsets, o0, out=s.h_offs.numpy()[: n + 1])   # rebased straight into the pinned buffer
         lb = s.lb
         pinned = isinstance(data, t.Tensor) and data.is_pinned()
         if not pinned:
