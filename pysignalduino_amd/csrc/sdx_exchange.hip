@@ -46,7 +46,6 @@ constexpr int XT = 256;       // threads per block; one message per thread in th
 constexpr int XB = XT;        // items per block
 constexpr int XMAX = SDX_XCHG_MAX_PARTS;
 constexpr int XRANKS = SDX_XCHG_MAX_RANKS;
-constexpr int LREC = 2048;    // records of a pack block listed in LDS for the coalesced payload copy
 constexpr uint64_t BADBIT = 1ull << 63;
 constexpr int CHAIN = 8;      // overlays per launch (general-path rows, re-runs, re-runs of re-runs)
 
@@ -378,17 +377,19 @@ __device__ inline void wire_copy(uint8_t* dst, const uint8_t* src, int dg, uint3
 }
 
 // block = 256 consecutive messages (the count blocks), grid.y = launch.
-// A (lane = message): the wire word, the wire records (contiguous per message) and the message's
-//   records' (source address, destination, digits) into an LDS list in output order;
-// B (lane = record of the list): its wire bytes (wire_copy).  One lane per record instead of one
-//   per 32 output bytes (round 3): no per-byte LDS walk and no 64 pointer registers -- the piece
-//   form took 182 VGPRs (2 waves/SIMD) and 200 us for the bench step's 1M messages in the nibble
-//   form.
+// A (lane = message): the wire word; the message's first record (block-local record prefix of the
+//   count), its resolved part and rec_begin into LDS;
+// B (lane = record, chunks of 256 in output order): the record's message by a binary search over the
+//   record prefixes, its sdx_result and class (the kernel-written xrec, or the scan), the wire record,
+//   a block scan of the wire bytes for its destination, and its payload bytes (wire_copy).
+// Every lane has work in both phases (round 3's phase A looped over each message's records with the
+// other lanes idle, and its payload phase took one lane per 32 output bytes: 182 VGPRs, 2 waves/SIMD,
+// 200 us for the bench step's 1M messages in the nibble form).
 __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restrict__ counts,
                                                 uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
-  __shared__ uint64_t l_src[LREC];
-  __shared__ uint32_t l_dst[LREC + 1];
-  __shared__ int32_t l_dig[LREC];   // nibble form: the digit count; raw: -1
+  __shared__ uint32_t l_r0[XB + 1];  // block-local index of each message's first record (+ the end)
+  __shared__ uint32_t l_rb[XB];      // its rec_begin in the resolved part
+  __shared__ uint8_t l_pt[XB];       // the resolved part
   const int k = blockIdx.y;
   const sdx_xchg_part& x = P.p[k];
   const uint32_t nb = nblk_of(x.n_msgs);
@@ -408,62 +409,64 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
   const uint64_t boff = w.blk[blockIdx.x];
   const uint64_t bnext = blockIdx.x + 1 < nb ? w.blk[blockIdx.x + 1] : (((uint64_t)ck[1] << 32) | ck[2]);
   const uint32_t brec = (uint32_t)((bnext >> 32) - (boff >> 32));   // the block's records
-  const uint32_t m = blockIdx.x * XB + threadIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t m = blockIdx.x * XB + tid;
   if (m < x.n_msgs) {
     sdx_desc d;
-    const sdx_xchg_part& y = P.p[resolve(P, k, m, &d)];
+    const int kr = resolve(P, k, m, &d);
     const uint64_t loc = w.loc[m];
     const bool bad = (loc & BADBIT) != 0;
     const uint32_t nr = (bad || d.status != SDX_ST_OK) ? 0u : d.n_rec;
     reinterpret_cast<uint32_t*>(s_msg)[m] =
         nr | ((uint32_t)(bad ? SDX_ST_OVF_OUT : d.status) << 16) | ((uint32_t)d.raise_kind << 24);
-    const sdx_result* rec = reinterpret_cast<const sdx_result*>(y.rec_dev) + d.rec_begin;
-    uint32_t lr = (uint32_t)((loc & ~BADBIT) >> 32), lb = (uint32_t)loc;   // block-local
-    const bool xr_on = y.xrec_dev != nullptr && nibble_on(P, y);
-    for (uint32_t j = 0; j < nr; ++j) {
-      const sdx_result r = rec[j];
-      const uint8_t* src = y.heap_dev + r.payload_off;
-      int dg;
+    l_r0[tid] = (uint32_t)((loc & ~BADBIT) >> 32);
+    l_rb[tid] = d.rec_begin;
+    l_pt[tid] = (uint8_t)kr;
+  } else {
+    l_r0[tid] = brec;   // past the launch's messages: no records
+  }
+  if (tid == 0) l_r0[XB] = brec;
+  __syncthreads();
+  uint8_t* bh = s_heap + (uint32_t)boff;
+  uint32_t carry = 0;   // block-local wire byte offset of the chunk
+  for (uint32_t c = 0; c < brec; c += XT) {   // block-uniform trip count (the scan below)
+    const uint32_t r = c + tid;
+    uint32_t wl = 0;
+    int dg = -1;
+    const uint8_t* s0 = nullptr;
+    if (r < brec) {
+      uint32_t lo = 0, hi = XB - 1;   // the last message whose first record is <= r
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (l_r0[mid] <= r) lo = mid;
+        else hi = mid - 1;
+      }
+      const sdx_xchg_part& y = P.p[l_pt[lo]];
+      const uint32_t ri = l_rb[lo] + (r - l_r0[lo]);
+      const sdx_result rr = reinterpret_cast<const sdx_result*>(y.rec_dev)[ri];
+      const uint8_t* src = y.heap_dev + rr.payload_off;
       uint32_t npre = 0;
       if (y.xrec_dev) {  // ABI 12: classified by the launch's kernel
-        const uint32_t xr = xr_on ? y.xrec_dev[d.rec_begin + j] : 0u;
+        const uint32_t xr = nibble_on(P, y) ? y.xrec_dev[ri] : 0u;
         dg = (xr & SDX_XREC_NIB) ? (int)(xr & 0xFFFFu) : -1;
         npre = (xr >> 16) & 0xFFu;
       } else {
-        const Affix a = affix_of(P.bank, y.kind, r.proto);
-        dg = nib_digits(a, src, r.payload_len);
+        const Affix a = affix_of(P.bank, y.kind, rr.proto);
+        dg = nib_digits(a, src, rr.payload_len);
         npre = a.npre;
       }
       sdx_wire_rec o;
-      o.proto = (uint16_t)(r.proto | (dg >= 0 ? SDX_WIRE_NIB : 0u));
-      o.payload_len = r.payload_len;
-      o.bit_length = r.bit_length;
-      s_rec[(uint32_t)(boff >> 32) + lr] = o;
-      const uint8_t* s0 = dg >= 0 ? src + npre : src;
-      const uint32_t wl = wire_bytes_of(dg, r.payload_len);
-      if (lr < LREC) {
-        l_src[lr] = (uint64_t)(uintptr_t)s0;
-        l_dst[lr] = lb;
-        l_dig[lr] = dg;
-      } else {  // past the LDS list (a block of unusually many records): copy here
-        if (lr == LREC) l_dst[LREC] = lb;   // the list's end
-        wire_copy(s_heap + (uint32_t)boff + lb, s0, dg, wl);
-      }
-      ++lr;
-      lb += wl;
+      o.proto = (uint16_t)(rr.proto | (dg >= 0 ? SDX_WIRE_NIB : 0u));
+      o.payload_len = rr.payload_len;
+      o.bit_length = rr.bit_length;
+      s_rec[(uint32_t)(boff >> 32) + r] = o;
+      s0 = dg >= 0 ? src + npre : src;
+      wl = wire_bytes_of(dg, rr.payload_len);
     }
-  }
-  const uint32_t nl = brec < LREC ? brec : LREC;
-  const uint32_t bbytes = (uint32_t)bnext - (uint32_t)boff;
-  if (threadIdx.x == 0 && nl == brec) l_dst[nl] = bbytes;   // the list's end (truncated lists: set above)
-  __syncthreads();
-  // B (lane = record of the list): its wire bytes from aligned dword loads (raw copy, or 8 digits ->
-  // 4 bytes with SWAR), byte stores into its range of the block's heap section
-  uint8_t* bh = s_heap + (uint32_t)boff;
-  for (uint32_t i = threadIdx.x; i < nl; i += XT) {
-    const uint8_t* src = reinterpret_cast<const uint8_t*>((uintptr_t)l_src[i]);
-    const uint32_t d0 = l_dst[i];
-    wire_copy(bh + d0, src, l_dig[i], l_dst[i + 1] - d0);
+    uint64_t tot;
+    const uint32_t pre = (uint32_t)block_excl(wl, &tot);
+    if (wl) wire_copy(bh + carry + pre, s0, dg, wl);
+    carry += (uint32_t)tot;
   }
 }
 

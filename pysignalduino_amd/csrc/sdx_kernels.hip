@@ -68,10 +68,19 @@ constexpr int POOL_HEAP_MS = 8192;
 struct StageRec {
   uint32_t off;
   uint16_t len, proto;
-  uint32_t bitlen;
+  uint32_t bitlen;  // bit_length; with STAGE_NIB set: bits 0-15 bit_length, 16-30 the payload's hex digits
   uint8_t msg, wave;
   uint16_t rank;
 };
+// The finishers build every payload as preamble + digits + postamble of its protocol; when the
+// digits are uppercase hex (all but f"{None}"), the record says so, and the flush writes the
+// exchange's nibble class (sdx_out.xrec_dev, ABI 12) without reading the payload again
+constexpr uint32_t STAGE_NIB = 0x80000000u;
+SDX_DEV uint32_t stage_bitlen(int bitlen, int hex_digits, int pre_len) {
+  return (hex_digits >= 0 && hex_digits < 32768 && pre_len <= 255 && (uint32_t)bitlen < 65536u)
+             ? (STAGE_NIB | ((uint32_t)hex_digits << 16) | (uint32_t)bitlen)
+             : (uint32_t)bitlen;
+}
 
 // MU (NW <= 4): a (message, protocol) pair that passed the pattern filters, queued for the
 // compacted decode (lane = pair)
@@ -448,7 +457,7 @@ SDX_DEV void finish_mu(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, con
   copy_str(dst, bv.str + cld(&rec->pre_off), cld(&rec->pre_len));
   for (int d = lane_id(); d < dlen; d += WAVE) dst[cld(&rec->pre_len) + d] = dchar(d);
   copy_str(dst + cld(&rec->pre_len) + dlen, bv.str + cld(&rec->post_off), cld(&rec->post_len));
-  pool_commit(L, slot, wave, s, p, off, total, nbp);
+  pool_commit(L, slot, wave, s, p, off, total, (int)stage_bitlen(nbp, isf ? -1 : dlen, cld(&rec->pre_len)));
   PROF_ADD(8, t_wr);
   PROF_CNT(20, 1);
 }
@@ -856,7 +865,7 @@ SDX_DEV void finish_mu_lane(T& L, const sdx_out& out, int wave, const BankView& 
   r.off = ps.off;
   r.len = (uint16_t)total;
   r.proto = (uint16_t)p;
-  r.bitlen = (uint32_t)nbp;
+  r.bitlen = stage_bitlen(nbp, anyf ? -1 : dlen, pre_len);
   r.msg = (uint8_t)mi;
   r.wave = (uint8_t)wave;
   r.rank = (uint16_t)j;  // match index within this (message, protocol) pair: monotone
@@ -1008,7 +1017,7 @@ SDX_DEV void finish_ms(TileLds<NW, TM, LM>& L, int wave, const BankView& bv, con
   hex_digits(buf, nb, dst + cld(&rec->pre_len), 0);
   copy_str(dst + cld(&rec->pre_len) + dl, bv.str + cld(&rec->post_off), cld(&rec->post_len));
   wave_sync();
-  pool_commit(L, slot, wave, s, p, off, total, nb);
+  pool_commit(L, slot, wave, s, p, off, total, (int)stage_bitlen(nb, dl, cld(&rec->pre_len)));
 }
 
 // MS decode loop (:172-189) for one surviving pair, wave-cooperative over chunks
@@ -1200,7 +1209,7 @@ SDX_DEV void finish_ms_lane(T& L, const sdx_out& out, const BankView& bv, const 
   r.off = ps.off;
   r.len = (uint16_t)total;
   r.proto = (uint16_t)p;
-  r.bitlen = (uint32_t)nbits;
+  r.bitlen = stage_bitlen(nbits, nd, pre_len);
   r.msg = (uint8_t)mi;
   r.wave = 0;
   r.rank = 0;  // one result per (message, protocol)
@@ -1442,15 +1451,21 @@ SDX_DEV void flush_tile(TileLds<NW, TM, LM>& L, const int* msg_of, int nvalid, c
       o.payload_off = L.heap_base + ((sr.off & HEAP_SPILLED) ? nh_l16 + (sr.off & ~HEAP_SPILLED) : sr.off);
       o.payload_len = sr.len;
       o.proto = sr.proto;
-      o.bit_length = sr.bitlen;
+      const bool staged_nib = (sr.bitlen & STAGE_NIB) != 0;
+      o.bit_length = staged_nib ? (sr.bitlen & 0xFFFFu) : sr.bitlen;
       o.msg = (uint32_t)msg_of[sr.msg];
       out.rec_dev[L.rec_base + b0 + rk] = o;
       if (wx) {
-        uint32_t xr;   // two call sites: one pointer per address space (a selected generic pointer
-        if (sr.off & HEAP_SPILLED)   // here crashed the ROCm 7.2 compiler)
+        uint32_t xr;
+        if (staged_nib) {   // classified by the finisher
+          const int pl = kind == SDX_KIND_MU ? bv.mu[sr.proto].pre_len : bv.ms[sr.proto].pre_len;
+          xr = SDX_XREC_NIB | ((uint32_t)pl << 16) | ((sr.bitlen >> 16) & 0x7FFFu);
+        } else if (sr.off & HEAP_SPILLED) {  // two call sites: one pointer per address space (a
+          // selected generic pointer here crashed the ROCm 7.2 compiler)
           xr = wire_class(bv, kind, sr.proto, sreg + SPILL_OFF_H + (sr.off & ~HEAP_SPILLED), sr.len);
-        else
+        } else {
           xr = wire_class(bv, kind, sr.proto, L.heap + sr.off, sr.len);
+        }
         if (out.xrec_dev) out.xrec_dev[L.rec_base + b0 + rk] = xr;
         atomicAdd(reinterpret_cast<unsigned long long*>(&wsum[sr.msg]),
                   (unsigned long long)(((uint64_t)sr.len << 32) | wire_bytes_x(xr, sr.len)));
