@@ -50,9 +50,6 @@ def parse():
     ap.add_argument("--mrec", action="store_true",
                     help="the grouping writes message records (sdx_msg_rec) and k_pulses reads its header fields "
                          "from them instead of the scattered SoA fields: less HBM traffic, measured slower (A/B)")
-    ap.add_argument("--ms-tail", action="store_true",
-                    help="MS on a low-priority stream started with MU (its tiles fill the CUs MU's tail leaves "
-                         "idle; MU's two tiles per CU leave no LDS for an MS tile before), MC beside MS (A/B)")
     ap.add_argument("--mc-tail", action="store_true",
                     help="MC on a low-priority stream started with MU (the dispatcher gives its workgroups "
                          "the CUs MU's tail leaves idle) instead of beside MS")
@@ -296,8 +293,6 @@ def main():
         kstream["MC"] = torch.cuda.Stream(dev)
     if args.mc_tail and "MC" in kinds:
         kstream["MC"] = torch.cuda.Stream(dev, priority=lo_prio)
-    if args.ms_tail and "MS" in kinds:
-        kstream["MS"] = torch.cuda.Stream(dev, priority=lo_prio)
 
     mu_done = [None]
 
