@@ -44,6 +44,8 @@ def parse():
                     help="one stream per kind: MU, MS and MC of a step run concurrently, one kernel's tail "
                          "overlapping the others' tiles (+3.5 %% msgs/s measured; per-kernel times then include "
                          "the sharing, so the roofline line is quoted on the default serial launches)")
+    ap.add_argument("--kev-every", type=int, default=1,
+                    help="per-kernel HIP events on every k-th timed step only (A/B of the events' own cost)")
     ap.add_argument("--serial", action="store_true",
                     help="MU, MS and MC one after another on one stream (default: MC on a second stream, "
                          "started when MU ends, so MC runs beside MS while MU runs alone)")
@@ -242,7 +244,7 @@ def main():
             n = corp[k].n
             o[k] = eng.alloc_out(n, caps[k][0] * n + 4096, caps[k][1] * n + 65536,
                                  eng.pulses_work_bytes(n) if k != "MC" else 0, wire=dist_on and not args.scan_wire)
-            o[k]["cursor"] = cursors[s_, i]   # one fill per step resets a slot's cursors
+            o[k]["cursor"] = cursors[s_, i]   # one fill per step and stream resets a slot's cursors
         outs.append(o)
     # the launch stream at high priority, the grouping's side stream at low priority: the hardware
     # scheduler dispatches the demodulation tiles first and the grouping's small kernels fill the
@@ -264,24 +266,30 @@ def main():
         if used[par] is not None:           # step j-2's launches have read this parity's order
             side.wait_event(used[par])
         with torch.cuda.stream(side):
-            if si is not None:
+            if si is not None and si % args.kev_every == 0:
                 gev[si][0].record(side)
             for k in gkinds:
                 eng.group(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], bufs=gbufs[k][par])
-                e = torch.cuda.Event()
-                e.record(side)
-                gdone[(k, par)] = e
-            if si is not None:
-                gev[si][1].record(side)
+            # one event for all kinds: the grouping of step j ends during step j - 1, long before
+            # step j's launches wait for it
+            e = gev[si][1] if si is not None and si % args.kev_every == 0 else torch.cuda.Event()
+            e.record(side)
+            gdone[par] = e
     # config 5's product entry: this rank's shard launches + the pipelined exchange with overflow re-runs
     shd = (sdist.ShardedDemodulator(engine=eng, defer=args.xchg == "defer", nibble=not args.raw_wire)
            if dist_on else None)
     exch = shd.exchange if shd is not None else None
     KIND = {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS, "MC": runtime.KIND_MC}
     done = [None] * nslot
-    # one event pair per kernel and timed step: read after the closing synchronize
-    ev = [{k: [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for k in kinds}
-          for _ in range(args.steps)]
+    # per timed step and kernel an (start, end) pair of timing events, read after the closing
+    # synchronize.  A kernel's start event is the end event its stream last recorded or waited on
+    # when there is one (MS after MU on the launch stream, MC waiting for MU's end), so a step records
+    # few events: every event record and cross-stream wait is a packet the command processor handles
+    # between two kernels.  Round 4: ten events and waits per step cost 1.80-1.81 vs 1.77-1.78 ms per
+    # step with events on one step in 100 (profiles/r04/s2/events_ab.log); with these four, 1.778 ms
+    # on every step (profiles/r04/s3/bench_events_modes.log).  MS's and MC's times include their
+    # launch gap.
+    kev = [dict() for _ in range(args.steps)]
 
     # --concurrent: one stream per kind, the three launches of a step run concurrently (the tail of
     # one kernel overlaps the others' tiles); default: one after another on the launch stream
@@ -293,6 +301,17 @@ def main():
         kstream["MC"] = torch.cuda.Stream(dev)
     if args.mc_tail and "MC" in kinds:
         kstream["MC"] = torch.cuda.Stream(dev, priority=lo_prio)
+    # launches on other streams than the launch stream join it at the end of their step only when
+    # the exchange reads the step's outputs; otherwise each stream resets its own kinds' cursors
+    # before its launch (its previous launch on the same slot is earlier on that stream)
+    join_now = exch is not None or any(kstream[k] is not stream for k in gkinds)
+    need_start = any(kstream[k] is not stream and not (mc_beside_ms and k == "MC") for k in kinds)
+    kidx = {k: i for i, k in enumerate(kinds)}
+    own = {}                                # stream -> the kinds whose cursors it resets
+    for k in kinds:
+        own.setdefault(kstream[k], []).append(kidx[k])
+    own = {st_: slice(ix[0], ix[-1] + 1) for st_, ix in own.items()}
+    assert sum(x.stop - x.start for x in own.values()) == len(kinds), "a stream's kinds are contiguous"
 
     mu_done = [None]
 
@@ -301,45 +320,64 @@ def main():
         if done[s_] is not None:            # the exchange that read this slot has finished
             stream.wait_event(done[s_])
             done[s_] = None
-        cursors[s_].zero_()
+        if join_now or len(own) == 1:
+            cursors[s_].zero_()
+        else:
+            for st_, ix in own.items():
+                if st_ is not stream:       # after that stream's launches of nslot steps ago
+                    with torch.cuda.stream(st_):
+                        cursors[s_, ix].zero_()
+            cursors[s_, own[stream]].zero_()
         if gkinds:
             if j == 0:
                 launch_group(0)
             launch_group(j + 1, si)         # the next step's grouping, concurrent with this step
         par = j % 2
-        start = torch.cuda.Event()
-        start.record(stream)                # cursors reset, previous exchange done
+        tm = si is not None and si % args.kev_every == 0
+        last = None                         # the latest event recorded on the launch stream
+        start = None
+        if need_start:
+            start = torch.cuda.Event(enable_timing=tm)
+            start.record(stream)            # cursors reset, previous exchange done
         for k in kinds:
             ks = kstream[k]
+            e0 = None
             if ks is not stream:
                 if mc_beside_ms and k == "MC":
-                    ks.wait_event(mu_done[0])
+                    e0 = mu_done[0]
                 else:
-                    ks.wait_event(start)
-            if k in gkinds:
-                ks.wait_event(gdone[(k, par)])
+                    e0 = start
+                ks.wait_event(e0)
+            else:
+                e0 = last
+            if k in gkinds and (k == gkinds[0] or ks is not kstream[gkinds[0]]):
+                ks.wait_event(gdone[par])
             with torch.cuda.stream(ks):
-                if si is not None:
-                    ev[si][k][0].record(ks)
+                if tm and e0 is None:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(ks)
                 if k == "MC":
                     eng.launch_mc(bds[k], outs[s_][k])
                 else:
                     eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[s_][k],
                                       sel=gbufs[k][par][0][:corp[k].n] if k in gkinds else None, group=False,
                                       mrec=gbufs[k][par][2] if k in gkinds and args.mrec else None)
-                if si is not None:
-                    ev[si][k][1].record(ks)
-                if k == "MU":
-                    mu_done[0] = torch.cuda.Event()
-                    mu_done[0].record(ks)
-            if ks is not stream:
-                e = torch.cuda.Event()
-                e.record(ks)
-                stream.wait_event(e)        # the step ends when all three launches have
+                e1 = torch.cuda.Event(enable_timing=tm)
+                e1.record(ks)
+            if tm:
+                kev[si][k] = (e0, e1)
+            if k == "MU":
+                mu_done[0] = e1
+            if ks is stream:
+                last = e1
+            elif join_now:
+                stream.wait_event(e1)       # the step ends when all three launches have
+                last = None
         if gkinds:
-            u = torch.cuda.Event()
-            u.record(stream)
-            used[par] = u
+            if last is None:
+                last = torch.cuda.Event()
+                last.record(stream)
+            used[par] = last                # the step's grouped launches have read this parity's order
         if exch is not None:  # RCCL all-gather of the decoded dmsg buffers (config 5), overlapped
             parts = [sdist.Part.from_out(outs[s_][k], KIND[k], src=(KIND[k], bds[k], 0, -1)) for k in kinds]
             rel = shd.submit(parts, stream, after=mu_done[0] if args.xchg != "eager" and "MU" in kinds else None)
@@ -377,8 +415,9 @@ def main():
     if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ktimes = {k: [ev[si][k][0].elapsed_time(ev[si][k][1]) * 1e-3 for si in range(args.steps)] for k in kinds}
-    gtime = float(np.mean([gev[si][0].elapsed_time(gev[si][1]) * 1e-3 for si in range(args.steps)])) if gkinds else 0.0
+    ktimes = {k: [kev[si][k][0].elapsed_time(kev[si][k][1]) * 1e-3 for si in range(0, args.steps, args.kev_every)]
+              for k in kinds}
+    gtime = float(np.mean([gev[si][0].elapsed_time(gev[si][1]) * 1e-3 for si in range(0, args.steps, args.kev_every)])) if gkinds else 0.0
     tt = torch.tensor([dt], dtype=torch.float64, device=dev)
     if dist_on:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -2295,47 +2295,45 @@ struct McLds {
   int nrec[4], nheap[4], ovf[4];
 };
 
-SDX_DEV int hexval(uint8_t c) {
-  if (c >= '0' && c <= '9') return c - '0';
-  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-  return -1;
-}
-
-// a[w] <<= S bits across the 4-word bitstring (MSB-first words, 0 <= S < 256), no dynamic
+// a[w] <<= S bits across the MW-word bitstring (MSB-first words, 0 <= S < 64 * MW), no dynamic
 // register indexing
-SDX_DEV void shl_words4(uint64_t* a, int S) {
+template <int MW>
+SDX_DEV void shl_words(uint64_t* a, int S) {
   const int q = S >> 6, r = S & 63;
-  uint64_t o[4];
+  uint64_t o[MW];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < MW; ++w) {
     uint64_t hi = 0, lo = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < MW; ++k) {
       hi |= a[k] & (0ull - (uint64_t)(k == w + q));
       lo |= a[k] & (0ull - (uint64_t)(k == w + q + 1));
     }
     o[w] = r ? ((hi << r) | (lo >> (64 - r))) : hi;
   }
 #pragma unroll
-  for (int w = 0; w < 4; ++w) a[w] = o[w];
+  for (int w = 0; w < MW; ++w) a[w] = o[w];
 }
 
-// hex -> MSB-first bits of a frame of 1..64 characters, both polarities, into the LDS words
+// hex -> MSB-first bits of a frame of 1..16 MW characters, both polarities, into the LDS words
 // dn[w * 256] / di[w * 256] (helpers.py:168-188, manchester.py:36; leading zero nibbles dropped as
-// bin(int(h, 16)) does, the last nibble always kept).  The characters come in with nine aligned
+// bin(int(h, 16)) does, the last nibble always kept).  The characters come in with 2 MW + 1 aligned
 // 8-byte loads issued together (hex_dev is readable 8 bytes past every frame's end) and are
 // decoded in registers; the LDS words are written once.
-SDX_DEV void mc_stage_short(const uint8_t* src, int hl, uint64_t* dn, uint64_t* di, int* nN, int* nI, bool* ok) {
+template <int MW>
+SDX_DEV void mc_stage(const uint8_t* src, int hl, uint64_t* dn, uint64_t* di, int* nN, int* nI, bool* ok) {
+  constexpr int NR = 2 * MW + 1;
   const int s = (int)((uintptr_t)src & 7);
   const uint64_t* wp = reinterpret_cast<const uint64_t*>(src - s);
-  uint64_t raw[9];
+  uint64_t raw[NR];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) raw[k] = (8 * k < s + hl) ? wp[k] : 0ull;
-  uint64_t wn[4] = {0, 0, 0, 0}, wi[4] = {0, 0, 0, 0};
+  for (int k = 0; k < NR; ++k) raw[k] = (8 * k < s + hl) ? wp[k] : 0ull;
+  uint64_t wn[MW], wi[MW];
+#pragma unroll
+  for (int w = 0; w < MW; ++w) wn[w] = wi[w] = 0;
   bool bad = false;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < 2 * MW; ++k) {
     const uint64_t x = s ? ((raw[k] >> (8 * s)) | (raw[k + 1] << (64 - 8 * s))) : raw[k];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -2354,20 +2352,20 @@ SDX_DEV void mc_stage_short(const uint8_t* src, int hl, uint64_t* dn, uint64_t* 
   *ok = !bad;
   // leading zero nibbles (at most hl - 1 of them)
   auto lead = [&](const uint64_t* a) -> int {
-    int f = 256;
+    int f = 64 * MW;
 #pragma unroll
-    for (int w = 3; w >= 0; --w)
+    for (int w = MW - 1; w >= 0; --w)
       if (a[w]) f = 64 * w + __clzll((long long)a[w]);
     const int lz = f >> 2;
     return lz < hl - 1 ? lz : hl - 1;
   };
   const int lzn = lead(wn), lzi = lead(wi);
-  shl_words4(wn, 4 * lzn);
-  shl_words4(wi, 4 * lzi);
+  shl_words<MW>(wn, 4 * lzn);
+  shl_words<MW>(wi, 4 * lzi);
   *nN = 4 * (hl - lzn);
   *nI = 4 * (hl - lzi);
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < MW; ++w) {
     dn[w * 256] = wn[w];
     di[w * 256] = wi[w];
   }
@@ -2417,34 +2415,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     flags = b.flags_dev[msg];
     if (b.only_dev) only = b.only_dev[msg];
     hex_ok = hl > 0 && hl <= MW * 16;
-    if constexpr (!LONG) {
-      if (hex_ok) mc_stage_short(b.hex_dev + off, hl, &L.bn[tid], &L.bi[tid], &nN, &nI, &hex_ok);
-    }
-  }
-  if (LONG && valid) {  // frames of 65..128 characters: character by character
-    const int64_t off = b.offsets_dev[msg];
-    const int hl = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
-    bool startedN = false, startedI = false;
-    for (int w = 0; w < MW; ++w) { L.bn[w * 256 + tid] = 0; L.bi[w * 256 + tid] = 0; }
-    for (int i = 0; i < hl && hex_ok; ++i) {
-      const uint8_t c = b.hex_dev[off + i];
-      const int v = hexval(c);
-      if (v < 0) { hex_ok = false; break; }
-      const bool upper = (c >= '0' && c <= '9') || (c >= 'A' && c <= 'F');  // str.translate table
-      const int vi = upper ? 15 - v : v;
-      if (v || startedN || i == hl - 1) {
-        startedN = true;
-        const int w = nN >> 6, o = nN & 63;
-        L.bn[w * 256 + tid] |= (uint64_t)v << (60 - o);
-        nN += 4;
-      }
-      if (vi || startedI || i == hl - 1) {
-        startedI = true;
-        const int w = nI >> 6, o = nI & 63;
-        L.bi[w * 256 + tid] |= (uint64_t)vi << (60 - o);
-        nI += 4;
-      }
-    }
+    if (hex_ok) mc_stage<MW>(b.hex_dev + off, hl, &L.bn[tid], &L.bi[tid], &nN, &nI, &hex_ok);
   }
   const int nmc = (int)bv.hdr->n_mc;
   int raise = 0, mycnt = 0;

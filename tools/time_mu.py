@@ -21,25 +21,40 @@ def main():
     # profile-guided processing order (bank.py MU_COST_KCYC / MS_COST_KCYC)
     corpus = os.environ.get("SDX_CORPUS", "bench")
     kw = {"dense": {"noise_frac": 0.0}, "zipf": {"skew": 1.2}}.get(corpus, {})
-    for kind, gen in (("MU", synth.mu_corpus), ("MS", synth.ms_corpus)):
-        pb = gen(bk.protocols, n, seed=42, **kw)
-        bd = eng.to_device_pulses(pb)
-        out = eng.alloc_out(pb.n, 12 * pb.n + 4096, 320 * pb.n + 65536, eng.pulses_work_bytes(pb.n))
+    # SDX_KINDS: the kinds to time (default MU,MS,MC; MC times k_mc's short + long launches)
+    kinds = os.environ.get("SDX_KINDS", "MU,MS,MC").split(",")
+    gens = {"MU": synth.mu_corpus, "MS": synth.ms_corpus, "MC": synth.mc_corpus}
+    for kind in kinds:
+        if kind == "MC":
+            pb = synth.mc_corpus(bk.protocols, n, seed=44)
+            bd = eng.to_device_mc(pb)
+            out = eng.alloc_out(pb.n, 4 * pb.n + 4096, 96 * pb.n + 65536, 0, wire=bool(os.environ.get("SDX_WIRE")))
+        else:
+            pb = gens[kind](bk.protocols, n, seed=42, **kw)
+            bd = eng.to_device_pulses(pb)
+            out = eng.alloc_out(pb.n, 12 * pb.n + 4096, 320 * pb.n + 65536, eng.pulses_work_bytes(pb.n),
+                                wire=bool(os.environ.get("SDX_WIRE")))
         k = runtime.KIND_MU if kind == "MU" else runtime.KIND_MS
-        eng.launch_pulses(k, bd, out, group=not os.environ.get("SDX_NOGROUP"))
+
+        def launch():
+            if kind == "MC":
+                eng.launch_mc(bd, out)
+            else:
+                eng.launch_pulses(k, bd, out, group=not os.environ.get("SDX_NOGROUP"))
+        launch()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ts = []
         for _ in range(reps):
             out["cursor"].zero_()
             e0.record()
-            eng.launch_pulses(k, bd, out, group=not os.environ.get("SDX_NOGROUP"))
+            launch()
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         cur = out["cursor"].cpu().numpy()
         res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) * 112 >> 10} MB)")
-    tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped") + (" order=" + os.environ.get("SDX_MU_ORDER", "lpt")) + " corpus=" + corpus
+    tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped") + (" order=" + os.environ.get("SDX_MU_ORDER", "lpt")) + " corpus=" + corpus + (" wire" if os.environ.get("SDX_WIRE") else "")
     print(tag, " | ".join(res), flush=True)
 
 
