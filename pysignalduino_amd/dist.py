@@ -449,6 +449,7 @@ class Exchange:
                 self._complete(_Pending(parts, allc, None, enc, rerun=rerun))
             return None
         if self.stream is None:
+            # (a low-priority exchange stream measured no different: profiles/r04/s3/xchg_sched_ab.log)
             self.stream = torch.cuda.Stream(dev)
         stream = stream or torch.cuda.current_stream(dev)
         if self.defer:

@@ -20,6 +20,7 @@
 #   time=V1,V2           tools/time_mu.py for in-tree libsdx + variants V (pysignalduino_amd/_lib/ab/libsdx_V.so), 2 rounds
 #   env=E1,E2            bench.py --no-cpu under env settings E (VAR=value), 2 rounds
 #   py=SCRIPT[,ARGS]     python SCRIPT ARGS (a tools/ measurement)          -> OUT/py_<n>.log
+#   benchenv=VAR=val[,ARGS]  bench.py ARGS with VAR=val in the environment -> OUT/bench_<n>.log
 #   pyenv=VAR=val,SCRIPT[,ARGS]  python SCRIPT ARGS with VAR=val in the environment -> OUT/pyenv_<n>.log
 #   pylib=V,SCRIPT[,ARGS] the same with SDX_LIB = pysignalduino_amd/_lib/ab/libsdx_V.so (e.g. the SDX_PROF build)
 set -u -o pipefail
@@ -83,6 +84,9 @@ for st in "$@"; do
         echo "$e $r: $(tail -1 "$O/env_${tag}_$r.log" | summ)"
       done; done ;;
     py) run 600 "$O/py_$n.log" python -u $args; echo "py $arg: $(tail -3 "$O/py_$n.log" | cut -c1-400)" ;;
+    benchenv) e=${args%% *}; rest=${args#* }; [ "$rest" = "$e" ] && rest=""
+      run 240 "$O/bench_$n.log" env "$e" python bench.py --no-cpu $rest
+      echo "bench $arg: $(tail -1 "$O/bench_$n.log" | summ)" ;;
     pyenv) e=${args%% *}; rest=${args#* }
       run 600 "$O/pyenv_$n.log" env "$e" python -u $rest
       echo "pyenv $arg: $(tail -3 "$O/pyenv_$n.log" | cut -c1-400)" ;;
