@@ -2334,6 +2334,9 @@ SDX_DEV void mc_stage(const uint8_t* src, int hl, uint64_t* dn, uint64_t* di, in
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < 2 * MW; ++k) {
+#ifdef SDX_MC_DYN
+    if (!__ballot(8 * k < hl)) break;  // no active lane has characters from here on (wave-uniform)
+#endif
     const uint64_t x = s ? ((raw[k] >> (8 * s)) | (raw[k + 1] << (64 - 8 * s))) : raw[k];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -2401,6 +2404,16 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     atomicOr(&out.cursor_dev[2], 2u);
   }
   if (LONG && !__ballot(valid)) return;  // whole wave without long frames (nothing staged yet)
+#ifdef SDX_PROF  // per-wave cycles of k_mc's phases (g_prof slots 27-31, tools/prof_phases.py)
+#define MCPROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define MCPROF_ADD(slot, v) \
+  if (lane == 0) atomicAdd(&g_prof[slot], __builtin_amdgcn_s_memtime() - (v))
+#else
+#define MCPROF_T(v)
+#define MCPROF_ADD(slot, v)
+#endif
+  MCPROF_T(t_all);
+  MCPROF_T(t_st);
   if (lane == 0) { L.nrec[wave] = 0; L.nheap[wave] = 0; L.ovf[wave] = 0; }
   const LaneBits BN{&L.bn[tid], MW, false}, BI{&L.bi[tid], MW, false};
   // hex -> bits for both polarities (helpers.py:168-188: leading zero nibbles are dropped)
@@ -2417,9 +2430,11 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     hex_ok = hl > 0 && hl <= MW * 16;
     if (hex_ok) mc_stage<MW>(b.hex_dev + off, hl, &L.bn[tid], &L.bi[tid], &nN, &nI, &hex_ok);
   }
+  MCPROF_ADD(27, t_st);
   const int nmc = (int)bv.hdr->n_mc;
   int raise = 0, mycnt = 0;
   for (int p = 0; p < nmc; ++p) {
+    MCPROF_T(t_m);
     const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
     bool go = valid && !raise && (only < 0 || only == p);
     // gates of _demodulate_mc_data (manchester.py:70-89; clockrange fixed to [0] / [1])
@@ -2439,7 +2454,9 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     }
     // stage results of the wave in lane (= frame) order for this protocol
     const bool has = o.rc == 1;
+    MCPROF_ADD(28, t_m);
     if (!ballot(has)) continue;  // no result in this wave: nothing to stage (wave-uniform)
+    MCPROF_T(t_r);
     const int plen = has ? cld(&r->pre_len) + o.len : 0;
     int incl = plen;  // inclusive scan over lanes
     for (int d = 1; d < WAVE; d <<= 1) {
@@ -2479,7 +2496,9 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
       else if (nnew) L.ovf[wave] = 1;
     }
     wave_sync();
+    MCPROF_ADD(29, t_r);
   }
+  MCPROF_T(t_f);
   // flush this wave's frames: records are staged in protocol-major order, each carrying its rank
   // among its frame's records; the wave writes them 64 at a time to (frame, protocol) order
   const int nr = L.nrec[wave];
@@ -2554,6 +2573,10 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     wave_sync();
     if (valid) out.wire_dev[msg] = (!raise && st == 0) ? (uint64_t)wsum[lane] : 0ull;
   }
+  MCPROF_ADD(30, t_f);
+  MCPROF_ADD(31, t_all);
+#undef MCPROF_T
+#undef MCPROF_ADD
 }
 
 }  // namespace sdx

@@ -63,6 +63,24 @@ def main():
         tot_g = g[0].sum()
         print("   " + " ".join(f"{int(i)}:{g[0, i] / tot_g * 100:.1f}%/{g[0, i] / max(g[1, i], 1):.0f}"
                               for i in order if g[1, i] > 0))
+    # k_mc (slots 27-31)
+    pb = synth.mc_corpus(bk.protocols, n, seed=44)
+    bd = eng.to_device_mc(pb)
+    out = eng.alloc_out(pb.n, 4 * pb.n + 4096, 96 * pb.n + 65536, 0)
+    for it in range(2):
+        out["cursor"].zero_()
+        lib.sdx_prof_read(buf, 1)
+        t = time.perf_counter()
+        eng.launch_mc(bd, out)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+    lib.sdx_prof_read(buf, 1)
+    v = np.array(list(buf), dtype=np.float64)
+    tot = v[31]
+    print(f"== MC: {pb.n} frames, {dt*1e3:.2f} ms wall; wave-cycles total {tot:.3e} ({tot/pb.n:.0f} per frame)")
+    for i, name in ((27, "stage (hex -> bits)"), (28, "protocol gates + method"), (29, "result staging"),
+                    (30, "flush"), (31, "kernel total")):
+        print(f"  {name:28s} {v[i]/tot*100:6.2f} %   {v[i]/pb.n:9.0f} wave-cycles/frame")
 
 
 if __name__ == "__main__":
