@@ -77,8 +77,14 @@ class BatchingParserTask:
             if k >= len(dq):          # the whole queue fits: one bulk move
                 batch.extend(dq)
                 dq.clear()
+            elif 8 * k >= len(dq):    # most of it: copy out and put the rest back (C-level copies)
+                rest = list(dq)
+                dq.clear()
+                batch.extend(rest[:k])
+                dq.extend(rest[k:])
             else:
-                batch.extend([dq.popleft() for _ in range(k)])
+                pop = dq.popleft
+                batch.extend([pop() for _ in range(k)])
             return
         for _ in range(k):
             try:
@@ -198,7 +204,7 @@ class BatchingParserTask:
         while not c._stop_event.is_set():
             try:
                 batch = await self._next_batch(self.max_delay if pending else None)
-                lines = [ln for ln in batch if ln]
+                lines = list(filter(None, batch))
                 if lines:
                     await asyncio.to_thread(ls.submit, lines)
                     pending.append(lines)
@@ -228,7 +234,7 @@ class BatchingParserTask:
         while not c._stop_event.is_set():
             try:
                 batch = await self._next_batch()
-                lines = [ln for ln in batch if ln]
+                lines = list(filter(None, batch))
                 if lines:
                     parse = c.parser.parse_lines_json if self.publish == "json" else c.parser.parse_lines
                     results = await asyncio.to_thread(parse, lines)

@@ -2292,7 +2292,6 @@ struct McLds {
   uint64_t bi[MW * 256];   // bits, polarity inverted
   StageRec rec[4][MC_REC_CAP];
   alignas(16) uint8_t heap[4][MC_HEAP_CAP];
-  int nrec[4], nheap[4], ovf[4];
 };
 
 // a[w] <<= S bits across the MW-word bitstring (MSB-first words, 0 <= S < 64 * MW), no dynamic
@@ -2334,9 +2333,6 @@ SDX_DEV void mc_stage(const uint8_t* src, int hl, uint64_t* dn, uint64_t* di, in
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < 2 * MW; ++k) {
-#ifdef SDX_MC_DYN
-    if (!__ballot(8 * k < hl)) break;  // no active lane has characters from here on (wave-uniform)
-#endif
     const uint64_t x = s ? ((raw[k] >> (8 * s)) | (raw[k + 1] << (64 - 8 * s))) : raw[k];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -2404,17 +2400,22 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     atomicOr(&out.cursor_dev[2], 2u);
   }
   if (LONG && !__ballot(valid)) return;  // whole wave without long frames (nothing staged yet)
-#ifdef SDX_PROF  // per-wave cycles of k_mc's phases (g_prof slots 27-31, tools/prof_phases.py)
+#ifdef SDX_PROF  // per-wave cycles of k_mc's phases (g_prof slots 27-31, tools/prof_phases.py), summed
+  // in registers; per protocol (g_gprof[0][p] cycles, [1][p] lanes through the gates) in LDS
+  unsigned long long mcacc[5] = {0, 0, 0, 0, 0};
+  __shared__ unsigned long long mcp[2][32];
+  if (tid < 64) mcp[tid >> 5][tid & 31] = 0;
+  if constexpr (!LONG) __syncthreads();
 #define MCPROF_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
-#define MCPROF_ADD(slot, v) \
-  if (lane == 0) atomicAdd(&g_prof[slot], __builtin_amdgcn_s_memtime() - (v))
+#define MCPROF_ADD(slot, v) mcacc[(slot) - 27] += __builtin_amdgcn_s_memtime() - (v)
 #else
 #define MCPROF_T(v)
 #define MCPROF_ADD(slot, v)
 #endif
   MCPROF_T(t_all);
   MCPROF_T(t_st);
-  if (lane == 0) { L.nrec[wave] = 0; L.nheap[wave] = 0; L.ovf[wave] = 0; }
+  int w_heap = 0, w_rec = 0;  // the wave's staged payload bytes and records (wave-uniform)
+  bool w_ovf = false;
   const LaneBits BN{&L.bn[tid], MW, false}, BI{&L.bi[tid], MW, false};
   // hex -> bits for both polarities (helpers.py:168-188: leading zero nibbles are dropped)
   int nN = 0, nI = 0;
@@ -2455,6 +2456,12 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     // stage results of the wave in lane (= frame) order for this protocol
     const bool has = o.rc == 1;
     MCPROF_ADD(28, t_m);
+#ifdef SDX_PROF
+    if (lane == 0 && p < 32) {
+      atomicAdd(&mcp[0][p], __builtin_amdgcn_s_memtime() - t_m);
+      atomicAdd(&mcp[1][p], (unsigned long long)__popcll(ballot(go)));
+    }
+#endif
     if (!ballot(has)) continue;  // no result in this wave: nothing to stage (wave-uniform)
     MCPROF_T(t_r);
     const int plen = has ? cld(&r->pre_len) + o.len : 0;
@@ -2466,7 +2473,7 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
     const int wtot = __shfl(incl, WAVE - 1);
     const uint64_t hm = ballot(has);
     const int nnew = popc64(hm);
-    const int hb = L.nheap[wave], rb = L.nrec[wave];
+    const int hb = w_heap, rb = w_rec;
     const bool fits = hb + wtot <= MC_HEAP_CAP && rb + nnew <= MC_REC_CAP;
     if (has && fits) {
       uint8_t* dst = &L.heap[wave][hb + incl - plen];
@@ -2490,20 +2497,21 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
       L.rec[wave][rb + lanes_below(hm)] = sr;
       ++mycnt;
     }
-    wave_sync();
-    if (lane == 0) {
-      if (fits) { L.nheap[wave] = hb + wtot; L.nrec[wave] = rb + nnew; }
-      else if (nnew) L.ovf[wave] = 1;
+    if (fits) {  // the wave's staging cursors are wave-uniform registers (every lane computes them)
+      w_heap = hb + wtot;
+      w_rec = rb + nnew;
+    } else if (nnew) {
+      w_ovf = true;
     }
-    wave_sync();
     MCPROF_ADD(29, t_r);
   }
+  wave_sync();  // the staged records and payloads of all lanes, for the flush
   MCPROF_T(t_f);
   // flush this wave's frames: records are staged in protocol-major order, each carrying its rank
   // among its frame's records; the wave writes them 64 at a time to (frame, protocol) order
-  const int nr = L.nrec[wave];
-  const int nh = (L.nheap[wave] + 15) & ~15;  // 16-B pieces: every reservation keeps hbase aligned
-  const bool bad = L.ovf[wave] != 0;
+  const int nr = w_rec;
+  const int nh = (w_heap + 15) & ~15;  // 16-B pieces: every reservation keeps hbase aligned
+  const bool bad = w_ovf;
   if (raise) mycnt = 0;
   int incl = mycnt;
   for (int d = 1; d < WAVE; d <<= 1) {
@@ -2575,6 +2583,14 @@ __global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_m
   }
   MCPROF_ADD(30, t_f);
   MCPROF_ADD(31, t_all);
+#ifdef SDX_PROF
+  if (lane == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_prof[27 + i], mcacc[i]);
+  if constexpr (!LONG) {
+    __syncthreads();
+    if (tid < 64) atomicAdd(&g_gprof[tid >> 5][tid & 31], mcp[tid >> 5][tid & 31]);
+  }
+#endif
 #undef MCPROF_T
 #undef MCPROF_ADD
 }

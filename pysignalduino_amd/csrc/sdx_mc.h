@@ -73,15 +73,31 @@ struct LaneBits {
   }
 };
 
-// bin_str_2_hex_str of bits [a, e) of LaneBits -> dst; returns the length
+// bin_str_2_hex_str of bits [a, e) of LaneBits -> dst; returns the length.  Digit d is
+// int(bits[e - 4 (nd - d) : e - 4 (nd - 1 - d)], 2), the first one clipped at a; 8 digits per step:
+// one 32-bit window (two LDS reads), nibble-reversed and converted with SWAR
 SDX_DEV int lane_hex(const LaneBits& B, int a, int e, uint8_t* dst) {
   const int nb = e - a;
   if (nb <= 0) return 0;
   const int nd = (nb + 3) >> 2;
-  for (int d = 0; d < nd; ++d) {
-    const int de = e - 4 * (nd - 1 - d), da = (de - 4 > a) ? de - 4 : a;
-    const int v = (int)B.win(da, de - da);  // int(bits[da:de], 2)
-    if (dst) dst[d] = (uint8_t)(v < 10 ? '0' + v : 'A' + v - 10);
+  if (!dst) return nd;
+  for (int c = 0; c < nd; c += 8) {
+    const int cnt = nd - c < 8 ? nd - c : 8;
+    const int s0 = e - 4 * (nd - c), s = s0 > a ? s0 : a;   // bits before a read as 0
+    const uint32_t v = B.win(s, 4 * cnt - (s - s0));        // the chunk's value, right-aligned
+    uint64_t x = (uint64_t)v << (64 - 4 * cnt);             // first digit in the top nibble
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);  // nibble reverse
+    x = ((x >> 8) & 0x00FF00FF00FF00FFull) | ((x & 0x00FF00FF00FF00FFull) << 8);
+    x = ((x >> 16) & 0x0000FFFF0000FFFFull) | ((x & 0x0000FFFF0000FFFFull) << 16);
+    x = (x >> 32) | (x << 32);                              // digit i in nibble i (i < cnt)
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;            // 8 nibbles -> 8 bytes
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    const uint64_t ge10 = ((x + 0x0606060606060606ull) >> 4) & 0x0101010101010101ull;
+    x += 0x3030303030303030ull + ge10 * 7ull;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < cnt) dst[c + i] = (uint8_t)(x >> (8 * i));
   }
   return nd;
 }

@@ -70,17 +70,24 @@ def main():
     for it in range(2):
         out["cursor"].zero_()
         lib.sdx_prof_read(buf, 1)
+        lib.sdx_gprof_read((ctypes.c_ulonglong * 256)(), 1)
         t = time.perf_counter()
         eng.launch_mc(bd, out)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
     lib.sdx_prof_read(buf, 1)
     v = np.array(list(buf), dtype=np.float64)
+    gb = (ctypes.c_ulonglong * 256)()
+    lib.sdx_gprof_read(gb, 1)
+    g = np.array(list(gb), dtype=np.float64).reshape(2, 128)
     tot = v[31]
     print(f"== MC: {pb.n} frames, {dt*1e3:.2f} ms wall; wave-cycles total {tot:.3e} ({tot/pb.n:.0f} per frame)")
     for i, name in ((27, "stage (hex -> bits)"), (28, "protocol gates + method"), (29, "result staging"),
                     (30, "flush"), (31, "kernel total")):
         print(f"  {name:28s} {v[i]/tot*100:6.2f} %   {v[i]/pb.n:9.0f} wave-cycles/frame")
+    print("  per protocol (bank MC index: share of the gates + method cycles, lanes through the gates per frame):")
+    print("   " + " ".join(f"{i}:{g[0, i] / max(v[28], 1) * 100:.1f}%/{g[1, i] / pb.n:.3f}"
+                          for i in range(32) if g[0, i] > 0))
 
 
 if __name__ == "__main__":
