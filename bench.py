@@ -44,6 +44,9 @@ def parse():
                     help="one stream per kind: MU, MS and MC of a step run concurrently, one kernel's tail "
                          "overlapping the others' tiles (+3.5 %% msgs/s measured; per-kernel times then include "
                          "the sharing, so the roofline line is quoted on the default serial launches)")
+    ap.add_argument("--group-at", default="mu", choices=("mu", "ms"),
+                    help="where the next step's grouping runs: beside this step's MU (default) or after it, "
+                         "beside MS / MC (A/B)")
     ap.add_argument("--kev-every", type=int, default=1,
                     help="per-kernel HIP events on every k-th timed step only (A/B of the events' own cost)")
     ap.add_argument("--serial", action="store_true",
@@ -263,10 +266,12 @@ def main():
     gdone, used = {}, [None, None]
     gev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps + 1)]
 
-    def launch_group(j, si=None):
+    def launch_group(j, si=None, after=None):
         par = j % 2
         if used[par] is not None:           # step j-2's launches have read this parity's order
             side.wait_event(used[par])
+        if after is not None:
+            side.wait_event(after)
         with torch.cuda.stream(side):
             if si is not None and si % args.kev_every == 0:
                 gev[si][0].record(side)
@@ -333,7 +338,8 @@ def main():
         if gkinds:
             if j == 0:
                 launch_group(0)
-            launch_group(j + 1, si)         # the next step's grouping, concurrent with this step
+            if args.group_at == "mu":
+                launch_group(j + 1, si)     # the next step's grouping, concurrent with this step
         par = j % 2
         tm = si is not None and si % args.kev_every == 0
         last = None                         # the latest event recorded on the launch stream
@@ -370,6 +376,8 @@ def main():
                 kev[si][k] = (e0, e1)
             if k == "MU":
                 mu_done[0] = e1
+                if gkinds and args.group_at == "ms":
+                    launch_group(j + 1, si, after=e1)   # beside this step's MS / MC
             if ks is stream:
                 last = e1
             elif join_now:
