@@ -1186,7 +1186,40 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(6))) void k_
   uint32_t* pvt = pv[threadIdx.x >> 6] + lane;
   int64_t cp_src = 0, cp_dst = 0;  // uncompressed OK lines: the D characters, copied by the wave
   int cp_len = 0;
+#ifdef SDX_LPROF  // k_parse_lines phases: g_lprof slots 10-15 (per wave: max over its lanes)
+  unsigned long long lpl[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long* lp = lpl - 10;
+#endif
+  LP_T(tk0);
+#ifndef SDX_NO_LPREFETCH
+  {  // The wave's 64 lines are contiguous in bytes_dev: read them once with coalesced 16-byte loads,
+     // all in flight together, so that the lane-private byte loads below (strip, header, the fast
+     // path's word scans) hit the caches instead of each lane starting its own chain of cold misses
+     // (the strip + header checks were 76 % of a wave's cycles, tools/prof_lines.py).  A 16-byte
+     // block holding a byte of the batch lies in that byte's page.
+    const int w0i = blockIdx.x * PT + (threadIdx.x & ~63);
+    if (w0i < in.n) {
+      const int w1i = w0i + 64 < in.n ? w0i + 64 : in.n;
+      const int64_t b0 = in.offsets_dev[w0i] & ~(int64_t)15, b1 = in.offsets_dev[w1i];
+      const uint4* base = reinterpret_cast<const uint4*>(in.bytes_dev + b0);
+      const int nq = (int)((b1 - b0 + 15) >> 4);
+      uint32_t acc = 0;
+      for (int q0 = 0; q0 < nq; q0 += 64 * 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int q = q0 + u * 64 + lane;
+          v[u] = q < nq ? base[q] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].w;
+      }
+      asm volatile("" ::"v"(acc));  // keeps the loads
+    }
+  }
+#endif
   if (valid) {
+    LP_T(tl0);
     const int64_t lo = in.offsets_dev[i], hi = in.offsets_dev[i + 1];
     const uint8_t* L = in.bytes_dev + lo;
     const int len = (int)(hi - lo);
@@ -1216,9 +1249,14 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(6))) void k_
       r.status = ST_RARE;
       decided = true;
     }
+    LP_ADD(10, tl0);
     if (!decided) {
       const uint8_t ty = P.n > 1 ? P.p[1] : 0;
-      if (!((ty == 'U' || ty == 'S' || ty == 'C') && fast_payload(P.p, P.n, r, out, i))) {
+      LP_T(tl1);
+      const bool fastok = (ty == 'U' || ty == 'S' || ty == 'C') && fast_payload(P.p, P.n, r, out, i);
+      LP_ADD(11, tl1);
+      if (!fastok) {
+        LP_T(tl2);
         bool c2 = false;
         if (!likely && !frame_check(L, a, b, c2)) {
           r.status = SDX_LS_NOFRAME;
@@ -1227,8 +1265,10 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(6))) void k_
         } else {
           parse_payload(P, r, out, i, pvt);
         }
+        LP_ADD(12, tl2);
       }
     }
+    LP_T(tl3);
     if (r.status == SDX_LS_OK || r.status == SDX_LS_GENERAL) {
       finish_fields(P, r, out, i);
       if (comp) {
@@ -1240,24 +1280,66 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(6))) void k_
         cp_len = r.dE - r.dS;
       }
     }
+    LP_ADD(13, tl3);
     out.doff_dev[i] = doff;
     out.plen_dev[i] = plen;
     out.kind_dev[i] = r.kind;
     out.status_dev[i] = r.status;
   }
+  LP_T(tl4);
   // the D characters of the wave's uncompressed OK lines, one line at a time: 4 bytes per lane
   // (aligned source words realigned with v_alignbyte), 256 bytes per store instruction
+  // Four lines per round: their first 64 words' loads are issued together, then stored (one memory
+  // latency per four lines instead of one per line); longer values continue word-strided.
   uint64_t cm = __ballot(cp_len > 0);
   while (cm) {
-    const int j = __builtin_ctzll(cm);
-    cm &= cm - 1;
-    const int64_t src = shfl64(cp_src, j);
-    const int sh = (int)(((uintptr_t)in.bytes_dev + src) & 3);
-    const uint32_t* sw = reinterpret_cast<const uint32_t*>(in.bytes_dev + src - sh);
-    uint32_t* dw = reinterpret_cast<uint32_t*>(out.slot_dev + shfl64(cp_dst, j));
-    const int nw = (__shfl(cp_len, j) + 3) >> 2;
-    for (int q = lane; q < nw; q += 64) dw[q] = __builtin_amdgcn_alignbyte(sw[q + 1], sw[q], sh);
+    constexpr int CB = 4;
+    const uint32_t* sw[CB];
+    uint32_t* dw[CB];
+    int sh[CB], nw[CB];
+#pragma unroll
+    for (int k = 0; k < CB; ++k) {
+      nw[k] = 0;
+      sh[k] = 0;
+      sw[k] = nullptr;
+      dw[k] = nullptr;
+      if (cm) {  // wave-uniform
+        const int j = __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const int64_t src = shfl64(cp_src, j);
+        sh[k] = (int)(((uintptr_t)in.bytes_dev + src) & 3);
+        sw[k] = reinterpret_cast<const uint32_t*>(in.bytes_dev + src - sh[k]);
+        dw[k] = reinterpret_cast<uint32_t*>(out.slot_dev + shfl64(cp_dst, j));
+        nw[k] = (__shfl(cp_len, j) + 3) >> 2;
+      }
+    }
+    uint32_t lo[CB], hi[CB];
+#pragma unroll
+    for (int k = 0; k < CB; ++k) {
+      lo[k] = hi[k] = 0;
+      if (lane < nw[k]) {
+        lo[k] = sw[k][lane];
+        hi[k] = sw[k][lane + 1];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CB; ++k) {
+      if (lane < nw[k]) dw[k][lane] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+      for (int q = lane + 64; q < nw[k]; q += 64) dw[k][q] = __builtin_amdgcn_alignbyte(sw[k][q + 1], sw[k][q], sh[k]);
+    }
   }
+  LP_ADD(14, tl4);
+  LP_ADD(15, tk0);
+#ifdef SDX_LPROF
+  for (int k = 0; k < 6; ++k) {
+    unsigned long long v = lpl[k];
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long w = __shfl_xor(v, o);
+      v = w > v ? w : v;
+    }
+    if (lane == 0) atomicAdd(&g_lprof[10 + k], v);
+  }
+#endif
 }
 
 // decompress_payload's output goes to the slot (RawFrame.line) and, without the characters of

@@ -45,6 +45,11 @@ def main():
     for k in range(8):
         if v[k]:
             print(f"  {NAMES.get(k, str(k)):36s} {100 * v[k] / tot:6.2f} %  {v[k] / max(v[9], 1):10.0f} cycles/line")
+    tl = v[15]
+    print(f"k_parse_lines (per wave: max over its lanes; {n} lines):")
+    for k, name in ((10, "strip + header checks"), (11, "fast_payload"), (12, "frame_check + parse_payload (declined)"),
+                    (13, "finish_fields"), (14, "D copy by the wave"), (15, "wave total")):
+        print(f"  {name:40s} {100 * v[k] / max(tl, 1):6.2f} %  {v[k] / (n / 64):10.0f} cycles/wave")
     # the status array: how many lines the parse marked compressed (decompressed payload length > 0)
     plen = lb.c_out  # noqa: F841 (kept for reference; the counts above are the kernel's own)
 
