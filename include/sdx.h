@@ -171,6 +171,12 @@ const char* sdx_source_hash(void);
  * 7 mu_desc */
 int sdx_layout_size(int which);
 
+/* stream-ordered byte copy / fill on the caller's stream (hipMemcpyAsync with hipMemcpyDefault,
+ * hipMemsetAsync): the streaming pipeline's per-chunk H2D / D2H transfers and buffer resets, without a
+ * framework's per-call dispatch.  Host buffers must be pinned for the copy to be asynchronous. */
+int sdx_copy_async(void* dst, const void* src, size_t nbytes, void* hip_stream);
+int sdx_fill_async(void* dst, int value, size_t nbytes, void* hip_stream);
+
 /* bank: compiled by pysignalduino_amd/bank.py (protocols.json -> blob) and uploaded once per device */
 int sdx_bank_create(const void* blob, size_t nbytes, int device, sdx_bank** out);
 int sdx_bank_destroy(sdx_bank* bank);

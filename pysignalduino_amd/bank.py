@@ -333,6 +333,13 @@ class Bank:
         self.compile()
 
     def affixes(self, kind: int) -> List[Tuple[bytes, bytes]]:
+        """Cached per compile (see _affixes)."""
+        c = self.__dict__.setdefault("_affix_cache", {})
+        if kind not in c:
+            c[kind] = self._affixes(kind)
+        return c[kind]
+
+    def _affixes(self, kind: int) -> List[Tuple[bytes, bytes]]:
         """Per record of a class table (kind 0 MU, 1 MS, 2 MC, 3 MN): the (preamble, postamble) bytes
         its payloads carry -- the affixes of the exchange's nibble form (include/sdx.h, wire v3), the
         same strings the compiler puts in the records' pre_off/post_off (message_unsynced.py:271-274,
@@ -404,6 +411,7 @@ class Bank:
     # -- compile -------------------------------------------------------------------------------
     def compile(self) -> None:
         P = self.protocols
+        self._affix_cache = {}
         self._heap = bytearray()
         self._ranks: List[int] = []                 # u16 gap-rank tables (sdx_patspec.rk_off)
         self._rank_off: Dict[Any, int] = {}

@@ -2725,6 +2725,20 @@ int sdx_bank_destroy(sdx_bank* bank) {
 
 const void* sdx_bank_device_ptr(const sdx_bank* bank) { return bank ? bank->dev : nullptr; }
 
+int sdx_copy_async(void* dst, const void* src, size_t nbytes, void* hip_stream) {
+  if (!nbytes) return SDX_OK;
+  if (!dst || !src) return fail(SDX_EINVAL, "sdx_copy_async: null pointer");
+  HIPCHK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, (hipStream_t)hip_stream));
+  return SDX_OK;
+}
+
+int sdx_fill_async(void* dst, int value, size_t nbytes, void* hip_stream) {
+  if (!nbytes) return SDX_OK;
+  if (!dst) return fail(SDX_EINVAL, "sdx_fill_async: null pointer");
+  HIPCHK(hipMemsetAsync(dst, value, nbytes, (hipStream_t)hip_stream));
+  return SDX_OK;
+}
+
 int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
                      void* hip_stream) {
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");

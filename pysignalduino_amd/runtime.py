@@ -45,7 +45,7 @@ EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_source_hash", "sdx_layout_
             "sdx_exchange_work_bytes", "sdx_exchange_send_bytes", "sdx_exchange_count", "sdx_exchange_pack", "sdx_exchange_pack_into", "sdx_exchange_unpack_work_bytes",
             "sdx_exchange_unpack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
             "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general",
-            "sdx_lines_general"]
+            "sdx_lines_general", "sdx_copy_async", "sdx_fill_async"]
 GROUP_MIN = 4096   # SDX_GROUP_MIN
 
 
@@ -161,6 +161,10 @@ def load_library(path: Optional[str] = None):
     lib.sdx_source_hash.restype = c_char_p
     lib.sdx_layout_size.argtypes = [c_int]
     lib.sdx_layout_size.restype = c_int
+    lib.sdx_copy_async.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.sdx_copy_async.restype = c_int
+    lib.sdx_fill_async.argtypes = [c_void_p, c_int, c_size_t, c_void_p]
+    lib.sdx_fill_async.restype = c_int
     lib.sdx_bank_create.argtypes = [c_void_p, c_size_t, c_int, POINTER(c_void_p)]
     lib.sdx_bank_create.restype = c_int
     lib.sdx_bank_destroy.argtypes = [c_void_p]
@@ -247,6 +251,24 @@ def _check(lib, rc):
 
 def _ptr(t) -> Optional[int]:
     return None if t is None else int(t.data_ptr())
+
+
+def copy_async(dst, src, stream) -> None:
+    """dst.copy_(src, non_blocking=True) on ``stream`` through sdx_copy_async: contiguous tensors of
+    the same byte size (device or pinned host), one runtime call instead of a framework dispatch."""
+    n = src.numel() * src.element_size()
+    if n != dst.numel() * dst.element_size() or not (dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("copy_async: contiguous tensors of the same byte size")
+    lib = load_library()
+    _check(lib, lib.sdx_copy_async(dst.data_ptr(), src.data_ptr(), n, stream.cuda_stream))
+
+
+def fill_async(dst, stream, value: int = 0) -> None:
+    """dst.fill_(value) bytewise on ``stream`` through sdx_fill_async (contiguous device tensor)."""
+    if not dst.is_contiguous():
+        raise ValueError("fill_async: contiguous tensor")
+    lib = load_library()
+    _check(lib, lib.sdx_fill_async(dst.data_ptr(), int(value), dst.numel() * dst.element_size(), stream.cuda_stream))
 
 
 class Engine:

@@ -247,12 +247,12 @@ class LineStream:
             s.h_bytes.numpy()[:nb] = data[o0: o0 + nb]
         with t.cuda.stream(self.cin):
             if pinned:   # straight from the caller's pinned buffer; the 16 pad bytes zeroed on the device
-                lb.bytes[:nb].copy_(data[o0: o0 + nb], non_blocking=True)
-                lb.bytes[nb: nb + 16].zero_()
+                lb.bytes[:nb].copy_(data[o0: o0 + nb], non_blocking=True)   # the caller's tensor: torch tracks it
+                runtime.fill_async(lb.bytes[nb: nb + 16], self.cin)
             else:
                 s.h_bytes.numpy()[nb: nb + 16] = 0
-                lb.bytes[: nb + 16].copy_(s.h_bytes[: nb + 16], non_blocking=True)
-            lb.offsets[: n + 1].copy_(s.h_offs[: n + 1], non_blocking=True)
+                runtime.copy_async(lb.bytes[: nb + 16], s.h_bytes[: nb + 16], self.cin)
+            runtime.copy_async(lb.offsets[: n + 1], s.h_offs[: n + 1], self.cin)
             h2d = t.cuda.Event()
             h2d.record(self.cin)
         self.h2d_bytes += nb + 8 * (n + 1)
@@ -264,7 +264,7 @@ class LineStream:
             e0.record(self.sp)
             lb.launch()
             e1.record(self.sp)
-            s.h_cnt.copy_(lb.counts, non_blocking=True)
+            runtime.copy_async(s.h_cnt, lb.counts, self.sp)
             ev = t.cuda.Event()
             ev.record(self.sp)
         s.parse_ev, s.ev, s.kt = e1, ev, [e0, e1]
@@ -282,16 +282,16 @@ class LineStream:
             self.sd.wait_event(s.parse_ev)
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
             e0.record(self.sd)
-            s.cursors.zero_()
+            runtime.fill_async(s.cursors, self.sd)
             pb = lb.pulse_batch()
             for name, kd, short, long_ in _KINDS:
                 o = s.outs.get(name)
                 if o is None:
                     continue
                 o["n"] = n
-                o["desc"][: 8 * n].zero_()          # lines of other classes keep an empty descriptor
+                runtime.fill_async(o["desc"][: 8 * n], self.sd)   # lines of other classes keep an empty descriptor
                 if o.get("wire") is not None:
-                    o["wire"][:n].zero_()           # ... and no exchange counts
+                    runtime.fill_async(o["wire"][:n], self.sd)     # ... and no exchange counts
                 if kd == runtime.KIND_MN:
                     if cnt[short]:
                         eng.launch_mn(lb.mn_batch(), o, elig=self.elig, sel=sels[short])
@@ -308,15 +308,15 @@ class LineStream:
             s.cnt = cnt
             if self.output == "json":
                 jo = s.jout
-                jo["cursor"].zero_()
-                jo["len"][:n].zero_()
+                runtime.fill_async(jo["cursor"], self.sd)
+                runtime.fill_async(jo["len"][:n], self.sd)
                 lo = {"meta": lb.meta, "pat_val": lb.pat_val, "cp_slot": lb.cp_slot}
                 for name, kd, short, long_ in _KINDS:
                     o = s.outs.get(name)
                     if o is not None and (cnt[short] or (long_ is not None and cnt[long_])):
                         eng.launch_json(kd, o, lo, n, jo, first_only=2)
-                s.h_sizes[:2].copy_(jo["cursor"], non_blocking=True)
-                s.h_sizes[2:].copy_(s.cursors.reshape(-1), non_blocking=True)
+                runtime.copy_async(s.h_sizes[:2], jo["cursor"], self.sd)
+                runtime.copy_async(s.h_sizes[2:], s.cursors.reshape(-1), self.sd)
             else:
                 from . import dist as sdist
                 parts = [sdist.Part(o["desc"], o["rec"], o["heap"], n, o["cursor"], kd, wire=o.get("wire"),
@@ -324,8 +324,8 @@ class LineStream:
                          for name, kd, _, _ in _KINDS for o in [s.outs.get(name)] if o is not None]
                 wc = s.ser._count_pack_device(sdist._flatten(parts), self.sd)
                 k = len(parts)
-                s.h_sizes[: runtime.XCHG_COUNTS * k].copy_(wc, non_blocking=True)
-                s.h_sizes[runtime.XCHG_COUNTS * k:].copy_(s.cursors.reshape(-1), non_blocking=True)
+                runtime.copy_async(s.h_sizes[: runtime.XCHG_COUNTS * k], wc, self.sd)
+                runtime.copy_async(s.h_sizes[runtime.XCHG_COUNTS * k:], s.cursors.reshape(-1), self.sd)
             e1.record(self.sd)
             ev = t.cuda.Event()
             ev.record(self.sd)
@@ -347,10 +347,10 @@ class LineStream:
                 T = int(min(hs[0], s.jcap))
                 s.ovf_json = bool(hs[1])
                 s.dcur = hs[2:].reshape(k, 4)
-                ho[:T].copy_(s.jout["json"][:T], non_blocking=True)
+                runtime.copy_async(ho[:T], s.jout["json"][:T], self.cout)
                 a = (T + 3) & ~3
-                ho[a: a + 4 * n].view(t.int32).copy_(s.jout["off"][:n].view(t.int32), non_blocking=True)
-                ho[a + 4 * n: a + 8 * n].view(t.int32).copy_(s.jout["len"][:n].view(t.int32), non_blocking=True)
+                runtime.copy_async(ho[a: a + 4 * n], s.jout["off"][:n], self.cout)
+                runtime.copy_async(ho[a + 4 * n: a + 8 * n], s.jout["len"][:n], self.cout)
                 b = a + 8 * n
                 s.lay = (T, a)
             else:
@@ -359,11 +359,11 @@ class LineStream:
                 s.dcur = hs[runtime.XCHG_COUNTS * k:].reshape(k, 4)
                 s.S = S
                 offs, nb, T = sdist._layout(S)
-                ho[:T].copy_(s.ser._bufs["send"][:T], non_blocking=True)
+                runtime.copy_async(ho[:T], s.ser._bufs["send"][:T], self.cout)
                 b = T
                 s.lay = (offs, nb, T)
-            ho[b: b + n].copy_(lb.kind[:n], non_blocking=True)
-            ho[b + n: b + 2 * n].copy_(lb.status[:n], non_blocking=True)
+            runtime.copy_async(ho[b: b + n], lb.kind[:n], self.cout)
+            runtime.copy_async(ho[b + n: b + 2 * n], lb.status[:n], self.cout)
             s.kb = b
             ev = t.cuda.Event()
             ev.record(self.cout)
