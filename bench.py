@@ -52,9 +52,10 @@ def parse():
     ap.add_argument("--serial", action="store_true",
                     help="MU, MS and MC one after another on one stream (default: MC on a second stream, "
                          "started when MU ends, so MC runs beside MS while MU runs alone)")
-    ap.add_argument("--mrec", action="store_true",
-                    help="the grouping writes message records (sdx_msg_rec) and k_pulses reads its header fields "
-                         "from them instead of the scattered SoA fields: less HBM traffic, measured slower (A/B)")
+    ap.add_argument("--mrec", nargs="?", const="MU,MS", default="",
+                    help="kinds (default both) whose grouping writes message records (sdx_msg_rec) and whose "
+                         "k_pulses reads its header fields from them instead of the scattered SoA fields: less "
+                         "HBM traffic, measured slower (A/B)")
     ap.add_argument("--mc-tail", action="store_true",
                     help="MC on a low-priority stream started with MU (the dispatcher gives its workgroups "
                          "the CUs MU's tail leaves idle) instead of beside MS")
@@ -224,7 +225,9 @@ def main():
     bk = bankmod.Bank()
     P = bk.protocols
     eng = runtime.Engine(bk, local)
-    eng.use_mrec = args.mrec  # the grouping writes message records only when the launches read them
+    mrec_kinds = {k for k in args.mrec.split(",") if k}
+    # the grouping writes message records only when the launches read them
+    eng.use_mrec = {runtime.KIND_MU if k == "MU" else runtime.KIND_MS for k in mrec_kinds}
     kinds = ("MU", "MS", "MC") if args.kind == "mixed" else (args.kind,)
     per = {k: (args.msgs // 3 if k != "MC" else args.msgs - 2 * (args.msgs // 3)) if args.kind == "mixed" else args.msgs
            for k in kinds}
@@ -369,7 +372,7 @@ def main():
                 else:
                     eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[s_][k],
                                       sel=gbufs[k][par][0][:corp[k].n] if k in gkinds else None, group=False,
-                                      mrec=gbufs[k][par][2] if k in gkinds and args.mrec else None)
+                                      mrec=gbufs[k][par][2] if k in gkinds and k in mrec_kinds else None)
                 e1 = torch.cuda.Event(enable_timing=tm)
                 e1.record(ks)
             if tm:

@@ -369,8 +369,10 @@ class Engine:
             bufs = c
         order, work, mrec = bufs
         b = self._pulse_batch(bd, sel)
+        um = self.use_mrec   # bool, or the set of kinds whose grouping writes message records
+        want = um if isinstance(um, bool) else kind in um
         _check(self.lib, self.lib.sdx_group_pulses(self.handle, kind, ctypes.byref(b), _ptr(order),
-                                                   _ptr(mrec) if self.use_mrec else None, _ptr(work),
+                                                   _ptr(mrec) if want else None, _ptr(work),
                                                    int(work.numel()), self.stream_ptr()))
         return order[:n]
 
@@ -417,7 +419,8 @@ class Engine:
         n = int(sel.numel()) if sel is not None else bd["n"]
         if group and not long_variant and n >= GROUP_MIN:
             sel = self.group(kind, bd, sel)
-            mrec = self._gcache[2] if self.use_mrec else None
+            um = self.use_mrec
+            mrec = self._gcache[2] if (um if isinstance(um, bool) else kind in um) else None
         b = self._pulse_batch(bd, sel, None if long_variant else mrec)
         o = self._out_struct(out)
         fn = self.lib.sdx_demod_pulses_long if long_variant else self.lib.sdx_demod_pulses

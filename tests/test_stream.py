@@ -130,3 +130,30 @@ def test_stream_pinned_submit_matches_batch_api(golden):
                 assert e == g, (i, e, g)
                 nres += e is not None
     assert nres > 1000
+
+
+def test_copy_and_fill_async_on_a_stream():
+    """sdx_copy_async / sdx_fill_async (the pipeline's per-chunk transfers and resets): pinned host ->
+    device, device -> device, device -> pinned host on a side stream, odd sizes and offsets; a
+    zero-byte call is a no-op; mismatched sizes are refused on the host."""
+    import torch
+    from pysignalduino_amd import runtime
+    runtime.load_library()
+    st = torch.cuda.Stream()
+    rng = np.random.default_rng(3)
+    src = torch.from_numpy(rng.integers(0, 256, 100_003, dtype=np.uint8)).pin_memory()
+    dev = torch.empty(100_019, dtype=torch.uint8, device="cuda")
+    dev2 = torch.empty_like(dev)
+    back = torch.zeros(100_003, dtype=torch.uint8).pin_memory()
+    with torch.cuda.stream(st):
+        runtime.copy_async(dev[5: 5 + 100_003], src, st)
+        runtime.copy_async(dev2[:100_003], dev[5: 5 + 100_003], st)
+        runtime.fill_async(dev2[7: 7 + 1001], st, 0xAB)
+        runtime.copy_async(back, dev2[:100_003], st)
+        runtime.copy_async(back[:0], dev2[:0], st)
+    st.synchronize()
+    want = src.numpy().copy()
+    want[7: 7 + 1001] = 0xAB
+    assert np.array_equal(back.numpy(), want)
+    with pytest.raises(ValueError):
+        runtime.copy_async(back[:10], dev[:11], st)
