@@ -175,7 +175,7 @@ def main():
     alg = int(offsets[-1]) + 8 * (n + 1) + 152 * n + int(dl[stv == runtime.LS_OK].sum())
     achieved = alg / km["parse"]
     traffic = None
-    tpath = next((p for p in (os.path.join(REPO, "profiles", r, "pmc_traffic_lines.json") for r in ("r02", "r01"))
+    tpath = next((p for p in (os.path.join(REPO, "profiles", r, "pmc_traffic_lines.json") for r in ("r04", "r03", "r02", "r01"))
                   if os.path.exists(p)), "")
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
