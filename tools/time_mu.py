@@ -53,7 +53,22 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         cur = out["cursor"].cpu().numpy()
-        res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) * 112 >> 10} MB)")
+        extra = ""
+        if kind != "MC" and not os.environ.get("SDX_NOGROUP"):
+            # the kernel alone, on the grouped order computed beforehand (the bench groups one step
+            # ahead on a side stream)
+            sel = eng.group(k, bd).clone()
+            torch.cuda.synchronize()
+            tk = []
+            for _ in range(reps):
+                out["cursor"].zero_()
+                e0.record()
+                eng.launch_pulses(k, bd, out, sel=sel, group=False)
+                e1.record()
+                torch.cuda.synchronize()
+                tk.append(e0.elapsed_time(e1))
+            extra = f", kernel alone {min(tk):.3f} ms"
+        res.append(f"{kind} {min(ts):.3f} ms (ovf {int(cur[2])}, spill {int(cur[3]) * 112 >> 10} MB{extra})")
     tag = os.path.basename(os.environ.get("SDX_LIB", "libsdx.so")) + (" plain" if os.environ.get("SDX_NOGROUP") else " grouped") + (" order=" + os.environ.get("SDX_MU_ORDER", "lpt")) + " corpus=" + corpus + (" wire" if os.environ.get("SDX_WIRE") else "")
     print(tag, " | ".join(res), flush=True)
 
