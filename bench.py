@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--mc-tail", action="store_true",
                     help="MC on a low-priority stream started with MU (the dispatcher gives its workgroups "
                          "the CUs MU's tail leaves idle) instead of beside MS")
+    ap.add_argument("--ms-with-mu", default="", choices=("", "normal", "low"),
+                    help="MS on its own stream started with MU at that priority (its tiles share the CUs with "
+                         "MU's from the start and fill MU's tail), MC beside MS after MU (A/B)")
     ap.add_argument("--xchg", default="defer", choices=("eager", "pack-after-mu", "defer"),
                     help="exchange scheduling (N > 1 / --exchange): eager = count and pack as soon as possible "
                          "(beside the next step's MU); pack-after-mu = the pack waits for the next step's MU; "
@@ -311,6 +314,8 @@ def main():
         kstream["MC"] = torch.cuda.Stream(dev)
     if args.mc_tail and "MC" in kinds:
         kstream["MC"] = torch.cuda.Stream(dev, priority=lo_prio)
+    if args.ms_with_mu and "MS" in kinds:
+        kstream["MS"] = torch.cuda.Stream(dev, priority=lo_prio if args.ms_with_mu == "low" else 0)
     # launches on other streams than the launch stream join it at the end of their step only when
     # the exchange reads the step's outputs; otherwise each stream resets its own kinds' cursors
     # before its launch (its previous launch on the same slot is earlier on that stream)
