@@ -311,7 +311,7 @@ def main():
     # side -- MC fills the CUs MS's tail leaves idle (482 vs 471M msgs/s serial, 20 steps)
     mc_beside_ms = not args.serial and not args.concurrent and not args.mc_tail and "MC" in kinds and "MU" in kinds
     if mc_beside_ms:
-        kstream["MC"] = torch.cuda.Stream(dev)
+        kstream["MC"] = torch.cuda.Stream(dev)   # (at the lowest priority: equal, profiles/r04/s3/dropped/mc_low_ab.log)
     if args.mc_tail and "MC" in kinds:
         kstream["MC"] = torch.cuda.Stream(dev, priority=lo_prio)
     if args.ms_with_mu and "MS" in kinds:
