@@ -131,7 +131,10 @@ def test_shard_bounds():
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
 
 
-def test_gloo_world2_allgather_matches_unsharded():
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_world_allgather_matches_unsharded(world):
+    """world 2 and 4 (gloo, CPU): every rank's gathered stream -- single launch, multi-launch, the
+    pipelined Exchange and the overflow re-run path -- equals the un-sharded one"""
     from pysignalduino_amd import bank
     P = bank.load_protocols()
     pb = synth.mu_corpus(P, 120, seed=5)
@@ -141,15 +144,15 @@ def test_gloo_world2_allgather_matches_unsharded():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, msgs, pids, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, msgs, pids, q)) for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     halves = []
-    for r in range(2):
-        lo, hi = sdist.shard_bounds(len(msgs), r, 2)
+    for r in range(world):
+        lo, hi = sdist.shard_bounds(len(msgs), r, world)
         halves += full[lo: lo + (hi - lo) // 2]
     for rank, got, got_multi, got_half, steps, got_rerun, reruns in outs:
         assert got_rerun == full, f"rank {rank}: the re-run exchange differs"
