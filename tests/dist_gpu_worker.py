@@ -1,4 +1,4 @@
-"""Rank process of tests/test_dist.py's world-2 GPU tests (GPU box only).
+"""Rank process of tests/test_dist.py's world-2 and world-4 GPU tests (GPU box only).
 
 World size 2 over gloo with both ranks on cuda:0 (the one-GPU rehearsal of config 5).  Modes
 (SDX_WORKER_MODE):
@@ -63,7 +63,7 @@ def main():
     eng = runtime.Engine(bk, 0)
     P = bk.protocols
     sd = sdist.ShardedDemodulator(group=None, engine=eng)
-    assert sd.world == 2
+    assert sd.world == world
     if mode == "dict":
         return dict_mode(sd, P, rank)
     dense = mode == "overflow"

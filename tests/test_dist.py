@@ -556,14 +556,14 @@ def test_exchange_rccl_world1():
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
-def _world2(mode, timeout=120):
+def _world2(mode, timeout=120, world=2):
     import subprocess
     import sys
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_gpu_worker.py")
     port = str(_free_port())
     procs = [subprocess.Popen([sys.executable, worker], env=dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
-                                                                 RANK=str(r), WORLD_SIZE="2", SDX_WORKER_MODE=mode),
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+                                                                 RANK=str(r), WORLD_SIZE=str(world), SDX_WORKER_MODE=mode),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
     outs = []
     for p in procs:
         try:
@@ -603,6 +603,14 @@ def test_world2_sharded_demodulate_batch_dicts():
     demodulate_batch of the whole list on both ranks: MU / MS with general-path messages and host
     conversion errors on both shards, MC fixed with long frames and a non-str frame."""
     _world2("dict")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["pipelined", "dict"])
+def test_world4_on_one_gpu_matches_unsharded(mode):
+    """The same at world size 4 (four gloo ranks on cuda:0): uneven shard boundaries, every rank's
+    gathered stream / dict results equal the un-sharded run."""
+    _world2(mode, timeout=150, world=4)
 
 
 @pytest.mark.gpu
