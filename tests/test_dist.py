@@ -631,3 +631,19 @@ def test_bench_self_launch_world2():
     res = json.loads(line[0])
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
     assert res["exchange"]["wire_bytes_per_rank_per_step"] > 0
+
+
+@pytest.mark.gpu
+def test_config5_rehearsal_world8_on_one_gpu():
+    """Config 5's shape on the one GPU: eight gloo ranks on cuda:0, each with a mixed MU/MS/MC shard
+    (300k messages here; the full 1M-per-rank run is profiles/r04/s3/config5_rehearsal/), the product
+    exchange and the device unpack of the whole job: every rank's own wire chunk equals the host
+    encoder's wire of its launches, the job sizes add up and all ranks hold identical bytes."""
+    import subprocess
+    import sys
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "config5_rehearsal.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"c5_{os.getpid()}")
+    r = subprocess.run([sys.executable, tool, "--world", "8", "--msgs", "300000", "--out", out, "--timeout", "130"],
+                       env=env, capture_output=True, text=True, timeout=145)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), (r.stdout[-3000:], r.stderr[-3000:])
