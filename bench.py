@@ -498,6 +498,7 @@ def main():
         res["exchange"] = {"format": "wire v3 (include/sdx.h): 4 B/message + 8 B/record + payloads "
                                      + ("raw" if args.raw_wire else "(preamble + hex + postamble as packed digits)"),
                            "scheduling": args.xchg,
+                           "branch": "pipelined" if exch.pipelined else "sync",
                            "send_bytes_per_rank_per_step": float(np.mean(nb)),
                            "wire_bytes_per_rank_per_step": float(np.mean(wb)),
                            "payload_bytes_per_rank_per_step": float(np.mean(exch.payload_bytes[-args.steps:])),

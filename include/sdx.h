@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 12
+#define SDX_ABI_VERSION 13
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -115,7 +115,12 @@ typedef struct {
   int32_t n, n_sel;
   const int16_t* only_dev;     /* optional [n]: evaluate only MC protocol only[i] (table index; -1 = every
                                 * protocol) -- demodulate_mc(msg_data) with a protocol_id (sd_protocols.py:79) */
+  int32_t max_hex;             /* ABI 13, optional: an upper bound on the length (hex characters) of every
+                                * frame run, 0 = unknown.  sdx_demod_mc launches its 65..128-character
+                                * variant only when max_hex is 0 or > SDX_MC_SHORT_HEX */
+  int32_t res;
 } sdx_mc_batch;
+#define SDX_MC_SHORT_HEX 64    /* frames up to this length run in sdx_demod_mc's 4-word variant */
 
 /* MN (FSK) batch: the hex characters of each frame (MN_PATTERN group 2, parser/mn.py:17) */
 typedef struct {

@@ -195,12 +195,25 @@ class BatchingParserTask:
             await self._publish_json(res)
 
     async def _run_stream(self) -> None:
-        """publish='json' through a pipelined LineStream (chunks = micro-batches)."""
+        """publish='json' through a pipelined LineStream (chunks = micro-batches).  Every line taken
+        off the queue is published, as in the reference loop: when the stop event is set or an error
+        ends the loop, the chunks still in flight are drained and published.  submit,
+        poll and drain run in worker threads (poll may launch kernels and run the host parse of
+        lines the device hands back), never on the event loop."""
         c = self.c
         if self._stream is None:
             self._stream = c.parser.stream(chunk_lines=self.max_batch, output="json", lag=self.lag)
         ls = self._stream
         pending: Deque[List[Any]] = collections.deque()
+
+        async def publish(done):
+            for r in done:
+                blines = pending.popleft()
+                items = r.items() if hasattr(r, "items") else [(i, t) for i, t in enumerate(r.texts())
+                                                              if t is not None]
+                await self._publish_items(blines, items)
+                self.lines += len(blines)
+
         while not c._stop_event.is_set():
             try:
                 batch = await self._next_batch(self.max_delay if pending else None)
@@ -209,23 +222,26 @@ class BatchingParserTask:
                     await asyncio.to_thread(ls.submit, lines)
                     pending.append(lines)
                     self.batches += 1
-                    done = ls.poll()
+                    done = await asyncio.to_thread(ls.poll)
                 elif pending:           # the queue ran dry: publish everything in flight
                     done = await asyncio.to_thread(ls.drain)
                 else:
                     done = []
-                for r in done:
-                    blines = pending.popleft()
-                    items = r.items() if hasattr(r, "items") else [(i, t) for i, t in enumerate(r.texts())
-                                                                  if t is not None]
-                    await self._publish_items(blines, items)
-                    self.lines += len(blines)
+                await publish(done)
                 await asyncio.sleep(0)
             except asyncio.CancelledError:
                 raise
             except Exception as e:  # noqa: BLE001  (controller.py:262-264)
                 self.logger.error(f"Parser task error: {e}")
                 break
+        if pending:                     # stopped or failed with chunks in flight: publish them
+            n = sum(len(b) for b in pending)
+            try:
+                await publish(await asyncio.to_thread(ls.drain))
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                self.logger.error(f"Parser task error while draining {n} in-flight lines: {e}")
 
     async def run(self) -> None:
         c = self.c

@@ -2808,6 +2808,8 @@ int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch*
   return SDX_OK;
 }
 
+static_assert(sdx::MC_SHORTW * 16 == SDX_MC_SHORT_HEX, "k_mc<MC_SHORTW> holds SDX_MC_SHORT_HEX characters");
+
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream) {
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
@@ -2815,7 +2817,10 @@ int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out*
   hipStream_t st = (hipStream_t)hip_stream;
   const int grid = (ntot + 255) / 256;
   hipLaunchKernelGGL((sdx::k_mc<sdx::MC_SHORTW, false>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
-  hipLaunchKernelGGL((sdx::k_mc<sdx::MC_MAXW, true>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
+  // the 65..128-character variant only when the caller cannot rule such frames out (VERDICT r04 #4:
+  // over a batch without one, its grid of early-exiting waves still held CU slots beside MS)
+  if (batch->max_hex <= 0 || batch->max_hex > SDX_MC_SHORT_HEX)
+    hipLaunchKernelGGL((sdx::k_mc<sdx::MC_MAXW, true>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
   HIPCHK(hipGetLastError());
   return SDX_OK;
 }

@@ -1195,14 +1195,16 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(6))) void k_
   {  // The wave's 64 lines are contiguous in bytes_dev: read them once with coalesced 16-byte loads,
      // all in flight together, so that the lane-private byte loads below (strip, header, the fast
      // path's word scans) hit the caches instead of each lane starting its own chain of cold misses
-     // (the strip + header checks were 76 % of a wave's cycles, tools/prof_lines.py).  A 16-byte
-     // block holding a byte of the batch lies in that byte's page.
+     // (the strip + header checks were 76 % of a wave's cycles, tools/prof_lines.py).  The blocks are
+     // 16-byte aligned in the ADDRESS space (whatever the alignment of bytes_dev), so a block holding
+     // a byte of the batch lies in that byte's page.
     const int w0i = blockIdx.x * PT + (threadIdx.x & ~63);
     if (w0i < in.n) {
       const int w1i = w0i + 64 < in.n ? w0i + 64 : in.n;
-      const int64_t b0 = in.offsets_dev[w0i] & ~(int64_t)15, b1 = in.offsets_dev[w1i];
-      const uint4* base = reinterpret_cast<const uint4*>(in.bytes_dev + b0);
-      const int nq = (int)((b1 - b0 + 15) >> 4);
+      const uintptr_t a0 = reinterpret_cast<uintptr_t>(in.bytes_dev + in.offsets_dev[w0i]) & ~(uintptr_t)15;
+      const uintptr_t a1 = reinterpret_cast<uintptr_t>(in.bytes_dev + in.offsets_dev[w1i]);
+      const uint4* base = reinterpret_cast<const uint4*>(a0);
+      const int nq = (int)((a1 - a0 + 15) >> 4);
       uint32_t acc = 0;
       for (int q0 = 0; q0 < nq; q0 += 64 * 8) {
         uint4 v[8];

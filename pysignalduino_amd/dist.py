@@ -30,11 +30,23 @@ its own HIP stream (:class:`Exchange`), overlapped with the next step's kernels:
                sdx_exchange_pack_into_k (this rank's chunk of the receive buffer) ─released_k─
                in-place all-gather data_k, and only then the wait on ready_{k+1} and step k+1's count.
 The same protocol runs synchronously on ``gloo`` (CPU tensors: numpy packing; CUDA tensors: the
-device kernels, the collective staged through host memory).
+device kernels, the collective staged through host memory).  ``Exchange(pipeline=True)`` (or
+``SDX_XCHG_PIPELINE=1``) runs the pipelined branch above over gloo as well, so the exact code an
+RCCL run executes (deferred count, in-place pack, recount after re-runs) is tested at world > 1 on
+one GPU; only the transport differs.
+
+Collective-size agreement.  Every count collective carries a fixed-size FRAME (FRAME_INTS int32 per
+rank: a header of magic, world size, number of primary launches, phase and flags, then the counts of
+up to SDX_XCHG_MAX_PARTS parts), so ranks that disagree on the number of launches can never issue
+collectives of different sizes (an RCCL hang, a gloo abort): every rank sees every header and raises
+:class:`ExchangeMismatch` together.  The data collective's size T is a function of the gathered counts
+alone, hence identical on every rank.  A re-run that fails on one rank is reported through the
+frame's flags, so all ranks take part in the recount and raise together.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -50,6 +62,44 @@ WIRE_MSG_BYTES = 4
 WIRE_REC_BYTES = 8
 RAISE_HOST = 0xFE   # raise_kind of a host overlay row: the host packing raised for this message
 OVF = (runtime.ST_OVF_TILE, runtime.ST_OVF_OUT)
+
+# the count collective's fixed-size frame (per rank): header + counts of up to XCHG_MAX_PARTS parts
+FRAME_HDR = 8
+FRAME_INTS = FRAME_HDR + XCHG_COUNTS * runtime.XCHG_MAX_PARTS
+FRAME_MAGIC = 0x53445846         # 'SDXF'
+PHASE_COUNT, PHASE_RECOUNT = 1, 2
+FLAG_RERUN_FAILED = 1
+
+
+class ExchangeMismatch(RuntimeError):
+    """The ranks disagree on an exchange's shape (world size, number of launches, protocol phase) or
+    a rank's re-run failed: raised on EVERY rank from the same all-gathered frame headers."""
+
+
+def check_frames(frames: np.ndarray, world: int, K: int, phase: int) -> Tuple[np.ndarray, np.ndarray]:
+    """All-gathered count frames [world * FRAME_INTS] -> (the primary launches' counts S[world, K,
+    XCHG_COUNTS], per-rank flags).  Raises ExchangeMismatch, identically on every rank, when a header
+    is not this exchange's (magic, world size, K, phase)."""
+    f = np.asarray(frames, np.int64).reshape(world, FRAME_INTS)
+    hdr = f[:, :FRAME_HDR]
+    want = np.array([FRAME_MAGIC, world, K, phase])
+    if not (hdr[:, :4] == want).all():
+        rows = {r: dict(magic=hex(int(h[0])), world=int(h[1]), launches=int(h[2]), phase=int(h[3]))
+                for r, h in enumerate(hdr)}
+        raise ExchangeMismatch(f"exchange: the ranks' count frames disagree (want world {world}, {K} launches, "
+                               f"phase {phase}): {rows}")
+    return f[:, FRAME_HDR: FRAME_HDR + K * XCHG_COUNTS].reshape(world, K, XCHG_COUNTS), hdr[:, 4].copy()
+
+
+def frame_header(world: int, K: int, phase: int, flags: int = 0) -> np.ndarray:
+    h = np.zeros(FRAME_HDR, np.int32)
+    h[:5] = (FRAME_MAGIC, world, K, phase, flags)
+    return h
+
+
+def _env_pipeline() -> Optional[bool]:
+    v = os.environ.get("SDX_XCHG_PIPELINE")
+    return None if v in (None, "") else v not in ("0", "false", "no")
 
 
 def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -312,12 +362,16 @@ class Exchange:
     every rank recounts; without a ``rerun`` the completing call raises.  ``engine``: the Engine whose
     bank gives the nibble form's affixes (None: raw payloads)."""
 
-    def __init__(self, group=None, engine=None, defer: bool = False):
+    def __init__(self, group=None, engine=None, defer: bool = False, pipeline: Optional[bool] = None):
         self.group = group
         # defer: a step's count AND pack run only in the NEXT submit, behind its ``after`` event (e.g.
         # the end of the next step's first launch), so the exchange kernels share the GPU with the
         # next step's later launches instead of its first one
         self.defer = defer
+        # pipeline: the overlapped branch (exchange stream, in-place pack) for device buffers.  None =
+        # with the nccl backend only (the product default); True also over gloo, the collective staged
+        # through host memory (tests / rehearsals of the RCCL code path on one GPU; SDX_XCHG_PIPELINE=1)
+        self.pipeline = pipeline if pipeline is not None else _env_pipeline()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.engine = engine
@@ -336,7 +390,7 @@ class Exchange:
         """The wire serialiser alone (sdx_exchange_count / _pack on one device, no process group): e.g.
         the streaming front end's compact results (stream.LineStream output='wire')."""
         ex = cls.__new__(cls)
-        ex.group, ex.world, ex.rank, ex.engine, ex.defer = None, 1, 0, engine, False
+        ex.group, ex.world, ex.rank, ex.engine, ex.defer, ex.pipeline = None, 1, 0, engine, False, False
         ex.pending, ex.stream, ex._bufs, ex.last = None, None, {}, None
         ex.bytes_sent, ex.wire_bytes, ex.payload_bytes, ex.heap_wire_bytes, ex.reruns = [], [], [], [], 0
         return ex
@@ -379,26 +433,54 @@ class Exchange:
         off = (-w.data_ptr()) % 256
         return w[off:], wb
 
-    def _count_device(self, flat, stream):
-        """sdx_exchange_count on `stream`: [K * XCHG_COUNTS] int32 device counts (the pack follows once
-        the host has them: _complete, sdx_exchange_pack_into)."""
+    def _frame(self, dev, K, phase, flags=0):
+        """A count frame on ``dev`` (FRAME_INTS int32): the header of this exchange (copied from a
+        cached pinned host tensor that is never written again, so the copy needs no host sync) and
+        room for the counts of up to XCHG_MAX_PARTS parts behind it."""
+        c = self.__dict__.setdefault("_hdr_cache", {})
+        key = (K, phase, flags)
+        if key not in c:
+            c[key] = torch.from_numpy(frame_header(self.world, K, phase, flags))
+            if dev.type == "cuda":
+                c[key] = c[key].pin_memory()
+        f = (torch.empty if dev.type == "cuda" else torch.zeros)(FRAME_INTS, dtype=torch.int32, device=dev)
+        f[:FRAME_HDR].copy_(c[key], non_blocking=True)
+        return f
+
+    def _gather_frame(self, frame):
+        """The fixed-size count collective: every rank's frame, [world * FRAME_INTS] on frame's device."""
+        allc = torch.empty(self.world * FRAME_INTS, dtype=torch.int32, device=frame.device)
+        _all_gather_flat(allc, frame, self.group)
+        return allc
+
+    def _count_device(self, flat, stream, frame=None):
+        """sdx_exchange_count on `stream`: [len(flat) * XCHG_COUNTS] int32 device counts (the pack
+        follows once the host has them: _complete, sdx_exchange_pack_into); written into ``frame``'s
+        count area when given."""
         lib = runtime.load_library()
         dev = flat[0][0].desc.device
         work, wb = self._work(flat, dev)
-        cnt = torch.empty(XCHG_COUNTS * len(flat), dtype=torch.int32, device=dev)
+        cnt = self._cnt_out(flat, dev, frame)
         runtime._check(lib, lib.sdx_exchange_count(self._bank(), self._xparts(flat), len(flat),
                                                    ctypes.c_void_p(work.data_ptr()), wb,
                                                    ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
         return cnt
 
-    def _count_pack_device(self, flat, stream):
-        """sdx_exchange_count + sdx_exchange_pack on `stream`: [K * XCHG_COUNTS] int32 device counts;
-        the wire form of this rank is in the "send" buffer (layout: _layout)."""
+    @staticmethod
+    def _cnt_out(flat, dev, frame):
+        if frame is None:
+            return torch.empty(XCHG_COUNTS * len(flat), dtype=torch.int32, device=dev)
+        return frame[FRAME_HDR: FRAME_HDR + XCHG_COUNTS * len(flat)]
+
+    def _count_pack_device(self, flat, stream, frame=None):
+        """sdx_exchange_count + sdx_exchange_pack on `stream`: [len(flat) * XCHG_COUNTS] int32 device
+        counts (in ``frame`` when given); the wire form of this rank is in the "send" buffer (layout:
+        _layout)."""
         lib = runtime.load_library()
         dev = flat[0][0].desc.device
         work, wb = self._work(flat, dev)
         xp = self._xparts(flat)
-        cnt = torch.empty(XCHG_COUNTS * len(flat), dtype=torch.int32, device=dev)
+        cnt = self._cnt_out(flat, dev, frame)
         sp = ctypes.c_void_p(stream.cuda_stream)
         runtime._check(lib, lib.sdx_exchange_count(self._bank(), xp, len(flat), ctypes.c_void_p(work.data_ptr()), wb,
                                                    ctypes.c_void_p(cnt.data_ptr()), sp))
@@ -422,30 +504,40 @@ class Exchange:
             out.append(enc + (int(enc[1]["payload_len"].astype(np.int64).sum()),))
         return out
 
-    def _counts_host(self, enc):
-        """K primary launches' counts (messages, records, wire bytes, bad, payload bytes, 0, 0, 0)."""
-        return torch.tensor([[len(m), len(w), len(p), b, pb, 0, 0, 0] for m, w, p, b, pb in enc],
-                            dtype=torch.int32).reshape(-1)
+    def _counts_host(self, enc, K, phase, flags=0):
+        """The count frame of K primary launches' host encodings (messages, records, wire bytes, bad,
+        payload bytes, 0, 0, 0 each)."""
+        f = self._frame(torch.device("cpu"), K, phase, flags)
+        c = torch.tensor([[len(m), len(w), len(p), b, pb, 0, 0, 0] for m, w, p, b, pb in enc], dtype=torch.int32)
+        f[FRAME_HDR: FRAME_HDR + c.numel()] = c.reshape(-1)
+        return f
+
+    @property
+    def pipelined(self) -> bool:
+        """Whether device buffers take the overlapped branch (exchange stream, in-place pack)."""
+        if self.pipeline is not None:
+            return bool(self.pipeline)
+        return dist.get_backend(self.group) == "nccl"
 
     # -- protocol ----------------------------------------------------------------------------------------
     def submit(self, parts, stream=None, rerun: Optional[Callable[[Part], Part]] = None, after=None):
         parts = [Part.of(p) for p in parts]
         dev = parts[0].desc.device
-        overlap = dev.type == "cuda" and dist.get_backend(self.group) == "nccl"
+        if self.pipeline and dev.type != "cuda":
+            raise ValueError("exchange: the pipelined branch needs device buffers")
+        overlap = dev.type == "cuda" and self.pipelined
+        K = len(parts)
         if not overlap:   # synchronous form: gloo (CPU tensors, or CUDA tensors staged through the host)
             if dev.type == "cuda":
                 stream = stream or torch.cuda.current_stream(dev)
                 with torch.cuda.stream(stream):
                     flat = _flatten(parts)
-                    cnt = self._count_pack_device(flat, stream)[: XCHG_COUNTS * len(parts)]
-                    allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
-                    _all_gather_flat(allc, cnt, self.group)
-                    self._complete(_Pending(parts, allc.cpu(), None, rerun=rerun))
+                    frame = self._frame(dev, K, PHASE_COUNT)
+                    self._count_pack_device(flat, stream, frame)
+                    self._complete(_Pending(parts, self._gather_frame(frame).cpu(), None, rerun=rerun))
             else:
                 enc = self._encode_host(parts)
-                cnt = self._counts_host(enc)
-                allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32)
-                _all_gather_flat(allc, cnt, self.group)
+                allc = self._gather_frame(self._counts_host(enc, K, PHASE_COUNT))
                 self._complete(_Pending(parts, allc, None, enc, rerun=rerun))
             return None
         if self.stream is None:
@@ -468,7 +560,7 @@ class Exchange:
         ready.record(stream)
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ready)
-            host, ev, cnt = self._count_to_host(_flatten(parts), dev)
+            host, ev, cnt = self._count_to_host(_flatten(parts), dev, K)
         self.pending = _Pending(parts, host, ev, cnt=cnt, rerun=rerun)
         return released
 
@@ -484,21 +576,20 @@ class Exchange:
                 self.stream.wait_event(prev.ready)
                 if after is not None:
                     self.stream.wait_event(after)
-                prev.counts_host, prev.event, prev.cnt = self._count_to_host(_flatten(prev.parts), dev)
+                prev.counts_host, prev.event, prev.cnt = self._count_to_host(_flatten(prev.parts), dev, len(prev.parts))
                 released = self._complete(prev)
         ready = torch.cuda.Event()
         ready.record(stream)
         self.pending = _Pending(parts, None, None, rerun=rerun, ready=ready)
         return released
 
-    def _count_to_host(self, flat, dev):
-        """count + count all-gather + pinned D2H on the current stream: (host counts, event, device counts).
-        Only the primary launches' counts travel: the ranks' overlay parts differ in number (an overlay
-        has no sections of its own), so the collective's size must not depend on them."""
-        cnt = self._count_device(flat, torch.cuda.current_stream(dev))
-        kp = _nprimary(flat)
-        allc = torch.empty(self.world * XCHG_COUNTS * kp, dtype=torch.int32, device=dev)
-        _all_gather_flat(allc, cnt[: XCHG_COUNTS * kp], self.group)
+    def _count_to_host(self, flat, dev, K, phase=PHASE_COUNT, flags=0):
+        """count + count-frame all-gather + pinned D2H on the current stream: (host frames, event,
+        device counts).  The frame has a fixed size whatever the number of launches and overlays, so
+        the collective's size never differs between ranks (check_frames then compares the headers)."""
+        frame = self._frame(dev, K, phase, flags)
+        cnt = self._count_device(flat, torch.cuda.current_stream(dev), frame)
+        allc = self._gather_frame(frame)
         host = torch.empty(allc.numel(), dtype=torch.int32, pin_memory=True)
         host.copy_(allc, non_blocking=True)
         ev = torch.cuda.Event()
@@ -514,53 +605,64 @@ class Exchange:
         with torch.cuda.stream(self.stream):
             if prev.counts_host is None:    # defer mode: not counted yet
                 self.stream.wait_event(prev.ready)
-                prev.counts_host, prev.event, prev.cnt = self._count_to_host(_flatten(prev.parts), prev.parts[0].desc.device)
+                prev.counts_host, prev.event, prev.cnt = self._count_to_host(
+                    _flatten(prev.parts), prev.parts[0].desc.device, len(prev.parts))
             return self._complete(prev)
 
     def _rerun_bad(self, p: _Pending, S: np.ndarray, K: int) -> np.ndarray:
         """Every rank: re-run the launches with overflowed messages on this rank (p.rerun), then
-        recount all launches (a collective every rank takes part in) -> the new counts."""
+        recount all launches (a collective every rank takes part in) -> the new counts.  A re-run that
+        raises on one rank is flagged in that rank's recount frame: every rank still recounts, and all
+        raise together (never a rank waiting in a collective that a failed peer left)."""
         for attempt in range(4):
             if not S[:, :K, 3].any():
                 return S
             if p.rerun is None:
                 bad = {(r, k): int(S[r, k, 3]) for r in range(self.world) for k in range(K) if S[r, k, 3]}
                 raise RuntimeError(f"exchange: overflowed messages in (rank, launch) {bad} and no re-run given")
+            err = None
             for k in range(K):
                 if S[self.rank, k, 3]:
-                    p.parts[k] = p.rerun(p.parts[k])
+                    try:
+                        p.parts[k] = p.rerun(p.parts[k])
+                    except Exception as e:   # reported through the recount frame, raised below on all ranks
+                        err = e
+                        break
                     self.reruns += 1
+            flags = FLAG_RERUN_FAILED if err is not None else 0
             dev = p.parts[0].desc.device
             if dev.type != "cuda":
-                p.enc = self._encode_host(p.parts)
-                cnt = self._counts_host(p.enc)
-                allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32)
-                _all_gather_flat(allc, cnt, self.group)
-                host = allc
+                if err is None:
+                    p.enc = self._encode_host(p.parts)
+                host = self._gather_frame(self._counts_host(p.enc, K, PHASE_RECOUNT, flags))
             elif p.cnt is None:        # gloo with device tensors: count + pack again
-                flat = _flatten(p.parts)
-                cnt = self._count_pack_device(flat, torch.cuda.current_stream(dev))[: XCHG_COUNTS * K]
-                allc = torch.empty(self.world * cnt.numel(), dtype=torch.int32, device=dev)
-                _all_gather_flat(allc, cnt, self.group)
-                host = allc.cpu()
+                frame = self._frame(dev, K, PHASE_RECOUNT, flags)
+                self._count_pack_device(_flatten(p.parts), torch.cuda.current_stream(dev), frame)
+                host = self._gather_frame(frame).cpu()
             else:
-                host, ev, p.cnt = self._count_to_host(_flatten(p.parts), dev)
+                host, ev, p.cnt = self._count_to_host(_flatten(p.parts), dev, K, PHASE_RECOUNT, flags)
                 ev.synchronize()
-            S = host.numpy().astype(np.int64).reshape(self.world, -1, XCHG_COUNTS)
+            S, fl = check_frames(host.numpy(), self.world, K, PHASE_RECOUNT)
+            if fl.any():
+                failed = [r for r in range(self.world) if fl[r] & FLAG_RERUN_FAILED]
+                msg = f"exchange: the overflow re-run failed on rank(s) {failed}"
+                if err is not None:
+                    raise ExchangeMismatch(f"{msg}: {type(err).__name__}: {err}") from err
+                raise ExchangeMismatch(msg)
         raise RuntimeError("exchange: overflow persists after 4 re-runs (pathological message)")
 
     def _complete(self, p: _Pending):
         """The data collective of a step whose counts are on (or on their way to) the host; device
-        buffers: on the current stream.  nccl: the step is packed here (sdx_exchange_pack_into) into
-        this rank's chunk of the receive buffer and gathered in place; returns the event after which
-        the step's output buffers may be overwritten."""
+        buffers: on the current stream.  Pipelined: the step is packed here (sdx_exchange_pack_into)
+        into this rank's chunk of the receive buffer and gathered in place; returns the event after
+        which the step's output buffers may be overwritten."""
         K = len(p.parts)
         if p.event is not None:
             p.event.synchronize()            # the counts (the GPU has moved on to the next step)
-        S = p.counts_host.numpy().astype(np.int64).reshape(self.world, -1, XCHG_COUNTS)
+        S, _ = check_frames(p.counts_host.numpy(), self.world, K, PHASE_COUNT)
         S = self._rerun_bad(p, S, K)
         flat = _flatten(p.parts) if p.enc is None else None
-        offs, nb, T = _layout(S)
+        offs, nb, T = _layout(S)             # T: a function of the gathered counts, the same on every rank
         dev = p.parts[0].desc.device
         self.bytes_sent.append(T)
         self.wire_bytes.append(int(nb[self.rank].sum()))
@@ -576,7 +678,7 @@ class Exchange:
                 sv[o[1]: o[1] + 8 * len(w)] = w.view(np.uint8)
                 sv[o[2]: o[2] + len(pay)] = pay
             recv = torch.empty(self.world * T, dtype=torch.uint8)
-        elif p.cnt is not None:              # nccl: pack into the rank's chunk, all-gather in place
+        elif p.cnt is not None:              # pipelined: pack into the rank's chunk, all-gather in place
             lib = runtime.load_library()
             recv = self._buf("recv", self.world * T, dev)[: self.world * T]
             send = recv[self.rank * T: (self.rank + 1) * T]
@@ -591,8 +693,18 @@ class Exchange:
             released = torch.cuda.Event()
             released.record(torch.cuda.current_stream(dev))   # the launches' buffers have been read
         else:
-            send = self._bufs["send"][:T]
+            # gloo with device buffers: the send buffer was sized from THIS rank's capacities, and T is
+            # the largest rank's wire (e.g. a peer that re-ran into bigger overlays): grow it to T,
+            # keeping the packed bytes, so every rank hands the collective exactly T bytes
+            send = self._bufs["send"]
+            if send.numel() < T:
+                grown = torch.zeros(T + 256, dtype=torch.uint8, device=dev)
+                grown[: send.numel()].copy_(send)
+                send = self._bufs["send"] = grown
+            send = send[:T]
             recv = self._buf("recv", self.world * T, dev)[: self.world * T]
+        if send.numel() != T:
+            raise ExchangeMismatch(f"exchange: rank {self.rank} would send {send.numel()} bytes, the collective is {T}")
         _all_gather_flat(recv, send, self.group)
         self.last = (recv, S, offs, nb, T, K, [q.kind for q in p.parts])
         return released
@@ -717,12 +829,14 @@ class ShardedDemodulator:
     device batch, ``submit(parts, stream)`` per step (re-runs happen inside the exchange when any rank
     reports overflowed messages), ``flush()``, ``gathered()``."""
 
-    def __init__(self, protocols=None, group=None, engine=None, defer: bool = False, nibble: bool = True):
+    def __init__(self, protocols=None, group=None, engine=None, defer: bool = False, nibble: bool = True,
+                 pipeline: Optional[bool] = None):
         from .sd_protocols import SDProtocols
         self.protocols = protocols if protocols is not None else SDProtocols(mc_mode="fixed")
         self.group = group
         self.defer = defer      # Exchange(defer=...): count + pack behind the next step's ``after`` event
         self.nibble = nibble    # the wire's nibble form (False: raw payloads)
+        self.pipeline = pipeline  # Exchange(pipeline=...): None = the overlapped branch with nccl only
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self._eng = engine
@@ -736,7 +850,7 @@ class ShardedDemodulator:
     def exchange(self) -> Exchange:
         want = self.eng if self.nibble else None
         if self._ex is None or self._ex.engine is not want:
-            self._ex = Exchange(self.group, want, defer=self.defer)
+            self._ex = Exchange(self.group, want, defer=self.defer, pipeline=self.pipeline)
         return self._ex
 
     def shard(self, n: int) -> Tuple[int, int]:

@@ -19,7 +19,7 @@ from . import bank as bankmod
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libsdx.so")
-ABI_VERSION = 12   # include/sdx.h SDX_ABI_VERSION
+ABI_VERSION = 13   # include/sdx.h SDX_ABI_VERSION
 
 KIND_MU, KIND_MS, KIND_MC = 0, 1, 2
 KIND_MN = 3        # host-side tag for Engine.run (sdx_demod_mn)
@@ -71,7 +71,7 @@ class SdxLinesGeneralOut(Structure):
 class SdxMcBatch(Structure):
     _fields_ = [("hex_dev", c_void_p), ("offsets_dev", c_void_p), ("clock_dev", c_void_p),
                 ("mcbitnum_dev", c_void_p), ("flags_dev", c_void_p), ("len_dev", c_void_p), ("sel_dev", c_void_p),
-                ("n", c_int32), ("n_sel", c_int32), ("only_dev", c_void_p)]
+                ("n", c_int32), ("n_sel", c_int32), ("only_dev", c_void_p), ("max_hex", c_int32), ("res", c_int32)]
 
 
 class SdxMnBatch(Structure):
@@ -335,6 +335,9 @@ class Engine:
             "flags": t.from_numpy(np.ascontiguousarray(flags, dtype=np.uint8)).to(d),
             "n": int(mb.n),
             "lengths": np.diff(mb.offsets),
+            # every frame's length is known here: sdx_demod_mc skips its long-frame launch when none
+            # is longer than SDX_MC_SHORT_HEX (ABI 13)
+            "max_hex": int(np.diff(mb.offsets).max(initial=0)),
         }
 
     def pulses_work_bytes(self, n: int, spill_frac: float = 0.5) -> int:
@@ -429,7 +432,7 @@ class Engine:
     def launch_mc(self, bd, out, sel=None) -> None:
         b = SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
                        _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"],
-                       0 if sel is None else int(sel.numel()), _ptr(bd.get("only")))
+                       0 if sel is None else int(sel.numel()), _ptr(bd.get("only")), int(bd.get("max_hex", 0)), 0)
         o = self._out_struct(out)
         _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 

@@ -12,10 +12,19 @@ World size 2 over gloo with both ranks on cuda:0 (the one-GPU rehearsal of confi
              (ST_OVF_TILE), MC frames longer than 128 hex characters launched on k_mc alone (which hands
              them over as ST_OVF_TILE; the routed launch sends them to the general kernel) -- the exchange re-runs them into overlays on each rank before it ships, and
              the gathered results equal the un-sharded Engine.run (its own re-runs) byte for byte;
+  overflow1  the overflow mode with only rank 1's MU launch overflowing (rank 0 has room): only that
+             rank re-runs, every rank recounts;
   dict       ShardedDemodulator.demodulate_batch on msg_data dicts (general-path messages with
              multi-digit ids, messages whose host conversion raises) == SDProtocols.demodulate_batch of
-             the whole list, on every rank.
-Prints "OK" on success.
+             the whole list, on every rank;
+  sizes      synthetic device launches: rank 0's outputs are small and exactly sized, rank 1's launch
+             overflows and its re-run overlay carries 40x larger payloads, so the collective's size T
+             exceeds everything rank 0 allocated; then rank 1 submits two launches where
+             rank 0 submits one, which must raise ExchangeMismatch on both ranks.
+SDX_XCHG_PIPELINE=1 runs the exchange's pipelined branch -- the one an RCCL run takes: counts behind
+the step's kernels on the exchange stream, in-place pack into the receive chunk, recount after
+re-runs -- over gloo (SDX_XCHG_DEFER=1: its deferred form, the bench's default); unset, gloo takes
+the synchronous branch.  Prints "OK" on success.
 """
 import os
 import sys
@@ -62,14 +71,19 @@ def main():
     bk = bankmod.Bank()
     eng = runtime.Engine(bk, 0)
     P = bk.protocols
-    sd = sdist.ShardedDemodulator(group=None, engine=eng)
+    pipe = os.environ.get("SDX_XCHG_PIPELINE") == "1"
+    sd = sdist.ShardedDemodulator(group=None, engine=eng, defer=os.environ.get("SDX_XCHG_DEFER") == "1")
     assert sd.world == world
+    assert sd.exchange.pipelined == pipe, (sd.exchange.pipelined, pipe)
     if mode == "dict":
         return dict_mode(sd, P, rank)
-    dense = mode == "overflow"
+    if mode == "sizes":
+        return sizes_mode(sd, dev, rank)
+    dense = mode in ("overflow", "overflow1")
+    tight = dense and (mode == "overflow" or rank == 1)   # this rank's MU launch overflows
     full = {"MU": synth.mu_corpus(P, N, seed=81, noise_frac=0.0 if dense else 0.15), "MS": synth.ms_corpus(P, N, seed=82),
             "MC": synth.mc_corpus(P, N, seed=83)}
-    if dense:
+    if mode == "overflow":
         full["MC"] = long_mc(P, full["MC"], 40, seed=84)
     kinds = ("MU", "MS", "MC")
     lo, hi = sd.shard(N)
@@ -77,7 +91,7 @@ def main():
     bds = {k: (eng.to_device_mc(c) if k == "MC" else eng.to_device_pulses(c)) for k, c in shard.items()}
 
     def alloc(n, k):
-        if dense and k == "MU":   # one record per message, no spill regions: ST_OVF_OUT and ST_OVF_TILE
+        if tight and k == "MU":   # one record per message, no spill regions: ST_OVF_OUT and ST_OVF_TILE
             return eng.alloc_out(n, n, 40 * n, 0, wire=True)
         # the kernels write the exchange's counts (ABI 12) in the pipelined mode; the overflow mode's
         # MS / MC launches leave the classification to the exchange kernels
@@ -92,23 +106,33 @@ def main():
         parts = []
         for k in kinds:
             o[k]["cursor"].zero_()
-            if dense and k == "MC":   # k_mc alone (no routing): it hands the > 128-character frames over
+            if mode == "overflow" and k == "MC":   # k_mc alone (no routing): it hands the > 128-character frames over
                 eng.launch_mc(bds[k], o[k])   # as ST_OVF_TILE, and the exchange re-runs them
                 parts.append(sdist.Part.from_out(o[k], KIND[k], src=(KIND[k], bds[k], 0, -1)))
             else:
                 parts.append(sd.launch(KIND[k], bds[k], o[k]))
-        if dense and j == 0:   # the first pass really overflowed on this rank
+        if dense and j == 0:   # the first pass really overflowed on this rank (or, overflow1, not)
             torch.cuda.synchronize()
             st = {k: o[k]["desc"][: (hi - lo) * 8].view(-1, 8)[:, 6].cpu().numpy() for k in kinds}
-            assert (st["MU"] == runtime.ST_OVF_OUT).any(), rank
+            assert (st["MU"] == runtime.ST_OVF_OUT).any() == tight, rank
             print("first-pass MU overflows: OUT", int((st["MU"] == runtime.ST_OVF_OUT).sum()), "TILE",
                   int((st["MU"] == runtime.ST_OVF_TILE).sum()), flush=True)
-            assert (st["MC"] == runtime.ST_OVF_TILE).any(), rank
-        sd.submit(parts, stream)
-        snaps.append([tuple(t.cpu().numpy() for t in g) for g in sd.gathered()])
+            assert (st["MC"] == runtime.ST_OVF_TILE).any() == (mode == "overflow"), rank
+        rel = sd.submit(parts, stream)
+        if not pipe:            # synchronous: this step is complete
+            snaps.append([tuple(t.cpu().numpy() for t in g) for g in sd.gathered()])
+        elif j >= 1:            # pipelined: the previous step completed inside this submit
+            snaps.append([tuple(t.cpu().numpy() for t in g) for g in sd.gathered()])
+            stream.wait_event(rel)
     sd.flush()
-    if dense:
-        assert sd.exchange.reruns >= 4, sd.exchange.reruns
+    if pipe:
+        assert sd.exchange.stream is not None, "the pipelined branch runs on the exchange stream"
+        snaps.append([tuple(t.cpu().numpy() for t in g) for g in sd.gathered()])
+    assert len(snaps) == 2, len(snaps)
+    if mode == "overflow" or (mode == "overflow1" and rank == 1):
+        assert sd.exchange.reruns >= (4 if mode == "overflow" else 2), sd.exchange.reruns
+    elif mode == "overflow1":
+        assert sd.exchange.reruns == 0, sd.exchange.reruns
     # the nibble form is on: the wire carries fewer payload bytes than it delivers
     assert sd.exchange.heap_wire_bytes[-1] < 0.8 * sd.exchange.payload_bytes[-1], (sd.exchange.heap_wire_bytes,
                                                                                   sd.exchange.payload_bytes)
@@ -123,6 +147,65 @@ def main():
             assert gr.tobytes() == cr.tobytes(), (rank, j, k, "rec")
             assert gh.tobytes() == ch.tobytes(), (rank, j, k, "heap")
         assert len(cr) > N // 4, (k, len(cr))
+    dist.barrier()
+    dist.destroy_process_group()
+    print("OK", flush=True)
+
+
+def sizes_mode(sd, dev, rank):
+    """ADVICE r04 (medium): a peer's wire larger than this rank's whole send capacity, and a
+    deliberately mismatched number of launches (VERDICT r04 #1)."""
+    n = 100
+    desc = np.zeros(n, runtime.DESC_DT)
+    desc["n_rec"] = 1
+    desc["rec_begin"] = np.arange(n)
+    plen = 4 if rank == 0 else 160
+    rec = np.zeros(n, runtime.RES_DT)
+    rec["payload_off"] = np.arange(n) * plen
+    rec["payload_len"] = plen
+    rec["proto"] = 1
+    rec["bit_length"] = 8 * plen
+    rec["msg"] = np.arange(n)
+    heap = (np.arange(n * plen) % 23 + 65).astype(np.uint8)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(dev)  # noqa: E731
+    cur = lambda: torch.tensor([n, n * plen, 0, 0], dtype=torch.int32, device=dev)  # noqa: E731
+    if rank == 0:
+        part = sdist.Part(t(desc), t(rec), t(heap), n, cur())
+    else:   # overflowed first pass; the overlay holds the real (large) results
+        d1 = desc.copy()
+        d1["status"] = runtime.ST_OVF_OUT
+        d1["n_rec"] = 0
+        part = sdist.Part(t(d1), t(rec[:1]), t(heap[:16]), n, torch.tensor([0, 0, 0, 0], dtype=torch.int32, device=dev))
+
+    def rerun(p):
+        p.overlays.append(sdist.Part(t(desc), t(rec), t(heap), n, cur()))
+        return p
+    ex = sdist.Exchange(pipeline=sd.exchange.pipeline)
+    rel = ex.submit([part], rerun=rerun)
+    ex.flush()
+    gd, gr, gh = (x.cpu().numpy() for x in ex.gathered()[0])
+    assert ex.bytes_sent[-1] > 8 * 1024, ex.bytes_sent   # T: rank 1's wire, > rank 0's 1.6 KB of outputs
+    want = []
+    for r, pl in ((0, 4), (1, 160)):
+        want += [((np.arange(pl) + i * pl) % 23 + 65).astype(np.uint8).tobytes() for i in range(n)]
+    got = [gh[int(x["payload_off"]): int(x["payload_off"]) + int(x["payload_len"])].tobytes()
+           for x in gr.view(runtime.RES_DT)]
+    assert got == want, rank
+    assert (gd.view(runtime.DESC_DT)["n_rec"] == 1).all()
+    # rank 1 submits two launches where rank 0 submits one: ExchangeMismatch on both ranks
+    ex2 = sdist.Exchange(pipeline=sd.exchange.pipeline)
+    raised = None
+    try:
+        ex2.submit([sdist.Part(t(desc), t(rec), t(heap[: n * plen]), n, cur())] * (1 + rank))
+        ex2.flush()
+    except sdist.ExchangeMismatch as e:
+        raised = str(e)
+    assert raised is not None and "launches" in raised, (rank, raised)
+    # and the ranks are still in step
+    ex3 = sdist.Exchange(pipeline=sd.exchange.pipeline)
+    ex3.submit([sdist.Part(t(desc), t(rec), t(heap), n, cur())])
+    ex3.flush()
+    assert ex3.gathered()[0][0].numel() == 2 * n * 8
     dist.barrier()
     dist.destroy_process_group()
     print("OK", flush=True)

@@ -269,3 +269,46 @@ def test_json_stream_command_turns_follow_state_changes():
     asyncio.run(go())
     assert [t for _, t in ctl.mqtt_publisher.sent] == [t for t in texts if t is not None]
     assert ctl.cmd == exp_cmd and 0 < len(exp_cmd) < len(lines)
+
+
+@pytest.mark.parametrize("how", ["stop", "error"])
+def test_json_stream_publishes_in_flight_chunks_on_exit(how):
+    """when the stop event is set (or an error ends the loop) while chunks are in flight
+    in the stream, those chunks are drained and published: every line taken off the queue gets its
+    publication and command-response turn, as in the reference loop."""
+    lines = [f"MC;D={i};" for i in range(1000)]
+    parser = FakeParser()
+
+    class StopPub(Pub):
+        async def publish(self, *a):
+            self.sent.append(a)
+            if len(self.sent) == 1:
+                ctl._stop_event.set()
+
+    class FailStream(FakeStream):
+        polls = 0
+
+        def poll(self):
+            FailStream.polls += 1
+            if FailStream.polls == 6:
+                raise RuntimeError("injected poll failure")
+            return super().poll()
+
+    ctl = Ctl(parser, callback=False)
+    if how == "stop":
+        ctl.mqtt_publisher = StopPub()
+    else:
+        parser.stream = lambda chunk_lines, output="json", lag=3: FailStream(parser, lag)
+    task = BatchingParserTask(ctl, publish="json", max_batch=40, max_delay=0.005)
+
+    async def go():
+        for ln in lines:
+            ctl._raw_message_queue.put_nowait(ln)
+        await asyncio.wait_for(task.run(), 30)
+
+    asyncio.run(go())
+    taken = len(lines) - ctl._raw_message_queue.qsize()
+    assert 3 * 40 < taken < len(lines), taken     # chunks were in flight when the loop ended
+    _, sent, cmd = reference_side_effects(FakeParser(), lines[:taken])
+    assert ctl.cmd == cmd and task.lines == taken
+    assert ctl.mqtt_publisher.sent == [("t/v1/state/messages", json.dumps(s[0])) for s in sent]

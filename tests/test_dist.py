@@ -163,6 +163,75 @@ def test_gloo_world_allgather_matches_unsharded(world):
         assert steps == [[full], [halves, full]], f"rank {rank}: Exchange steps differ"
 
 
+def _guard_worker(rank, world, port, q):
+    """Collective-size agreement: rank 1 submits two launches where rank 0 submits
+    one; then rank 1's overflow re-run raises.  Each case must raise ExchangeMismatch on EVERY rank
+    (fixed-size count frames), with no rank left waiting in a collective; a third exchange after them
+    still works (the ranks are back in step)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(40 + rank)
+    d, r, h = synth_launch(rng, 300, spill=False)
+    part = lambda dd: (torch.from_numpy(dd.view(np.uint8).copy()), torch.from_numpy(r.view(np.uint8).copy()),  # noqa: E731
+                       torch.from_numpy(h.copy()), len(dd), torch.tensor([len(r), len(h), 0, 0], dtype=torch.int32))
+    got = []
+    try:
+        sdist.Exchange().submit([part(d)] * (1 if rank == 0 else 2))
+        got.append("no error")
+    except sdist.ExchangeMismatch as e:
+        got.append("mismatch" if "launches" in str(e) else str(e))
+    d2 = d.copy()
+    d2["status"][:3] = runtime.ST_OVF_OUT
+
+    def rerun(p):
+        if rank == 1:
+            raise MemoryError("injected re-run failure")
+        od = d.copy()
+        od["status"][3:] = runtime.ST_ABSENT
+        p.overlays.append(sdist.Part(*part(od)))
+        return p
+    try:
+        sdist.Exchange().submit([part(d2)], rerun=rerun)
+        got.append("no error")
+    except sdist.ExchangeMismatch as e:
+        got.append("rerun failed" if "[1]" in str(e) else str(e))
+    ex = sdist.Exchange()
+    ex.submit([part(d)])
+    ex.flush()
+    got.append(int(ex.gathered()[0][0].numel()) // 8)
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+def test_exchange_mismatch_raises_on_every_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert outs == {0: ["mismatch", "rerun failed", 600], 1: ["mismatch", "rerun failed", 600]}, outs
+
+
+def test_check_frames_header_rules():
+    """check_frames: the counts of K launches come back per rank; any header difference raises."""
+    f = np.zeros((3, sdist.FRAME_INTS), np.int32)
+    for r in range(3):
+        f[r, :sdist.FRAME_HDR] = sdist.frame_header(3, 2, sdist.PHASE_COUNT)
+        f[r, sdist.FRAME_HDR: sdist.FRAME_HDR + 16] = np.arange(16) + 100 * r
+    S, fl = sdist.check_frames(f.reshape(-1), 3, 2, sdist.PHASE_COUNT)
+    assert S.shape == (3, 2, 8) and S[2, 1, 7] == 215 and not fl.any()
+    for field, val in ((0, 0), (1, 4), (2, 3), (3, sdist.PHASE_RECOUNT)):
+        g = f.copy()
+        g[1, field] = val
+        with pytest.raises(sdist.ExchangeMismatch):
+            sdist.check_frames(g.reshape(-1), 3, 2, sdist.PHASE_COUNT)
+
+
 def synth_affix(rng, nproto=129):
     """A per-protocol (preamble, postamble) table shaped like Bank.affixes (preambles such as 'W54#',
     's', '', postambles mostly empty)."""
@@ -556,12 +625,21 @@ def test_exchange_rccl_world1():
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
-def _world2(mode, timeout=120, world=2):
+BRANCH_ENV = {"sync": {}, "pipelined": {"SDX_XCHG_PIPELINE": "1"},
+              "defer": {"SDX_XCHG_PIPELINE": "1", "SDX_XCHG_DEFER": "1"}}
+
+
+def _world2(mode, timeout=120, world=2, branch="sync"):
+    """world ranks of dist_gpu_worker.py on cuda:0 over gloo; ``branch``: the exchange's synchronous
+    gloo branch, or the pipelined branch an RCCL run takes (eager or deferred count + pack), forced
+    over gloo (VERDICT r04 #1)."""
     import subprocess
     import sys
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_gpu_worker.py")
     port = str(_free_port())
-    procs = [subprocess.Popen([sys.executable, worker], env=dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+    env = {k: v for k, v in os.environ.items() if k not in ("SDX_XCHG_PIPELINE", "SDX_XCHG_DEFER")}
+    env.update(BRANCH_ENV[branch])
+    procs = [subprocess.Popen([sys.executable, worker], env=dict(env, MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
                                                                  RANK=str(r), WORLD_SIZE=str(world), SDX_WORKER_MODE=mode),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
     outs = []
@@ -579,22 +657,40 @@ def _world2(mode, timeout=120, world=2):
 
 
 @pytest.mark.gpu
-def test_world2_real_kernels_match_unsharded():
+@pytest.mark.parametrize("branch", ["sync", "pipelined", "defer"])
+def test_world2_real_kernels_match_unsharded(branch):
     """Config 5's path at world size 2 on the one GPU (gloo, both ranks on cuda:0): each rank
     demodulates its contiguous shard of a real MU + MS + MC batch with the product launches
-    (ShardedDemodulator: grouped order, spill regions), the pipelined exchange (nibble wire form)
-    gathers two steps, and the gathered descriptors, records and heap equal an un-sharded device run
-    (canonical form) byte for byte."""
-    _world2("pipelined")
+    (ShardedDemodulator: grouped order, spill regions), the exchange (nibble wire form) gathers two
+    double-buffered steps, and the gathered descriptors, records and heap equal an un-sharded device
+    run (canonical form) byte for byte -- through the synchronous gloo branch and through the
+    pipelined branch RCCL runs (eager and deferred)."""
+    _world2("pipelined", branch=branch)
 
 
 @pytest.mark.gpu
-def test_world2_overflow_reruns_match_unsharded():
+@pytest.mark.parametrize("branch", ["sync", "pipelined", "defer"])
+def test_world2_overflow_reruns_match_unsharded(branch):
     """a corpus and capacities that force ST_OVF_OUT / ST_OVF_TILE (dense MU corpus,
     one record per message, no spill workspace; MC frames of 129..800 hex characters): the ranks
-    re-run their overflowed messages into overlays inside the exchange (no RuntimeError) and the
-    gathered results equal the un-sharded Engine.run byte for byte."""
-    _world2("overflow")
+    re-run their overflowed messages into overlays inside the exchange (no RuntimeError), every rank
+    recounts, and the gathered results equal the un-sharded Engine.run byte for byte."""
+    _world2("overflow", branch=branch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("branch", ["sync", "defer"])
+def test_world2_one_rank_overflows(branch):
+    """Only rank 1 overflows and re-runs; rank 0 takes part in the recount only."""
+    _world2("overflow1", branch=branch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("branch", ["sync", "pipelined"])
+def test_world2_collective_sizes(branch):
+    """ADVICE r04 / VERDICT r04 #1: a peer's wire larger than this rank's whole send capacity is
+    gathered correctly, and a mismatched number of launches raises ExchangeMismatch on both ranks."""
+    _world2("sizes", branch=branch)
 
 
 @pytest.mark.gpu
@@ -606,23 +702,27 @@ def test_world2_sharded_demodulate_batch_dicts():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["pipelined", "dict"])
-def test_world4_on_one_gpu_matches_unsharded(mode):
+@pytest.mark.parametrize("mode,branch", [("pipelined", "sync"), ("pipelined", "defer"), ("overflow", "defer"),
+                                         ("dict", "sync"), ("dict", "pipelined")])
+def test_world4_on_one_gpu_matches_unsharded(mode, branch):
     """The same at world size 4 (four gloo ranks on cuda:0): uneven shard boundaries, every rank's
-    gathered stream / dict results equal the un-sharded run."""
-    _world2(mode, timeout=150, world=4)
+    gathered stream / dict results equal the un-sharded run, on both exchange branches."""
+    _world2(mode, timeout=150, world=4, branch=branch)
 
 
 @pytest.mark.gpu
-def test_bench_self_launch_world2():
+@pytest.mark.parametrize("branch", ["sync", "defer"])
+def test_bench_self_launch_world2(branch):
     """``bench.py --gpus 2`` without a launcher starts 2 ranks itself and reports n_gpus 2 with the
-    exchange's wire bytes (gloo rehearsal: both ranks on cuda:0)."""
+    exchange's wire bytes (gloo rehearsal: both ranks on cuda:0); ``defer``: the bench's own N > 1
+    step -- the deferred pipelined exchange an RCCL run takes -- over gloo."""
     import json
     import subprocess
     import sys
     bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["SDX_DIST_BACKEND"] = "gloo"
+    env["SDX_XCHG_PIPELINE"] = "1" if branch == "defer" else "0"
     r = subprocess.run([sys.executable, bench, "--gpus", "2", "--steps", "2", "--warmup", "1", "--msgs", "30000",
                         "--no-cpu"], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
@@ -631,10 +731,12 @@ def test_bench_self_launch_world2():
     res = json.loads(line[0])
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
     assert res["exchange"]["wire_bytes_per_rank_per_step"] > 0
+    assert res["exchange"]["branch"] == ("pipelined" if branch == "defer" else "sync"), res["exchange"]
 
 
 @pytest.mark.gpu
-def test_config5_rehearsal_world8_on_one_gpu():
+@pytest.mark.parametrize("branch", ["sync", "defer"])
+def test_config5_rehearsal_world8_on_one_gpu(branch):
     """Config 5's shape on the one GPU: eight gloo ranks on cuda:0, each with a mixed MU/MS/MC shard
     (300k messages here; the full 1M-per-rank run is profiles/r04/s3/config5_rehearsal/), the product
     exchange and the device unpack of the whole job: every rank's own wire chunk equals the host
@@ -644,6 +746,7 @@ def test_config5_rehearsal_world8_on_one_gpu():
     tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "config5_rehearsal.py")
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"c5_{os.getpid()}")
-    r = subprocess.run([sys.executable, tool, "--world", "8", "--msgs", "300000", "--out", out, "--timeout", "130"],
+    r = subprocess.run([sys.executable, tool, "--world", "8", "--msgs", "300000", "--out", out, "--timeout", "130",
+                        "--branch", branch],
                        env=env, capture_output=True, text=True, timeout=145)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), (r.stdout[-3000:], r.stderr[-3000:])

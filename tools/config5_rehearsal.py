@@ -8,7 +8,10 @@ wire) and unpack the WHOLE job on the device.  Checks, per rank:
   * every rank's SHA-256 of the whole receive buffer is the same (all-gathered digests).
 Rank 0 prints one JSON line.  The RCCL / xGMI rate of the real 8-GPU run is not measured here (gloo
 stages through host memory); this is the correctness rehearsal of the sizes.
-usage: python tools/config5_rehearsal.py [--world 8] [--msgs 1000000] [--out gpurun_out/c5]"""
+--branch pipelined / defer runs the exchange's pipelined branch (the code an RCCL run executes: count
+on the exchange stream, in-place pack, eager or deferred) over gloo; sync (default) the gloo branch.
+usage: python tools/config5_rehearsal.py [--world 8] [--msgs 1000000] [--branch sync|pipelined|defer]
+       [--out gpurun_out/c5]"""
 import argparse
 import hashlib
 import json
@@ -37,7 +40,8 @@ def launcher(args):
         log = open(os.path.join(args.out, f"rank{r}.log"), "w")
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.world), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--msgs", str(args.msgs),
-                                       "--out", args.out], env=env, stdout=log, stderr=subprocess.STDOUT))
+                                       "--out", args.out, "--branch", args.branch], env=env, stdout=log,
+                                      stderr=subprocess.STDOUT))
         logs.append(log)
     t0 = time.time()
     rc = 0
@@ -79,8 +83,8 @@ def rank_main(args):
     KIND = {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS, "MC": runtime.KIND_MC}
     bds = {k: (eng.to_device_mc(c) if k == "MC" else eng.to_device_pulses(c)) for k, c in corp.items()}
     print(f"rank {rank}: shard of {args.msgs} messages generated in {time.time() - t:.1f} s", flush=True)
-    sd = sdist.ShardedDemodulator(engine=eng)
-    assert sd.world == world
+    sd = sdist.ShardedDemodulator(engine=eng, pipeline=args.branch != "sync", defer=args.branch == "defer")
+    assert sd.world == world and sd.exchange.pipelined == (args.branch != "sync")
     t = time.time()
     parts = [sd.launch(KIND[k], bds[k]) for k in ("MU", "MS", "MC")]
     sd.submit(parts)
@@ -120,6 +124,7 @@ def rank_main(args):
     dist.barrier()
     if rank == 0:
         print(json.dumps({"config": "config 5 rehearsal on one GPU (gloo, all ranks on cuda:0)", "world": world,
+                          "exchange_branch": args.branch,
                           "msgs_per_rank": args.msgs, "msgs_total": world * args.msgs,
                           "records_total": int(S[:, :, 1].sum()), "wire_bytes_per_rank": int(T),
                           "launch_exchange_s_rank0": round(t_x, 3), "unpack_job_s_rank0": round(t_u, 3),
@@ -136,6 +141,7 @@ def main():
     ap.add_argument("--msgs", type=int, default=1_000_000)
     ap.add_argument("--out", default="gpurun_out/c5")
     ap.add_argument("--timeout", type=float, default=600.0)
+    ap.add_argument("--branch", default="sync", choices=("sync", "pipelined", "defer"))
     args = ap.parse_args()
     if "RANK" in os.environ:
         return rank_main(args)
