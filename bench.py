@@ -446,10 +446,23 @@ def main():
     # roofline of the dominant kernel: SURVEY §8(d) algorithmic bytes / its HIP-event time
     kt = {k: float(np.mean(v)) for k, v in ktimes.items()}
     dom = max(kt, key=kt.get)
+    # every kind's launch against the same HBM roofline: its algorithmic bytes (the
+    # outputs of the last step) / its HIP-event time.  In the mixed step MS and MC run side by side
+    # after MU (MC on its own stream, started at MU's end), so their times include that sharing;
+    # --kind MU|MS|MC times each kernel alone
+    kern_tag = {"MU": "k_pulses<MU>", "MS": "k_pulses<MS>", "MC": "k_mc"}
+    kernels = {}
+    for k in kinds:
+        ok_ = outs[(j - 1) % nslot][k]
+        ck = ok_["cursor"].cpu().numpy().astype(np.int64)
+        rk = ok_["rec"][: int(ck[0]) * RES_DT.itemsize].cpu().numpy().view(RES_DT)
+        ak = alg_bytes(k, bds[k], rk)
+        kernels[k] = {"kernel": kern_tag[k], "alg_bytes_per_launch": ak, "results_per_launch": int(ck[0]),
+                      "ms": 1e3 * kt[k], "achieved_GBps": ak / kt[k] / 1e9, "frac": ak / kt[k] / HBM_PEAK,
+                      "shares_gpu_with": ("MC" if k == "MS" else "MS") if mc_beside_ms and k in ("MS", "MC") else None}
     o = outs[(j - 1) % nslot][dom]
     cur = o["cursor"].cpu().numpy().astype(np.int64)
-    rec_np = o["rec"][: int(cur[0]) * RES_DT.itemsize].cpu().numpy().view(RES_DT)
-    alg = alg_bytes(dom, bds[dom], rec_np)
+    alg = kernels[dom]["alg_bytes_per_launch"]
     n = bds[dom]["n"]
     layout = (int(bds[dom]["lengths"].sum()) + n * ((8 + 4 + 4 + 1) if dom == "MC" else
                                                     (8 + 1 + 10 + 80 + (2 if dom == "MS" else 0)))
@@ -490,7 +503,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": tag,
                      "alg_bytes_per_launch": alg, "layout_bytes_per_launch": layout,
-                     "results_per_launch": int(cur[0]), "issue": issue},
+                     "results_per_launch": int(cur[0]), "issue": issue, "per_kernel": kernels},
     }
     if exch is not None and exch.bytes_sent:
         nb = exch.bytes_sent[-args.steps:]

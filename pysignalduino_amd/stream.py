@@ -11,7 +11,9 @@ come back -- with every stage of chunk k overlapping other chunks' stages on fou
   parse     sdx_parse_lines + sdx_select_lines, class counts D2H  (stage A)
   demod     the MU / MS short+long, MC ('fixed'), MN launches over the selection lists, then either
             the publish-ready JSON texts (sdx_serialize_json, sparse: all kinds into one buffer)
-            or the exchange's wire form (sdx_exchange_count/pack), their sizes D2H   (stage B)
+            or the exchange's wire form (sdx_exchange_count/pack), their sizes D2H   (stage B;
+            consecutive chunks alternate between two demodulation streams, so one chunk's
+            kernels fill the CUs that the tail of the previous chunk's leaves idle)
   copy-out  the texts (or wire) + per-line kind/status D2H, sized from the device sizes  (stage C)
 
 The host only waits for events of chunks enqueued ``lag`` submits earlier (stage B of chunk k-1
@@ -167,7 +169,12 @@ class LineStream:
         self.lag = max(1, int(lag))
         self.slots = [_Slot(self) for _ in range(self.lag + 1)]
         dev = self.eng.dev
-        self.cin, self.sp, self.sd, self.cout = (torch.cuda.Stream(dev) for _ in range(4))
+        self.cin, self.sp, self.cout = (torch.cuda.Stream(dev) for _ in range(3))
+        # two demodulation streams, chunk k on sds[k % 2]: every buffer a chunk's stage B touches is
+        # its slot's own, so chunk k+1's launches may run beside chunk k's (one stream
+        # serialised the chunks' kernels and each chunk's tail idled the CUs)
+        self.sds = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+        self.sd = self.sds[0]
         self.inflight: Deque[_Slot] = collections.deque()
         self.done: Deque[ChunkResult] = collections.deque()
         self.next_id = 0
@@ -278,20 +285,21 @@ class LineStream:
         start = np.concatenate([[0], np.cumsum(cnt)])
         lb, n = s.lb, s.n
         sels = [lb.sel[int(start[i]): int(start[i + 1])] for i in range(runtime.SEL_NCLASS)]
-        with t.cuda.stream(self.sd):
-            self.sd.wait_event(s.parse_ev)
+        sd = sds[s.cid % 2]
+        with t.cuda.stream(sd):
+            sd.wait_event(s.parse_ev)
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
-            e0.record(self.sd)
-            runtime.fill_async(s.cursors, self.sd)
+            e0.record(sd)
+            runtime.fill_async(s.cursors, sd)
             pb = lb.pulse_batch()
             for name, kd, short, long_ in _KINDS:
                 o = s.outs.get(name)
                 if o is None:
                     continue
                 o["n"] = n
-                runtime.fill_async(o["desc"][: 8 * n], self.sd)   # lines of other classes keep an empty descriptor
+                runtime.fill_async(o["desc"][: 8 * n], sd)   # lines of other classes keep an empty descriptor
                 if o.get("wire") is not None:
-                    runtime.fill_async(o["wire"][:n], self.sd)     # ... and no exchange counts
+                    runtime.fill_async(o["wire"][:n], sd)     # ... and no exchange counts
                 if kd == runtime.KIND_MN:
                     if cnt[short]:
                         eng.launch_mn(lb.mn_batch(), o, elig=self.elig, sel=sels[short])
@@ -308,27 +316,27 @@ class LineStream:
             s.cnt = cnt
             if self.output == "json":
                 jo = s.jout
-                runtime.fill_async(jo["cursor"], self.sd)
-                runtime.fill_async(jo["len"][:n], self.sd)
+                runtime.fill_async(jo["cursor"], sd)
+                runtime.fill_async(jo["len"][:n], sd)
                 lo = {"meta": lb.meta, "pat_val": lb.pat_val, "cp_slot": lb.cp_slot}
                 for name, kd, short, long_ in _KINDS:
                     o = s.outs.get(name)
                     if o is not None and (cnt[short] or (long_ is not None and cnt[long_])):
                         eng.launch_json(kd, o, lo, n, jo, first_only=2)
-                runtime.copy_async(s.h_sizes[:2], jo["cursor"], self.sd)
-                runtime.copy_async(s.h_sizes[2:], s.cursors.reshape(-1), self.sd)
+                runtime.copy_async(s.h_sizes[:2], jo["cursor"], sd)
+                runtime.copy_async(s.h_sizes[2:], s.cursors.reshape(-1), sd)
             else:
                 from . import dist as sdist
                 parts = [sdist.Part(o["desc"], o["rec"], o["heap"], n, o["cursor"], kd, wire=o.get("wire"),
                                     xrec=o.get("xrec"))
                          for name, kd, _, _ in _KINDS for o in [s.outs.get(name)] if o is not None]
-                wc = s.ser._count_pack_device(sdist._flatten(parts), self.sd)
+                wc = s.ser._count_pack_device(sdist._flatten(parts), sd)
                 k = len(parts)
-                runtime.copy_async(s.h_sizes[: runtime.XCHG_COUNTS * k], wc, self.sd)
-                runtime.copy_async(s.h_sizes[runtime.XCHG_COUNTS * k:], s.cursors.reshape(-1), self.sd)
-            e1.record(self.sd)
+                runtime.copy_async(s.h_sizes[: runtime.XCHG_COUNTS * k], wc, sd)
+                runtime.copy_async(s.h_sizes[runtime.XCHG_COUNTS * k:], s.cursors.reshape(-1), sd)
+            e1.record(sd)
             ev = t.cuda.Event()
-            ev.record(self.sd)
+            ev.record(sd)
         s.demod_ev, s.ev = e1, ev
         s.kt += [e0, e1]
         s.stage = 2
