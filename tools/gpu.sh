@@ -23,6 +23,8 @@
 #   benchenv=VAR=val[,ARGS]  bench.py ARGS with VAR=val in the environment -> OUT/bench_<n>.log
 #   pyenv=VAR=val,SCRIPT[,ARGS]  python SCRIPT ARGS with VAR=val in the environment -> OUT/pyenv_<n>.log
 #   pylib=V,SCRIPT[,ARGS] the same with SDX_LIB = pysignalduino_amd/_lib/ab/libsdx_V.so (e.g. the SDX_PROF build)
+#   testlib=V[,PYTEST_K]  the -m gpu suite (or -k) on the variant library V (like testc)
+#   benchlib=V[,ARGS]     bench.py ARGS on the variant library V
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONUNBUFFERED=1
@@ -93,6 +95,15 @@ for st in "$@"; do
     pylib) v=${args%% *}; rest=${args#* }
       SDX_LIB=pysignalduino_amd/_lib/ab/libsdx_$v.so run 600 "$O/pylib_$n.log" python -u $rest
       echo "pylib $arg: $(tail -3 "$O/pylib_$n.log" | cut -c1-400)" ;;
+    testlib) v=${args%% *}; k=${args#* }; [ "$k" = "$v" ] && k=""
+      SDX_LIB=pysignalduino_amd/_lib/ab/libsdx_$v.so timeout -k 10 900 python -u -m pytest tests -m gpu -v ${k:+-k "$k"} --timeout 150 --timeout-method thread > "$O/testlib_$n.txt" 2>&1
+      rc=$?
+      echo "testlib $arg: $(tail -1 "$O/testlib_$n.txt")"
+      grep -E "^(FAILED|ERROR)" "$O/testlib_$n.txt" | head -20 || true
+      case $rc in 124|134|137|139) echo "tests stopped ($rc): no further GPU steps"; exit 1 ;; esac ;;
+    benchlib) v=${args%% *}; rest=${args#* }; [ "$rest" = "$v" ] && rest=""
+      SDX_LIB=pysignalduino_amd/_lib/ab/libsdx_$v.so run 240 "$O/bench_$n.log" python bench.py --no-cpu $rest
+      echo "benchlib $arg: $(tail -1 "$O/bench_$n.log" | summ)" ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
