@@ -2355,7 +2355,14 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
 // =============================================================================================
 // MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
 // =============================================================================================
-constexpr int MC_REC_CAP = 152, MC_HEAP_CAP = 3584;  // per wave: k_mc<4> fits 4 workgroups per CU
+#ifndef SDX_MC_REC_CAP
+#define SDX_MC_REC_CAP 152
+#define SDX_MC_HEAP_CAP 3584
+#endif
+#ifndef SDX_MC_WPE
+#define SDX_MC_WPE 4
+#endif
+constexpr int MC_REC_CAP = SDX_MC_REC_CAP, MC_HEAP_CAP = SDX_MC_HEAP_CAP;  // per wave: k_mc<4> fits 4 workgroups per CU
 
 template <int MW>
 struct McLds {
@@ -2444,7 +2451,7 @@ SDX_DEV void mc_stage(const uint8_t* src, int hl, uint64_t* dn, uint64_t* di, in
 // MW = 4: frames of <= 64 hex characters, longer ones are left to the MW = 8 launch (LONG = true),
 // which takes only those (sdx_demod_mc launches both; a wave without long frames exits at once)
 template <int MW, bool LONG>
-__global__ __launch_bounds__(256) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : SDX_MC_WPE))) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
   __shared__ McLds<MW> L;
   const BankView bv = bank_view(bank);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
