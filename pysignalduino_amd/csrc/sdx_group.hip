@@ -46,12 +46,9 @@ constexpr int SIG_PROTOS = 32;
 #endif
 template <int KIND>
 __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_pulse_batch b, uint32_t* __restrict__ key,
-                                             uint32_t* __restrict__ msg_out, sdx_msg_rec* __restrict__ mrec,
-                                             uint32_t* __restrict__ zero, int nzero) {
+                                             uint32_t* __restrict__ msg_out, sdx_msg_rec* __restrict__ mrec) {
   const BankView bv = bank_view(bank);
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (blockIdx.x == 0)  // the one-sweep sort's digit totals and partition counters (k_os_hist adds to them)
-    for (int z = threadIdx.x; z < nzero; z += 256) zero[z] = 0;
   const int ntot = b.sel_dev ? b.n_sel : b.n;
   const bool valid = i < ntot;
   const int msg = valid ? (b.sel_dev ? b.sel_dev[i] : i) : 0;
@@ -274,153 +271,6 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// One-sweep form of the same sort (13 launches per kind became 6).  k_os_hist counts
-// the four digits of every key at once (per partition in LDS, then one atomic per non-empty bin into
-// the global digit totals) and clears the partitions' status words; then one k_os_scatter per digit:
-// a workgroup takes the next partition from an atomic counter, publishes its digit counts as
-// (AGG | count) status words, looks back over the earlier partitions' words until one carries its
-// inclusive prefix (PRE | prefix), publishes its own prefix and scatters its elements stably.  The
-// status words are single atomic words at agent scope: no other data passes between workgroups of
-// one launch, so no fence is needed.  A workgroup only waits on partitions taken before its own,
-// which are resident and finish their publication without waiting on later ones; the look-back is
-// bounded all the same (OS_SPIN, seconds): a workgroup that ran out of it sets the workspace's error
-// word (a diagnostic; tests/test_gpu_parity.py checks every grouped order is a permutation).
-// ---------------------------------------------------------------------------------------------
-#ifndef SDX_RS_ONESWEEP
-#define SDX_RS_ONESWEEP 0
-#endif
-constexpr uint32_t OS_AGG = 1u << 30, OS_PRE = 2u << 30, OS_VAL = (1u << 30) - 1;
-constexpr uint32_t OS_SPIN = 1u << 22;
-// global counters: [pass][256] digit totals, [pass] partition counters, 1 error word
-constexpr int OS_NZERO = 4 * 256 + 4 + 1;
-
-__global__ __launch_bounds__(RS_T) void k_os_hist(const uint32_t* __restrict__ key, int n, int np,
-                                                  uint32_t* __restrict__ ghist, uint32_t* __restrict__ status) {
-  __shared__ uint32_t c[4][256];
-  const int tid = threadIdx.x, p = blockIdx.x;
-  for (int x = tid; x < 4 * 256; x += RS_T) (&c[0][0])[x] = 0;
-  for (int d = 0; d < RS_PASSES; ++d)   // this partition's status words of every pass: not ready
-    for (int x = tid; x < 256; x += RS_T) status[((size_t)d * np + p) * 256 + x] = 0;
-  __syncthreads();
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const int e = p * RS_PART + r * RS_T + tid;
-    if (e < n) {
-      const uint32_t k = key[e];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) atomicAdd(&c[d][(k >> (8 * d)) & 255u], 1u);
-    }
-  }
-  __syncthreads();
-  for (int x = tid; x < 4 * 256; x += RS_T) {
-    const uint32_t v = (&c[0][0])[x];
-    if (v) atomicAdd(&ghist[x], v);
-  }
-}
-
-__global__ __launch_bounds__(RS_T) void k_os_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                     int n, int np, int d, const uint32_t* __restrict__ ghist,
-                                                     uint32_t* __restrict__ status, uint32_t* __restrict__ ctr,
-                                                     uint32_t* __restrict__ err, uint32_t* __restrict__ kout,
-                                                     uint32_t* __restrict__ vout) {
-  __shared__ uint32_t run[256];    // digit -> next output position of this partition's elements
-  __shared__ uint32_t cnt[256];    // this partition's digit counts
-  __shared__ uint32_t wc[RS_T / 64][256];
-  __shared__ int pid_s;
-  const int tid = threadIdx.x, wave = tid >> 6;
-  if (tid == 0) pid_s = (int)atomicAdd(ctr, 1u);
-  if (tid < 256) cnt[tid] = 0;
-  __syncthreads();
-  const int p = pid_s;
-  uint32_t k[RS_ROUNDS], v[RS_ROUNDS];
-#pragma unroll
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const int e = p * RS_PART + r * RS_T + tid;
-    k[r] = e < n ? kin[e] : 0u;
-    v[r] = e < n ? vin[e] : 0u;
-    if (e < n) atomicAdd(&cnt[(k[r] >> (8 * d)) & 255u], 1u);
-  }
-  __syncthreads();
-  uint32_t* st = status;   // this pass's [np][256] status words
-  if (tid < 256) {
-    const uint32_t mine = cnt[tid];
-    __hip_atomic_store(&st[(size_t)p * 256 + tid], (p == 0 ? OS_PRE : OS_AGG) | mine, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t excl = 0;
-    bool ok = true;
-    for (int j = p - 1; j >= 0;) {   // look back until a partition that knows its inclusive prefix
-      uint32_t w = 0, spin = 0;
-      do {
-        w = __hip_atomic_load(&st[(size_t)j * 256 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } while ((w & ~OS_VAL) == 0 && ++spin < OS_SPIN);
-      if ((w & ~OS_VAL) == 0) {
-        ok = false;
-        break;
-      }
-      excl += w & OS_VAL;
-      if (w & OS_PRE) break;
-      --j;
-    }
-    if (!ok) atomicOr(err, 1u);
-    if (p > 0)
-      __hip_atomic_store(&st[(size_t)p * 256 + tid], OS_PRE | (excl + mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    run[tid] = excl;
-  }
-  // + the digit's global base: exclusive prefix of this pass's digit totals (wave 0, 4 per lane)
-  const int lane = tid & 63;
-  uint32_t g[4] = {0, 0, 0, 0}, base = 0;
-  if (wave == 0) {
-    const uint32_t* gh = ghist + d * 256;
-    uint32_t t = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      g[q] = gh[4 * lane + q];
-      t += g[q];
-    }
-    uint32_t x = t;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    base = x - t;
-  }
-  __syncthreads();   // run[] written by the look-back threads (waves 0-3)
-  if (wave == 0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      run[4 * lane + q] += base;
-      base += g[q];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const int e = p * RS_PART + r * RS_T + tid;
-    const bool valid = e < n;
-    const uint32_t dig = (k[r] >> (8 * d)) & 255u;
-    for (int x = tid; x < RS_T / 64 * 256; x += RS_T) (&wc[0][0])[x] = 0;
-    __syncthreads();
-    const uint64_t peers = peers8(dig, valid);
-    if (valid && lane_id() == ffs64(peers)) wc[wave][dig] = (uint32_t)popc64(peers);
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = run[dig] + (uint32_t)lanes_below_mask(peers);
-      for (int w = 0; w < wave; ++w) pos += wc[w][dig];
-      kout[pos] = k[r];
-      vout[pos] = v[r];
-    }
-    __syncthreads();
-    if (tid < 256) {
-      uint32_t add = 0;
-#pragma unroll
-      for (int w = 0; w < RS_T / 64; ++w) add += wc[w][tid];
-      run[tid] += add;
-    }
-    __syncthreads();
-  }
-}
-
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // workspace of the grouping: keys and message indices (two copies; the sorted indices end in the
@@ -428,9 +278,7 @@ constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t group_bytes(int n) {
   if (n <= 0) return 0;
   const size_t np = (size_t)(n + RS_PART - 1) / RS_PART;
-  // keys / indices x2, the per-partition digit rows (LSD: hist; one-sweep: status words of every
-  // pass), the digit totals + counters
-  return 4 * align256(4 * (size_t)n) + align256(4 * 256 * np * RS_PASSES) + align256(4 * (size_t)OS_NZERO);
+  return 4 * align256(4 * (size_t)n) + align256(4 * 256 * np) + align256(4 * 256);
 }
 
 // The grouped order of a batch's messages (or of its sel_dev subset): order[0, n) = message indices
@@ -447,27 +295,12 @@ bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, in
   uint32_t* k1 = reinterpret_cast<uint32_t*>(work + 2 * a);
   uint32_t* v1 = reinterpret_cast<uint32_t*>(work + 3 * a);
   uint32_t* hist = reinterpret_cast<uint32_t*>(work + 4 * a);
-  uint32_t* tot = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)np * RS_PASSES));
+  uint32_t* tot = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)np));
   const int grid = (n + 255) / 256;
-  // one-sweep counters: [4][256] digit totals, [4] partition counters, 1 error word (zeroed by k_sig)
-  uint32_t* ghist = tot;
-  uint32_t* ctr = tot + 4 * 256;
-  uint32_t* err = ctr + 4;
   if (kind == SDX_KIND_MU)
-    hipLaunchKernelGGL((k_sig<SDX_KIND_MU>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec, tot, OS_NZERO);
+    hipLaunchKernelGGL((k_sig<SDX_KIND_MU>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec);
   else
-    hipLaunchKernelGGL((k_sig<SDX_KIND_MS>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec, tot, OS_NZERO);
-  if (SDX_RS_ONESWEEP) {
-    hipLaunchKernelGGL(k_os_hist, dim3(np), dim3(RS_T), 0, st, k0, n, np, ghist, hist);
-    for (int pi = 0; pi < RS_PASSES; ++pi) {
-      const int d = 4 - RS_PASSES + pi;
-      const bool even = (pi & 1) == 0;
-      uint32_t* vout = pi == RS_PASSES - 1 ? reinterpret_cast<uint32_t*>(order) : (even ? v1 : v0);
-      hipLaunchKernelGGL(k_os_scatter, dim3(np), dim3(RS_T), 0, st, even ? k0 : k1, even ? v0 : v1, n, np, d, ghist,
-                         hist + (size_t)pi * np * 256, ctr + pi, err, even ? k1 : k0, vout);
-    }
-    return hipGetLastError() == hipSuccess;
-  }
+    hipLaunchKernelGGL((k_sig<SDX_KIND_MS>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec);
   // the key's top RS_PASSES bytes (LSD order): (k0, v0) -> (k1, v1) -> (k0, v0) -> ..., the last
   // pass writing the message indices to order
   for (int pi = 0; pi < RS_PASSES; ++pi) {

@@ -58,10 +58,6 @@ __device__ unsigned long long g_gprof[2][128];  // per MU clock group / MS proto
 #define PROF_CNTL(slot)
 #endif
 
-#ifndef SDX_MS_PREFILTER
-#define SDX_MS_PREFILTER 0
-#endif
-
 namespace sdx {
 
 constexpr int POOL_REC = 640;    // MU/MS: staged results per tile (shared by the 4 waves)
@@ -187,7 +183,6 @@ struct TileLds {
   uint32_t spill_base, sp_rec, sp_heap;  // the tile's spill region (SPILL_NONE: none yet) and its fill
   int ovf, next_p;
   int mm_states, nmatch;
-  uint64_t pact[2];  // MS: processing-order positions that some message of the tile can pass (prefilter)
   MuMatch mlist[LM == 1 ? MATCH_CAP : 1];
   alignas(16) sdx_mu_desc desc[LM == 1 ? SDX_MUDESC_LDS : 1];
   // the decode queues live only during the protocol loop, the modulematch tables only in the
@@ -1559,7 +1554,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     L.sp_heap = 0;
     L.ovf = 0;
     L.nsurv = 0;
-    L.pact[0] = L.pact[1] = 0;
   }
   if constexpr (LANE_MU) {  // MU decode descriptors + modulematch tables -> LDS (16-B pieces)
     const int ndesc = (int)bv.hdr->n_mu < SDX_MUDESC_LDS ? (int)bv.hdr->n_mu : SDX_MUDESC_LDS;
@@ -1940,73 +1934,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     wave_sync();
   };
   // MU: a wave takes a whole clock group (one normalisation per group); MS: one protocol
-  int ngrab = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu_groups : nproto;
+  const int ngrab = KIND == SDX_KIND_MU ? (int)bv.hdr->n_mu_groups : nproto;
   const uint16_t* gstart = bv.order + bv.hdr->n_mu + bv.hdr->n_ms;
-  // MS tile prefilter: the protocols no message of the tile can pass -- the clock gate
-  // (message_synced.py:83-88) and the candidate test of the sync list (pattern_utils.py:53-80, a
-  // necessary condition of its pattern_exists, :128) -- are dropped before the loop.  The grab of such
-  // a protocol cost a wave a whole chain of dependent loads (LDS counter, order, record) for nothing:
-  // 4-7k wave-cycles each, about 48 of the 66 per tile on the bench corpus.  Here every wave tests its
-  // share of the positions with independent loads, and the loop grabs only the marked ones.
-  uint64_t pact0 = ~0ull, pact1 = ~0ull;
-  bool use_pact = false;
-  if constexpr (LANE_MS && SDX_MS_PREFILTER) {
-    if (nproto <= 128) {
-      use_pact = true;
-      for (int i = wave; i < nproto; i += NWAVE) {
-        const int pp = cld(&order[i]);
-        const sdx_ms_filt* fq = uniform_ptr(bv.msfilt + pp);
-        const uint32_t fq_ff = cld(&fq->flags);
-        const double fq_clk = cld(&fq->pclock);
-        const int fq_kl = (int)((cld(&fq->spec[0].rk2_len_nu) >> 16) & 0xFF);
-        bool pass = lane_ok && !(fq_ff & 2u);
-        if (fq_clk > 0.0) pass = pass && !(fabs(fq_clk - clock) > clock * 0.3);
-        if (fq_kl) {
-          const SpecV sv = (fq_ff & 8u) ? spec_full(&bv.ms[pp].key[0]) : spec_compact(&fq->spec[0], cld(&fq->sync_upk));
-#pragma unroll
-          for (int u = 0; u < SDX_MAXUNIQ; ++u) {
-            if (u < sv.nu) {
-              bool any = false;
-#pragma unroll
-              for (int j = 0; j < SDX_MAXPAT; ++j) any |= k_in(kq[j], sv.klo[u], sv.khi[u]);
-              pass = pass && any;
-            }
-          }
-        }
-        if (ballot(pass) != 0 && lane == 0) atomicOr(&L.pact[i >> 6], 1ull << (i & 63));
-      }
-      __syncthreads();
-      pact0 = __builtin_amdgcn_readfirstlane(L.pact[0] & 0xFFFFFFFFull) |
-              ((uint64_t)__builtin_amdgcn_readfirstlane(L.pact[0] >> 32) << 32);
-      pact1 = __builtin_amdgcn_readfirstlane(L.pact[1] & 0xFFFFFFFFull) |
-              ((uint64_t)__builtin_amdgcn_readfirstlane(L.pact[1] >> 32) << 32);
-      ngrab = popc64(pact0) + popc64(pact1);
-    }
-  }
-  // the g-th marked position (wave-uniform scalar code)
-  auto nth_active = [&](int g) -> int {
-    uint64_t w = pact0;
-    int base = 0;
-    const int c0 = popc64(pact0);
-    if (g >= c0) {
-      g -= c0;
-      w = pact1;
-      base = 64;
-    }
-#pragma unroll
-    for (int sh = 32; sh; sh >>= 1) {
-      const uint64_t lo = w & ((1ull << sh) - 1);
-      const int c = popc64(lo);
-      if (g >= c) {
-        g -= c;
-        w >>= sh;
-        base += sh;
-      } else {
-        w = lo;
-      }
-    }
-    return base;
-  };
   int cur = 0, cend = 0;
 #ifdef SDX_PROF
   int g_cur = -1;
@@ -2030,8 +1959,8 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
         cur = cld(&gstart[g]);
         cend = cld(&gstart[g + 1]);
       } else {
-        cur = use_pact ? nth_active(g) : g;
-        cend = cur + 1;
+        cur = g;
+        cend = g + 1;
       }
     }
     const int p = cld(&order[cur]);
@@ -2362,7 +2291,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
 #ifndef SDX_MC_WPE
 #define SDX_MC_WPE 4
 #endif
-constexpr int MC_REC_CAP = SDX_MC_REC_CAP, MC_HEAP_CAP = SDX_MC_HEAP_CAP;  // per wave: k_mc<4> fits 4 workgroups per CU
+// per wave: k_mc<4> fits 4 workgroups per CU (5 waves/SIMD with 96 / 2560 measured no faster:
+// profiles/r05/dropped/time_mc5_*.log)
+constexpr int MC_REC_CAP = SDX_MC_REC_CAP, MC_HEAP_CAP = SDX_MC_HEAP_CAP;
 
 template <int MW>
 struct McLds {
