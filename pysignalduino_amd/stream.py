@@ -285,7 +285,7 @@ class LineStream:
         start = np.concatenate([[0], np.cumsum(cnt)])
         lb, n = s.lb, s.n
         sels = [lb.sel[int(start[i]): int(start[i + 1])] for i in range(runtime.SEL_NCLASS)]
-        sd = sds[s.cid % 2]
+        sd = self.sds[s.cid % 2]
         with t.cuda.stream(sd):
             sd.wait_event(s.parse_ev)
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
