@@ -180,6 +180,12 @@ int sdx_layout_size(int which);
  * hipMemsetAsync): the streaming pipeline's per-chunk H2D / D2H transfers and buffer resets, without a
  * framework's per-call dispatch.  Host buffers must be pinned for the copy to be asynchronous. */
 int sdx_copy_async(void* dst, const void* src, size_t nbytes, void* hip_stream);
+/* the same with the direction given (a hipMemcpyKind: 1 host->device, 2 device->host, 3 device->device,
+ * 4 inferred as sdx_copy_async does): the HIP runtime picks its copy engine by it */
+int sdx_copy_async_kind(void* dst, const void* src, size_t nbytes, int kind, void* hip_stream);
+/* a device -> pinned-host (or any device-accessible) copy by a kernel of nwg 256-thread workgroups:
+ * occupies nwg CU slots for the transfer instead of the runtime's blit kernel on every CU */
+int sdx_copy_async_narrow(void* dst, const void* src, size_t nbytes, int nwg, void* hip_stream);
 int sdx_fill_async(void* dst, int value, size_t nbytes, void* hip_stream);
 
 /* bank: compiled by pysignalduino_amd/bank.py (protocols.json -> blob) and uploaded once per device */

@@ -2281,6 +2281,31 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
 #endif
 }
 
+// A copy on a few workgroups (sdx_copy_async_narrow): the streaming front end's device -> pinned-host
+// result copies.  hipMemcpyAsync ran them as a blit kernel of 256 workgroups that held a slot on every CU
+// for the whole PCIe transfer (0.4 ms per 500k-line chunk), beside the next chunks' demodulation
+// tiles; this one holds nwg slots.  16-byte pieces when both ends are 16-byte aligned, bytes otherwise.
+__global__ __launch_bounds__(256) void k_copy_narrow(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, size_t n) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
+  size_t done = 0;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15u) == 0) {
+    const size_t n16 = n >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (size_t i = t; i < n16; i += 4 * nt) {  // four 16-byte pieces in flight per thread
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + u * nt < n16) v[u] = s4[i + u * nt];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + u * nt < n16) d4[i + u * nt] = v[u];
+    }
+    done = n16 << 4;
+  }
+  for (size_t i = done + t; i < n; i += nt) dst[i] = src[i];
+}
+
 // =============================================================================================
 // MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
 // =============================================================================================
@@ -2738,6 +2763,24 @@ int sdx_copy_async(void* dst, const void* src, size_t nbytes, void* hip_stream) 
   if (!nbytes) return SDX_OK;
   if (!dst || !src) return fail(SDX_EINVAL, "sdx_copy_async: null pointer");
   HIPCHK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, (hipStream_t)hip_stream));
+  return SDX_OK;
+}
+
+int sdx_copy_async_kind(void* dst, const void* src, size_t nbytes, int kind, void* hip_stream) {
+  if (!nbytes) return SDX_OK;
+  if (!dst || !src) return fail(SDX_EINVAL, "sdx_copy_async_kind: null pointer");
+  if (kind < 0 || kind > 4) return fail(SDX_EINVAL, "sdx_copy_async_kind: kind must be a hipMemcpyKind (0-4)");
+  HIPCHK(hipMemcpyAsync(dst, src, nbytes, (hipMemcpyKind)kind, (hipStream_t)hip_stream));
+  return SDX_OK;
+}
+
+int sdx_copy_async_narrow(void* dst, const void* src, size_t nbytes, int nwg, void* hip_stream) {
+  if (!nbytes) return SDX_OK;
+  if (!dst || !src) return fail(SDX_EINVAL, "sdx_copy_async_narrow: null pointer");
+  if (nwg < 1 || nwg > 1024) return fail(SDX_EINVAL, "sdx_copy_async_narrow: 1..1024 workgroups");
+  hipLaunchKernelGGL(sdx::k_copy_narrow, dim3(nwg), dim3(256), 0, (hipStream_t)hip_stream, (uint8_t*)dst,
+                     (const uint8_t*)src, nbytes);
+  HIPCHK(hipGetLastError());
   return SDX_OK;
 }
 

@@ -45,8 +45,9 @@ EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_source_hash", "sdx_layout_
             "sdx_exchange_work_bytes", "sdx_exchange_send_bytes", "sdx_exchange_count", "sdx_exchange_pack", "sdx_exchange_pack_into", "sdx_exchange_unpack_work_bytes",
             "sdx_exchange_unpack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
             "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general",
-            "sdx_lines_general", "sdx_copy_async", "sdx_fill_async"]
-GROUP_MIN = 4096   # SDX_GROUP_MIN
+            "sdx_lines_general", "sdx_copy_async", "sdx_copy_async_kind", "sdx_copy_async_narrow",
+            "sdx_fill_async"]
+GROUP_MIN = int(os.environ.get("SDX_GROUP_MIN", "4096"))   # SDX_GROUP_MIN (the env: A/B of the grouping)
 
 
 class SdxPulseBatch(Structure):
@@ -163,6 +164,10 @@ def load_library(path: Optional[str] = None):
     lib.sdx_layout_size.restype = c_int
     lib.sdx_copy_async.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p]
     lib.sdx_copy_async.restype = c_int
+    lib.sdx_copy_async_kind.argtypes = [c_void_p, c_void_p, c_size_t, c_int, c_void_p]
+    lib.sdx_copy_async_kind.restype = c_int
+    lib.sdx_copy_async_narrow.argtypes = [c_void_p, c_void_p, c_size_t, c_int, c_void_p]
+    lib.sdx_copy_async_narrow.restype = c_int
     lib.sdx_fill_async.argtypes = [c_void_p, c_int, c_size_t, c_void_p]
     lib.sdx_fill_async.restype = c_int
     lib.sdx_bank_create.argtypes = [c_void_p, c_size_t, c_int, POINTER(c_void_p)]
@@ -260,7 +265,30 @@ def copy_async(dst, src, stream) -> None:
     if n != dst.numel() * dst.element_size() or not (dst.is_contiguous() and src.is_contiguous()):
         raise ValueError("copy_async: contiguous tensors of the same byte size")
     lib = load_library()
-    _check(lib, lib.sdx_copy_async(dst.data_ptr(), src.data_ptr(), n, stream.cuda_stream))
+    if _COPY_DEFAULT:
+        _check(lib, lib.sdx_copy_async(dst.data_ptr(), src.data_ptr(), n, stream.cuda_stream))
+        return
+    # the direction named explicitly (hipMemcpyKind): with hipMemcpyDefault the runtime ran the
+    # device -> pinned-host copies as blit kernels on every CU (__amd_rocclr_copyBuffer, 256 workgroups
+    # held for the PCIe transfer), beside the next chunks' demodulation tiles
+    kind = (3 if src.is_cuda else 1) if dst.is_cuda else (2 if src.is_cuda else 0)
+    _check(lib, lib.sdx_copy_async_kind(dst.data_ptr(), src.data_ptr(), n, kind, stream.cuda_stream))
+
+
+_COPY_DEFAULT = os.environ.get("SDX_COPY_DEFAULT") == "1"   # A/B: every copy with hipMemcpyDefault
+D2H_NARROW_WG = int(os.environ.get("SDX_D2H_WG", "16"))      # copy_d2h's workgroups (0: hipMemcpyAsync)
+
+
+def copy_d2h(dst, src, stream) -> None:
+    """A device -> pinned-host copy that occupies few CUs (sdx_copy_async_narrow, D2H_NARROW_WG
+    workgroups): for result copies that run beside demodulation kernels."""
+    if D2H_NARROW_WG <= 0 or not dst.is_pinned():
+        return copy_async(dst, src, stream)
+    n = src.numel() * src.element_size()
+    if n != dst.numel() * dst.element_size() or not (dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("copy_d2h: contiguous tensors of the same byte size")
+    lib = load_library()
+    _check(lib, lib.sdx_copy_async_narrow(dst.data_ptr(), src.data_ptr(), n, D2H_NARROW_WG, stream.cuda_stream))
 
 
 def fill_async(dst, stream, value: int = 0) -> None:

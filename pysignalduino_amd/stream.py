@@ -169,7 +169,12 @@ class LineStream:
         self.lag = max(1, int(lag))
         self.slots = [_Slot(self) for _ in range(self.lag + 1)]
         dev = self.eng.dev
-        self.cin, self.sp, self.cout = (torch.cuda.Stream(dev) for _ in range(3))
+        # the parse at the highest priority: the host waits for chunk k's class counts before it can
+        # enqueue chunk k's demodulation, and a parse queued behind the previous chunks' demodulation
+        # tiles got CUs only as those drained -- the chunks' kernels then ran one after another
+        lo_prio, hi_prio = torch.cuda.Stream.priority_range()
+        self.cin, self.cout = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        self.sp = torch.cuda.Stream(dev, priority=hi_prio)
         # two demodulation streams, chunk k on sds[k % 2]: every buffer a chunk's stage B touches is
         # its slot's own, so chunk k+1's launches may run beside chunk k's (one stream
         # serialised the chunks' kernels and each chunk's tail idled the CUs)
@@ -355,7 +360,7 @@ class LineStream:
                 T = int(min(hs[0], s.jcap))
                 s.ovf_json = bool(hs[1])
                 s.dcur = hs[2:].reshape(k, 4)
-                runtime.copy_async(ho[:T], s.jout["json"][:T], self.cout)
+                runtime.copy_d2h(ho[:T], s.jout["json"][:T], self.cout)
                 a = (T + 3) & ~3
                 runtime.copy_async(ho[a: a + 4 * n], s.jout["off"][:n], self.cout)
                 runtime.copy_async(ho[a + 4 * n: a + 8 * n], s.jout["len"][:n], self.cout)
@@ -367,7 +372,7 @@ class LineStream:
                 s.dcur = hs[runtime.XCHG_COUNTS * k:].reshape(k, 4)
                 s.S = S
                 offs, nb, T = sdist._layout(S)
-                runtime.copy_async(ho[:T], s.ser._bufs["send"][:T], self.cout)
+                runtime.copy_d2h(ho[:T], s.ser._bufs["send"][:T], self.cout)
                 b = T
                 s.lay = (offs, nb, T)
             runtime.copy_async(ho[b: b + n], lb.kind[:n], self.cout)
