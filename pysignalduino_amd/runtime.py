@@ -276,7 +276,9 @@ def copy_async(dst, src, stream) -> None:
 
 
 _COPY_DEFAULT = os.environ.get("SDX_COPY_DEFAULT") == "1"   # A/B: every copy with hipMemcpyDefault
-D2H_NARROW_WG = int(os.environ.get("SDX_D2H_WG", "16"))      # copy_d2h's workgroups (0: hipMemcpyAsync)
+# copy_d2h's workgroups; 0 (default): hipMemcpyAsync.  16 narrow workgroups measured no faster in the
+# streaming front end (profiles/r05/stream/r05k_*: 207 vs 212M lines/s, 64: 178M)
+D2H_NARROW_WG = int(os.environ.get("SDX_D2H_WG", "0"))
 
 
 def copy_d2h(dst, src, stream) -> None:

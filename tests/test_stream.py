@@ -157,3 +157,24 @@ def test_copy_and_fill_async_on_a_stream():
     assert np.array_equal(back.numpy(), want)
     with pytest.raises(ValueError):
         runtime.copy_async(back[:10], dev[:11], st)
+
+
+@pytest.mark.parametrize("wg", [1, 16])
+def test_narrow_device_to_host_copy(wg):
+    """sdx_copy_async_narrow (the few-workgroup device -> pinned-host copy of the streaming output):
+    16-byte aligned and unaligned ends, a tail of odd length, and a zero-byte copy."""
+    import torch
+    from pysignalduino_amd import runtime
+    lib = runtime.load_library()
+    st = torch.cuda.Stream()
+    rng = np.random.default_rng(4)
+    src = torch.from_numpy(rng.integers(0, 256, 300_017, dtype=np.uint8)).cuda()
+    for a, b, n in ((0, 0, 300_000), (3, 0, 299_990), (0, 5, 123_457), (16, 32, 17)):
+        back = torch.zeros(300_064, dtype=torch.uint8).pin_memory()
+        runtime._check(lib, lib.sdx_copy_async_narrow(back.data_ptr() + b, src.data_ptr() + a, n, wg, st.cuda_stream))
+        st.synchronize()
+        h = back.numpy()
+        assert np.array_equal(h[b: b + n], src.cpu().numpy()[a: a + n]), (a, b, n)
+        assert not h[:b].any() and not h[b + n:].any()
+    runtime._check(lib, lib.sdx_copy_async_narrow(back.data_ptr(), src.data_ptr(), 0, wg, st.cuda_stream))
+    assert lib.sdx_copy_async_narrow(back.data_ptr(), src.data_ptr(), 8, 0, st.cuda_stream) < 0
