@@ -58,6 +58,10 @@ __device__ unsigned long long g_gprof[2][128];  // per MU clock group / MS proto
 #define PROF_CNTL(slot)
 #endif
 
+#ifndef SDX_NO_RAISE_CHECK
+#define SDX_NO_RAISE_CHECK 1
+#endif
+
 namespace sdx {
 
 constexpr int POOL_REC = 640;    // MU/MS: staged results per tile (shared by the 4 waves)
@@ -1971,7 +1975,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const uint32_t ff = cld(&fr->flags);
       if ((ff & 2u) || !(ff & 4u)) continue;  // never / not active
       const bool full = (ff & 8u) != 0;
-      bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
+      // (a raise of this message in an earlier protocol: the flush drops all its results anyway, so
+      // the test only saves work; SDX_NO_RAISE_CHECK A/B)
+      bool alive = lane_ok && (SDX_NO_RAISE_CHECK || (L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
       int idx = 0;
       uint64_t st_tgt = 0, ut0 = 0, ut1 = 0, ut2 = 0;
       int fmask = 0;
@@ -1995,6 +2001,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           for (int k = 0; k < SDX_MAXPAT; ++k) {
             if (k < npat) {
               const bool slow = !ivalid || ((slowm >> k) & 1u);
+              const bool negk = ((negm >> k) & 1u) != 0;
               int kk = 0;
               if (!slow) {
                 const uint32_t x = xk[k];
@@ -2002,7 +2009,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
                 const int d2 = 2 * (int)(x - q * cc) - (int)cc;
                 kk = (int)q + (d2 > 0 ? 1 : 0);
                 if (d2 == 0) kk = py_round1_k((double)(2 * q + 1) / 20.0);  // exact rational tie
-                if ((((negm >> k) & 1u) != 0) != cneg) kk = -kk;
+                if (negk != cneg) kk = -kk;
               }
               if (slow) kk = py_round1_k(b.pat_val_dev[msg_of[mi] * SDX_MAXPAT + k] / pclk);
               kq[k] = kk;
@@ -2089,7 +2096,9 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
       const uint32_t ff = cld(&fr->flags);
       if (ff & 2u) continue;  // never
       const bool full = (ff & 8u) != 0;
-      bool alive = lane_ok && ((L.raise_key[mi] >> 8) > (uint32_t)p || L.raise_key[mi] == 0xFFFFFFFFu);
+      // the lane variant decodes after the loop, so no message of the tile has raised yet here
+      bool alive = lane_ok && ((LANE_MS && SDX_NO_RAISE_CHECK) || (L.raise_key[mi] >> 8) > (uint32_t)p ||
+                               L.raise_key[mi] == 0xFFFFFFFFu);
       const double pclk = cld(&fr->pclock);
       if (alive && pclk > 0.0)  // clock tolerance gate (:83-88)
         alive = !(fabs(pclk - clock) > clock * 0.3);
