@@ -468,7 +468,7 @@ def main():
                                                     (8 + 1 + 10 + 80 + (2 if dom == "MS" else 0)))
               + n * runtime.DESC_DT.itemsize + int(cur[0]) * RES_DT.itemsize + int(cur[1]) + len(bk.blob))
     achieved = alg / kt[dom]
-    traffic = issue = None
+    traffic = issue = traffic_src = None
     tag = f"k_pulses<{dom}>" if dom != "MC" else "k_mc"
     tpath = latest_pmc()
     if tpath and args.corpus == "bench":
@@ -478,6 +478,10 @@ def main():
         if cfg.get("msgs_per_gpu") == args.msgs and cfg.get("kind", "mixed") == args.kind and \
                 tj.get(tag, {}).get("traffic_bytes"):
             traffic = float(tj[tag]["traffic_bytes"])
+            traffic_src = {"pmc": os.path.relpath(tpath, REPO), "fetch_bytes": 2 * 1024 * float(tj[tag]["fetch_size_kib"]),
+                           "write_bytes": 1024 * float(tj[tag]["write_size_kib"]),
+                           "calibration": "profiles/r05/calib/calib_traffic.json (FETCH_SIZE x 2 holds for every "
+                                          "vector load width this kernel uses; scalar loads count exactly)"}
             issue = issue_view(tj[tag], kt[dom])
     wl = {"mixed": "mixed MU/MS/MC stream, 1/3 each per rank: MU 256-pulse messages x 129-id MU bank, MS sync+bits x "
                    "66-id MS bank (clock x U(0.6,1.4)), MC frames x 12 clockrange ids ('fixed' chain)",
@@ -503,7 +507,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": tag,
                      "alg_bytes_per_launch": alg, "layout_bytes_per_launch": layout,
-                     "results_per_launch": int(cur[0]), "issue": issue, "per_kernel": kernels},
+                     "results_per_launch": int(cur[0]), "issue": issue, "traffic_source": traffic_src,
+                     "per_kernel": kernels},
     }
     if exch is not None and exch.bytes_sent:
         nb = exch.bytes_sent[-args.steps:]

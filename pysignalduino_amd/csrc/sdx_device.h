@@ -14,6 +14,13 @@
 
 #define SDX_DEV __device__ __forceinline__
 
+// MS tiles of short messages on the NW = SDX_MS_NARROW_W instantiation of k_pulses (sdx_kernels.hip
+// sdx_demod_pulses; the MS grouping key's top bit separates them, sdx_group.hip k_sig)
+#ifndef SDX_MS_NARROW
+#define SDX_MS_NARROW 1
+#endif
+#define SDX_MS_NARROW_W 2
+
 namespace sdx {
 
 constexpr int WAVE = 64;

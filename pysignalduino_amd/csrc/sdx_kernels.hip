@@ -1526,8 +1526,11 @@ template <int KIND, int NW>
 constexpr int pulses_min_blocks() { return NW <= 4 ? 16 / LANE_WAVES : 1; }
 
 // MR = 1: the short variant reads its header fields from the message records (b.mrec_dev); a
-// separate instantiation, so the default one carries no trace of that path
-template <int KIND, int NW, int TM, int MR = 0>
+// separate instantiation, so the default one carries no trace of that path.
+// SPLIT (MS, two launches over the same tiles): 1 = this NW = 2 launch takes the tiles whose messages
+// all have <= 128 pulses, 2 = this NW = 4 launch takes the others; a tile that is not its launch's
+// returns before it touches anything (a block-uniform test on the tile's lengths)
+template <int KIND, int NW, int TM, int MR = 0, int SPLIT = 0>
 __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
     (NW <= 4 ? 4 : 1)))) void k_pulses(
     const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
@@ -1544,6 +1547,17 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   if (tid == 0 && blockIdx.x < 65536) g_wgt[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
   __shared__ int msg_of[TM];
+  if constexpr (SPLIT != 0) {
+    bool longm = false;
+    if (tid < nvalid) {
+      const int msg = b.sel_dev ? b.sel_dev[tile0 + tid] : tile0 + tid;
+      const int64_t o = b.offsets_dev[msg];
+      const int len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - o);
+      longm = len > 64 * SDX_MS_NARROW_W;
+    }
+    const bool any_long = __syncthreads_or(longm) != 0;
+    if (SPLIT == 1 ? any_long : !any_long) return;
+  }
   if (tid < TM) {
     msg_of[tid] = (tid < nvalid) ? (b.sel_dev ? b.sel_dev[tile0 + tid] : tile0 + tid) : 0;
     L.raise_key[tid] = 0xFFFFFFFFu;
@@ -1597,9 +1611,10 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   int64_t pf_off = 0;
   int pf_n = 0;
   // SWAR staging (short variants): 16 characters per lane, 4 messages per pass over the wave
-  constexpr int SMSG = 64 / 16;                    // messages per pass
+  constexpr int LPM = NW <= 4 ? 4 * NW : 16;        // lanes per message (16 characters each)
+  constexpr int SMSG = 64 / LPM;                    // messages per pass
   constexpr int SPASS = (MPW + SMSG - 1) / SMSG;   // passes per wave
-  static_assert(NW > 4 || NW == 4, "SWAR staging: 256-character rows, 16 lanes per message");
+  static_assert(NW > 4 || NW == 4 || NW == 2, "SWAR staging: 128- or 256-character rows");
   uint32_t sx[NW <= 4 ? SPASS : 1][5];
   if constexpr (NW <= 4) {
     // every header load of the tile is issued before any of them is used: the data offsets of the
@@ -1686,11 +1701,11 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     // byte of the message cannot cross a page, so the loads past the message end stay in bounds)
 #pragma unroll
     for (int ps = 0; ps < SPASS; ++ps) {
-      const int k = ps * SMSG + (lane >> 4);
+      const int k = ps * SMSG + lane / LPM;
       const int lo = __shfl((int)(uint32_t)pf_off, k), hi = __shfl((int)(uint32_t)((uint64_t)pf_off >> 32), k);
       const int64_t off = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
       const int n = __shfl(pf_n, k);
-      const int64_t base = off + 16 * (lane & 15);
+      const int64_t base = off + 16 * (lane % LPM);
       const int64_t a = base & ~(int64_t)3;
       const bool on = wave + k * NWAVE < nvalid;
       const uint32_t* src = reinterpret_cast<const uint32_t*>(b.data_dev + a);
@@ -1705,7 +1720,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   uint32_t ndmsg = 0;  // bit k: tile message k of the wave holds a non-digit character
 #pragma unroll
   for (int ps = 0; ps < SPASS; ++ps) {
-    const int k = ps * SMSG + (lane >> 4), j = lane & 15;
+    const int k = ps * SMSG + lane / LPM, j = lane % LPM;
     const int mi = wave + k * NWAVE;
     const int n = __shfl(pf_n, k);
     const int lo = __shfl((int)(uint32_t)pf_off, k);
@@ -1737,7 +1752,7 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
     const uint64_t ndb = ballot(nondigit);
 #pragma unroll
     for (int g = 0; g < SMSG; ++g)
-      if ((ndb >> (16 * g)) & 0xFFFFull) ndmsg |= 1u << (ps * SMSG + g);
+      if ((ndb >> (LPM * g)) & ((1ull << LPM) - 1)) ndmsg |= 1u << (ps * SMSG + g);
     if (mi < nvalid) {
       const uint32_t N0 = ~P0, N1 = ~P1, N2 = ~P2, N3 = ~P3;
       uint16_t* row = reinterpret_cast<uint16_t*>(&L.bm[mi * T::MSTRIDE + (j >> 2)]) + (j & 3);
@@ -2826,7 +2841,14 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
   else if (b.mrec_dev)
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
-  else
+  else if (SDX_MS_NARROW) {
+    // MS messages are mostly short (87 % of the bench corpus have <= 128 pulses): tiles whose
+    // messages all fit 2 words per id run the NW = 2 instantiation (half the bitmap words and mask
+    // arithmetic), the others the NW = 4 one; the grouping puts the long messages last (k_sig)
+    static_assert(sdx::pulses_threads<SDX_KIND_MS, SDX_MS_NARROW_W>() == sdx::pulses_threads<SDX_KIND_MS, 4>(), "block shape");
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, SDX_MS_NARROW_W, 64, 0, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 0, 2>), dim3(grid), blk, 0, st, bank->dev, b, o);
+  } else
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
   HIPCHK(hipGetLastError());
   return SDX_OK;
