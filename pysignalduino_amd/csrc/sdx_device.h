@@ -17,9 +17,8 @@
 // MS tiles of short messages on the NW = SDX_MS_NARROW_W instantiation of k_pulses (sdx_kernels.hip
 // sdx_demod_pulses; the MS grouping key's top bit separates them, sdx_group.hip k_sig)
 #ifndef SDX_MS_NARROW
-#define SDX_MS_NARROW 1
+#define SDX_MS_NARROW 1  /* MS length classes <= 128 / <= 256 pulses */
 #endif
-#define SDX_MS_NARROW_W 2
 
 namespace sdx {
 

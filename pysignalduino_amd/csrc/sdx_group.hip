@@ -166,13 +166,13 @@ __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_
 #elif SDX_MS_KEY == 3  // survivor count ascending, then signature
     const uint32_t ms_key = ((uint32_t)popc64(sig) << 26) | (sig >> 6);
 #else
-    // (SDX_MS_NARROW: the top bit = more than 64 * SDX_MS_NARROW_W pulses, so the tiles of short
-    // messages -- sdx_demod_pulses' narrow instantiation -- come first, the signature below it)
+    // (SDX_MS_NARROW: the top bit = the length class of sdx_demod_pulses' MS launches, more than 128
+    // pulses, so each class's tiles come together, the signature below it)
     uint32_t ms_key = sig;
     if (SDX_MS_NARROW) {
       const int64_t o = b.offsets_dev[msg];
       const int len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - o);
-      ms_key = ((len > 64 * SDX_MS_NARROW_W) ? 0x80000000u : 0u) | (sig >> 1);
+      ms_key = ((len > 128) ? 0x80000000u : 0u) | (sig >> 1);
     }
 #endif
     key[i] = KIND == SDX_KIND_MU ? ~sig : ms_key;

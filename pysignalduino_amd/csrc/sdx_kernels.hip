@@ -1527,9 +1527,9 @@ constexpr int pulses_min_blocks() { return NW <= 4 ? 16 / LANE_WAVES : 1; }
 
 // MR = 1: the short variant reads its header fields from the message records (b.mrec_dev); a
 // separate instantiation, so the default one carries no trace of that path.
-// SPLIT (MS, two launches over the same tiles): 1 = this NW = 2 launch takes the tiles whose messages
-// all have <= 128 pulses, 2 = this NW = 4 launch takes the others; a tile that is not its launch's
-// returns before it touches anything (a block-uniform test on the tile's lengths)
+// SPLIT (MS, one launch per length class over the same tiles): > 0 = this launch takes the tiles
+// whose longest message has more than 64 * (SPLIT - 1) and at most 64 * NW pulses; a tile that is not
+// its launch's returns before it touches anything (a block-uniform test on the tile's lengths)
 template <int KIND, int NW, int TM, int MR = 0, int SPLIT = 0>
 __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
     (NW <= 4 ? 4 : 1)))) void k_pulses(
@@ -1548,15 +1548,15 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
 #endif
   __shared__ int msg_of[TM];
   if constexpr (SPLIT != 0) {
-    bool longm = false;
+    int len = 0;
     if (tid < nvalid) {
       const int msg = b.sel_dev ? b.sel_dev[tile0 + tid] : tile0 + tid;
       const int64_t o = b.offsets_dev[msg];
-      const int len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - o);
-      longm = len > 64 * SDX_MS_NARROW_W;
+      len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - o);
     }
-    const bool any_long = __syncthreads_or(longm) != 0;
-    if (SPLIT == 1 ? any_long : !any_long) return;
+    const bool above = __syncthreads_or(len > 64 * NW) != 0;           // another launch's (wider) tile
+    const bool below = SPLIT == 1 || __syncthreads_or(len > 64 * (SPLIT - 1)) != 0;
+    if (above || !below) return;
   }
   if (tid < TM) {
     msg_of[tid] = (tid < nvalid) ? (b.sel_dev ? b.sel_dev[tile0 + tid] : tile0 + tid) : 0;
@@ -2845,9 +2845,10 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
     // MS messages are mostly short (87 % of the bench corpus have <= 128 pulses): tiles whose
     // messages all fit 2 words per id run the NW = 2 instantiation (half the bitmap words and mask
     // arithmetic), the others the NW = 4 one; the grouping puts the long messages last (k_sig)
-    static_assert(sdx::pulses_threads<SDX_KIND_MS, SDX_MS_NARROW_W>() == sdx::pulses_threads<SDX_KIND_MS, 4>(), "block shape");
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, SDX_MS_NARROW_W, 64, 0, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 0, 2>), dim3(grid), blk, 0, st, bank->dev, b, o);
+    static_assert(sdx::pulses_threads<SDX_KIND_MS, 2>() == sdx::pulses_threads<SDX_KIND_MS, 4>(), "block shape");
+    // (an NW = 1 class for <= 64 pulses spilled thousands of VGPRs: not used)
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 2, 64, 0, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
+    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 0, 3>), dim3(grid), blk, 0, st, bank->dev, b, o);
   } else
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
   HIPCHK(hipGetLastError());
