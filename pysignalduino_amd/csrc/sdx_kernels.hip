@@ -58,9 +58,6 @@ __device__ unsigned long long g_gprof[2][128];  // per MU clock group / MS proto
 #define PROF_CNTL(slot)
 #endif
 
-#ifndef SDX_NORM_BL
-#define SDX_NORM_BL 0
-#endif
 #ifndef SDX_NO_RAISE_CHECK
 #define SDX_NO_RAISE_CHECK 1
 #endif
@@ -2015,40 +2012,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
           const uint32_t csh = cld(&fr->clk_sh);
           const uint32_t cc = cld(&fr->clk_c), cm = cld(&fr->clk_m), sh = csh & 0xFFu;
           const bool ivalid = (csh & 0x100u) != 0, cneg = (csh & 0x200u) != 0;
-#if SDX_NORM_BL
-          // straight-line integer form for every slot (xk = 0 past npat), the rare slots -- exact
-          // ties, the fp64 path -- fixed up behind one test
-          uint32_t rare = 0;
-#pragma unroll
-          for (int k = 0; k < SDX_MAXPAT; ++k) {
-            const bool in = k < npat;
-            const uint32_t x = xk[k];
-            const uint32_t q = (uint32_t)(((uint64_t)x * cm) >> sh);
-            const int d2 = 2 * (int)(x - q * cc) - (int)cc;
-            const int kk = (int)q + (d2 > 0 ? 1 : 0);
-            const bool flip = (((negm >> k) & 1u) != 0) != cneg;
-            if (in) kq[k] = flip ? -kk : kk;
-            const bool slow = !ivalid || ((slowm >> k) & 1u);
-            rare |= (in && (slow || d2 == 0)) ? (1u << k) : 0u;
-          }
-          if (rare) {
-#pragma unroll
-            for (int k = 0; k < SDX_MAXPAT; ++k) {
-              if ((rare >> k) & 1u) {
-                const bool slow = !ivalid || ((slowm >> k) & 1u);
-                int kk;
-                if (slow) {
-                  kk = py_round1_k(b.pat_val_dev[msg_of[mi] * SDX_MAXPAT + k] / pclk);
-                } else {
-                  const uint32_t q = (uint32_t)(((uint64_t)xk[k] * cm) >> sh);
-                  kk = py_round1_k((double)(2 * q + 1) / 20.0);  // exact rational tie
-                  if ((((negm >> k) & 1u) != 0) != cneg) kk = -kk;
-                }
-                kq[k] = kk;
-              }
-            }
-          }
-#else
 #pragma unroll
           for (int k = 0; k < SDX_MAXPAT; ++k) {
             if (k < npat) {
@@ -2067,7 +2030,6 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
               kq[k] = kk;
             }
           }
-#endif
         } else {
 #pragma unroll
           for (int k = 0; k < SDX_MAXPAT; ++k)
