@@ -89,6 +89,33 @@ def test_synthetic_vs_oracle(proto, obank, kind, seed, n):
     assert not bad, f"{len(bad)}/{n} mismatches; first: {bad[:2]}"
 
 
+@pytest.mark.parametrize("n", [6000, 900])
+def test_ms_length_classes_at_the_boundary_vs_oracle(proto, obank, n):
+    """sdx_demod_pulses runs MS as two launches by tile length class (<= 128 pulses on the NW = 2
+    instantiation, the rest on NW = 4): messages of 120..136 pulses around the
+    class boundary, mixed with the corpus' own lengths, grouped (n >= GROUP_MIN: the key's top bit
+    separates the classes) and ungrouped (n < GROUP_MIN: mixed tiles), equal the oracle message by
+    message."""
+    from pysignalduino_amd import synth
+    pb = synth.ms_corpus(proto.get_protocol_list(), n, seed=8800 + n)
+    msgs = [pb.to_msg_dict(i) for i in range(pb.n)]
+    rng = np.random.default_rng(n)
+    for i in rng.choice(n, n // 2, replace=False):
+        d = msgs[int(i)]["data"]
+        L = int(rng.integers(120, 137))
+        msgs[int(i)] = dict(msgs[int(i)], data=(d * (L // max(1, len(d)) + 1))[:L])
+    lens = np.array([len(m["data"]) for m in msgs])
+    assert (lens == 128).any() and (lens == 129).any()
+    got = proto.demodulate_batch(msgs, "MS")
+    bad = []
+    for i, (m, g) in enumerate(zip(msgs, got)):
+        exp = _oracle(obank, m, "MS")
+        if _flat(g) != exp:
+            bad.append((i, len(m["data"]), exp, _flat(g)))
+    assert not bad, f"{len(bad)}/{n} mismatches; first: {bad[:2]}"
+    assert sum(1 for g in got if isinstance(g, list) and g) > n // 10
+
+
 def test_mu_exact_rational_ties_vs_oracle(proto, obank):
     """MU pattern values planted on exact rational ties of the bank's clocks (10|P| = q c + c / 2):
     the device rounds those by fl((2q + 1) / 20) instead of reloading P (round 4); every message
