@@ -72,6 +72,11 @@ def parse():
                     help="exchange payloads raw (no nibble form: A/B of the wire size)")
     ap.add_argument("--scan-wire", action="store_true",
                     help="the exchange classifies every payload itself (no kernel-written counts, ABI 12: A/B)")
+    ap.add_argument("--no-fuse", dest="fuse", action="store_false",
+                    help="one launch per kind (MU, then MS beside MC) instead of the default ONE kernel for the "
+                         "step's MU, MS and MC tiles (sdx_demod_step, ABI 14, where each kind's tiles take the CU "
+                         "slots the previous kind's last tiles free: 603.0-603.7M vs 579.5-580.9M msgs/s, "
+                         "profiles/r05/fused/)")
     ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
                     help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
@@ -183,6 +188,31 @@ def alg_bytes(kind, bd, rec_np):
         inp = int(bd["lengths"].sum()) + 48 * n
     out = 16 * len(rec_np) + int(rec_np["payload_len"].astype(np.int64).sum())
     return inp + out + 16384
+
+
+def attribute_alone(torch, eng, stream, kinds, bds, outs, gbufs, corp, mrec_kinds, reps=5):
+    """--fuse: each kind's own kernel alone on the launch stream (after the timed loop, untimed), so
+    the line still carries MU's, MS's and MC's separate rooflines; returns {kind: seconds}."""
+    from pysignalduino_amd import runtime
+    res = {}
+    with torch.cuda.stream(stream):
+        for k in kinds:
+            ts = []
+            for _ in range(reps):
+                outs[k]["cursor"].zero_()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                if k == "MC":
+                    eng.launch_mc(bds[k], outs[k])
+                else:
+                    eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[k],
+                                      sel=gbufs[k][0][0][:corp[k].n], group=False,
+                                      mrec=gbufs[k][0][2] if k in mrec_kinds else None)
+                e1.record(stream)
+                stream.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e-3)
+            res[k] = float(np.median(ts))
+    return res
 
 
 def latest_pmc():
@@ -309,7 +339,9 @@ def main():
     kstream = {k: (torch.cuda.Stream(dev) if args.concurrent else stream) for k in kinds}
     # default: MU alone (the roofline kernel keeps an attributable duration), then MS and MC side by
     # side -- MC fills the CUs MS's tail leaves idle (482 vs 471M msgs/s serial, 20 steps)
-    mc_beside_ms = not args.serial and not args.concurrent and not args.mc_tail and "MC" in kinds and "MU" in kinds
+    mc_beside_ms = (not args.serial and not args.concurrent and not args.mc_tail and "MC" in kinds and "MU" in kinds
+                    and not (args.fuse and args.kind == "mixed" and not args.no_group and args.group_at == "mu"
+                             and not args.ms_with_mu))
     if mc_beside_ms:
         kstream["MC"] = torch.cuda.Stream(dev)   # (at the lowest priority: equal, profiles/r04/s3/dropped/mc_low_ab.log)
     if args.mc_tail and "MC" in kinds:
@@ -329,6 +361,10 @@ def main():
     assert sum(x.stop - x.start for x in own.values()) == len(kinds), "a stream's kinds are contiguous"
 
     mu_done = [None]
+    # the default mixed step runs as one k_step launch; the A/B modes (--serial, --concurrent, --mc-tail,
+    # --ms-with-mu, --group-at ms, --no-group) and the single-kind configs keep one launch per kind
+    fused = (args.fuse and kinds == ("MU", "MS", "MC") and bool(gkinds) and args.group_at == "mu" and not
+             (args.serial or args.concurrent or args.mc_tail or args.ms_with_mu))
 
     def step(j, si=None):
         s_ = j % nslot
@@ -355,7 +391,23 @@ def main():
         if need_start:
             start = torch.cuda.Event(enable_timing=tm)
             start.record(stream)            # cursors reset, previous exchange done
-        for k in kinds:
+        if fused:   # one k_step launch for the whole step (sdx_demod_step)
+            stream.wait_event(gdone[par])
+            e0 = None
+            if tm:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            parts = {}
+            for k in ("MU", "MS"):
+                parts[k.lower()] = (bds[k], outs[s_][k], gbufs[k][par][0][:corp[k].n],
+                                    gbufs[k][par][2] if k in mrec_kinds else None)
+            eng.launch_step(mu=parts["mu"], ms=parts["ms"], mc=(bds["MC"], outs[s_]["MC"], None))
+            e1 = torch.cuda.Event(enable_timing=tm)
+            e1.record(stream)
+            if tm:
+                kev[si]["step"] = (e0, e1)
+            mu_done[0] = last = e1
+        for k in (() if fused else kinds):
             ks = kstream[k]
             e0 = None
             if ks is not stream:
@@ -434,7 +486,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     ktimes = {k: [kev[si][k][0].elapsed_time(kev[si][k][1]) * 1e-3 for si in range(0, args.steps, args.kev_every)]
-              for k in kinds}
+              for k in (("step",) if fused else kinds)}
     gtime = float(np.mean([gev[si][0].elapsed_time(gev[si][1]) * 1e-3 for si in range(0, args.steps, args.kev_every)])) if gkinds else 0.0
     tt = torch.tensor([dt], dtype=torch.float64, device=dev)
     if dist_on:
@@ -445,6 +497,9 @@ def main():
 
     # roofline of the dominant kernel: SURVEY §8(d) algorithmic bytes / its HIP-event time
     kt = {k: float(np.mean(v)) for k, v in ktimes.items()}
+    if fused:   # each kind's kernel alone (untimed attribution pass): its own roofline entry
+        kt_step = kt["step"]
+        kt = attribute_alone(torch, eng, stream, kinds, bds, outs[(j - 1) % nslot], gbufs, corp, mrec_kinds)
     dom = max(kt, key=kt.get)
     # every kind's launch against the same HBM roofline: its algorithmic bytes (the
     # outputs of the last step) / its HIP-event time.  In the mixed step MS and MC run side by side
@@ -459,7 +514,15 @@ def main():
         ak = alg_bytes(k, bds[k], rk)
         kernels[k] = {"kernel": kern_tag[k], "alg_bytes_per_launch": ak, "results_per_launch": int(ck[0]),
                       "ms": 1e3 * kt[k], "achieved_GBps": ak / kt[k] / 1e9, "frac": ak / kt[k] / HBM_PEAK,
-                      "shares_gpu_with": ("MC" if k == "MS" else "MS") if mc_beside_ms and k in ("MS", "MC") else None}
+                      "shares_gpu_with": ("MC" if k == "MS" else "MS") if mc_beside_ms and k in ("MS", "MC") and not fused
+                      else None}
+        if fused:
+            kernels[k]["timed"] = "alone, untimed attribution pass after the timed loop (the timed step runs k_step)"
+    step_roof = None
+    if fused:
+        salg = sum(kernels[k]["alg_bytes_per_launch"] for k in kinds)
+        step_roof = {"kernel": "k_step (MU + MS + MC tiles, one launch)", "alg_bytes_per_launch": salg,
+                     "ms": 1e3 * kt_step, "achieved_GBps": salg / kt_step / 1e9, "frac": salg / kt_step / HBM_PEAK}
     o = outs[(j - 1) % nslot][dom]
     cur = o["cursor"].cpu().numpy().astype(np.int64)
     alg = kernels[dom]["alg_bytes_per_launch"]
@@ -470,6 +533,11 @@ def main():
     achieved = alg / kt[dom]
     traffic = issue = traffic_src = None
     tag = f"k_pulses<{dom}>" if dom != "MC" else "k_mc"
+    t_dom = kt[dom]
+    if fused:   # the timed region's one kernel: k_step over the whole step's algorithmic bytes
+        tag, alg, t_dom = "k_step", step_roof["alg_bytes_per_launch"], kt_step
+        achieved = alg / kt_step
+        layout = None
     tpath = latest_pmc()
     if tpath and args.corpus == "bench":
         with open(tpath) as fh:
@@ -482,7 +550,7 @@ def main():
                            "write_bytes": 1024 * float(tj[tag]["write_size_kib"]),
                            "calibration": "profiles/r05/calib/calib_traffic.json (FETCH_SIZE x 2 holds for every "
                                           "vector load width this kernel uses; scalar loads count exactly)"}
-            issue = issue_view(tj[tag], kt[dom])
+            issue = issue_view(tj[tag], t_dom)
     wl = {"mixed": "mixed MU/MS/MC stream, 1/3 each per rank: MU 256-pulse messages x 129-id MU bank, MS sync+bits x "
                    "66-id MS bank (clock x U(0.6,1.4)), MC frames x 12 clockrange ids ('fixed' chain)",
           "MU": "config 2: 256-pulse MU messages x 129-id MU bank",
@@ -499,16 +567,18 @@ def main():
                 (", noise-free dense corpus)" if args.corpus == "dense" else ")"),
         "config": {"workload": wl, "kind": args.kind, "corpus": args.corpus, "msgs_per_gpu": sum(per.values()),
                    "parallelism": f"dp{world}", "grouped": bool(gkinds),
-                   "streams": ("one per kind" if args.concurrent and len(kinds) > 1 else
+                   "streams": ("one kernel (k_step: MU, then MS, then MC tiles)" if fused else
+                               "one per kind" if args.concurrent and len(kinds) > 1 else
                                "MU, then MS beside MC" if mc_beside_ms else "serial")},
-        "per_kernel_ms": {k: 1e3 * v for k, v in kt.items()},
+        "per_kernel_ms": {**({"step": 1e3 * kt_step} if fused else {}), **{k: 1e3 * v for k, v in kt.items()}},
         "group_ms": 1e3 * gtime,   # sdx_group_pulses of all kinds per step (side stream, one step ahead)
         "per_type_msgs_per_s": {k: per[k] / kt[k] for k in kinds},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": tag,
                      "alg_bytes_per_launch": alg, "layout_bytes_per_launch": layout,
-                     "results_per_launch": int(cur[0]), "issue": issue, "traffic_source": traffic_src,
-                     "per_kernel": kernels},
+                     "results_per_launch": sum(k_["results_per_launch"] for k_ in kernels.values()) if fused else int(cur[0]),
+                     "issue": issue, "traffic_source": traffic_src,
+                     "per_kernel": kernels, **({"step": step_roof} if fused else {})},
     }
     if exch is not None and exch.bytes_sent:
         nb = exch.bytes_sent[-args.steps:]

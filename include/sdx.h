@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SDX_ABI_VERSION 13
+#define SDX_ABI_VERSION 14
 
 enum { SDX_OK = 0, SDX_EINVAL = -1, SDX_EHIP = -2, SDX_EBANK = -3, SDX_ECONTRACT = -4 };
 
@@ -216,6 +216,22 @@ int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch*
 /* MC "fixed" chain: every frame x every clockrange protocol.  Frames of more than SDX_MC_HEX_MAX
  * characters get status SDX_ST_OVF_TILE (cursor[2] bit 1): run them with sdx_demod_mc_general */
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream);
+/* ABI 14: one mixed step -- the MU launch, the MS launch and the MC launch of a step, each optional
+ * (NULL batch = none) -- as ONE kernel (k_step): workgroups [0, MU tiles) run MU's tiles, then MS's,
+ * then MC's frames, so each kind's tiles take the CU slots the previous kind's last tiles free instead
+ * of waiting for its whole launch to end.  Results are those of sdx_demod_pulses(MU),
+ * sdx_demod_pulses(MS) and sdx_demod_mc on the same stream in that order (record order inside a launch
+ * is tile order either way).  Parts the fused kernel does not cover (an MS batch with mrec_dev, MC frames
+ * that may exceed SDX_MC_SHORT_HEX characters) run their own launches after it on the stream. */
+typedef struct sdx_step {
+  const sdx_pulse_batch* mu;
+  const sdx_out* mu_out;
+  const sdx_pulse_batch* ms;
+  const sdx_out* ms_out;
+  const sdx_mc_batch* mc;
+  const sdx_out* mc_out;
+} sdx_step;
+int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream);
 /* MN (FSK): every frame x every 'modulation' protocol (parser mode) or one method (method mode).
  * Frames must hold hex digits only ([0-9A-Fa-f]; the front end guarantees [0-9A-F]) and at most
  * SDX_MN_HEX_MAX of them.  sdx_result.proto = MN table index (parser mode) / the method (method mode). */

@@ -1530,23 +1530,25 @@ constexpr int pulses_min_blocks() { return NW <= 4 ? 16 / LANE_WAVES : 1; }
 // SPLIT (MS, one launch per length class over the same tiles): > 0 = this launch takes the tiles
 // whose longest message has more than 64 * (SPLIT - 1) and at most 64 * NW pulses; a tile that is not
 // its launch's returns before it touches anything (a block-uniform test on the tile's lengths)
-template <int KIND, int NW, int TM, int MR = 0, int SPLIT = 0>
-__global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
-    (NW <= 4 ? 4 : 1)))) void k_pulses(
-    const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
+template <int KIND, int NW, int TM>
+using PulsesLds = TileLds<NW, TM, (KIND == SDX_KIND_MU && NW <= 4) ? 1 : ((KIND == SDX_KIND_MS && NW <= 4) ? 2 : 0)>;
+
+// one tile (TM messages, blk = the tile's index in the launch) of a k_pulses launch; the tile's LDS
+// and message list come from the calling kernel (k_pulses, or k_step's union)
+template <int KIND, int NW, int TM, int MR, int SPLIT>
+SDX_DEV void pulses_tile(const void* __restrict__ bank, const sdx_pulse_batch& b, const sdx_out& out, const int blk,
+                         PulsesLds<KIND, NW, TM>& L, int* msg_of) {
   constexpr bool LANE_MU = KIND == SDX_KIND_MU && NW <= 4;
   constexpr bool LANE_MS = KIND == SDX_KIND_MS && NW <= 4;
-  using T = TileLds<NW, TM, LANE_MU ? 1 : (LANE_MS ? 2 : 0)>;
-  __shared__ T L;
+  using T = PulsesLds<KIND, NW, TM>;
   const BankView bv = bank_view(bank);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int ntot = b.sel_dev ? b.n_sel : b.n;
-  const int tile0 = blockIdx.x * TM;
+  const int tile0 = blk * TM;
   const int nvalid = (ntot - tile0 < TM) ? ntot - tile0 : TM;
 #ifdef SDX_WGTIME
-  if (tid == 0 && blockIdx.x < 65536) g_wgt[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0 && blk < 65536) g_wgt[2 * blk] = __builtin_amdgcn_s_memrealtime();
 #endif
-  __shared__ int msg_of[TM];
   if constexpr (SPLIT != 0) {
     int len = 0;
     if (tid < nvalid) {
@@ -2298,11 +2300,20 @@ __global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu
   PROF_ADD(15, t_kernel);
 #ifdef SDX_WGTIME
   __syncthreads();
-  if (tid == 0 && blockIdx.x < 65536) g_wgt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0 && blk < 65536) g_wgt[2 * blk + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
 #ifdef SDX_PROF
   if (lane < 28) atomicAdd(&g_prof[lane], (unsigned long long)L.prof[wave][lane]);
 #endif
+}
+
+template <int KIND, int NW, int TM, int MR = 0, int SPLIT = 0>
+__global__ __launch_bounds__((pulses_threads<KIND, NW>())) __attribute__((amdgpu_waves_per_eu(
+    (NW <= 4 ? 4 : 1)))) void k_pulses(
+    const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
+  __shared__ PulsesLds<KIND, NW, TM> L;
+  __shared__ int msg_of[TM];
+  pulses_tile<KIND, NW, TM, MR, SPLIT>(bank, b, out, (int)blockIdx.x, L, msg_of);
 }
 
 // A copy on a few workgroups (sdx_copy_async_narrow): the streaming front end's device -> pinned-host
@@ -2430,13 +2441,15 @@ SDX_DEV void mc_stage(const uint8_t* src, int hl, uint64_t* dn, uint64_t* di, in
 
 // MW = 4: frames of <= 64 hex characters, longer ones are left to the MW = 8 launch (LONG = true),
 // which takes only those (sdx_demod_mc launches both; a wave without long frames exits at once)
+// 256 frames (blk = the block's index in the launch, tid = 0..255 the frame's thread) of a k_mc
+// launch; the LDS comes from the calling kernel (k_mc, or one half of a k_step block)
 template <int MW, bool LONG>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : SDX_MC_WPE))) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
-  __shared__ McLds<MW> L;
+SDX_DEV void mc_block(const void* __restrict__ bank, const sdx_mc_batch& b, const sdx_out& out, const int blk,
+                      const int tid, McLds<MW>& L) {
   const BankView bv = bank_view(bank);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wave = tid >> 6, lane = tid & 63;
   const int ntot = b.sel_dev ? b.n_sel : b.n;
-  const int gi = blockIdx.x * 256 + tid;
+  const int gi = blk * 256 + tid;
   bool valid = gi < ntot;
   const int msg = valid ? (b.sel_dev ? b.sel_dev[gi] : gi) : 0;
   bool toolong = false;  // > MC_MAXW * 16 characters: left to sdx_demod_mc_general (status OVF_TILE)
@@ -2651,6 +2664,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : 
 #endif
 #undef MCPROF_T
 #undef MCPROF_ADD
+}
+
+template <int MW, bool LONG>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : SDX_MC_WPE))) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
+  __shared__ McLds<MW> L;
+  mc_block<MW, LONG>(bank, b, out, (int)blockIdx.x, (int)threadIdx.x, L);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_step: a mixed step's MU, MS and MC launches as one grid (sdx_demod_step).  Workgroups are
+// dispatched in index order, so MU's tiles go first, then MS's two length classes (each over all MS
+// tiles, the other class's tiles returning at once, as in sdx_demod_pulses), then MC's frames, two
+// 256-frame blocks per workgroup.  A kind's tiles start on the CU slots the previous kind's last tiles
+// free: with one launch per kind, each launch's tail (its last round of tiles finishing unevenly)
+// idled the CUs until the whole launch had ended.  One LDS union serves every kind (the MU tile is the
+// largest at 80.7 KB; two MC blocks 80.9 KB) and every body fits the MU tile's 128 VGPRs, so each kind
+// keeps its own occupancy (2 tiles per CU).
+// ---------------------------------------------------------------------------------------------
+struct StepArgs {
+  sdx_pulse_batch mu, ms;
+  sdx_mc_batch mc;
+  sdx_out mu_out, ms_out, mc_out;
+  int t_mu, t_ms, b_mc;  // workgroups of each range (b_mc: pairs of 256-frame blocks)
+};
+union StepLds {
+  PulsesLds<SDX_KIND_MU, 4, 64> mu;
+  PulsesLds<SDX_KIND_MS, 2, 64> ms2;
+  PulsesLds<SDX_KIND_MS, 4, 64> ms4;
+  McLds<MC_SHORTW> mc[2];
+};
+static_assert(sizeof(StepLds) <= 81920, "two k_step workgroups per CU (160 KB of LDS)");
+
+template <int MRU>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_step(const void* __restrict__ bank,
+                                                                                      StepArgs a) {
+  static_assert(pulses_threads<SDX_KIND_MU, 4>() == 512 && pulses_threads<SDX_KIND_MS, 2>() == 512, "512-thread tiles");
+  __shared__ StepLds U;
+  __shared__ int msg_of[64];
+  int w = (int)blockIdx.x;
+  if (w < a.t_mu) {
+    pulses_tile<SDX_KIND_MU, 4, 64, MRU, 0>(bank, a.mu, a.mu_out, w, U.mu, msg_of);
+    return;
+  }
+  w -= a.t_mu;
+  if (w < a.t_ms) {
+    pulses_tile<SDX_KIND_MS, 2, 64, 0, 1>(bank, a.ms, a.ms_out, w, U.ms2, msg_of);
+    return;
+  }
+  w -= a.t_ms;
+  if (w < a.t_ms) {
+    pulses_tile<SDX_KIND_MS, 4, 64, 0, 3>(bank, a.ms, a.ms_out, w, U.ms4, msg_of);
+    return;
+  }
+  w -= a.t_ms;
+  const int half = (int)threadIdx.x >> 8;
+  mc_block<MC_SHORTW, false>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
 }
 
 }  // namespace sdx
@@ -2893,6 +2962,58 @@ int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch*
 }
 
 static_assert(sdx::MC_SHORTW * 16 == SDX_MC_SHORT_HEX, "k_mc<MC_SHORTW> holds SDX_MC_SHORT_HEX characters");
+
+int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream) {
+  if (!bank || !step) return fail(SDX_EINVAL, "null argument");
+  if ((step->mu && !step->mu_out) || (step->ms && !step->ms_out) || (step->mc && !step->mc_out))
+    return fail(SDX_EINVAL, "sdx_demod_step: a batch without its sdx_out");
+  hipStream_t st = (hipStream_t)hip_stream;
+  sdx::StepArgs a{};
+  auto count = [](int n, int n_sel, const void* sel) { return sel ? n_sel : n; };
+  // the fused kernel's forms: MU short (with or without message records), MS short without records
+  // (the two length classes), MC frames of <= SDX_MC_SHORT_HEX characters; anything else keeps its
+  // own launches, after the fused kernel on the same stream
+  const bool ms_fused = step->ms && !step->ms->mrec_dev && SDX_MS_NARROW;
+  const bool mc_fused = step->mc && step->mc->max_hex > 0 && step->mc->max_hex <= SDX_MC_SHORT_HEX;
+  if (step->mu) {
+    const sdx_pulse_batch& b = *step->mu;
+    if ((uintptr_t)b.mrec_dev & 127) return fail(SDX_EINVAL, "mrec_dev must be 128-byte aligned");
+    if (step->mu_out->work_dev && step->mu_out->work_cap > 0xFFFFFFFFull - sdx::SPILL_BYTES)
+      return fail(SDX_EINVAL, "work_cap above 4 GiB - 112 KB: spill offsets are 32-bit");
+    a.mu = b;
+    a.mu_out = *step->mu_out;
+    a.t_mu = (count(b.n, b.n_sel, b.sel_dev) + 63) / 64;
+  }
+  if (ms_fused) {
+    const sdx_pulse_batch& b = *step->ms;
+    if (!b.cp_slot_dev || !b.ms_ok_dev) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+    if (step->ms_out->work_dev && step->ms_out->work_cap > 0xFFFFFFFFull - sdx::SPILL_BYTES)
+      return fail(SDX_EINVAL, "work_cap above 4 GiB - 112 KB: spill offsets are 32-bit");
+    a.ms = b;
+    a.ms_out = *step->ms_out;
+    a.t_ms = (count(b.n, b.n_sel, b.sel_dev) + 63) / 64;
+  }
+  if (mc_fused) {
+    a.mc = *step->mc;
+    a.mc_out = *step->mc_out;
+    a.b_mc = (count(a.mc.n, a.mc.n_sel, a.mc.sel_dev) + 511) / 512;
+  }
+  const long long grid = (long long)a.t_mu + 2ll * a.t_ms + a.b_mc;
+  if (grid > 0x7FFFFFFFll) return fail(SDX_EINVAL, "sdx_demod_step: grid too large");
+  if (grid > 0) {
+    if (a.mu.mrec_dev)
+      hipLaunchKernelGGL((sdx::k_step<1>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
+    else
+      hipLaunchKernelGGL((sdx::k_step<0>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
+    HIPCHK(hipGetLastError());
+  }
+  if (step->ms && !ms_fused) {
+    const int rc = sdx_demod_pulses(bank, SDX_KIND_MS, step->ms, step->ms_out, hip_stream);
+    if (rc) return rc;
+  }
+  if (step->mc && !mc_fused) return sdx_demod_mc(bank, step->mc, step->mc_out, hip_stream);
+  return SDX_OK;
+}
 
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream) {
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");

@@ -19,7 +19,7 @@ from . import bank as bankmod
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libsdx.so")
-ABI_VERSION = 13   # include/sdx.h SDX_ABI_VERSION
+ABI_VERSION = 14   # include/sdx.h SDX_ABI_VERSION
 
 KIND_MU, KIND_MS, KIND_MC = 0, 1, 2
 KIND_MN = 3        # host-side tag for Engine.run (sdx_demod_mn)
@@ -46,7 +46,7 @@ EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_source_hash", "sdx_layout_
             "sdx_exchange_unpack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
             "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general",
             "sdx_lines_general", "sdx_copy_async", "sdx_copy_async_kind", "sdx_copy_async_narrow",
-            "sdx_fill_async"]
+            "sdx_fill_async", "sdx_demod_step"]
 GROUP_MIN = int(os.environ.get("SDX_GROUP_MIN", "4096"))   # SDX_GROUP_MIN (the env: A/B of the grouping)
 
 
@@ -125,6 +125,11 @@ class SdxOut(Structure):
                 ("wire_dev", c_void_p), ("xrec_dev", c_void_p)]
 
 
+class SdxStep(Structure):
+    _fields_ = [("mu", POINTER(SdxPulseBatch)), ("mu_out", POINTER(SdxOut)), ("ms", POINTER(SdxPulseBatch)),
+                ("ms_out", POINTER(SdxOut)), ("mc", POINTER(SdxMcBatch)), ("mc_out", POINTER(SdxOut))]
+
+
 class SdxLines(Structure):
     _fields_ = [("bytes_dev", c_void_p), ("offsets_dev", c_void_p), ("n", c_int32)]
 
@@ -199,6 +204,8 @@ def load_library(path: Optional[str] = None):
                                       POINTER(SdxLinesGeneralOut), c_void_p]
     lib.sdx_lines_general.restype = c_int
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
+    lib.sdx_demod_step.restype = c_int
+    lib.sdx_demod_step.argtypes = [c_void_p, POINTER(SdxStep), c_void_p]
     lib.sdx_demod_mc.restype = c_int
     lib.sdx_demod_mn.argtypes = [c_void_p, POINTER(SdxMnBatch), POINTER(SdxOut), c_void_p]
     lib.sdx_demod_mn.restype = c_int
@@ -459,12 +466,37 @@ class Engine:
         fn = self.lib.sdx_demod_pulses_long if long_variant else self.lib.sdx_demod_pulses
         _check(self.lib, fn(self.handle, kind, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
 
+    @staticmethod
+    def _mc_batch(bd, sel) -> SdxMcBatch:
+        return SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
+                          _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"],
+                          0 if sel is None else int(sel.numel()), _ptr(bd.get("only")), int(bd.get("max_hex", 0)), 0)
+
     def launch_mc(self, bd, out, sel=None) -> None:
-        b = SdxMcBatch(_ptr(bd["hex"]), _ptr(bd["offsets"]), _ptr(bd["clock"]), _ptr(bd["mcbitnum"]),
-                       _ptr(bd["flags"]), _ptr(bd.get("len")), _ptr(sel), bd["n"],
-                       0 if sel is None else int(sel.numel()), _ptr(bd.get("only")), int(bd.get("max_hex", 0)), 0)
+        b = self._mc_batch(bd, sel)
         o = self._out_struct(out)
         _check(self.lib, self.lib.sdx_demod_mc(self.handle, ctypes.byref(b), ctypes.byref(o), self.stream_ptr()))
+
+    def launch_step(self, mu=None, ms=None, mc=None) -> None:
+        """One mixed step as one kernel (sdx_demod_step, ABI 14): ``mu`` / ``ms`` = (batch, out, sel,
+        mrec) and ``mc`` = (batch, out, sel), each optional; the same results as launch_pulses(MU,
+        group=False), launch_pulses(MS, group=False) and launch_mc on the current stream.  The caller
+        groups (``sel`` = group()'s order): the fused launch takes its kinds' orders as given."""
+        keep = []
+        st = SdxStep()
+        for name, part in (("mu", mu), ("ms", ms)):
+            if part is not None:
+                bd, out, sel, mrec = part
+                b, o = self._pulse_batch(bd, sel, mrec), self._out_struct(out)
+                keep += [b, o]
+                setattr(st, name, ctypes.pointer(b))
+                setattr(st, name + "_out", ctypes.pointer(o))
+        if mc is not None:
+            bd, out, sel = mc
+            b, o = self._mc_batch(bd, sel), self._out_struct(out)
+            keep += [b, o]
+            st.mc, st.mc_out = ctypes.pointer(b), ctypes.pointer(o)
+        _check(self.lib, self.lib.sdx_demod_step(self.handle, ctypes.byref(st), self.stream_ptr()))
 
     def launch_mc_general(self, bd, out, sel, max_hex: int) -> None:
         """sdx_demod_mc_general over `sel` (frames of any length; its own bit workspace)."""

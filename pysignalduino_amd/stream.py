@@ -27,6 +27,7 @@ line's result is exactly the batch API's.
 from __future__ import annotations
 
 import collections
+import os
 from typing import Any, Deque, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
@@ -38,6 +39,9 @@ _KINDS = (("MU", runtime.KIND_MU, runtime.SEL_MU_SHORT, runtime.SEL_MU_LONG),
           ("MS", runtime.KIND_MS, runtime.SEL_MS_SHORT, runtime.SEL_MS_LONG),
           ("MC", runtime.KIND_MC, runtime.SEL_MC, None),
           ("MN", runtime.KIND_MN, runtime.SEL_MN, None))
+
+
+_FUSE = os.environ.get("SDX_STREAM_FUSE", "1") != "0"
 
 
 class ChunkResult:
@@ -297,6 +301,9 @@ class LineStream:
             e0.record(sd)
             runtime.fill_async(s.cursors, sd)
             pb = lb.pulse_batch()
+            # MU short, MS short and MC as ONE k_step launch (sdx_demod_step: each kind's tiles take the
+            # slots the previous kind's last tiles free); the long variants and MN keep their own
+            step = {}
             for name, kd, short, long_ in _KINDS:
                 o = s.outs.get(name)
                 if o is None:
@@ -310,14 +317,22 @@ class LineStream:
                         eng.launch_mn(lb.mn_batch(), o, elig=self.elig, sel=sels[short])
                 elif kd == runtime.KIND_MC:
                     if cnt[short]:
-                        eng.launch_mc(lb.mc_batch(), o, sel=sels[short])
-                else:
-                    if cnt[short]:   # the grouped order (the slot's own grouping buffers: no shared cache)
-                        sel = (eng.group(kd, pb, sels[short], bufs=s.gbufs[name]) if cnt[short] >= runtime.GROUP_MIN
-                               else sels[short])
-                        eng.launch_pulses(kd, pb, o, sel=sel, group=False)
-                    if cnt[long_]:
-                        eng.launch_pulses(kd, pb, o, sel=sels[long_], long_variant=True)
+                        step["mc"] = (lb.mc_batch(), o, sels[short])
+                elif cnt[short]:   # the grouped order (the slot's own grouping buffers: no shared cache)
+                    sel = (eng.group(kd, pb, sels[short], bufs=s.gbufs[name]) if cnt[short] >= runtime.GROUP_MIN
+                           else sels[short])
+                    step[name.lower()] = (pb, o, sel, None)
+            if step and _FUSE:
+                eng.launch_step(**step)
+            elif step:   # A/B (SDX_STREAM_FUSE=0): one launch per kind
+                for k, kd in (("mu", runtime.KIND_MU), ("ms", runtime.KIND_MS)):
+                    if k in step:
+                        eng.launch_pulses(kd, pb, step[k][1], sel=step[k][2], group=False)
+                if "mc" in step:
+                    eng.launch_mc(step["mc"][0], step["mc"][1], sel=step["mc"][2])
+            for name, kd, short, long_ in _KINDS:
+                if long_ is not None and cnt[long_] and name in s.outs:
+                    eng.launch_pulses(kd, pb, s.outs[name], sel=sels[long_], long_variant=True)
             s.cnt = cnt
             if self.output == "json":
                 jo = s.jout

@@ -165,7 +165,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert decl == set(runtime.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.sdx_abi_version() == runtime.ABI_VERSION == 13
+    assert lib.sdx_abi_version() == runtime.ABI_VERSION == 14
     runtime.check_layout(lib)
 
 

@@ -349,6 +349,56 @@ def test_message_records_match_soa_and_results(kind):
     assert all(x.tobytes() == y.tobytes() for x, y in zip(a, b))
 
 
+@pytest.mark.parametrize("mrec,mc_known,n", [(False, True, 20000), (True, True, 6000), (False, False, 3000),
+                                            (False, True, 1)])
+def test_fused_step_matches_the_separate_launches(mrec, mc_known, n):
+    """sdx_demod_step (ABI 14: the MU, MS and MC launches of a step as one k_step grid) gives the
+    results of sdx_demod_pulses(MU), sdx_demod_pulses(MS) and sdx_demod_mc: descriptors, records and
+    payloads (canonical form: record placement follows the tiles' atomics) and the exchange's per-message
+    counts, byte for byte.  MS carries messages on both sides of the 128-pulse length class boundary;
+    mrec: MU reads message records; mc_known = False: MC's length bound unknown (its frames run in
+    their own launch after the fused kernel); n = 1: near-empty ranges."""
+    import torch
+    from pysignalduino_amd import bank as B, dist, runtime, synth
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    P = bk.protocols
+    mu = synth.mu_corpus(P, n, seed=9401)
+    ms = synth.ms_corpus(P, n, seed=9402)
+    mc = synth.mc_corpus(P, n, seed=9403)
+    bds = {"MU": eng.to_device_pulses(mu), "MS": eng.to_device_pulses(ms), "MC": eng.to_device_mc(mc)}
+    if not mc_known:
+        bds["MC"]["max_hex"] = 0
+    eng.use_mrec = {runtime.KIND_MU} if mrec else set()
+    orders = {}
+    bufs = {}
+    for k, kd in (("MU", runtime.KIND_MU), ("MS", runtime.KIND_MS)):
+        bufs[k] = eng.group_buffers(n)
+        orders[k] = eng.group(kd, bds[k], bufs=bufs[k]) if n >= runtime.GROUP_MIN else None
+
+    def alloc():
+        caps = {"MU": (40, 1024), "MS": (8, 256), "MC": (8, 256)}
+        return {k: eng.alloc_out(n, caps[k][0] * n + 4096, caps[k][1] * n + 65536,
+                                 eng.pulses_work_bytes(n) if k != "MC" else 0, wire=True) for k in caps}
+
+    sep, fus = alloc(), alloc()
+    mr = bufs["MU"][2] if (mrec and orders["MU"] is not None) else None
+    eng.launch_pulses(runtime.KIND_MU, bds["MU"], sep["MU"], sel=orders["MU"], group=False, mrec=mr)
+    eng.launch_pulses(runtime.KIND_MS, bds["MS"], sep["MS"], sel=orders["MS"], group=False)
+    eng.launch_mc(bds["MC"], sep["MC"])
+    eng.launch_step(mu=(bds["MU"], fus["MU"], orders["MU"], mr), ms=(bds["MS"], fus["MS"], orders["MS"], None),
+                    mc=(bds["MC"], fus["MC"], None))
+    torch.cuda.synchronize()
+    nres = 0
+    for k in ("MU", "MS", "MC"):
+        a, b = eng.fetch(sep[k]), eng.fetch(fus[k])
+        nres += len(a[1])
+        ca, cb = dist.canonical(*a), dist.canonical(*b)
+        assert all(x.tobytes() == y.tobytes() for x, y in zip(ca, cb)), k
+        assert torch.equal(sep[k]["wire"][:n], fus[k]["wire"][:n]), k
+    assert n == 1 or nres > n
+
+
 @pytest.mark.parametrize("kind,n", [("MU", 333333), ("MS", 5000), ("MU", 2049), ("MS", 1)])
 def test_grouping_is_a_stable_sort_of_the_keys(kind, n):
     """sdx_group_pulses (k_sig + the 2-launch-per-pass radix sort, sdx_group.hip): the order is a

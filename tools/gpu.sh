@@ -15,6 +15,7 @@
 #   kt                   rocprofv3 --kernel-trace --stats of bench.py      -> OUT/kt_bench/
 #   ktlines              the same for tools/bench_lines.py                 -> OUT/kt_lines/
 #   ktpy=SCRIPT[,ARGS]   the same for python3 SCRIPT ARGS                  -> OUT/kt_<n>/
+#   ktpyenv=VAR=val,SCRIPT[,ARGS]  the same with VAR=val in the environment -> OUT/kt_<n>/
 #   ktx[=ARGS]           the same for bench.py --no-cpu ARGS (',' separates) -> OUT/ktx_<n>/
 #   pmc[=PASSES]         tools/pmc.sh (default sq1,sq2,fetch,write)        -> OUT/pmc/, OUT/pmc_traffic.json
 #   time=V1,V2           tools/time_mu.py for in-tree libsdx + variants V (pysignalduino_amd/_lib/ab/libsdx_V.so), 2 rounds
@@ -67,6 +68,9 @@ for st in "$@"; do
         echo "kt: $(tail -1 "$O/kt_bench.log" | summ)" ;;
     ktpy) run 300 "$O/ktpy_$n.log" rocprofv3 --kernel-trace --stats -d "$O/kt_$n" -o k --output-format csv -- python3 $args
         echo "ktpy $arg: $(tail -1 "$O/ktpy_$n.log" | cut -c1-300)" ;;
+    ktpyenv) e=${args%% *}; rest=${args#* }
+      run 300 "$O/ktpyenv_$n.log" env "$e" rocprofv3 --kernel-trace --stats -d "$O/kt_$n" -o k --output-format csv -- python3 $rest
+      echo "ktpyenv $arg: $(tail -3 "$O/ktpyenv_$n.log" | cut -c1-300)" ;;
     ktx) run 300 "$O/ktx_$n.log" rocprofv3 --kernel-trace --stats -d "$O/ktx_$n" -o b --output-format csv -- python3 bench.py --no-cpu $args
         echo "ktx $arg: $(tail -1 "$O/ktx_$n.log" | summ)" ;;
     ktlines) run 300 "$O/kt_lines.log" rocprofv3 --kernel-trace --stats -d "$O/kt_lines" -o l --output-format csv -- python3 tools/bench_lines.py --no-cpu
