@@ -450,7 +450,11 @@ def main():
             used[par] = last                # the step's grouped launches have read this parity's order
         if exch is not None:  # RCCL all-gather of the decoded dmsg buffers (config 5), overlapped
             parts = [sdist.Part.from_out(outs[s_][k], KIND[k], src=(KIND[k], bds[k], 0, -1)) for k in kinds]
-            rel = shd.submit(parts, stream, after=mu_done[0] if args.xchg != "eager" and "MU" in kinds else None)
+            # (fused: no "after MU" point inside the step; the previous step's count and pack run behind
+            # its own end, beside this step's k_step -- waiting for this step's end would hold the host
+            # until the GPU had drained)
+            rel = shd.submit(parts, stream, after=mu_done[0] if args.xchg != "eager" and "MU" in kinds and not fused
+                             else None)
             if rel is not None:             # the previous step's pack has read its slot
                 done[(j - 1) % nslot] = rel
 
