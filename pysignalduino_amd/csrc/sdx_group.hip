@@ -41,6 +41,9 @@ SDX_DEV uint64_t peers8(uint32_t v, bool active) {
 // the clock-grouped processing order.)
 // ---------------------------------------------------------------------------------------------
 constexpr int SIG_PROTOS = 32;
+#ifndef SDX_MS_LONG_FIRST
+#define SDX_MS_LONG_FIRST 0  // 1: the MS length class of more than 128 pulses first (A/B)
+#endif
 #ifndef SDX_MS_KEY
 #define SDX_MS_KEY 0  // MS key form (A/B experiments; 0 = ascending signature)
 #endif
@@ -172,7 +175,7 @@ __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_
     if (SDX_MS_NARROW) {
       const int64_t o = b.offsets_dev[msg];
       const int len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - o);
-      ms_key = ((len > 128) ? 0x80000000u : 0u) | (sig >> 1);
+      ms_key = (((len > 128) != (SDX_MS_LONG_FIRST != 0)) ? 0x80000000u : 0u) | (sig >> 1);
     }
 #endif
     key[i] = KIND == SDX_KIND_MU ? ~sig : ms_key;

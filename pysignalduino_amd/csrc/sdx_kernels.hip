@@ -2344,6 +2344,9 @@ __global__ __launch_bounds__(256) void k_copy_narrow(uint8_t* __restrict__ dst, 
 // =============================================================================================
 // MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
 // =============================================================================================
+#ifndef SDX_MS_TWO_LAUNCHES
+#define SDX_MS_TWO_LAUNCHES 0
+#endif
 #ifndef SDX_MC_REC_CAP
 #define SDX_MC_REC_CAP 152
 #define SDX_MC_HEAP_CAP 3584
@@ -2674,14 +2677,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : 
 
 // ---------------------------------------------------------------------------------------------
 // k_step: a mixed step's MU, MS and MC launches as one grid (sdx_demod_step).  Workgroups are
-// dispatched in index order, so MU's tiles go first, then MS's two length classes (each over all MS
-// tiles, the other class's tiles returning at once, as in sdx_demod_pulses), then MC's frames, two
-// 256-frame blocks per workgroup.  A kind's tiles start on the CU slots the previous kind's last tiles
+// dispatched in index order, so MU's tiles go first, then MS's (each tile on the instantiation of its
+// length class, NW = 2 when no message has more than 128 pulses), then MC's frames, two 256-frame
+// blocks per workgroup.  A kind's tiles start on the CU slots the previous kind's last tiles
 // free: with one launch per kind, each launch's tail (its last round of tiles finishing unevenly)
 // idled the CUs until the whole launch had ended.  One LDS union serves every kind (the MU tile is the
 // largest at 80.7 KB; two MC blocks 80.9 KB) and every body fits the MU tile's 128 VGPRs, so each kind
 // keeps its own occupancy (2 tiles per CU).
 // ---------------------------------------------------------------------------------------------
+// one MS tile on the instantiation of its length class: NW = 2 (2 bitmap words per id, 118 VGPRs)
+// when none of its messages has more than 128 pulses, NW = 4 otherwise -- decided per tile, so no
+// workgroup exists only to find that the tile is another launch's
+SDX_DEV void ms_tile_by_class(const void* __restrict__ bank, const sdx_pulse_batch& b, const sdx_out& out, const int w,
+                              PulsesLds<SDX_KIND_MS, 2, 64>& L2, PulsesLds<SDX_KIND_MS, 4, 64>& L4, int* msg_of) {
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int m = w * 64 + (int)threadIdx.x;
+  int len = 0;
+  if (threadIdx.x < 64 && m < ntot) {
+    const int msg = b.sel_dev ? b.sel_dev[m] : m;
+    len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - b.offsets_dev[msg]);
+  }
+  if (__syncthreads_or(len > 128) == 0)
+    pulses_tile<SDX_KIND_MS, 2, 64, 0, 0>(bank, b, out, w, L2, msg_of);
+  else
+    pulses_tile<SDX_KIND_MS, 4, 64, 0, 0>(bank, b, out, w, L4, msg_of);
+}
+
+// sdx_demod_pulses(MS) without message records: every tile on its length class's instantiation
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ms_classes(
+    const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
+  __shared__ union {
+    PulsesLds<SDX_KIND_MS, 2, 64> n2;
+    PulsesLds<SDX_KIND_MS, 4, 64> n4;
+  } U;
+  __shared__ int msg_of[64];
+  ms_tile_by_class(bank, b, out, (int)blockIdx.x, U.n2, U.n4, msg_of);
+}
+
 struct StepArgs {
   sdx_pulse_batch mu, ms;
   sdx_mc_batch mc;
@@ -2709,12 +2741,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   }
   w -= a.t_mu;
   if (w < a.t_ms) {
-    pulses_tile<SDX_KIND_MS, 2, 64, 0, 1>(bank, a.ms, a.ms_out, w, U.ms2, msg_of);
-    return;
-  }
-  w -= a.t_ms;
-  if (w < a.t_ms) {
-    pulses_tile<SDX_KIND_MS, 4, 64, 0, 3>(bank, a.ms, a.ms_out, w, U.ms4, msg_of);
+    ms_tile_by_class(bank, a.ms, a.ms_out, w, U.ms2, U.ms4, msg_of);
     return;
   }
   w -= a.t_ms;
@@ -2915,9 +2942,15 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
     // messages all fit 2 words per id run the NW = 2 instantiation (half the bitmap words and mask
     // arithmetic), the others the NW = 4 one; the grouping puts the long messages last (k_sig)
     static_assert(sdx::pulses_threads<SDX_KIND_MS, 2>() == sdx::pulses_threads<SDX_KIND_MS, 4>(), "block shape");
-    // (an NW = 1 class for <= 64 pulses spilled thousands of VGPRs: not used)
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 2, 64, 0, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
-    hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 0, 3>), dim3(grid), blk, 0, st, bank->dev, b, o);
+    // (an NW = 1 class for <= 64 pulses spilled thousands of VGPRs: not used).  One launch decides per
+    // tile (k_ms_classes); SDX_MS_TWO_LAUNCHES=1 keeps round 5's two launches over all tiles, each
+    // tile returning at once from the other class's launch (A/B)
+    if (SDX_MS_TWO_LAUNCHES) {
+      hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 2, 64, 0, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
+      hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 0, 3>), dim3(grid), blk, 0, st, bank->dev, b, o);
+    } else {
+      hipLaunchKernelGGL(sdx::k_ms_classes, dim3(grid), blk, 0, st, bank->dev, b, o);
+    }
   } else
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
   HIPCHK(hipGetLastError());
@@ -2998,7 +3031,7 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
     a.mc_out = *step->mc_out;
     a.b_mc = (count(a.mc.n, a.mc.n_sel, a.mc.sel_dev) + 511) / 512;
   }
-  const long long grid = (long long)a.t_mu + 2ll * a.t_ms + a.b_mc;
+  const long long grid = (long long)a.t_mu + a.t_ms + a.b_mc;
   if (grid > 0x7FFFFFFFll) return fail(SDX_EINVAL, "sdx_demod_step: grid too large");
   if (grid > 0) {
     if (a.mu.mrec_dev)
