@@ -72,6 +72,8 @@ def parse():
                     help="exchange payloads raw (no nibble form: A/B of the wire size)")
     ap.add_argument("--scan-wire", action="store_true",
                     help="the exchange classifies every payload itself (no kernel-written counts, ABI 12: A/B)")
+    ap.add_argument("--settle-steps", type=int, default=100,
+                    help="untimed steps before the --warmup steps (~0.2 s: GPU clocks out of idle)")
     ap.add_argument("--no-fuse", dest="fuse", action="store_false",
                     help="one launch per kind (MU, then MS beside MC) instead of the default ONE kernel for the "
                          "step's MU, MS and MC tiles (sdx_demod_step, ABI 14, where each kind's tiles take the CU "
@@ -467,6 +469,14 @@ def main():
         torch.cuda.synchronize()
 
     j = 0
+    # settle (untimed, before the W warmup steps): ~0.2 s of steps, so that the timed steps do not
+    # start on a GPU still ramping up from idle -- a fresh box's first bench once ran MS at twice its
+    # time with 3 warmup steps (profiles/r05/dropped/radix_passes/bench_1.log, 417M vs 581M msgs/s)
+    # (a fixed count, not a time: every rank must run the same steps -- each step holds collectives)
+    settle = max(0, args.settle_steps)
+    for _ in range(settle):
+        step(j)
+        j += 1
     for _ in range(args.warmup):
         step(j)
         j += 1
@@ -565,6 +575,7 @@ def main():
     res = {
         "metric": "RF messages/sec demodulated (MU+MS+MC, full protocol bank)",
         "value": value, "unit": "msgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "settle_steps": settle,
         "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8+f64",
         "data": "synthetic (seeded generators, pysignalduino_amd/synth.py" +
