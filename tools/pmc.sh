@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 # PMC_BENCH / PMC_OUT / PMC_TRAFFIC / PMC_CONFIG select another workload (e.g. tools/bench_lines.py)
 OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
-BENCH=${PMC_BENCH:-"python3 bench.py --steps 3 --warmup 1 --no-cpu"}
+BENCH=${PMC_BENCH:-"python3 bench.py --steps 3 --warmup 1 --settle-steps 2 --no-cpu"}
 declare -A P
 P[sq1]="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
 P[sq2]="SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"

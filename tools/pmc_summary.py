@@ -8,7 +8,7 @@ import sys
 
 
 def short(name: str) -> str:
-    for key, tag in (("k_step", "k_step"), ("k_pulses<0, 4,", "k_pulses<MU>"), ("k_pulses<1, 4,", "k_pulses<MS>"),
+    for key, tag in (("k_step", "k_step"), ("k_ms_classes", "k_pulses<MS>"), ("k_pulses<0, 4,", "k_pulses<MU>"), ("k_pulses<1, 4,", "k_pulses<MS>"),
                      ("k_pulses<1, 2,", "k_pulses<MS,narrow>"), ("k_pulsesILi1ELi2E", "k_pulses<MS,narrow>"),
                      ("k_pulses<0, 64,", "k_pulses<MU,long>"), ("k_pulses<1, 64,", "k_pulses<MS,long>"),
                      ("k_pulsesILi0ELi4E", "k_pulses<MU>"), ("k_pulsesILi1ELi4E", "k_pulses<MS>"),
