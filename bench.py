@@ -72,6 +72,9 @@ def parse():
                     help="exchange payloads raw (no nibble form: A/B of the wire size)")
     ap.add_argument("--scan-wire", action="store_true",
                     help="the exchange classifies every payload itself (no kernel-written counts, ABI 12: A/B)")
+    ap.add_argument("--group-reuse", action="store_true",
+                    help="DIAGNOSTIC, not a valid line: group the batch in the first two steps only and reuse "
+                         "the orders (what the per-step grouping costs the step)")
     ap.add_argument("--settle-steps", type=int, default=100,
                     help="untimed steps before the --warmup steps (~0.2 s: GPU clocks out of idle)")
     ap.add_argument("--no-fuse", dest="fuse", action="store_false",
@@ -384,7 +387,7 @@ def main():
         if gkinds:
             if j == 0:
                 launch_group(0)
-            if args.group_at == "mu":
+            if args.group_at == "mu" and not (args.group_reuse and j >= 1):
                 launch_group(j + 1, si)     # the next step's grouping, concurrent with this step
         par = j % 2
         tm = si is not None and si % args.kev_every == 0
@@ -501,7 +504,8 @@ def main():
     dt = time.perf_counter() - t0
     ktimes = {k: [kev[si][k][0].elapsed_time(kev[si][k][1]) * 1e-3 for si in range(0, args.steps, args.kev_every)]
               for k in (("step",) if fused else kinds)}
-    gtime = float(np.mean([gev[si][0].elapsed_time(gev[si][1]) * 1e-3 for si in range(0, args.steps, args.kev_every)])) if gkinds else 0.0
+    gtime = float(np.mean([gev[si][0].elapsed_time(gev[si][1]) * 1e-3 for si in range(0, args.steps, args.kev_every)])) \
+        if gkinds and not args.group_reuse else 0.0
     tt = torch.tensor([dt], dtype=torch.float64, device=dev)
     if dist_on:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -578,6 +582,8 @@ def main():
         "settle_steps": settle,
         "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8+f64",
+        **({"diagnostic": "--group-reuse: the batch was grouped once, not per step -- NOT a valid line"}
+           if args.group_reuse else {}),
         "data": "synthetic (seeded generators, pysignalduino_amd/synth.py" +
                 (", noise-free dense corpus)" if args.corpus == "dense" else ")"),
         "config": {"workload": wl, "kind": args.kind, "corpus": args.corpus, "msgs_per_gpu": sum(per.values()),
