@@ -193,8 +193,12 @@ constexpr int RS_T = 512, RS_ROUNDS = 4, RS_PART = RS_T * RS_ROUNDS;
 #ifndef SDX_RS_PASSES
 #define SDX_RS_PASSES 4
 #endif
+#ifndef SDX_RS_PASSES_MS
+#define SDX_RS_PASSES_MS SDX_RS_PASSES
+#endif
 constexpr int RS_PASSES = SDX_RS_PASSES;  // bytes of the key sorted on, from the top
-static_assert(RS_PASSES >= 1 && RS_PASSES <= 4, "1..4 radix passes");
+constexpr int RS_PASSES_MS = SDX_RS_PASSES_MS;  // (MS: A/B)
+static_assert(RS_PASSES >= 1 && RS_PASSES <= 4 && RS_PASSES_MS >= 1 && RS_PASSES_MS <= 4, "1..4 radix passes");
 
 // hist[digit * np + part] = elements of the partition with that digit in pass d
 __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ key, int n, int np, int d,
@@ -313,11 +317,12 @@ bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, in
     hipLaunchKernelGGL((k_sig<SDX_KIND_MS>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec);
   // the key's top RS_PASSES bytes (LSD order): (k0, v0) -> (k1, v1) -> (k0, v0) -> ..., the last
   // pass writing the message indices to order
-  for (int pi = 0; pi < RS_PASSES; ++pi) {
-    const int d = 4 - RS_PASSES + pi;
+  const int passes = kind == SDX_KIND_MU ? RS_PASSES : RS_PASSES_MS;
+  for (int pi = 0; pi < passes; ++pi) {
+    const int d = 4 - passes + pi;
     const bool even = (pi & 1) == 0;
     uint32_t* kin = even ? k0 : k1;
-    uint32_t* vout = pi == RS_PASSES - 1 ? reinterpret_cast<uint32_t*>(order) : (even ? v1 : v0);
+    uint32_t* vout = pi == passes - 1 ? reinterpret_cast<uint32_t*>(order) : (even ? v1 : v0);
     hipLaunchKernelGGL(k_rs_hist, dim3(np), dim3(RS_T), 0, st, kin, n, np, d, hist);
     hipLaunchKernelGGL(k_rs_scan_rows, dim3(256 / 4), dim3(256), 0, st, hist, np, tot);
     hipLaunchKernelGGL(k_rs_scatter, dim3(np), dim3(RS_T), 0, st, kin, even ? v0 : v1, n, np, d, hist, tot,
