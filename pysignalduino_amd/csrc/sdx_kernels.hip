@@ -2344,6 +2344,9 @@ __global__ __launch_bounds__(256) void k_copy_narrow(uint8_t* __restrict__ dst, 
 // =============================================================================================
 // MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
 // =============================================================================================
+#ifndef SDX_STEP_ORDER
+#define SDX_STEP_ORDER 0
+#endif
 #ifndef SDX_MS_TWO_LAUNCHES
 #define SDX_MS_TWO_LAUNCHES 0
 #endif
@@ -2734,19 +2737,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   static_assert(pulses_threads<SDX_KIND_MU, 4>() == 512 && pulses_threads<SDX_KIND_MS, 2>() == 512, "512-thread tiles");
   __shared__ StepLds U;
   __shared__ int msg_of[64];
-  int w = (int)blockIdx.x;
-  if (w < a.t_mu) {
+  // the ranges in dispatch order (SDX_STEP_ORDER): 0 = MU, MS, MC; 1 = MC, MU, MS; 2 = MU, MC, MS
+  constexpr int R0 = SDX_STEP_ORDER == 0 ? 0 : (SDX_STEP_ORDER == 1 ? 2 : 0);
+  constexpr int R1 = SDX_STEP_ORDER == 0 ? 1 : (SDX_STEP_ORDER == 1 ? 0 : 2);
+  constexpr int R2 = SDX_STEP_ORDER == 0 ? 2 : 1;
+  const int cnt[3] = {a.t_mu, a.t_ms, a.b_mc};
+  int w = (int)blockIdx.x, r = R2;
+  if (w < cnt[R0]) {
+    r = R0;
+  } else {
+    w -= cnt[R0];
+    if (w < cnt[R1]) r = R1;
+    else w -= cnt[R1];
+  }
+  if (r == 0) {
     pulses_tile<SDX_KIND_MU, 4, 64, MRU, 0>(bank, a.mu, a.mu_out, w, U.mu, msg_of);
-    return;
-  }
-  w -= a.t_mu;
-  if (w < a.t_ms) {
+  } else if (r == 1) {
     ms_tile_by_class(bank, a.ms, a.ms_out, w, U.ms2, U.ms4, msg_of);
-    return;
+  } else {
+    const int half = (int)threadIdx.x >> 8;
+    mc_block<MC_SHORTW, false>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
   }
-  w -= a.t_ms;
-  const int half = (int)threadIdx.x >> 8;
-  mc_block<MC_SHORTW, false>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
 }
 
 }  // namespace sdx
