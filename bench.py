@@ -72,6 +72,9 @@ def parse():
                     help="exchange payloads raw (no nibble form: A/B of the wire size)")
     ap.add_argument("--scan-wire", action="store_true",
                     help="the exchange classifies every payload itself (no kernel-written counts, ABI 12: A/B)")
+    ap.add_argument("--group-separate", action="store_true",
+                    help="the MU and MS groupings as two sdx_group_pulses calls (26 launches) instead of one "
+                         "sdx_group_step (13 launches; A/B)")
     ap.add_argument("--group-reuse", action="store_true",
                     help="DIAGNOSTIC, not a valid line: group the batch in the first two steps only and reuse "
                          "the orders (what the per-step grouping costs the step)")
@@ -316,8 +319,11 @@ def main():
         with torch.cuda.stream(side):
             if si is not None and si % args.kev_every == 0:
                 gev[si][0].record(side)
-            for k in gkinds:
-                eng.group(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], bufs=gbufs[k][par])
+            if gkinds == ["MU", "MS"] and not args.group_separate:   # both sorts' passes in the same launches
+                eng.group_step(bds["MU"], bds["MS"], gbufs["MU"][par], gbufs["MS"][par])
+            else:
+                for k in gkinds:
+                    eng.group(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], bufs=gbufs[k][par])
             # one event for all kinds: the grouping of step j ends during step j - 1, long before
             # step j's launches wait for it
             e = gev[si][1] if si is not None and si % args.kev_every == 0 else torch.cuda.Event()

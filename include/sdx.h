@@ -210,6 +210,16 @@ size_t sdx_group_work_bytes(int n);
 int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, int32_t* order_dev,
                      sdx_msg_rec* mrec_dev, void* work_dev, size_t work_cap, void* hip_stream);
 #define SDX_GROUP_MIN 4096  /* batches from this size are grouped by the host wrappers */
+/* ABI 14: a mixed step's MU and MS groupings (the results of two sdx_group_pulses calls) with both
+ * sorts' passes in the same launches: 13 launches instead of 26 */
+typedef struct sdx_group_job {
+  const sdx_pulse_batch* batch;
+  int32_t* order_dev;
+  sdx_msg_rec* mrec_dev;  /* optional */
+  void* work_dev;
+  size_t work_cap;
+} sdx_group_job;
+int sdx_group_step(const sdx_bank* bank, const sdx_group_job* mu, const sdx_group_job* ms, void* hip_stream);
 /* same, for messages of 257..4096 pulses (4 messages per workgroup tile) */
 int sdx_demod_pulses_long(const sdx_bank* bank, int kind, const sdx_pulse_batch* batch, const sdx_out* out,
                           void* hip_stream);

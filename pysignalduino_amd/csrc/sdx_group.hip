@@ -48,10 +48,10 @@ constexpr int SIG_PROTOS = 32;
 #define SDX_MS_KEY 0  // MS key form (A/B experiments; 0 = ascending signature)
 #endif
 template <int KIND>
-__global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_pulse_batch b, uint32_t* __restrict__ key,
-                                             uint32_t* __restrict__ msg_out, sdx_msg_rec* __restrict__ mrec) {
+SDX_DEV void sig_block(const void* __restrict__ bank, const sdx_pulse_batch& b, uint32_t* __restrict__ key,
+                       uint32_t* __restrict__ msg_out, sdx_msg_rec* __restrict__ mrec, const int blk) {
   const BankView bv = bank_view(bank);
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = blk * 256 + threadIdx.x;
   const int ntot = b.sel_dev ? b.n_sel : b.n;
   const bool valid = i < ntot;
   const int msg = valid ? (b.sel_dev ? b.sel_dev[i] : i) : 0;
@@ -183,6 +183,27 @@ __global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_
   }
 }
 
+template <int KIND>
+__global__ __launch_bounds__(256) void k_sig(const void* __restrict__ bank, sdx_pulse_batch b, uint32_t* __restrict__ key,
+                                             uint32_t* __restrict__ msg_out, sdx_msg_rec* __restrict__ mrec) {
+  sig_block<KIND>(bank, b, key, msg_out, mrec, (int)blockIdx.x);
+}
+
+// the step's two groupings in one launch (sdx_group_step): blocks [0, g_mu) key the MU batch, the rest
+// the MS batch
+struct SigSide {
+  sdx_pulse_batch b;
+  uint32_t* key;
+  uint32_t* msg;
+  sdx_msg_rec* mrec;
+};
+__global__ __launch_bounds__(256) void k_sig2(const void* __restrict__ bank, SigSide mu, SigSide ms, int g_mu) {
+  if ((int)blockIdx.x < g_mu)
+    sig_block<SDX_KIND_MU>(bank, mu.b, mu.key, mu.msg, mu.mrec, (int)blockIdx.x);
+  else
+    sig_block<SDX_KIND_MS>(bank, ms.b, ms.key, ms.msg, ms.mrec, (int)blockIdx.x - g_mu);
+}
+
 // ---------------------------------------------------------------------------------------------
 // stable LSD radix sort of (key, message) pairs: 4 passes of 8 bits over partitions of RS_PART
 // elements; per pass the partitions' digit counts (k_rs_hist), their prefix over the partitions (a
@@ -201,10 +222,9 @@ constexpr int RS_PASSES_MS = SDX_RS_PASSES_MS;  // (MS: A/B)
 static_assert(RS_PASSES >= 1 && RS_PASSES <= 4 && RS_PASSES_MS >= 1 && RS_PASSES_MS <= 4, "1..4 radix passes");
 
 // hist[digit * np + part] = elements of the partition with that digit in pass d
-__global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ key, int n, int np, int d,
-                                                  uint32_t* __restrict__ hist) {
-  __shared__ uint32_t c[256];
-  const int tid = threadIdx.x, p = blockIdx.x;
+SDX_DEV void rs_hist(const uint32_t* __restrict__ key, int n, int np, int d, uint32_t* __restrict__ hist, const int p,
+                     uint32_t* c) {
+  const int tid = threadIdx.x;
   if (tid < 256) c[tid] = 0;
   __syncthreads();
   for (int r = 0; r < RS_ROUNDS; ++r) {
@@ -217,10 +237,15 @@ __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ k
   __syncthreads();
   if (tid < 256) hist[(size_t)tid * np + p] = c[tid];
 }
+__global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ key, int n, int np, int d,
+                                                  uint32_t* __restrict__ hist) {
+  __shared__ uint32_t c[256];
+  rs_hist(key, n, np, d, hist, (int)blockIdx.x, c);
+}
 
 // each digit's row: exclusive prefix over the partitions (one wave per row); tot[digit] = total
-__global__ __launch_bounds__(256) void k_rs_scan_rows(uint32_t* __restrict__ hist, int np, uint32_t* __restrict__ tot) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+SDX_DEV void rs_scan_rows(uint32_t* __restrict__ hist, int np, uint32_t* __restrict__ tot, const int blk) {
+  const int row = blk * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   uint32_t* h = hist + (size_t)row * np;
   uint32_t run = 0;
   for (int b0 = 0; b0 < np; b0 += 64) {
@@ -237,16 +262,16 @@ __global__ __launch_bounds__(256) void k_rs_scan_rows(uint32_t* __restrict__ his
   }
   if (lane == 0) tot[row] = run;
 }
+__global__ __launch_bounds__(256) void k_rs_scan_rows(uint32_t* __restrict__ hist, int np, uint32_t* __restrict__ tot) {
+  rs_scan_rows(hist, np, tot, (int)blockIdx.x);
+}
 
 // pass d: every partition scatters its elements, in order (stable), to
 // (digit base = prefix of the digit totals) + (row offset of the partition) + (rank inside it)
-__global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                     int n, int np, int d, const uint32_t* __restrict__ hist,
-                                                     const uint32_t* __restrict__ tot, uint32_t* __restrict__ kout,
-                                                     uint32_t* __restrict__ vout) {
-  __shared__ uint32_t run[256];
-  __shared__ uint32_t wc[RS_T / 64][256];
-  const int tid = threadIdx.x, p = blockIdx.x, wave = tid >> 6;
+SDX_DEV void rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int n, int np, int d,
+                        const uint32_t* __restrict__ hist, const uint32_t* __restrict__ tot, uint32_t* __restrict__ kout,
+                        uint32_t* __restrict__ vout, const int p, uint32_t* run, uint32_t (*wc)[256]) {
+  const int tid = threadIdx.x, wave = tid >> 6;
   const uint32_t t = tid < 256 ? tot[tid] : 0u;
   if (tid < 256) run[tid] = t;
   __syncthreads();
@@ -283,6 +308,45 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
     }
     __syncthreads();
   }
+}
+__global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     int n, int np, int d, const uint32_t* __restrict__ hist,
+                                                     const uint32_t* __restrict__ tot, uint32_t* __restrict__ kout,
+                                                     uint32_t* __restrict__ vout) {
+  __shared__ uint32_t run[256];
+  __shared__ uint32_t wc[RS_T / 64][256];
+  rs_scatter(kin, vin, n, np, d, hist, tot, kout, vout, (int)blockIdx.x, run, wc);
+}
+
+// one radix pass of two sorts in each launch (sdx_group_step): partitions [0, a.np) sort a's keys,
+// the rest b's
+struct RsPass {
+  const uint32_t* kin;
+  const uint32_t* vin;
+  uint32_t* kout;
+  uint32_t* vout;
+  uint32_t* hist;
+  uint32_t* tot;
+  int n, np;
+};
+__global__ __launch_bounds__(RS_T) void k_rs_hist2(RsPass a, RsPass b, int d) {
+  __shared__ uint32_t c[256];
+  const bool second = (int)blockIdx.x >= a.np;
+  const RsPass& x = second ? b : a;
+  rs_hist(x.kin, x.n, x.np, d, x.hist, second ? (int)blockIdx.x - a.np : (int)blockIdx.x, c);
+}
+__global__ __launch_bounds__(256) void k_rs_scan_rows2(RsPass a, RsPass b) {
+  const bool second = blockIdx.x >= 256 / 4;
+  const RsPass& x = second ? b : a;
+  rs_scan_rows(x.hist, x.np, x.tot, (int)blockIdx.x - (second ? 256 / 4 : 0));
+}
+__global__ __launch_bounds__(RS_T) void k_rs_scatter2(RsPass a, RsPass b, int d) {
+  __shared__ uint32_t run[256];
+  __shared__ uint32_t wc[RS_T / 64][256];
+  const bool second = (int)blockIdx.x >= a.np;
+  const RsPass& x = second ? b : a;
+  rs_scatter(x.kin, x.vin, x.n, x.np, d, x.hist, x.tot, x.kout, x.vout,
+             second ? (int)blockIdx.x - a.np : (int)blockIdx.x, run, wc);
 }
 
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -327,6 +391,51 @@ bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, in
     hipLaunchKernelGGL(k_rs_scan_rows, dim3(256 / 4), dim3(256), 0, st, hist, np, tot);
     hipLaunchKernelGGL(k_rs_scatter, dim3(np), dim3(RS_T), 0, st, kin, even ? v0 : v1, n, np, d, hist, tot,
                        even ? k1 : k0, vout);
+  }
+  return hipGetLastError() == hipSuccess;
+}
+
+// The step's MU and MS groupings (same results as two group_messages calls) in 13 launches instead of
+// 26: one k_sig2, then per radix pass one hist, one scan and one scatter launch over both sorts' partitions
+bool group_messages2(const void* bank_dev, const sdx_pulse_batch& bmu, int32_t* omu, sdx_msg_rec* rmu, uint8_t* wmu,
+                     size_t cmu, const sdx_pulse_batch& bms, int32_t* oms, sdx_msg_rec* rms, uint8_t* wms, size_t cms,
+                     hipStream_t st) {
+  static_assert(RS_PASSES == RS_PASSES_MS, "one pass count for both sorts");
+  const int nmu = bmu.sel_dev ? bmu.n_sel : bmu.n, nms = bms.sel_dev ? bms.n_sel : bms.n;
+  if (nmu <= 0 || nms <= 0 || cmu < group_bytes(nmu) || cms < group_bytes(nms)) return false;
+  struct Side {
+    uint32_t *k0, *v0, *k1, *v1, *hist, *tot;
+    int n, np;
+  };
+  auto side = [](uint8_t* work, int n) {
+    Side x;
+    const size_t a = align256(4 * (size_t)n);
+    x.n = n;
+    x.np = (n + RS_PART - 1) / RS_PART;
+    x.k0 = reinterpret_cast<uint32_t*>(work);
+    x.v0 = reinterpret_cast<uint32_t*>(work + a);
+    x.k1 = reinterpret_cast<uint32_t*>(work + 2 * a);
+    x.v1 = reinterpret_cast<uint32_t*>(work + 3 * a);
+    x.hist = reinterpret_cast<uint32_t*>(work + 4 * a);
+    x.tot = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)x.np));
+    return x;
+  };
+  const Side A = side(wmu, nmu), B = side(wms, nms);
+  const int gmu = (nmu + 255) / 256, gms = (nms + 255) / 256;
+  hipLaunchKernelGGL(k_sig2, dim3(gmu + gms), dim3(256), 0, st, bank_dev, SigSide{bmu, A.k0, A.v0, rmu},
+                     SigSide{bms, B.k0, B.v0, rms}, gmu);
+  for (int pi = 0; pi < RS_PASSES; ++pi) {
+    const int d = 4 - RS_PASSES + pi;
+    const bool even = (pi & 1) == 0;
+    const bool last = pi == RS_PASSES - 1;
+    auto pass = [&](const Side& x, int32_t* order) {
+      return RsPass{even ? x.k0 : x.k1, even ? x.v0 : x.v1, even ? x.k1 : x.k0,
+                    last ? reinterpret_cast<uint32_t*>(order) : (even ? x.v1 : x.v0), x.hist, x.tot, x.n, x.np};
+    };
+    const RsPass pa = pass(A, omu), pb = pass(B, oms);
+    hipLaunchKernelGGL(k_rs_hist2, dim3(A.np + B.np), dim3(RS_T), 0, st, pa, pb, d);
+    hipLaunchKernelGGL(k_rs_scan_rows2, dim3(2 * (256 / 4)), dim3(256), 0, st, pa, pb);
+    hipLaunchKernelGGL(k_rs_scatter2, dim3(A.np + B.np), dim3(RS_T), 0, st, pa, pb, d);
   }
   return hipGetLastError() == hipSuccess;
 }

@@ -2781,6 +2781,9 @@ namespace sdx {
 size_t group_bytes(int n);  // sdx_group.hip
 bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, int32_t* order, sdx_msg_rec* mrec, uint8_t* work,
                     size_t bytes, hipStream_t st);
+bool group_messages2(const void* bank_dev, const sdx_pulse_batch& bmu, int32_t* omu, sdx_msg_rec* rmu, uint8_t* wmu,
+                     size_t cmu, const sdx_pulse_batch& bms, int32_t* oms, sdx_msg_rec* rms, uint8_t* wms, size_t cms,
+                     hipStream_t st);
 // for the other translation units (sdx_lines.hip, sdx_mn.hip): the error text of sdx_last_error()
 // and the bank handle's fields
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
@@ -2984,6 +2987,33 @@ int sdx_group_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
   if (!sdx::group_messages(bank->dev, kind, *batch, order_dev, mrec_dev, (uint8_t*)work_dev, work_cap,
                            (hipStream_t)hip_stream))
     return fail(SDX_EHIP, "message grouping (k_sig / radix sort) launch failed");
+  return SDX_OK;
+}
+
+int sdx_group_step(const sdx_bank* bank, const sdx_group_job* mu, const sdx_group_job* ms, void* hip_stream) {
+  if (!bank || !mu || !ms || !mu->batch || !ms->batch) return fail(SDX_EINVAL, "null argument");
+  const sdx_group_job* job[2] = {mu, ms};
+  for (int k = 0; k < 2; ++k) {
+    const sdx_group_job& j = *job[k];
+    if (!j.order_dev || !j.work_dev) return fail(SDX_EINVAL, "sdx_group_step: null order / work");
+    if ((uintptr_t)j.mrec_dev & 127) return fail(SDX_EINVAL, "mrec_dev must be 128-byte aligned");
+    const int n = j.batch->sel_dev ? j.batch->n_sel : j.batch->n;
+    if (n > 0 && j.work_cap < sdx::group_bytes(n))
+      return fail(SDX_EINVAL, "grouping workspace smaller than sdx_group_work_bytes(n)");
+  }
+  if (!ms->batch->cp_slot_dev || !ms->batch->ms_ok_dev) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+  const int nmu = mu->batch->sel_dev ? mu->batch->n_sel : mu->batch->n;
+  const int nms = ms->batch->sel_dev ? ms->batch->n_sel : ms->batch->n;
+  if (nmu <= 0 || nms <= 0) {  // one side empty: the single grouping of the other
+    const sdx_group_job& j = nmu > 0 ? *mu : *ms;
+    if ((nmu > 0 ? nmu : nms) <= 0) return SDX_OK;
+    return sdx_group_pulses(bank, nmu > 0 ? SDX_KIND_MU : SDX_KIND_MS, j.batch, j.order_dev, j.mrec_dev, j.work_dev,
+                            j.work_cap, hip_stream);
+  }
+  if (!sdx::group_messages2(bank->dev, *mu->batch, mu->order_dev, mu->mrec_dev, (uint8_t*)mu->work_dev, mu->work_cap,
+                            *ms->batch, ms->order_dev, ms->mrec_dev, (uint8_t*)ms->work_dev, ms->work_cap,
+                            (hipStream_t)hip_stream))
+    return fail(SDX_EHIP, "message grouping (k_sig2 / radix sort) launch failed");
   return SDX_OK;
 }
 

@@ -46,7 +46,7 @@ EXPORTED = ["sdx_abi_version", "sdx_last_error", "sdx_source_hash", "sdx_layout_
             "sdx_exchange_unpack", "sdx_pulses_work_bytes", "sdx_group_work_bytes", "sdx_group_pulses",
             "sdx_general_work_bytes", "sdx_demod_pulses_general", "sdx_mc_general_work_bytes", "sdx_demod_mc_general",
             "sdx_lines_general", "sdx_copy_async", "sdx_copy_async_kind", "sdx_copy_async_narrow",
-            "sdx_fill_async", "sdx_demod_step"]
+            "sdx_fill_async", "sdx_demod_step", "sdx_group_step"]
 GROUP_MIN = int(os.environ.get("SDX_GROUP_MIN", "4096"))   # SDX_GROUP_MIN (the env: A/B of the grouping)
 
 
@@ -130,6 +130,11 @@ class SdxStep(Structure):
                 ("ms_out", POINTER(SdxOut)), ("mc", POINTER(SdxMcBatch)), ("mc_out", POINTER(SdxOut))]
 
 
+class SdxGroupJob(Structure):
+    _fields_ = [("batch", POINTER(SdxPulseBatch)), ("order_dev", c_void_p), ("mrec_dev", c_void_p),
+                ("work_dev", c_void_p), ("work_cap", c_size_t)]
+
+
 class SdxLines(Structure):
     _fields_ = [("bytes_dev", c_void_p), ("offsets_dev", c_void_p), ("n", c_int32)]
 
@@ -204,6 +209,8 @@ def load_library(path: Optional[str] = None):
                                       POINTER(SdxLinesGeneralOut), c_void_p]
     lib.sdx_lines_general.restype = c_int
     lib.sdx_demod_mc.argtypes = [c_void_p, POINTER(SdxMcBatch), POINTER(SdxOut), c_void_p]
+    lib.sdx_group_step.restype = c_int
+    lib.sdx_group_step.argtypes = [c_void_p, POINTER(SdxGroupJob), POINTER(SdxGroupJob), c_void_p]
     lib.sdx_demod_step.restype = c_int
     lib.sdx_demod_step.argtypes = [c_void_p, POINTER(SdxStep), c_void_p]
     lib.sdx_demod_mc.restype = c_int
@@ -415,6 +422,24 @@ class Engine:
                                                    _ptr(mrec) if want else None, _ptr(work),
                                                    int(work.numel()), self.stream_ptr()))
         return order[:n]
+
+    def group_step(self, mu_bd, ms_bd, mu_bufs, ms_bufs, mu_sel=None, ms_sel=None):
+        """The MU and MS groupings of one mixed step in the same launches (sdx_group_step, ABI 14): the
+        orders group(KIND_MU, ...) and group(KIND_MS, ...) return, as (mu_order, ms_order)."""
+        um = self.use_mrec
+        jobs, keep = [], []
+        for kind, bd, bufs, sel in ((KIND_MU, mu_bd, mu_bufs, mu_sel), (KIND_MS, ms_bd, ms_bufs, ms_sel)):
+            order, work, mrec = bufs
+            b = self._pulse_batch(bd, sel)
+            want = um if isinstance(um, bool) else kind in um
+            keep.append(b)
+            jobs.append(SdxGroupJob(ctypes.pointer(b), _ptr(order), _ptr(mrec) if want else None, _ptr(work),
+                                    int(work.numel())))
+        _check(self.lib, self.lib.sdx_group_step(self.handle, ctypes.byref(jobs[0]), ctypes.byref(jobs[1]),
+                                                 self.stream_ptr()))
+        n_mu = int(mu_sel.numel()) if mu_sel is not None else mu_bd["n"]
+        n_ms = int(ms_sel.numel()) if ms_sel is not None else ms_bd["n"]
+        return mu_bufs[0][:n_mu], ms_bufs[0][:n_ms]
 
     def alloc_out(self, n: int, rec_cap: int, heap_cap: int, work_bytes: int = 0, wire: bool = False):
         """Output buffers of one launch.  ``wire``: also the exchange's per-message counts and

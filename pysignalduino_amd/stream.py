@@ -42,6 +42,7 @@ _KINDS = (("MU", runtime.KIND_MU, runtime.SEL_MU_SHORT, runtime.SEL_MU_LONG),
 
 
 _FUSE = os.environ.get("SDX_STREAM_FUSE", "1") != "0"
+_GROUP2 = os.environ.get("SDX_STREAM_GROUP2", "1") != "0"   # A/B: one sdx_group_step vs two groupings
 
 
 class ChunkResult:
@@ -304,6 +305,11 @@ class LineStream:
             # MU short, MS short and MC as ONE k_step launch (sdx_demod_step: each kind's tiles take the
             # slots the previous kind's last tiles free); the long variants and MN keep their own
             step = {}
+            # both short classes grouped: one sdx_group_step (the two sorts' passes in the same launches)
+            orders = {}
+            mu_s, ms_s = runtime.SEL_MU_SHORT, runtime.SEL_MS_SHORT
+            if _GROUP2 and "MU" in s.outs and "MS" in s.outs and min(cnt[mu_s], cnt[ms_s]) >= runtime.GROUP_MIN:
+                orders["MU"], orders["MS"] = eng.group_step(pb, pb, s.gbufs["MU"], s.gbufs["MS"], sels[mu_s], sels[ms_s])
             for name, kd, short, long_ in _KINDS:
                 o = s.outs.get(name)
                 if o is None:
@@ -319,7 +325,8 @@ class LineStream:
                     if cnt[short]:
                         step["mc"] = (lb.mc_batch(), o, sels[short])
                 elif cnt[short]:   # the grouped order (the slot's own grouping buffers: no shared cache)
-                    sel = (eng.group(kd, pb, sels[short], bufs=s.gbufs[name]) if cnt[short] >= runtime.GROUP_MIN
+                    sel = (orders[name] if name in orders else
+                           eng.group(kd, pb, sels[short], bufs=s.gbufs[name]) if cnt[short] >= runtime.GROUP_MIN
                            else sels[short])
                     step[name.lower()] = (pb, o, sel, None)
             if step and _FUSE:

@@ -399,6 +399,33 @@ def test_fused_step_matches_the_separate_launches(mrec, mc_known, n):
     assert n == 1 or nres > n
 
 
+@pytest.mark.parametrize("n_mu,n_ms,mrec", [(333333, 333333, False), (5000, 2049, True), (2049, 1, False)])
+def test_group_step_matches_two_groupings(n_mu, n_ms, mrec):
+    """sdx_group_step (ABI 14: the MU and MS sorts' radix passes in the same launches) writes the orders
+    (and message records) of two sdx_group_pulses calls, byte for byte -- at the bench size, with
+    records, and with a one-message side."""
+    import torch
+    from pysignalduino_amd import bank as B, runtime, synth
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    eng.use_mrec = mrec
+    bd = {"MU": eng.to_device_pulses(synth.mu_corpus(bk.protocols, n_mu, seed=9501)),
+          "MS": eng.to_device_pulses(synth.ms_corpus(bk.protocols, n_ms, seed=9502))}
+    one = {k: eng.group_buffers(bd[k]["n"]) for k in bd}
+    two = {k: eng.group_buffers(bd[k]["n"]) for k in bd}
+    for k, kd in (("MU", runtime.KIND_MU), ("MS", runtime.KIND_MS)):
+        eng.group(kd, bd[k], bufs=one[k])
+    o_mu, o_ms = eng.group_step(bd["MU"], bd["MS"], two["MU"], two["MS"])
+    torch.cuda.synchronize()
+    assert o_mu.numel() == n_mu and o_ms.numel() == n_ms
+    for k in bd:
+        n = bd[k]["n"]
+        assert torch.equal(one[k][0][:n], two[k][0][:n]), k
+        if mrec:
+            nb = n * runtime.MREC_BYTES
+            assert torch.equal(one[k][2][:nb], two[k][2][:nb]), k
+
+
 @pytest.mark.parametrize("kind,n", [("MU", 333333), ("MS", 5000), ("MU", 2049), ("MS", 1)])
 def test_grouping_is_a_stable_sort_of_the_keys(kind, n):
     """sdx_group_pulses (k_sig + the 2-launch-per-pass radix sort, sdx_group.hip): the order is a
