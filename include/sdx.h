@@ -560,13 +560,15 @@ int sdx_exchange_unpack(const sdx_bank* bank, int kind, const sdx_xchg_wire* ran
 #define SDX_LONG_MAX 4096   /* sdx_demod_pulses_long */
 #define SDX_MC_HEX_MAX 128  /* sdx_demod_mc */
 #define SDX_MN_HEX_MAX 4096 /* sdx_demod_mn */
+/* ABI 14: MC lines of <= SDX_MC_SHORT_HEX characters (SDX_SEL_MC) and longer ones (SDX_SEL_MC_LONG) are
+ * separate classes, so a caller knows the short list's length bound (sdx_mc_batch.max_hex, sdx_demod_step) */
 enum sdx_sel_class { SDX_SEL_MU_SHORT = 0, SDX_SEL_MU_LONG = 1, SDX_SEL_MS_SHORT = 2, SDX_SEL_MS_LONG = 3,
-                     SDX_SEL_MC = 4, SDX_SEL_MN = 5, SDX_SEL_NCLASS = 6 };
+                     SDX_SEL_MC = 4, SDX_SEL_MC_LONG = 5, SDX_SEL_MN = 6, SDX_SEL_NCLASS = 7 };
 #define SDX_SEL_CHUNK 1024  /* lines per selection workgroup */
 /* Selection lists for the demodulation launches, built on the device in line order: the OK lines
  * of each class (MS lines whose string gates failed are left out -- they have no results).  Class
  * k's line indices are sel_dev[start_k, start_k + counts[k]) with start_k = counts[0] + ... +
- * counts[k-1]; counts_dev[0..5] receives the class sizes (the only value a host needs back, to size
+ * counts[k-1]; counts_dev[0..6] receives the class sizes (the only value a host needs back, to size
  * the launches).  scratch_dev: 8 * ceil(n / SDX_SEL_CHUNK) int32.  Pass each list as sel_dev of an
  * sdx_pulse_batch / sdx_mc_batch whose arrays are the sdx_lines_out arrays (offsets = doff_dev,
  * len = dlen_dev, data = slot_dev). */

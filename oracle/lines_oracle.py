@@ -354,4 +354,6 @@ def sel_class(r: Dict[str, Any]) -> int:
         return 0 if n <= SHORT_MAX else 1
     if r["kind"] == MS:
         return -1 if not r["ms_ok"] else (2 if n <= SHORT_MAX else 3)
-    return 4 if r["kind"] == MC else 5 if r["kind"] == MN else -1
+    if r["kind"] == MC:   # ABI 14: <= SDX_MC_SHORT_HEX (64) characters, longer
+        return 4 if n <= 64 else 5
+    return 6 if r["kind"] == MN else -1

@@ -1552,7 +1552,7 @@ LD int sel_class(const sdx_lines_out& o, int i) {
     if (!o.ms_ok_dev[i]) return -1;
     return n <= SDX_SHORT_MAX ? SDX_SEL_MS_SHORT : SDX_SEL_MS_LONG;
   }
-  if (k == SDX_LINE_MC) return SDX_SEL_MC;
+  if (k == SDX_LINE_MC) return n <= SDX_MC_SHORT_HEX ? SDX_SEL_MC : SDX_SEL_MC_LONG;
   if (k == SDX_LINE_MN) return SDX_SEL_MN;
   return -1;
 }

@@ -135,6 +135,12 @@ class LineBatch:
         start = np.concatenate([[0], np.cumsum(cnt)])
         return [self.sel[int(start[k]): int(start[k + 1])] for k in range(runtime.SEL_NCLASS)], cnt
 
+    def mc_all(self, cnt):
+        """Every MC line's index (the short and the long class: adjacent in sel) and their count."""
+        a = int(np.sum(cnt[: runtime.SEL_MC]))
+        k = int(cnt[runtime.SEL_MC]) + int(cnt[runtime.SEL_MC_LONG])
+        return self.sel[a: a + k], k
+
     def pulse_batch(self):
         return {"data": self.slot, "offsets": self.doff, "npat": self.npat, "pat_id": self.pat_id,
                 "pat_val": self.pat_val, "cp_slot": self.cp_slot, "ms_ok": self.ms_ok, "len": self.dlen, "n": self.n}
@@ -263,8 +269,9 @@ class SignalParser:
         if cnt[runtime.SEL_MS_SHORT] or cnt[runtime.SEL_MS_LONG]:
             res["MS"] = eng.run(runtime.KIND_MS, pb, sel_short=sels[runtime.SEL_MS_SHORT],
                                 sel_long=sels[runtime.SEL_MS_LONG])
-        if self.protocols.mc_mode == "fixed" and cnt[runtime.SEL_MC]:
-            res["MC"] = eng.run(runtime.KIND_MC, lb.mc_batch(), sel_short=sels[runtime.SEL_MC])
+        mc_sel, mc_n = lb.mc_all(cnt)
+        if self.protocols.mc_mode == "fixed" and mc_n:
+            res["MC"] = eng.run(runtime.KIND_MC, lb.mc_batch(), sel_short=mc_sel)
         if cnt[runtime.SEL_MN]:
             # result space: <= (MN protocols) records of <= (preamble + frame) bytes per line
             nmn = int(cnt[runtime.SEL_MN])
@@ -465,10 +472,10 @@ class SignalParser:
             k = int(cnt[runtime.SEL_MS_SHORT] + cnt[runtime.SEL_MS_LONG])
             jobs.append((runtime.KIND_MS, 4 * k + 1024, 64 * k + 65536, 300 * k + 65536,
                          [(pb, sels[runtime.SEL_MS_SHORT], False), (pb, sels[runtime.SEL_MS_LONG], True)]))
-        if self.protocols.mc_mode == "fixed" and cnt[runtime.SEL_MC]:
-            k = int(cnt[runtime.SEL_MC])
+        mc_sel, k = lb.mc_all(cnt)
+        if self.protocols.mc_mode == "fixed" and k:
             jobs.append((runtime.KIND_MC, 4 * k + 1024, 96 * k + 65536, 400 * k + 65536,
-                         [(lb.mc_batch(), sels[runtime.SEL_MC], False)]))
+                         [(lb.mc_batch(), mc_sel, False)]))
         if cnt[runtime.SEL_MN]:
             k = int(cnt[runtime.SEL_MN])
             jobs.append((runtime.KIND_MN, len(bk.mn_pids) * k + 1024, int(4 * len(data) + 64 * k + 65536),

@@ -148,7 +148,9 @@ class SdxLinesOut(Structure):
 # include/sdx.h front-end constants
 LINE_NONE, LINE_MU, LINE_MS, LINE_MC, LINE_MN = 0, 1, 2, 3, 4
 LS_OK, LS_NOFRAME, LS_NOPARSER, LS_INVALID, LS_NODATA, LS_UNSUPPORTED, LS_RAISES, LS_GENERAL = 0, 1, 2, 3, 4, 5, 6, 7
-SEL_MU_SHORT, SEL_MU_LONG, SEL_MS_SHORT, SEL_MS_LONG, SEL_MC, SEL_MN, SEL_NCLASS = 0, 1, 2, 3, 4, 5, 6
+# (ABI 14: MC lines of <= SDX_MC_SHORT_HEX characters and longer ones are separate classes)
+SEL_MU_SHORT, SEL_MU_LONG, SEL_MS_SHORT, SEL_MS_LONG, SEL_MC, SEL_MC_LONG, SEL_MN, SEL_NCLASS = 0, 1, 2, 3, 4, 5, 6, 7
+MC_SHORT_HEX = 64   # SDX_MC_SHORT_HEX
 SEL_CHUNK = 1024
 
 _LIB = None

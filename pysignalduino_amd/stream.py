@@ -37,12 +37,13 @@ from .packing import ContractError
 
 _KINDS = (("MU", runtime.KIND_MU, runtime.SEL_MU_SHORT, runtime.SEL_MU_LONG),
           ("MS", runtime.KIND_MS, runtime.SEL_MS_SHORT, runtime.SEL_MS_LONG),
-          ("MC", runtime.KIND_MC, runtime.SEL_MC, None),
+          ("MC", runtime.KIND_MC, runtime.SEL_MC, runtime.SEL_MC_LONG),
           ("MN", runtime.KIND_MN, runtime.SEL_MN, None))
 
 
 _FUSE = os.environ.get("SDX_STREAM_FUSE", "1") != "0"
 _GROUP2 = os.environ.get("SDX_STREAM_GROUP2", "1") != "0"   # A/B: one sdx_group_step vs two groupings
+_MC_SEP = os.environ.get("SDX_STREAM_MC_SEP") == "1"   # A/B: MC's short class in its own launch
 
 
 class ChunkResult:
@@ -124,7 +125,21 @@ class _Slot:
             self.outs[name] = eng.alloc_out(C, rc, hc, eng.pulses_work_bytes(C) if name in ("MU", "MS") else 0,
                                             wire=ls.output == "wire" and name != "MN")
         self.gbufs = {name: eng.group_buffers(C) for name in ("MU", "MS")}
-        self.cursors = t.zeros((len(self.outs), 4), dtype=t.int32, device=eng.dev)
+        # what a chunk resets before its launches -- the cursors, every kind's descriptors (lines of other
+        # classes keep an empty one) and exchange counts -- in ONE block, reset by one fill per chunk
+        # (seven hipMemsetAsync blit kernels per chunk before)
+        parts, off = [], 0
+        for name, o in self.outs.items():
+            parts.append((name, "desc", off, 8 * C))
+            off = (off + 8 * C + 255) & ~255
+            if o.get("wire") is not None:
+                parts.append((name, "wire", off, 8 * C))
+                off = (off + 8 * C + 255) & ~255
+        self.zblock = t.zeros(off + 16 * len(self.outs), dtype=t.uint8, device=eng.dev)
+        for name, field, o0, nb in parts:
+            v = self.zblock[o0: o0 + nb]
+            self.outs[name][field] = v.view(t.int64) if field == "wire" else v
+        self.cursors = self.zblock[off:].view(t.int32).view(len(self.outs), 4)
         for j, o in enumerate(self.outs.values()):
             o["cursor"] = self.cursors[j]
         if ls.output == "json":
@@ -300,7 +315,7 @@ class LineStream:
             sd.wait_event(s.parse_ev)
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
             e0.record(sd)
-            runtime.fill_async(s.cursors, sd)
+            runtime.fill_async(s.zblock, sd)   # cursors, descriptors, exchange counts
             pb = lb.pulse_batch()
             # MU short, MS short and MC as ONE k_step launch (sdx_demod_step: each kind's tiles take the
             # slots the previous kind's last tiles free); the long variants and MN keep their own
@@ -315,15 +330,13 @@ class LineStream:
                 if o is None:
                     continue
                 o["n"] = n
-                runtime.fill_async(o["desc"][: 8 * n], sd)   # lines of other classes keep an empty descriptor
-                if o.get("wire") is not None:
-                    runtime.fill_async(o["wire"][:n], sd)     # ... and no exchange counts
                 if kd == runtime.KIND_MN:
                     if cnt[short]:
                         eng.launch_mn(lb.mn_batch(), o, elig=self.elig, sel=sels[short])
                 elif kd == runtime.KIND_MC:
-                    if cnt[short]:
-                        step["mc"] = (lb.mc_batch(), o, sels[short])
+                    if cnt[short]:   # <= 64 characters (the class's bound): part of the fused kernel
+                        step["mc"] = (dict(lb.mc_batch(), max_hex=0 if _MC_SEP else runtime.MC_SHORT_HEX), o,
+                                      sels[short])
                 elif cnt[short]:   # the grouped order (the slot's own grouping buffers: no shared cache)
                     sel = (orders[name] if name in orders else
                            eng.group(kd, pb, sels[short], bufs=s.gbufs[name]) if cnt[short] >= runtime.GROUP_MIN
@@ -339,7 +352,10 @@ class LineStream:
                     eng.launch_mc(step["mc"][0], step["mc"][1], sel=step["mc"][2])
             for name, kd, short, long_ in _KINDS:
                 if long_ is not None and cnt[long_] and name in s.outs:
-                    eng.launch_pulses(kd, pb, s.outs[name], sel=sels[long_], long_variant=True)
+                    if kd == runtime.KIND_MC:   # 65..128 characters
+                        eng.launch_mc(lb.mc_batch(), s.outs[name], sel=sels[long_])
+                    else:
+                        eng.launch_pulses(kd, pb, s.outs[name], sel=sels[long_], long_variant=True)
             s.cnt = cnt
             if self.output == "json":
                 jo = s.jout

@@ -199,7 +199,7 @@ def _compare(lines, dv):
 
 def _check_selection(lines, dv):
     classes = [LO.sel_class(LO.parse_line(ln)) for ln in lines]
-    for k in range(6):
+    for k in range(7):
         exp = [i for i, c in enumerate(classes) if c == k]
         assert int(dv["counts"][k]) == len(exp), k
         assert list(dv["sels"][k]) == exp, k

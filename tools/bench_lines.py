@@ -124,12 +124,14 @@ def main():
             ev["parse+select"][1].record(stream)
         sels, cnt = lb.selections()  # 32-byte read-back: sizes the launches
         for k, short, long_ in (("MU", runtime.SEL_MU_SHORT, runtime.SEL_MU_LONG),
-                                ("MS", runtime.SEL_MS_SHORT, runtime.SEL_MS_LONG), ("MC", runtime.SEL_MC, None)):
+                                ("MS", runtime.SEL_MS_SHORT, runtime.SEL_MS_LONG), ("MC", runtime.SEL_MC, runtime.SEL_MC_LONG)):
             if record:
                 ev[k][0].record(stream)
             if k == "MC":
-                if cnt[short]:
-                    eng.launch_mc(mb, outs[k], sel=sels[short])
+                if cnt[short]:   # frames of <= 64 characters: the 4-word kernel only
+                    eng.launch_mc(dict(mb, max_hex=runtime.MC_SHORT_HEX), outs[k], sel=sels[short])
+                if cnt[long_]:
+                    eng.launch_mc(mb, outs[k], sel=sels[long_])
             else:
                 kind = runtime.KIND_MU if k == "MU" else runtime.KIND_MS
                 if cnt[short]:

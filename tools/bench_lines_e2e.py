@@ -49,7 +49,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lines", type=int, default=1_000_000, help="corpus lines (streamed --passes times)")
     ap.add_argument("--chunk", type=int, default=250_000)
-    ap.add_argument("--passes", type=int, default=8)
+    ap.add_argument("--passes", type=int, default=40, help="timed passes over the corpus (40 x 1M lines: ~0.2 s, steadier than 8)")
     ap.add_argument("--lag", type=int, default=3)
     ap.add_argument("--output", default="wire", choices=("wire", "json"))
     ap.add_argument("--check", action="store_true")
