@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--group-separate", action="store_true",
                     help="the MU and MS groupings as two sdx_group_pulses calls (26 launches) instead of one "
                          "sdx_group_step (13 launches; A/B)")
+    ap.add_argument("--mc-apart", action="store_true",
+                    help="A/B: MC's frames in their own launch after k_step (MU + MS) instead of k_step's last range")
     ap.add_argument("--group-reuse", action="store_true",
                     help="DIAGNOSTIC, not a valid line: group the batch in the first two steps only and reuse "
                          "the orders (what the per-step grouping costs the step)")
@@ -412,7 +414,8 @@ def main():
             for k in ("MU", "MS"):
                 parts[k.lower()] = (bds[k], outs[s_][k], gbufs[k][par][0][:corp[k].n],
                                     gbufs[k][par][2] if k in mrec_kinds else None)
-            eng.launch_step(mu=parts["mu"], ms=parts["ms"], mc=(bds["MC"], outs[s_]["MC"], None))
+            eng.launch_step(mu=parts["mu"], ms=parts["ms"],
+                            mc=(dict(bds["MC"], max_hex=0) if args.mc_apart else bds["MC"], outs[s_]["MC"], None))
             e1 = torch.cuda.Event(enable_timing=tm)
             e1.record(stream)
             if tm:
