@@ -2344,13 +2344,6 @@ __global__ __launch_bounds__(256) void k_copy_narrow(uint8_t* __restrict__ dst, 
 // =============================================================================================
 // MC engine (manchester.py "fixed" chain), lane = frame, 12 clockrange protocols uniform
 // =============================================================================================
-#ifndef SDX_MC_SPLIT
-#ifdef SDX_PROF
-#define SDX_MC_SPLIT 0  // the phase probes live in mc_block
-#else
-#define SDX_MC_SPLIT 1  // k_mc's short frames: the protocol loop split over wave pairs (mc_block_split)
-#endif
-#endif
 #ifndef SDX_STEP_ORDER
 #define SDX_STEP_ORDER 0
 #endif
@@ -2679,210 +2672,10 @@ SDX_DEV void mc_block(const void* __restrict__ bank, const sdx_mc_batch& b, cons
 #undef MCPROF_ADD
 }
 
-// The short frames with the protocol loop split over a wave PAIR (SDX_MC_SPLIT): 128 frames per 256
-// threads; waves 2q and 2q + 1 both hold frames [64q, 64q + 64) of the block and evaluate the even and
-// the odd protocols.  A wave's time is its frames' serial chain through the protocols, and the last
-// round of k_mc's (or k_step's MC range's) waves ran alone for that long; the split halves it.  Outcome
-// as the sequential loop: a frame's records in protocol order (a protocol gives a frame at most one
-// record, so a record's rank is the number of the frame's result protocols below it), and the first
-// raise in protocol order -- the smaller of the two waves' first raises -- drops all its results.  The
-// pair allocates one record range and one heap range; the exchange after the loop reuses the (then
-// dead) bit rows.  Every wave runs the same barriers (k_step's two MC halves included).
-template <int MW>
-SDX_DEV void mc_block_split(const void* __restrict__ bank, const sdx_mc_batch& b, const sdx_out& out, const int blk,
-                            const int tid, McLds<MW>& L) {
-  static_assert(MW * 256 * 8 >= 4 * (256 + 64) && MW * 256 * 8 >= 8 * 4 * 64, "exchange fits the bit rows");
-  const BankView bv = bank_view(bank);
-  const int wave = tid >> 6, lane = tid & 63, sub = wave & 1, pair = wave >> 1;
-  const int ntot = b.sel_dev ? b.n_sel : b.n;
-  const int gi = blk * 128 + pair * 64 + lane;
-  bool valid = gi < ntot;
-  const int msg = valid ? (b.sel_dev ? b.sel_dev[gi] : gi) : 0;
-  if (valid) {
-    const int hl0 = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - b.offsets_dev[msg]);
-    valid = hl0 <= MC_SHORTW * 16;  // longer frames: the LONG launch's
-  }
-  int w_heap = 0, w_rec = 0;
-  bool w_ovf = false;
-  const LaneBits BN{&L.bn[tid], MW, false}, BI{&L.bi[tid], MW, false};
-  int nN = 0, nI = 0;
-  bool hex_ok = false;
-  int clock = 0, mcbit = 0, flags = 0, only = -1;
-  if (valid) {
-    const int64_t off = b.offsets_dev[msg];
-    const int hl = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
-    clock = b.clock_dev[msg];
-    mcbit = b.mcbitnum_dev[msg];
-    flags = b.flags_dev[msg];
-    if (b.only_dev) only = b.only_dev[msg];
-    hex_ok = hl > 0 && hl <= MW * 16;
-    if (hex_ok) mc_stage<MW>(b.hex_dev + off, hl, &L.bn[tid], &L.bi[tid], &nN, &nI, &hex_ok);
-  }
-  const int nmc = (int)bv.hdr->n_mc;
-  int raise = 0, rproto = 255;
-  uint32_t mask = 0;  // this wave's protocols with a record for the lane's frame
-  for (int p = sub; p < nmc; p += 2) {
-    const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
-    bool go = valid && !raise && (only < 0 || only == p);
-    if (go && mcbit < (cld(&r->has_lmin) ? cld(&r->lmin) : -1)) go = false;
-    if (go && mcbit > (cld(&r->has_lmax) ? cld(&r->lmax) : 9999)) go = false;
-    if (go && cld(&r->has_cr) && !((double)clock > cld(&r->cr_lo) && (double)clock < cld(&r->cr_hi))) go = false;
-    McOut o{0, 0, 0, 0, 0, 0, 0, 0};
-    const bool inv = (cld(&r->invert) != 0) ^ ((flags & 3) != 0);
-    const LaneBits& B = inv ? BI : BN;
-    const int nb = inv ? nI : nN;
-    if (go && !hex_ok) { raise = SDX_RAISE_TYPE; rproto = p; go = false; }
-    if (go) {
-      const LaneBits DM{B.base, MW, true};
-      o = mc_method(r, cld(&r->method), B, nb, nb, DM);
-      if (o.rc == -1) { raise = SDX_RAISE_TYPE; rproto = p; o.rc = 0; }
-      if (o.rc == -2) { raise = SDX_RAISE_VALUE; rproto = p; o.rc = 0; }
-    }
-    const bool has = o.rc == 1;
-    if (!ballot(has)) continue;
-    const int plen = has ? cld(&r->pre_len) + o.len : 0;
-    int incl = plen;
-    for (int d = 1; d < WAVE; d <<= 1) {
-      const int t = __shfl_up(incl, d);
-      if (lane >= d) incl += t;
-    }
-    const int wtot = __shfl(incl, WAVE - 1);
-    const uint64_t hm = ballot(has);
-    const int nnew = popc64(hm);
-    const int hb = w_heap, rb = w_rec;
-    const bool fits = hb + wtot <= MC_HEAP_CAP && rb + nnew <= MC_REC_CAP;
-    if (has && fits) {
-      uint8_t* dst = &L.heap[wave][hb + incl - plen];
-      const int pl = cld(&r->pre_len), po = cld(&r->pre_off);
-      for (int i = 0; i < pl; i += 8) {
-        uint8_t c[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) c[j] = (i + j < pl) ? bv.str[po + i + j] : (uint8_t)0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (i + j < pl) dst[i + j] = c[j];
-      }
-      mc_write(r, o, B, nb, nb, dst + cld(&r->pre_len));
-      StageRec sr;
-      sr.off = (uint32_t)(hb + incl - plen);
-      sr.len = (uint16_t)plen;
-      sr.proto = (uint16_t)p;
-      sr.bitlen = 0;
-      sr.msg = (uint16_t)lane;
-      sr.rank = 0;
-      L.rec[wave][rb + lanes_below(hm)] = sr;
-      mask |= 1u << p;
-    }
-    if (fits) {
-      w_heap = hb + wtot;
-      w_rec = rb + nnew;
-    } else if (nnew) {
-      w_ovf = true;
-    }
-  }
-  __syncthreads();  // both waves of every pair are past the loop: the bit rows are dead
-  uint32_t* X = reinterpret_cast<uint32_t*>(&L.bi[0]);  // [256] lane words, [256 + 4 wave] totals, [288 + 2 pair] bases
-  const int nh = (w_heap + 15) & ~15;  // 16-B pieces: every reservation keeps hbase aligned
-  X[tid] = (mask & 0xFFFFu) | ((uint32_t)raise << 16) | ((uint32_t)rproto << 24);
-  if (lane == 0) {
-    X[256 + 4 * wave + 0] = (uint32_t)w_rec;
-    X[256 + 4 * wave + 1] = (uint32_t)nh;
-    X[256 + 4 * wave + 2] = w_ovf ? 1u : 0u;
-  }
-  unsigned long long* wsum = reinterpret_cast<unsigned long long*>(&L.bn[0]) + 64 * pair;  // per pair, per frame
-  const bool wx = out.wire_dev != nullptr;
-  if (wx && sub == 0) wsum[lane] = 0ull;
-  __syncthreads();
-  const uint32_t me = X[tid], peer = X[tid ^ 64];
-  const uint32_t cmask = (me | peer) & 0xFFFFu;
-  const uint32_t ra = (me >> 16) & 0xFFu, rb_ = (peer >> 16) & 0xFFu;
-  const uint32_t pa = me >> 24, pb_ = peer >> 24;
-  const int fraise = (int)(ra && rb_ ? (pa < pb_ ? ra : rb_) : (ra ? ra : rb_));  // the first raise in protocol order
-  const int pw0 = 2 * pair;  // the pair's waves: pw0 (even protocols), pw0 + 1 (odd)
-  const bool bad = X[256 + 4 * pw0 + 2] || X[256 + 4 * (pw0 + 1) + 2];
-  const int mycnt = fraise ? 0 : popc64(cmask);
-  int incl = mycnt;
-  for (int d = 1; d < WAVE; d <<= 1) {
-    const int t = __shfl_up(incl, d);
-    if (lane >= d) incl += t;
-  }
-  const int wrec = __shfl(incl, WAVE - 1);
-  const uint32_t nh0 = X[256 + 4 * pw0 + 1], nh1 = X[256 + 4 * (pw0 + 1) + 1];
-  if (sub == 0 && lane == 0) {
-    uint32_t rbase = 0, hbase = 0, st = bad ? 2u : 0u;
-    if (!bad) {
-      rbase = atomicAdd(&out.cursor_dev[0], (uint32_t)wrec);
-      hbase = atomicAdd(&out.cursor_dev[1], nh0 + nh1);
-      if (rbase + wrec > out.rec_cap || hbase + nh0 + nh1 > out.heap_cap) {
-        st = 3;
-        atomicOr(&out.cursor_dev[2], 1u);
-      }
-    } else {
-      atomicOr(&out.cursor_dev[2], 2u);
-    }
-    X[288 + 4 * pair + 0] = rbase;
-    X[288 + 4 * pair + 1] = hbase;
-    X[288 + 4 * pair + 2] = st;
-  }
-  __syncthreads();
-  const uint32_t rbase = X[288 + 4 * pair + 0], hbase0 = X[288 + 4 * pair + 1];
-  const int st = (int)X[288 + 4 * pair + 2];
-  const uint32_t hbase = hbase0 + (sub ? nh0 : 0u);  // this wave's payload bytes after its partner's
-  if (st == 0) {
-    const int excl = incl - mycnt;
-    for (int i0 = 0; i0 < w_rec; i0 += WAVE) {
-      const int i = i0 + lane;
-      StageRec sr{};
-      if (i < w_rec) sr = L.rec[wave][i];
-      const int fl = i < w_rec ? (int)sr.msg : 0;
-      const int fbase = __shfl(excl, fl), fmsg = __shfl(msg, fl), fr = __shfl(fraise, fl);
-      const uint32_t fm = (uint32_t)__shfl((int)cmask, fl);
-      if (i < w_rec && !fr) {
-        const int rank = popc64(fm & ((1u << sr.proto) - 1u));
-        sdx_result o;
-        o.payload_off = hbase + sr.off;
-        o.payload_len = sr.len;
-        o.proto = sr.proto;
-        o.bit_length = 0;
-        o.msg = (uint32_t)fmsg;
-        out.rec_dev[rbase + fbase + rank] = o;
-        if (wx) {
-          const uint32_t xr = wire_class(bv, SDX_KIND_MC, sr.proto, &L.heap[wave][sr.off], sr.len);
-          if (out.xrec_dev) out.xrec_dev[rbase + fbase + rank] = xr;
-          atomicAdd(&wsum[fl], (unsigned long long)(((uint64_t)sr.len << 32) | wire_bytes_x(xr, sr.len)));
-        }
-      }
-    }
-    const int nhw = sub ? (int)nh1 : (int)nh0;
-    uint4* hd = reinterpret_cast<uint4*>(out.heap_dev + hbase);
-    const uint4* hs = reinterpret_cast<const uint4*>(L.heap[wave]);
-    if ((((uintptr_t)hd) & 15u) == 0) {
-      for (int i = lane; i < (nhw >> 4); i += WAVE) hd[i] = hs[i];
-    } else {
-      for (int i = lane; i < nhw; i += WAVE) out.heap_dev[hbase + i] = L.heap[wave][i];
-    }
-  }
-  if (valid && sub == 0) {
-    sdx_desc d;
-    d.rec_begin = rbase + (uint32_t)(incl - mycnt);
-    if (fraise) { d.status = SDX_ST_RAISED; d.raise_kind = (uint8_t)fraise; d.n_rec = 0; }
-    else if (st) { d.status = st == 2 ? SDX_ST_OVF_TILE : SDX_ST_OVF_OUT; d.raise_kind = 0; d.n_rec = 0; }
-    else { d.status = SDX_ST_OK; d.raise_kind = 0; d.n_rec = (uint16_t)mycnt; }
-    out.desc_dev[msg] = d;
-  }
-  if (wx) {
-    __syncthreads();  // both waves' counts are in
-    if (valid && sub == 0) out.wire_dev[msg] = (!fraise && st == 0) ? (uint64_t)wsum[lane] : 0ull;
-  }
-}
-
 template <int MW, bool LONG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : SDX_MC_WPE))) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
   __shared__ McLds<MW> L;
-  if constexpr (!LONG && SDX_MC_SPLIT)
-    mc_block_split<MW>(bank, b, out, (int)blockIdx.x, (int)threadIdx.x, L);
-  else
-    mc_block<MW, LONG>(bank, b, out, (int)blockIdx.x, (int)threadIdx.x, L);
+  mc_block<MW, LONG>(bank, b, out, (int)blockIdx.x, (int)threadIdx.x, L);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2963,10 +2756,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     ms_tile_by_class(bank, a.ms, a.ms_out, w, U.ms2, U.ms4, msg_of);
   } else {
     const int half = (int)threadIdx.x >> 8;
-    if (SDX_MC_SPLIT)
-      mc_block_split<MC_SHORTW>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
-    else
-      mc_block<MC_SHORTW, false>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
+    mc_block<MC_SHORTW, false>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
   }
 }
 
@@ -3278,10 +3068,9 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
     a.t_ms = (count(b.n, b.n_sel, b.sel_dev) + 63) / 64;
   }
   if (mc_fused) {
-    if (SDX_MC_SPLIT && bank->hdr.n_mc > 16) return fail(SDX_EBANK, "the split MC kernel holds 16 protocols per frame mask");
     a.mc = *step->mc;
     a.mc_out = *step->mc_out;
-    a.b_mc = (count(a.mc.n, a.mc.n_sel, a.mc.sel_dev) + (SDX_MC_SPLIT ? 255 : 511)) / (SDX_MC_SPLIT ? 256 : 512);
+    a.b_mc = (count(a.mc.n, a.mc.n_sel, a.mc.sel_dev) + 511) / 512;
   }
   const long long grid = (long long)a.t_mu + a.t_ms + a.b_mc;
   if (grid > 0x7FFFFFFFll) return fail(SDX_EINVAL, "sdx_demod_step: grid too large");
@@ -3302,13 +3091,11 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
 
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream) {
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
-  if (SDX_MC_SPLIT && bank->hdr.n_mc > 16) return fail(SDX_EBANK, "the split MC kernel holds 16 protocols per frame mask");
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
   if (ntot <= 0) return SDX_OK;
   hipStream_t st = (hipStream_t)hip_stream;
   const int grid = (ntot + 255) / 256;
-  const int grid_short = SDX_MC_SPLIT ? (ntot + 127) / 128 : grid;  // (128 frames per block split over wave pairs)
-  hipLaunchKernelGGL((sdx::k_mc<sdx::MC_SHORTW, false>), dim3(grid_short), dim3(256), 0, st, bank->dev, *batch, *out);
+  hipLaunchKernelGGL((sdx::k_mc<sdx::MC_SHORTW, false>), dim3(grid), dim3(256), 0, st, bank->dev, *batch, *out);
   // the 65..128-character variant only when the caller cannot rule such frames out (VERDICT r04 #4:
   // over a batch without one, its grid of early-exiting waves still held CU slots beside MS)
   if (batch->max_hex <= 0 || batch->max_hex > SDX_MC_SHORT_HEX)
