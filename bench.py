@@ -307,7 +307,12 @@ def main():
     # step j+1 (latency-bound small kernels) runs while step j demodulates; order buffers are
     # double-buffered by step parity.  Every step still groups once.
     gkinds = [k for k in kinds if k != "MC"] if not args.no_group else []
-    side = torch.cuda.Stream(dev, priority=lo_prio)
+    # (SDX_GROUP_PRIO=high / equal: A/B of the side stream's priority)
+    gp = os.environ.get("SDX_GROUP_PRIO", "low")
+    side = torch.cuda.Stream(dev, priority={"low": lo_prio, "high": hi_prio}.get(gp, 0))
+    if gp == "high":   # the launch stream below the grouping's
+        stream = torch.cuda.Stream(dev, priority=lo_prio)
+        torch.cuda.set_stream(stream)
     gbufs = {k: [eng.group_buffers(corp[k].n) for _ in range(2)] for k in gkinds}
     gdone, used = {}, [None, None]
     gev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps + 1)]
