@@ -532,6 +532,24 @@ def main():
     if fused:   # each kind's kernel alone (untimed attribution pass): its own roofline entry
         kt_step = kt["step"]
         kt = attribute_alone(torch, eng, stream, kinds, bds, outs[(j - 1) % nslot], gbufs, corp, mrec_kinds)
+    # the grouping's own time (one step's groupings alone on the launch stream, untimed): group_ms is
+    # the side stream's wall time beside the step's kernel, mostly waiting for CU slots
+    g_alone = None
+    if gkinds:
+        gts = []
+        with torch.cuda.stream(stream):
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                if gkinds == ["MU", "MS"] and not args.group_separate:
+                    eng.group_step(bds["MU"], bds["MS"], gbufs["MU"][0], gbufs["MS"][0])
+                else:
+                    for k in gkinds:
+                        eng.group(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], bufs=gbufs[k][0])
+                e1.record(stream)
+                stream.synchronize()
+                gts.append(e0.elapsed_time(e1) * 1e-3)
+        g_alone = float(np.median(gts))
     dom = max(kt, key=kt.get)
     # every kind's launch against the same HBM roofline: its algorithmic bytes (the
     # outputs of the last step) / its HIP-event time.  In the mixed step MS and MC run side by side
@@ -607,6 +625,7 @@ def main():
                                "MU, then MS beside MC" if mc_beside_ms else "serial")},
         "per_kernel_ms": {**({"step": 1e3 * kt_step} if fused else {}), **{k: 1e3 * v for k, v in kt.items()}},
         "group_ms": 1e3 * gtime,   # sdx_group_pulses of all kinds per step (side stream, one step ahead)
+        "group_alone_ms": None if g_alone is None else 1e3 * g_alone,   # the same groupings alone, untimed
         "per_type_msgs_per_s": {k: per[k] / kt[k] for k in kinds},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": tag,
