@@ -3001,9 +3001,9 @@ int sdx_group_step(const sdx_bank* bank, const sdx_group_job* mu, const sdx_grou
     if (n > 0 && j.work_cap < sdx::group_bytes(n))
       return fail(SDX_EINVAL, "grouping workspace smaller than sdx_group_work_bytes(n)");
   }
-  if (!ms->batch->cp_slot_dev || !ms->batch->ms_ok_dev) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
   const int nmu = mu->batch->sel_dev ? mu->batch->n_sel : mu->batch->n;
   const int nms = ms->batch->sel_dev ? ms->batch->n_sel : ms->batch->n;
+  if (nms > 0 && (!ms->batch->cp_slot_dev || !ms->batch->ms_ok_dev)) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
   if (nmu <= 0 || nms <= 0) {  // one side empty: the single grouping of the other
     const sdx_group_job& j = nmu > 0 ? *mu : *ms;
     if ((nmu > 0 ? nmu : nms) <= 0) return SDX_OK;
