@@ -169,6 +169,25 @@ def test_library_loads_and_exports_every_declared_symbol():
     runtime.check_layout(lib)
 
 
+def test_step_entries_reject_bad_arguments_without_a_gpu():
+    """sdx_demod_step / sdx_group_step (ABI 14) validate before any HIP call: null arguments and a batch
+    without its output come back as SDX_EINVAL with a message (runs on the CPU)."""
+    import ctypes
+    from pysignalduino_amd import runtime
+    lib = runtime.load_library()
+    assert lib.sdx_demod_step(None, None, None) == -1
+    assert b"null" in lib.sdx_last_error()
+    st = runtime.SdxStep()
+    b = runtime.SdxPulseBatch()
+    st.mu = ctypes.pointer(b)                      # a batch without its sdx_out
+    fake_bank = ctypes.c_void_p(1)                 # never dereferenced: the check comes first
+    assert lib.sdx_demod_step(fake_bank, ctypes.byref(st), None) == -1
+    assert b"sdx_out" in lib.sdx_last_error()
+    job = runtime.SdxGroupJob()
+    assert lib.sdx_group_step(None, ctypes.byref(job), ctypes.byref(job), None) == -1
+    assert lib.sdx_group_step(fake_bank, ctypes.byref(job), ctypes.byref(job), None) == -1   # no batches
+
+
 def test_bank_rejects_unmodelled():
     P = bankmod.load_protocols()
     bad = dict(P)
