@@ -8,6 +8,8 @@ all-gather of the decoded dmsg buffers (BASELINE config 5).  Weak scaling: each 
 ``--msgs`` messages (1/3 of each type).
 
 Prints ONE JSON line on rank 0 (contract in the task statement); see DESIGN.md §Measurement.
+The mixed step runs as ONE kernel (k_step, sdx_demod_step: MU, then MS, then MC tiles) beside the
+next step's grouping on a low-priority side stream (sdx_group_step).
 """
 from __future__ import annotations
 
@@ -355,7 +357,7 @@ def main():
     # --concurrent: one stream per kind, the three launches of a step run concurrently (the tail of
     # one kernel overlaps the others' tiles); default: one after another on the launch stream
     kstream = {k: (torch.cuda.Stream(dev) if args.concurrent else stream) for k in kinds}
-    # default: MU alone (the roofline kernel keeps an attributable duration), then MS and MC side by
+    # the mixed step's default is one k_step launch (below); --no-fuse: MU alone, then MS and MC side by
     # side -- MC fills the CUs MS's tail leaves idle (482 vs 471M msgs/s serial, 20 steps)
     mc_beside_ms = (not args.serial and not args.concurrent and not args.mc_tail and "MC" in kinds and "MU" in kinds
                     and not (args.fuse and args.kind == "mixed" and not args.no_group and args.group_at == "mu"
@@ -552,9 +554,9 @@ def main():
         g_alone = float(np.median(gts))
     dom = max(kt, key=kt.get)
     # every kind's launch against the same HBM roofline: its algorithmic bytes (the
-    # outputs of the last step) / its HIP-event time.  In the mixed step MS and MC run side by side
-    # after MU (MC on its own stream, started at MU's end), so their times include that sharing;
-    # --kind MU|MS|MC times each kernel alone
+    # outputs of the last step) / its HIP-event time -- with the fused step each kernel timed alone in
+    # the attribution pass; with --no-fuse MS and MC run side by side after MU (MC on its own stream,
+    # started at MU's end), so their times include that sharing; --kind MU|MS|MC times each kernel alone
     kern_tag = {"MU": "k_pulses<MU>", "MS": "k_pulses<MS>", "MC": "k_mc"}
     kernels = {}
     for k in kinds:
