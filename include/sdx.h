@@ -117,7 +117,9 @@ typedef struct {
                                 * protocol) -- demodulate_mc(msg_data) with a protocol_id (sd_protocols.py:79) */
   int32_t max_hex;             /* ABI 13, optional: an upper bound on the length (hex characters) of every
                                 * frame run, 0 = unknown.  sdx_demod_mc launches its 65..128-character
-                                * variant only when max_hex is 0 or > SDX_MC_SHORT_HEX */
+                                * variant only when max_hex is 0 or > SDX_MC_SHORT_HEX; a frame longer
+                                * than a bound of <= SDX_MC_SHORT_HEX gets SDX_ST_OVF_TILE (cursor[2]
+                                * bit 1), as frames past SDX_MC_HEX_MAX do */
   int32_t res;
 } sdx_mc_batch;
 #define SDX_MC_SHORT_HEX 64    /* frames up to this length run in sdx_demod_mc's 4-word variant */

@@ -2466,8 +2466,11 @@ SDX_DEV void mc_block(const void* __restrict__ bank, const sdx_mc_batch& b, cons
       toolong = true;
       valid = false;
     }
+    // a frame longer than the batch's promised bound (0 < max_hex <= 64: no long launch follows) is
+    // marked for a re-run instead of being left without a descriptor
+    if (!LONG && !valid && b.max_hex > 0 && b.max_hex <= MC_SHORTW * 16) toolong = true;
   }
-  if (LONG && toolong) {
+  if (toolong) {
     sdx_desc d;
     d.rec_begin = 0;
     d.n_rec = 0;

@@ -399,6 +399,45 @@ def test_fused_step_matches_the_separate_launches(mrec, mc_known, n):
     assert n == 1 or nres > n
 
 
+def test_mc_frames_past_a_promised_length_bound_are_flagged():
+    """A batch whose max_hex promises <= 64 characters (no 65..128 launch follows) but holds longer
+    frames: k_mc marks them SDX_ST_OVF_TILE (cursor[2] bit 1) for a re-run instead of leaving them
+    without a descriptor -- through sdx_demod_mc and through the fused sdx_demod_step -- and the
+    frames within the bound keep their results (equal to a launch with the true bound)."""
+    import numpy as np
+    import torch
+    from pysignalduino_amd import bank as B, packing, runtime
+    bk = B.Bank()
+    eng = runtime.Engine(bk, 0)
+    rng = np.random.default_rng(5)
+    frames = []
+    for i in range(2000):
+        n = int(rng.integers(65, 129)) if i % 3 == 0 else int(rng.integers(8, 65))
+        frames.append(("".join("0123456789ABCDEF"[int(v)] for v in rng.integers(0, 16, size=n)),
+                       int(rng.integers(300, 700)), 4 * n, "MC", None))
+    bd = eng.to_device_mc(packing.mc_batch_from_frames(frames))
+    assert bd["max_hex"] > 64
+    true = eng.alloc_out(bd["n"], 8 * bd["n"] + 4096, 256 * bd["n"] + 65536)
+    eng.launch_mc(bd, true)
+    lie = dict(bd, max_hex=64)
+    long_ = np.array([len(f[0]) > 64 for f in frames])
+    for via in ("mc", "step"):
+        o = eng.alloc_out(bd["n"], 8 * bd["n"] + 4096, 256 * bd["n"] + 65536)
+        if via == "mc":
+            eng.launch_mc(lie, o)
+        else:
+            eng.launch_step(mc=(lie, o, None))
+        torch.cuda.synchronize()
+        assert int(o["cursor"][2].item()) & 2, via
+        d = eng.fetch(o)[0]
+        assert (d["status"][long_] == runtime.ST_OVF_TILE).all(), via
+        dt, rt, ht = eng.fetch(true)
+        keep = np.nonzero(~long_)[0]
+        a = [(int(d["n_rec"][i]), int(d["status"][i])) for i in keep]
+        b = [(int(dt["n_rec"][i]), int(dt["status"][i])) for i in keep]
+        assert a == b, via
+
+
 @pytest.mark.parametrize("n_mu,n_ms,mrec", [(333333, 333333, False), (5000, 2049, True), (2049, 1, False)])
 def test_group_step_matches_two_groupings(n_mu, n_ms, mrec):
     """sdx_group_step (ABI 14: the MU and MS sorts' radix passes in the same launches) writes the orders
