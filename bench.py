@@ -89,6 +89,10 @@ def parse():
                          "step's MU, MS and MC tiles (sdx_demod_step, ABI 14, where each kind's tiles take the CU "
                          "slots the previous kind's last tiles free: 603.0-603.7M vs 579.5-580.9M msgs/s, "
                          "profiles/r05/fused/)")
+    ap.add_argument("--batches", type=int, default=1,
+                    help="K distinct seeded corpora, all resident in HBM, cycled step by step (step j runs batch "
+                         "j mod K): with K x ~200 MB of inputs above the 256 MiB Infinity Cache no step re-reads a "
+                         "batch the previous step left in the cache (VERDICT r05 #6)")
     ap.add_argument("--corpus", default="bench", choices=("bench", "dense"),
                     help="dense: no noise messages (every message carries a protocol's frames)")
     return ap.parse_args()
@@ -202,7 +206,7 @@ def alg_bytes(kind, bd, rec_np):
     return inp + out + 16384
 
 
-def attribute_alone(torch, eng, stream, kinds, bds, outs, gbufs, corp, mrec_kinds, reps=5):
+def attribute_alone(torch, eng, stream, kinds, bds, outs, gbufs, corp, mrec_kinds, par, reps=5):
     """--fuse: each kind's own kernel alone on the launch stream (after the timed loop, untimed), so
     the line still carries MU's, MS's and MC's separate rooflines; returns {kind: seconds}."""
     from pysignalduino_amd import runtime
@@ -218,8 +222,8 @@ def attribute_alone(torch, eng, stream, kinds, bds, outs, gbufs, corp, mrec_kind
                     eng.launch_mc(bds[k], outs[k])
                 else:
                     eng.launch_pulses(runtime.KIND_MU if k == "MU" else runtime.KIND_MS, bds[k], outs[k],
-                                      sel=gbufs[k][0][0][:corp[k].n], group=False,
-                                      mrec=gbufs[k][0][2] if k in mrec_kinds else None)
+                                      sel=gbufs[k][par][0][:corp[k].n], group=False,
+                                      mrec=gbufs[k][par][2] if k in mrec_kinds else None)
                 e1.record(stream)
                 stream.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e-3)
@@ -227,10 +231,14 @@ def attribute_alone(torch, eng, stream, kinds, bds, outs, gbufs, corp, mrec_kind
     return res
 
 
+# the committed per-kernel PMC summary the line's roofline.traffic / issue come from: a tracked file that
+# ships to the GPU box (profiles/ does not: VERDICT r05 #2), made by tools/pmc_commit.py from a
+# tools/pmc.sh run, with the commit and the libsdx source hash the counters were taken on
+PMC_FILE = os.path.join(REPO, "PMC_TRAFFIC.json")
+
+
 def latest_pmc():
-    import glob
-    c = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_traffic.json")))
-    return c[-1] if c else None
+    return PMC_FILE if os.path.exists(PMC_FILE) else None
 
 
 def main():
@@ -277,16 +285,24 @@ def main():
     per = {k: (args.msgs // 3 if k != "MC" else args.msgs - 2 * (args.msgs // 3)) if args.kind == "mixed" else args.msgs
            for k in kinds}
     seeds = {"MU": 42, "MS": 43, "MC": 44}
-    corp, bds = {}, {}
-    for k in kinds:
-        sd = seeds[k] + 1000 * rank
-        if k == "MU":
-            corp[k] = synth.mu_corpus(P, per[k], seed=sd, noise_frac=0.0 if args.corpus == "dense" else 0.15)
-        elif k == "MS":
-            corp[k] = synth.ms_corpus(P, per[k], seed=sd, noise_frac=0.0 if args.corpus == "dense" else 0.1)
-        else:
-            corp[k] = synth.mc_corpus(P, per[k], seed=sd)
-        bds[k] = eng.to_device_mc(corp[k]) if k == "MC" else eng.to_device_pulses(corp[k])
+    nb = max(1, args.batches)
+    corps, bdl = [], []
+    for b in range(nb):   # batch b: seeds + 100 b (batch 0 is the corpus of every earlier round's line)
+        corp, bds = {}, {}
+        for k in kinds:
+            sd = seeds[k] + 1000 * rank + 100 * b
+            if k == "MU":
+                corp[k] = synth.mu_corpus(P, per[k], seed=sd, noise_frac=0.0 if args.corpus == "dense" else 0.15)
+            elif k == "MS":
+                corp[k] = synth.ms_corpus(P, per[k], seed=sd, noise_frac=0.0 if args.corpus == "dense" else 0.1)
+            else:
+                corp[k] = synth.mc_corpus(P, per[k], seed=sd)
+            bds[k] = eng.to_device_mc(corp[k]) if k == "MC" else eng.to_device_pulses(corp[k])
+        corps.append(corp)
+        bdl.append(bds)
+    corp = corps[0]
+    input_bytes = sum(v.numel() * v.element_size() for bds_ in bdl for bd in bds_.values() for v in bd.values()
+                      if hasattr(v, "numel"))
     caps = {"MU": (12, 320), "MS": (4, 64), "MC": (4, 96)}
     nslot = 2 if dist_on else 1   # double-buffered outputs: step k+1 computes while step k is exchanged
     outs = []
@@ -321,6 +337,7 @@ def main():
 
     def launch_group(j, si=None, after=None):
         par = j % 2
+        bds = bdl[j % nb]
         if used[par] is not None:           # step j-2's launches have read this parity's order
             side.wait_event(used[par])
         if after is not None:
@@ -388,6 +405,7 @@ def main():
 
     def step(j, si=None):
         s_ = j % nslot
+        bds = bdl[j % nb]
         if done[s_] is not None:            # the exchange that read this slot has finished
             stream.wait_event(done[s_])
             done[s_] = None
@@ -531,9 +549,11 @@ def main():
 
     # roofline of the dominant kernel: SURVEY §8(d) algorithmic bytes / its HIP-event time
     kt = {k: float(np.mean(v)) for k, v in ktimes.items()}
+    bds, corp = bdl[(j - 1) % nb], corps[(j - 1) % nb]   # the last timed step's batch (its order: parity j-1)
     if fused:   # each kind's kernel alone (untimed attribution pass): its own roofline entry
         kt_step = kt["step"]
-        kt = attribute_alone(torch, eng, stream, kinds, bds, outs[(j - 1) % nslot], gbufs, corp, mrec_kinds)
+        kt = attribute_alone(torch, eng, stream, kinds, bds, outs[(j - 1) % nslot], gbufs, corp, mrec_kinds,
+                             (j - 1) % 2)
     # the grouping's own time (one step's groupings alone on the launch stream, untimed): group_ms is
     # the side stream's wall time beside the step's kernel, mostly waiting for CU slots
     g_alone = None
@@ -598,7 +618,13 @@ def main():
         if cfg.get("msgs_per_gpu") == args.msgs and cfg.get("kind", "mixed") == args.kind and \
                 tj.get(tag, {}).get("traffic_bytes"):
             traffic = float(tj[tag]["traffic_bytes"])
-            traffic_src = {"pmc": os.path.relpath(tpath, REPO), "fetch_bytes": 2 * 1024 * float(tj[tag]["fetch_size_kib"]),
+            src = tj.get("_source", {})
+            loaded = runtime.load_library().sdx_source_hash().decode()
+            traffic_src = {"pmc": os.path.relpath(tpath, REPO), "commit": src.get("commit"),
+                           "sdx_source_hash": src.get("sdx_source_hash"),
+                           "same_kernels_as_this_run": src.get("sdx_source_hash") == loaded,
+                           "profiles": src.get("profiles"),
+                           "fetch_bytes": 2 * 1024 * float(tj[tag]["fetch_size_kib"]),
                            "write_bytes": 1024 * float(tj[tag]["write_size_kib"]),
                            "calibration": "profiles/r05/calib/calib_traffic.json (FETCH_SIZE x 2 holds for every "
                                           "vector load width this kernel uses; scalar loads count exactly)"}
@@ -621,6 +647,7 @@ def main():
         "data": "synthetic (seeded generators, pysignalduino_amd/synth.py" +
                 (", noise-free dense corpus)" if args.corpus == "dense" else ")"),
         "config": {"workload": wl, "kind": args.kind, "corpus": args.corpus, "msgs_per_gpu": sum(per.values()),
+                   "batches": nb, "input_bytes_resident": input_bytes,
                    "parallelism": f"dp{world}", "grouped": bool(gkinds),
                    "streams": ("one kernel (k_step: MU, then MS, then MC tiles)" if fused else
                                "one per kind" if args.concurrent and len(kinds) > 1 else
@@ -656,7 +683,8 @@ def main():
             res["overflow"][k] = {"flags": ovf[k], "tile_msgs": int((d["status"] == runtime.ST_OVF_TILE).sum()),
                                   "out_msgs": int((d["status"] == runtime.ST_OVF_OUT).sum())}
     if rank == 0 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(corp.get("MU"), corp.get("MS"), corp.get("MC"), args.cpu_seconds, kinds)
+        res["cpu_baseline"] = cpu_baseline(corps[0].get("MU"), corps[0].get("MS"), corps[0].get("MC"), args.cpu_seconds,
+                                           kinds)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist_on:

@@ -89,6 +89,66 @@ def test_stream_matches_batch_api(output, golden):
     assert nres > 3000 and nhost > 50, (nres, nhost)
 
 
+@pytest.mark.parametrize("output", ["json", "wire"])
+def test_stream_chunk_matches_reference_line_goldens(output, golden):
+    """LineStream against the REFERENCE's recorded results, not against the batch API:
+    the reference-run lines of tests/golden/lines_golden.json.gz (every hot-path test line, synthetic
+    and mutated lines, compressed lines) tiled 5x into one chunk -- so that both short classes pass
+    GROUP_MIN and the chunk runs the product's sdx_group_step + ONE k_step -- then per line the MQTT
+    text the reference publishes (json: controller.py:254-257, mqtt.py:227-245) or its full
+    (protocol_id, payload) list (wire: parser/mu.py:75-80, ms.py:51, mc.py:78)."""
+    from oracle import json_oracle as J
+    from pysignalduino_amd import runtime
+    from pysignalduino_amd.frontend import SignalParser
+    from pysignalduino_amd.packing import ContractError
+    cases = golden("lines_golden.json.gz")
+    lines = [c["line"].encode("latin-1") for c in cases] * 5
+    exp_all = [c.get("e2e", []) for c in cases] * 5
+    sp = SignalParser()                        # the reference's configuration: MC 'strict'
+    ls = sp.stream(chunk_lines=len(lines), chunk_bytes=sum(map(len, lines)) + 4096, output=output, lag=2)
+    ls.submit(lines)
+    got = [r.detach() for r in ls.drain()]
+    assert len(got) == 1 and got[0].n == len(lines)
+    r = got[0]
+    kinds = r.kind
+    assert int((kinds == runtime.LINE_MU).sum()) >= runtime.GROUP_MIN and \
+        int((kinds == runtime.LINE_MS).sum()) >= runtime.GROUP_MIN
+    nres = contract = 0
+    if output == "json":
+        for i, (e, g) in enumerate(zip(exp_all, r.texts())):
+            if isinstance(g, ContractError):
+                contract += 1
+                continue
+            assert g == J.published(e), (i, lines[i][:80], g, e)
+            nres += g is not None
+    else:
+        bk = sp.protocols._bank
+        pid = {"MU": bk.mu_pids, "MS": bk.ms_pids, "MC": bk.mc_pids, "MN": bk.mn_pids}
+        lk = {runtime.LINE_MU: "MU", runtime.LINE_MS: "MS", runtime.LINE_MC: "MC", runtime.LINE_MN: "MN"}
+        dec = {nm: r.decode(j) for j, nm in enumerate(r.names)}
+        for i, e in enumerate(exp_all):
+            want = [(x[0], x[1]) for x in e]
+            if i in r.host:
+                g = r.host[i]
+                if isinstance(g, Exception):
+                    contract += 1
+                    continue
+                got_i = [(m.protocol_id, m.payload) for m in g]
+            else:
+                nm = lk.get(int(r.kind[i]))
+                if int(r.status[i]) != runtime.LS_OK or nm not in dec:
+                    got_i = []
+                else:
+                    d, rc, h = dec[nm]
+                    got_i = [(str(pid[nm][int(x["proto"])]),
+                              h[int(x["payload_off"]): int(x["payload_off"]) + int(x["payload_len"])].tobytes()
+                              .decode("latin-1"))
+                             for x in rc[int(d[i]["rec_begin"]): int(d[i]["rec_begin"]) + int(d[i]["n_rec"])]]
+            assert got_i == want, (i, lines[i][:80], got_i, want)
+            nres += bool(want)
+    assert nres >= 5 * 1200 and contract <= 0.05 * len(lines), (nres, contract)
+
+
 def test_stream_capacity_and_empty_chunk():
     from pysignalduino_amd.frontend import SignalParser
     sp = SignalParser()
