@@ -39,7 +39,7 @@ from __future__ import annotations
 import asyncio
 import collections
 import logging
-from typing import Any, Deque, List, Optional
+from typing import Any, Deque, Dict, List, Optional
 
 
 class BatchingParserTask:
@@ -204,23 +204,29 @@ class BatchingParserTask:
         if self._stream is None:
             self._stream = c.parser.stream(chunk_lines=self.max_batch, output="json", lag=self.lag)
         ls = self._stream
-        pending: Deque[List[Any]] = collections.deque()
+        # chunk id -> its lines: results are matched to their lines by id, never by position, so a
+        # publication that fails part-way through a chunk cannot shift later chunks onto the wrong lines
+        # (ADVICE r05); ``ready`` holds the finished chunks not yet published (a failure leaves the rest
+        # of its poll's chunks there, and the exit drain publishes them)
+        pending: Dict[int, List[Any]] = {}
+        ready: Deque[Any] = collections.deque()
 
         async def publish(done):
-            for r in done:
-                blines = pending.popleft()
+            ready.extend(done)
+            while ready:
+                r = ready.popleft()
+                blines = pending.pop(r.id)
                 items = r.items() if hasattr(r, "items") else [(i, t) for i, t in enumerate(r.texts())
                                                               if t is not None]
-                await self._publish_items(blines, items)
                 self.lines += len(blines)
+                await self._publish_items(blines, items)
 
         while not c._stop_event.is_set():
             try:
                 batch = await self._next_batch(self.max_delay if pending else None)
                 lines = list(filter(None, batch))
                 if lines:
-                    await asyncio.to_thread(ls.submit, lines)
-                    pending.append(lines)
+                    pending[await asyncio.to_thread(ls.submit, lines)] = lines
                     self.batches += 1
                     done = await asyncio.to_thread(ls.poll)
                 elif pending:           # the queue ran dry: publish everything in flight
@@ -235,7 +241,7 @@ class BatchingParserTask:
                 self.logger.error(f"Parser task error: {e}")
                 break
         if pending:                     # stopped or failed with chunks in flight: publish them
-            n = sum(len(b) for b in pending)
+            n = sum(len(b) for b in pending.values())
             try:
                 await publish(await asyncio.to_thread(ls.drain))
             except asyncio.CancelledError:

@@ -68,7 +68,14 @@ FRAME_HDR = 8
 FRAME_INTS = FRAME_HDR + XCHG_COUNTS * runtime.XCHG_MAX_PARTS
 FRAME_MAGIC = 0x53445846         # 'SDXF'
 PHASE_COUNT, PHASE_RECOUNT = 1, 2
-FLAG_RERUN_FAILED = 1
+FLAG_RERUN_FAILED = 1   # this rank's overflow re-run raised
+FLAG_LOCAL_ERROR = 2    # this rank failed before its counts (e.g. too many overlays, a bad buffer): no counts
+BRANCH_SYNC, BRANCH_PIPELINED = 0, 1   # header word 5: the exchange branch (the collective sequence) of the rank
+
+
+def _nullctx():
+    import contextlib
+    return contextlib.nullcontext()
 
 
 class ExchangeMismatch(RuntimeError):
@@ -79,21 +86,27 @@ class ExchangeMismatch(RuntimeError):
 def check_frames(frames: np.ndarray, world: int, K: int, phase: int) -> Tuple[np.ndarray, np.ndarray]:
     """All-gathered count frames [world * FRAME_INTS] -> (the primary launches' counts S[world, K,
     XCHG_COUNTS], per-rank flags).  Raises ExchangeMismatch, identically on every rank, when a header
-    is not this exchange's (magic, world size, K, phase)."""
+    is not this exchange's (magic, world size, K, phase), when the ranks run different exchange branches
+    (synchronous / pipelined: their collective sequences are equal only by construction), or when a rank
+    flagged a local error (FLAG_LOCAL_ERROR: its frame holds no counts)."""
     f = np.asarray(frames, np.int64).reshape(world, FRAME_INTS)
     hdr = f[:, :FRAME_HDR]
     want = np.array([FRAME_MAGIC, world, K, phase])
-    if not (hdr[:, :4] == want).all():
-        rows = {r: dict(magic=hex(int(h[0])), world=int(h[1]), launches=int(h[2]), phase=int(h[3]))
+    if not (hdr[:, :4] == want).all() or not (hdr[:, 5] == hdr[0, 5]).all():
+        rows = {r: dict(magic=hex(int(h[0])), world=int(h[1]), launches=int(h[2]), phase=int(h[3]),
+                        branch="pipelined" if h[5] == BRANCH_PIPELINED else "sync")
                 for r, h in enumerate(hdr)}
         raise ExchangeMismatch(f"exchange: the ranks' count frames disagree (want world {world}, {K} launches, "
-                               f"phase {phase}): {rows}")
+                               f"phase {phase}, one branch): {rows}")
+    local = [r for r in range(world) if hdr[r, 4] & FLAG_LOCAL_ERROR]
+    if local:
+        raise ExchangeMismatch(f"exchange: rank(s) {local} failed before counting (phase {phase})")
     return f[:, FRAME_HDR: FRAME_HDR + K * XCHG_COUNTS].reshape(world, K, XCHG_COUNTS), hdr[:, 4].copy()
 
 
-def frame_header(world: int, K: int, phase: int, flags: int = 0) -> np.ndarray:
+def frame_header(world: int, K: int, phase: int, flags: int = 0, branch: int = BRANCH_SYNC) -> np.ndarray:
     h = np.zeros(FRAME_HDR, np.int32)
-    h[:5] = (FRAME_MAGIC, world, K, phase, flags)
+    h[:6] = (FRAME_MAGIC, world, K, phase, flags, branch)
     return h
 
 
@@ -433,17 +446,21 @@ class Exchange:
         off = (-w.data_ptr()) % 256
         return w[off:], wb
 
-    def _frame(self, dev, K, phase, flags=0):
+    def _frame(self, dev, K, phase, flags=0, branch=None):
         """A count frame on ``dev`` (FRAME_INTS int32): the header of this exchange (copied from a
         cached pinned host tensor that is never written again, so the copy needs no host sync) and
-        room for the counts of up to XCHG_MAX_PARTS parts behind it."""
+        room for the counts of up to XCHG_MAX_PARTS parts behind it.  A FLAG_LOCAL_ERROR frame is
+        header + zeros (the rank has no counts)."""
+        if branch is None:
+            branch = BRANCH_PIPELINED if dev.type == "cuda" and self.pipelined else BRANCH_SYNC
         c = self.__dict__.setdefault("_hdr_cache", {})
-        key = (K, phase, flags)
+        key = (K, phase, flags, branch, dev.type)
         if key not in c:
-            c[key] = torch.from_numpy(frame_header(self.world, K, phase, flags))
+            c[key] = torch.from_numpy(frame_header(self.world, K, phase, flags, branch))
             if dev.type == "cuda":
                 c[key] = c[key].pin_memory()
-        f = (torch.empty if dev.type == "cuda" else torch.zeros)(FRAME_INTS, dtype=torch.int32, device=dev)
+        zero = dev.type != "cuda" or bool(flags & FLAG_LOCAL_ERROR)
+        f = (torch.zeros if zero else torch.empty)(FRAME_INTS, dtype=torch.int32, device=dev)
         f[:FRAME_HDR].copy_(c[key], non_blocking=True)
         return f
 
@@ -504,10 +521,10 @@ class Exchange:
             out.append(enc + (int(enc[1]["payload_len"].astype(np.int64).sum()),))
         return out
 
-    def _counts_host(self, enc, K, phase, flags=0):
+    def _counts_host(self, enc, K, phase, flags=0, branch=BRANCH_SYNC):
         """The count frame of K primary launches' host encodings (messages, records, wire bytes, bad,
         payload bytes, 0, 0, 0 each)."""
-        f = self._frame(torch.device("cpu"), K, phase, flags)
+        f = self._frame(torch.device("cpu"), K, phase, flags, branch)
         c = torch.tensor([[len(m), len(w), len(p), b, pb, 0, 0, 0] for m, w, p, b, pb in enc], dtype=torch.int32)
         f[FRAME_HDR: FRAME_HDR + c.numel()] = c.reshape(-1)
         return f
@@ -523,21 +540,44 @@ class Exchange:
     def submit(self, parts, stream=None, rerun: Optional[Callable[[Part], Part]] = None, after=None):
         parts = [Part.of(p) for p in parts]
         dev = parts[0].desc.device
-        if self.pipeline and dev.type != "cuda":
-            raise ValueError("exchange: the pipelined branch needs device buffers")
         overlap = dev.type == "cuda" and self.pipelined
         K = len(parts)
         if not overlap:   # synchronous form: gloo (CPU tensors, or CUDA tensors staged through the host)
+            # whatever fails on this rank before its counts are known (the pipelined setting on host
+            # buffers, more launches + overlays than a frame holds, the local count / encode) is sent as a
+            # FLAG_LOCAL_ERROR frame: the peers are in the same collective and every rank raises together
+            err = ValueError("exchange: the pipelined branch needs device buffers") \
+                if self.pipeline and dev.type != "cuda" else None
+            branch = BRANCH_PIPELINED if self.pipeline else BRANCH_SYNC
+            enc = frame = None
             if dev.type == "cuda":
                 stream = stream or torch.cuda.current_stream(dev)
                 with torch.cuda.stream(stream):
-                    flat = _flatten(parts)
-                    frame = self._frame(dev, K, PHASE_COUNT)
-                    self._count_pack_device(flat, stream, frame)
-                    self._complete(_Pending(parts, self._gather_frame(frame).cpu(), None, rerun=rerun))
+                    try:
+                        flat = _flatten(parts)
+                        frame = self._frame(dev, K, PHASE_COUNT, branch=branch)
+                        self._count_pack_device(flat, stream, frame)
+                    except Exception as e:
+                        err, frame = e, self._frame(dev, K, PHASE_COUNT, FLAG_LOCAL_ERROR, branch=branch)
+                    allc = self._gather_frame(frame).cpu()
             else:
-                enc = self._encode_host(parts)
-                allc = self._gather_frame(self._counts_host(enc, K, PHASE_COUNT))
+                if err is None:
+                    try:
+                        _flatten(parts)      # the same launch + overlay limit on every branch
+                        enc = self._encode_host(parts)
+                        frame = self._counts_host(enc, K, PHASE_COUNT, branch=branch)
+                    except Exception as e:
+                        err = e
+                if err is not None:
+                    frame = self._frame(dev, K, PHASE_COUNT, FLAG_LOCAL_ERROR, branch=branch)
+                allc = self._gather_frame(frame)
+            try:
+                check_frames(allc.numpy(), self.world, K, PHASE_COUNT)
+            except ExchangeMismatch as m:
+                if err is not None:
+                    raise ExchangeMismatch(f"{m}: {type(err).__name__}: {err}") from err
+                raise
+            with torch.cuda.stream(stream) if dev.type == "cuda" else _nullctx():
                 self._complete(_Pending(parts, allc, None, enc, rerun=rerun))
             return None
         if self.stream is None:
@@ -631,17 +671,35 @@ class Exchange:
                     self.reruns += 1
             flags = FLAG_RERUN_FAILED if err is not None else 0
             dev = p.parts[0].desc.device
-            if dev.type != "cuda":
-                if err is None:
-                    p.enc = self._encode_host(p.parts)
-                host = self._gather_frame(self._counts_host(p.enc, K, PHASE_RECOUNT, flags))
-            elif p.cnt is None:        # gloo with device tensors: count + pack again
-                frame = self._frame(dev, K, PHASE_RECOUNT, flags)
-                self._count_pack_device(_flatten(p.parts), torch.cuda.current_stream(dev), frame)
-                host = self._gather_frame(frame).cpu()
+            # the local recount preparation (flatten -- at most XCHG_MAX_PARTS launches + overlays --,
+            # encode, count) may raise on this rank alone: its frame then carries the failure flag and no
+            # counts, and the collective below still runs, so the peers never wait in it
+            frame = None
+            if err is None:
+                try:
+                    if dev.type != "cuda":
+                        _flatten(p.parts)    # the same launch + overlay limit on every branch
+                        p.enc = self._encode_host(p.parts)
+                        frame = self._counts_host(p.enc, K, PHASE_RECOUNT, flags)
+                    else:
+                        flat = _flatten(p.parts)
+                        frame = self._frame(dev, K, PHASE_RECOUNT, flags)
+                        if p.cnt is None:        # gloo with device tensors: count + pack again
+                            self._count_pack_device(flat, torch.cuda.current_stream(dev), frame)
+                        else:
+                            p.cnt = self._count_device(flat, torch.cuda.current_stream(dev), frame)
+                except Exception as e:
+                    err, frame = e, None
+            if frame is None:
+                frame = self._frame(dev, K, PHASE_RECOUNT, FLAG_RERUN_FAILED)
+                frame[FRAME_HDR:].zero_()
+            allc = self._gather_frame(frame)
+            if dev.type == "cuda":
+                host = torch.empty(allc.numel(), dtype=torch.int32, pin_memory=True)
+                host.copy_(allc, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
             else:
-                host, ev, p.cnt = self._count_to_host(_flatten(p.parts), dev, K, PHASE_RECOUNT, flags)
-                ev.synchronize()
+                host = allc
             S, fl = check_frames(host.numpy(), self.world, K, PHASE_RECOUNT)
             if fl.any():
                 failed = [r for r in range(self.world) if fl[r] & FLAG_RERUN_FAILED]

@@ -54,16 +54,22 @@ class ChunkResult:
     ``host`` holds the lines the batch API took (line index -> its parse_lines result).
 
     The arrays are views of the stream's pinned buffers (no host copy on the critical path): they
-    stay valid until the stream's next submit(); ``detach()`` copies them out."""
+    stay valid until the stream's next submit(); ``detach()`` copies them out.  A result the stream
+    still holds (finished, not yet returned by poll / drain) is detached by the stream itself before its
+    slot's buffers are written again, so submitting several chunks between polls loses nothing."""
 
     def __init__(self, cid: int, n: int, kind: np.ndarray, status: np.ndarray):
         self.id, self.n, self.kind, self.status = cid, n, kind, status
+        self.slot = None          # the _Slot whose pinned buffers the arrays view (None once detached)
         self.json = self.off = self.len = None
         self.wire = self.layout = None
         self.host = {}            # line -> result of the batch API (fallback lines)
         self.affix = {}
 
     def detach(self) -> "ChunkResult":
+        if self.slot is None:
+            return self
+        self.slot = None
         for f in ("kind", "status", "off", "len", "wire"):
             v = getattr(self, f)
             if isinstance(v, np.ndarray):
@@ -387,6 +393,9 @@ class LineStream:
     def _stage_c(self, s: _Slot):
         """The results D2H, sized by the device sizes (on the host by now)."""
         t = self.torch
+        for r in self.done:                # an earlier chunk of this slot not yet handed out: copy it out
+            if r.slot is s:
+                r.detach()
         s.ev.synchronize()
         n, lb = s.n, s.lb
         hs = s.h_sizes.numpy().astype(np.int64)
@@ -429,6 +438,7 @@ class LineStream:
         kind = ho[b: b + n]
         status = ho[b + n: b + 2 * n]
         r = ChunkResult(s.cid, n, kind, status)
+        r.slot = s
         self.kernel_events.append(tuple(s.kt))
         names = list(s.outs)
         redo_kinds = {names[j] for j in range(len(names)) if s.dcur[j, 2]}   # ST_OVF_* in that launch

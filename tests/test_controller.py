@@ -45,8 +45,9 @@ class FakeParser:
 
 
 class _Chunk:
-    def __init__(self, texts):
+    def __init__(self, texts, cid=0):
         self._t = texts
+        self.id = cid
 
     def texts(self):
         return self._t
@@ -60,7 +61,7 @@ class FakeStream:
         self.parser, self.lag, self.q, self.submitted = parser, lag, [], 0
 
     def submit(self, lines):
-        self.q.append(_Chunk(self.parser.parse_lines_json(lines)))
+        self.q.append(_Chunk(self.parser.parse_lines_json(lines), self.submitted))
         self.submitted += 1
         return self.submitted - 1
 
@@ -312,3 +313,46 @@ def test_json_stream_publishes_in_flight_chunks_on_exit(how):
     _, sent, cmd = reference_side_effects(FakeParser(), lines[:taken])
     assert ctl.cmd == cmd and task.lines == taken
     assert ctl.mqtt_publisher.sent == [("t/v1/state/messages", json.dumps(s[0])) for s in sent]
+
+
+def test_json_stream_publish_failure_mid_chunk_keeps_lines_aligned():
+    """a command-response turn that raises part-way through a chunk ends the loop (as in the
+    reference, controller.py:262-264); the chunks the stream still holds are drained and published with
+    THEIR OWN lines (results matched by chunk id, not by position): every publication is followed by the
+    turn of the line it belongs to, nothing raises IndexError, and the failing chunk's later lines get
+    nothing."""
+    lines = [f"MC;D={i};" for i in range(600)]
+    parser = FakeParser()
+    texts = dict(zip(lines, parser.parse_lines_json(lines)))
+    ctl = Ctl(parser, callback=False)
+    ctl._pending_responses = ["cmd"]          # every line gets its turn
+    bad = "MC;D=101;"
+
+    async def handle(line):
+        if line == bad:
+            raise RuntimeError("injected command-response failure")
+        ctl.cmd.append(line)
+    ctl._handle_as_command_response = handle
+    order = []
+    orig = ctl.mqtt_publisher.publish
+
+    async def pub(*a):
+        order.append(("pub", a[1]))
+        await orig(*a)
+    ctl.mqtt_publisher.publish = pub
+    task = BatchingParserTask(ctl, publish="json", max_batch=40, max_delay=0.005, lag=3)
+
+    async def go():
+        for ln in lines:
+            ctl._raw_message_queue.put_nowait(ln)
+        await asyncio.wait_for(task.run(), 30)
+
+    asyncio.run(go())
+    assert bad not in ctl.cmd and "MC;D=102;" not in ctl.cmd      # the failing chunk stops at the failure
+    assert ctl.cmd[:101] == lines[:101]
+    later = ctl.cmd[101:]
+    assert later and all(int(x[5:-1]) >= 120 for x in later)        # only whole later chunks follow
+    # each published text belongs to the line whose turn comes next (or to the failing line)
+    pubs = [t for _, t in order]
+    want = [texts[ln] for ln in ctl.cmd[:101] + [bad] + later if texts[ln] is not None]
+    assert pubs == want

@@ -196,6 +196,25 @@ def _guard_worker(rank, world, port, q):
         got.append("no error")
     except sdist.ExchangeMismatch as e:
         got.append("rerun failed" if "[1]" in str(e) else str(e))
+    # rank 1's re-run succeeds but leaves more launches + overlays than a count frame holds
+    # (XCHG_MAX_PARTS): the local recount preparation raises on rank 1 alone -- both ranks raise
+    def rerun_many(p):
+        od = d.copy()
+        od["status"][3:] = runtime.ST_ABSENT
+        for _ in range(runtime.XCHG_MAX_PARTS if rank == 1 else 1):
+            p.overlays.append(sdist.Part(*part(od)))
+        return p
+    try:
+        sdist.Exchange().submit([part(d2)], rerun=rerun_many)
+        got.append("no error")
+    except sdist.ExchangeMismatch as e:
+        got.append("local" if "[1]" in str(e) else str(e))
+    # the pipelined setting on host buffers (rank 1 only): flagged in the frame, both ranks raise
+    try:
+        sdist.Exchange(pipeline=rank == 1).submit([part(d)])
+        got.append("no error")
+    except sdist.ExchangeMismatch as e:
+        got.append("branch" if "branch" in str(e) else str(e))
     ex = sdist.Exchange()
     ex.submit([part(d)])
     ex.flush()
@@ -214,7 +233,8 @@ def test_exchange_mismatch_raises_on_every_rank():
     outs = dict(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert outs == {0: ["mismatch", "rerun failed", 600], 1: ["mismatch", "rerun failed", 600]}, outs
+    want = ["mismatch", "rerun failed", "local", "branch", 600]
+    assert outs == {0: want, 1: want}, outs
 
 
 def test_check_frames_header_rules():
