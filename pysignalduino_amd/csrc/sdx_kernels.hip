@@ -2693,7 +2693,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : 
 // ---------------------------------------------------------------------------------------------
 // one MS tile on the instantiation of its length class: NW = 2 (2 bitmap words per id, 118 VGPRs)
 // when none of its messages has more than 128 pulses, NW = 4 otherwise -- decided per tile, so no
-// workgroup exists only to find that the tile is another launch's
+// workgroup exists only to find that the tile is another launch's.  MR = 1: the header fields (and the
+// length deciding the class) from the message records the grouping wrote (one 128-byte line per
+// message instead of a sector of each SoA field)
+template <int MR>
 SDX_DEV void ms_tile_by_class(const void* __restrict__ bank, const sdx_pulse_batch& b, const sdx_out& out, const int w,
                               PulsesLds<SDX_KIND_MS, 2, 64>& L2, PulsesLds<SDX_KIND_MS, 4, 64>& L4, int* msg_of) {
   const int ntot = b.sel_dev ? b.n_sel : b.n;
@@ -2701,15 +2704,19 @@ SDX_DEV void ms_tile_by_class(const void* __restrict__ bank, const sdx_pulse_bat
   int len = 0;
   if (threadIdx.x < 64 && m < ntot) {
     const int msg = b.sel_dev ? b.sel_dev[m] : m;
-    len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - b.offsets_dev[msg]);
+    if (MR)
+      len = b.mrec_dev[msg].len;
+    else
+      len = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - b.offsets_dev[msg]);
   }
   if (__syncthreads_or(len > 128) == 0)
-    pulses_tile<SDX_KIND_MS, 2, 64, 0, 0>(bank, b, out, w, L2, msg_of);
+    pulses_tile<SDX_KIND_MS, 2, 64, MR, 0>(bank, b, out, w, L2, msg_of);
   else
-    pulses_tile<SDX_KIND_MS, 4, 64, 0, 0>(bank, b, out, w, L4, msg_of);
+    pulses_tile<SDX_KIND_MS, 4, 64, MR, 0>(bank, b, out, w, L4, msg_of);
 }
 
-// sdx_demod_pulses(MS) without message records: every tile on its length class's instantiation
+// sdx_demod_pulses(MS): every tile on its length class's instantiation
+template <int MR>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ms_classes(
     const void* __restrict__ bank, sdx_pulse_batch b, sdx_out out) {
   __shared__ union {
@@ -2717,7 +2724,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     PulsesLds<SDX_KIND_MS, 4, 64> n4;
   } U;
   __shared__ int msg_of[64];
-  ms_tile_by_class(bank, b, out, (int)blockIdx.x, U.n2, U.n4, msg_of);
+  ms_tile_by_class<MR>(bank, b, out, (int)blockIdx.x, U.n2, U.n4, msg_of);
 }
 
 struct StepArgs {
@@ -2734,7 +2741,7 @@ union StepLds {
 };
 static_assert(sizeof(StepLds) <= 81920, "two k_step workgroups per CU (160 KB of LDS)");
 
-template <int MRU>
+template <int MRU, int MRS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_step(const void* __restrict__ bank,
                                                                                       StepArgs a) {
   static_assert(pulses_threads<SDX_KIND_MU, 4>() == 512 && pulses_threads<SDX_KIND_MS, 2>() == 512, "512-thread tiles");
@@ -2756,7 +2763,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   if (r == 0) {
     pulses_tile<SDX_KIND_MU, 4, 64, MRU, 0>(bank, a.mu, a.mu_out, w, U.mu, msg_of);
   } else if (r == 1) {
-    ms_tile_by_class(bank, a.ms, a.ms_out, w, U.ms2, U.ms4, msg_of);
+    ms_tile_by_class<MRS>(bank, a.ms, a.ms_out, w, U.ms2, U.ms4, msg_of);
   } else {
     const int half = (int)threadIdx.x >> 8;
     mc_block<MC_SHORTW, false>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
@@ -2952,6 +2959,8 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
   else if (kind == SDX_KIND_MU)
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MU, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
+  else if (b.mrec_dev && SDX_MS_NARROW)
+    hipLaunchKernelGGL(sdx::k_ms_classes<1>, dim3(grid), blk, 0, st, bank->dev, b, o);
   else if (b.mrec_dev)
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
   else if (SDX_MS_NARROW) {
@@ -2966,7 +2975,7 @@ int sdx_demod_pulses(const sdx_bank* bank, int kind, const sdx_pulse_batch* batc
       hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 2, 64, 0, 1>), dim3(grid), blk, 0, st, bank->dev, b, o);
       hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64, 0, 3>), dim3(grid), blk, 0, st, bank->dev, b, o);
     } else {
-      hipLaunchKernelGGL(sdx::k_ms_classes, dim3(grid), blk, 0, st, bank->dev, b, o);
+      hipLaunchKernelGGL(sdx::k_ms_classes<0>, dim3(grid), blk, 0, st, bank->dev, b, o);
     }
   } else
     hipLaunchKernelGGL((sdx::k_pulses<SDX_KIND_MS, 4, 64>), dim3(grid), blk, 0, st, bank->dev, b, o);
@@ -3047,10 +3056,10 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
   hipStream_t st = (hipStream_t)hip_stream;
   sdx::StepArgs a{};
   auto count = [](int n, int n_sel, const void* sel) { return sel ? n_sel : n; };
-  // the fused kernel's forms: MU short (with or without message records), MS short without records
-  // (the two length classes), MC frames of <= SDX_MC_SHORT_HEX characters; anything else keeps its
-  // own launches, after the fused kernel on the same stream
-  const bool ms_fused = step->ms && !step->ms->mrec_dev && SDX_MS_NARROW;
+  // the fused kernel's forms: MU short and MS short (the two length classes), each with or without
+  // message records, MC frames of <= SDX_MC_SHORT_HEX characters; anything else keeps its own launches,
+  // after the fused kernel on the same stream
+  const bool ms_fused = step->ms && SDX_MS_NARROW;
   const bool mc_fused = step->mc && step->mc->max_hex > 0 && step->mc->max_hex <= SDX_MC_SHORT_HEX;
   if (step->mu) {
     const sdx_pulse_batch& b = *step->mu;
@@ -3064,6 +3073,7 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
   if (ms_fused) {
     const sdx_pulse_batch& b = *step->ms;
     if (!b.cp_slot_dev || !b.ms_ok_dev) return fail(SDX_EINVAL, "MS needs cp_slot/ms_ok");
+    if ((uintptr_t)b.mrec_dev & 127) return fail(SDX_EINVAL, "mrec_dev must be 128-byte aligned");
     if (step->ms_out->work_dev && step->ms_out->work_cap > 0xFFFFFFFFull - sdx::SPILL_BYTES)
       return fail(SDX_EINVAL, "work_cap above 4 GiB - 112 KB: spill offsets are 32-bit");
     a.ms = b;
@@ -3078,10 +3088,15 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
   const long long grid = (long long)a.t_mu + a.t_ms + a.b_mc;
   if (grid > 0x7FFFFFFFll) return fail(SDX_EINVAL, "sdx_demod_step: grid too large");
   if (grid > 0) {
-    if (a.mu.mrec_dev)
-      hipLaunchKernelGGL((sdx::k_step<1>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
+    const bool mru = a.mu.mrec_dev != nullptr, mrs = a.ms.mrec_dev != nullptr;
+    if (mru && mrs)
+      hipLaunchKernelGGL((sdx::k_step<1, 1>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
+    else if (mru)
+      hipLaunchKernelGGL((sdx::k_step<1, 0>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
+    else if (mrs)
+      hipLaunchKernelGGL((sdx::k_step<0, 1>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
     else
-      hipLaunchKernelGGL((sdx::k_step<0>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
+      hipLaunchKernelGGL((sdx::k_step<0, 0>), dim3((unsigned)grid), dim3(512), 0, st, bank->dev, a);
     HIPCHK(hipGetLastError());
   }
   if (step->ms && !ms_fused) {

@@ -349,15 +349,16 @@ def test_message_records_match_soa_and_results(kind):
     assert all(x.tobytes() == y.tobytes() for x, y in zip(a, b))
 
 
-@pytest.mark.parametrize("mrec,mc_known,n", [(False, True, 20000), (True, True, 6000), (False, False, 3000),
-                                            (False, True, 1)])
+@pytest.mark.parametrize("mrec,mc_known,n", [("", True, 20000), ("MU", True, 6000), ("MS", True, 6000),
+                                            ("MU,MS", True, 6000), ("", False, 3000), ("", True, 1)])
 def test_fused_step_matches_the_separate_launches(mrec, mc_known, n):
     """sdx_demod_step (ABI 14: the MU, MS and MC launches of a step as one k_step grid) gives the
     results of sdx_demod_pulses(MU), sdx_demod_pulses(MS) and sdx_demod_mc: descriptors, records and
     payloads (canonical form: record placement follows the tiles' atomics) and the exchange's per-message
     counts, byte for byte.  MS carries messages on both sides of the 128-pulse length class boundary;
     mrec: MU reads message records; mc_known = False: MC's length bound unknown (its frames run in
-    their own launch after the fused kernel); n = 1: near-empty ranges."""
+    their own launch after the fused kernel); n = 1: near-empty ranges.  mrec: the kinds whose launches
+    read their header fields from the grouping's message records."""
     import torch
     from pysignalduino_amd import bank as B, dist, runtime, synth
     bk = B.Bank()
@@ -369,7 +370,8 @@ def test_fused_step_matches_the_separate_launches(mrec, mc_known, n):
     bds = {"MU": eng.to_device_pulses(mu), "MS": eng.to_device_pulses(ms), "MC": eng.to_device_mc(mc)}
     if not mc_known:
         bds["MC"]["max_hex"] = 0
-    eng.use_mrec = {runtime.KIND_MU} if mrec else set()
+    kinds_mrec = {"MU": runtime.KIND_MU, "MS": runtime.KIND_MS}
+    eng.use_mrec = {kinds_mrec[k] for k in mrec.split(",") if k}
     orders = {}
     bufs = {}
     for k, kd in (("MU", runtime.KIND_MU), ("MS", runtime.KIND_MS)):
@@ -382,11 +384,11 @@ def test_fused_step_matches_the_separate_launches(mrec, mc_known, n):
                                  eng.pulses_work_bytes(n) if k != "MC" else 0, wire=True) for k in caps}
 
     sep, fus = alloc(), alloc()
-    mr = bufs["MU"][2] if (mrec and orders["MU"] is not None) else None
-    eng.launch_pulses(runtime.KIND_MU, bds["MU"], sep["MU"], sel=orders["MU"], group=False, mrec=mr)
+    mr = {k: bufs[k][2] if (k in mrec and orders[k] is not None) else None for k in ("MU", "MS")}
+    eng.launch_pulses(runtime.KIND_MU, bds["MU"], sep["MU"], sel=orders["MU"], group=False)
     eng.launch_pulses(runtime.KIND_MS, bds["MS"], sep["MS"], sel=orders["MS"], group=False)
     eng.launch_mc(bds["MC"], sep["MC"])
-    eng.launch_step(mu=(bds["MU"], fus["MU"], orders["MU"], mr), ms=(bds["MS"], fus["MS"], orders["MS"], None),
+    eng.launch_step(mu=(bds["MU"], fus["MU"], orders["MU"], mr["MU"]), ms=(bds["MS"], fus["MS"], orders["MS"], mr["MS"]),
                     mc=(bds["MC"], fus["MC"], None))
     torch.cuda.synchronize()
     nres = 0
