@@ -211,9 +211,6 @@ __global__ __launch_bounds__(256) void k_sig2(const void* __restrict__ bank, Sig
 // totals).  No inter-workgroup waiting: a decoupled look-back sort is latency-bound at these sizes.
 // ---------------------------------------------------------------------------------------------
 constexpr int RS_T = 512, RS_ROUNDS = 4, RS_PART = RS_T * RS_ROUNDS;
-#ifndef SDX_GROUP_FOLD
-#define SDX_GROUP_FOLD 1  // sdx_group_step: the next pass's histogram counted by the scatter (0: A/B)
-#endif
 #ifndef SDX_RS_PASSES
 #define SDX_RS_PASSES 4
 #endif
@@ -246,18 +243,14 @@ __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ k
   rs_hist(key, n, np, d, hist, (int)blockIdx.x, c);
 }
 
-// each digit's row: exclusive prefix over the partitions (one wave per row); tot[digit] = total.
-// hzero (the folded form, sdx_group_step): the next pass's histogram row is zeroed on the way, for the
-// scatter of this pass to count into
-SDX_DEV void rs_scan_rows(uint32_t* __restrict__ hist, int np, uint32_t* __restrict__ tot, const int blk,
-                          uint32_t* __restrict__ hzero = nullptr) {
+// each digit's row: exclusive prefix over the partitions (one wave per row); tot[digit] = total
+SDX_DEV void rs_scan_rows(uint32_t* __restrict__ hist, int np, uint32_t* __restrict__ tot, const int blk) {
   const int row = blk * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   uint32_t* h = hist + (size_t)row * np;
   uint32_t run = 0;
   for (int b0 = 0; b0 < np; b0 += 64) {
     const int x = b0 + lane;
     const uint32_t v = x < np ? h[x] : 0u;
-    if (hzero && x < np) hzero[(size_t)row * np + x] = 0u;
     uint32_t incl = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -275,12 +268,9 @@ __global__ __launch_bounds__(256) void k_rs_scan_rows(uint32_t* __restrict__ his
 
 // pass d: every partition scatters its elements, in order (stable), to
 // (digit base = prefix of the digit totals) + (row offset of the partition) + (rank inside it)
-// hnext (the folded form): every element also counts itself into the NEXT pass's histogram, at its
-// output partition (pos / RS_PART) and next digit -- the separate histogram launch of that pass goes
 SDX_DEV void rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int n, int np, int d,
                         const uint32_t* __restrict__ hist, const uint32_t* __restrict__ tot, uint32_t* __restrict__ kout,
-                        uint32_t* __restrict__ vout, const int p, uint32_t* run, uint32_t (*wc)[256],
-                        uint32_t* __restrict__ hnext = nullptr) {
+                        uint32_t* __restrict__ vout, const int p, uint32_t* run, uint32_t (*wc)[256]) {
   const int tid = threadIdx.x, wave = tid >> 6;
   const uint32_t t = tid < 256 ? tot[tid] : 0u;
   if (tid < 256) run[tid] = t;
@@ -308,7 +298,6 @@ SDX_DEV void rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __rest
       for (int w = 0; w < wave; ++w) pos += wc[w][dig];
       kout[pos] = k;
       vout[pos] = v;
-      if (hnext) atomicAdd(&hnext[(size_t)((k >> (8 * (d + 1))) & 255u) * np + pos / RS_PART], 1u);
     }
     __syncthreads();
     if (tid < 256) {
@@ -339,7 +328,6 @@ struct RsPass {
   uint32_t* hist;
   uint32_t* tot;
   int n, np;
-  uint32_t* hnext;  // folded form: the next pass's histogram (counted by this scatter), or null
 };
 __global__ __launch_bounds__(RS_T) void k_rs_hist2(RsPass a, RsPass b, int d) {
   __shared__ uint32_t c[256];
@@ -350,7 +338,7 @@ __global__ __launch_bounds__(RS_T) void k_rs_hist2(RsPass a, RsPass b, int d) {
 __global__ __launch_bounds__(256) void k_rs_scan_rows2(RsPass a, RsPass b) {
   const bool second = blockIdx.x >= 256 / 4;
   const RsPass& x = second ? b : a;
-  rs_scan_rows(x.hist, x.np, x.tot, (int)blockIdx.x - (second ? 256 / 4 : 0), x.hnext);
+  rs_scan_rows(x.hist, x.np, x.tot, (int)blockIdx.x - (second ? 256 / 4 : 0));
 }
 __global__ __launch_bounds__(RS_T) void k_rs_scatter2(RsPass a, RsPass b, int d) {
   __shared__ uint32_t run[256];
@@ -358,18 +346,17 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter2(RsPass a, RsPass b, int d)
   const bool second = (int)blockIdx.x >= a.np;
   const RsPass& x = second ? b : a;
   rs_scatter(x.kin, x.vin, x.n, x.np, d, x.hist, x.tot, x.kout, x.vout,
-             second ? (int)blockIdx.x - a.np : (int)blockIdx.x, run, wc, x.hnext);
+             second ? (int)blockIdx.x - a.np : (int)blockIdx.x, run, wc);
 }
 
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // workspace of the grouping: keys and message indices (two copies; the sorted indices end in the
-// caller's order buffer) + the sort's counts (two histograms: the folded form counts pass d + 1 while
-// pass d scatters)
+// caller's order buffer) + the sort's counts
 size_t group_bytes(int n) {
   if (n <= 0) return 0;
   const size_t np = (size_t)(n + RS_PART - 1) / RS_PART;
-  return 4 * align256(4 * (size_t)n) + 2 * align256(4 * 256 * np) + align256(4 * 256);
+  return 4 * align256(4 * (size_t)n) + align256(4 * 256 * np) + align256(4 * 256);
 }
 
 // The grouped order of a batch's messages (or of its sel_dev subset): order[0, n) = message indices
@@ -386,7 +373,7 @@ bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, in
   uint32_t* k1 = reinterpret_cast<uint32_t*>(work + 2 * a);
   uint32_t* v1 = reinterpret_cast<uint32_t*>(work + 3 * a);
   uint32_t* hist = reinterpret_cast<uint32_t*>(work + 4 * a);
-  uint32_t* tot = reinterpret_cast<uint32_t*>(work + 4 * a + 2 * align256(4 * 256 * (size_t)np));
+  uint32_t* tot = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)np));
   const int grid = (n + 255) / 256;
   if (kind == SDX_KIND_MU)
     hipLaunchKernelGGL((k_sig<SDX_KIND_MU>), dim3(grid), dim3(256), 0, st, bank_dev, b, k0, v0, mrec);
@@ -408,10 +395,8 @@ bool group_messages(const void* bank_dev, int kind, const sdx_pulse_batch& b, in
   return hipGetLastError() == hipSuccess;
 }
 
-// The step's MU and MS groupings (same results as two group_messages calls) in 10 launches instead of
-// 26: one k_sig2 and the first pass's histogram, then per radix pass one scan and one scatter launch over
-// both sorts' partitions, each scatter counting the next pass's histogram (SDX_GROUP_FOLD=0:
-// round 5's 13 launches, a histogram launch per pass)
+// The step's MU and MS groupings (same results as two group_messages calls) in 13 launches instead of
+// 26: one k_sig2, then per radix pass one hist, one scan and one scatter launch over both sorts' partitions
 bool group_messages2(const void* bank_dev, const sdx_pulse_batch& bmu, int32_t* omu, sdx_msg_rec* rmu, uint8_t* wmu,
                      size_t cmu, const sdx_pulse_batch& bms, int32_t* oms, sdx_msg_rec* rms, uint8_t* wms, size_t cms,
                      hipStream_t st) {
@@ -419,7 +404,7 @@ bool group_messages2(const void* bank_dev, const sdx_pulse_batch& bmu, int32_t* 
   const int nmu = bmu.sel_dev ? bmu.n_sel : bmu.n, nms = bms.sel_dev ? bms.n_sel : bms.n;
   if (nmu <= 0 || nms <= 0 || cmu < group_bytes(nmu) || cms < group_bytes(nms)) return false;
   struct Side {
-    uint32_t *k0, *v0, *k1, *v1, *hist, *hist2, *tot;
+    uint32_t *k0, *v0, *k1, *v1, *hist, *tot;
     int n, np;
   };
   auto side = [](uint8_t* work, int n) {
@@ -432,8 +417,7 @@ bool group_messages2(const void* bank_dev, const sdx_pulse_batch& bmu, int32_t* 
     x.k1 = reinterpret_cast<uint32_t*>(work + 2 * a);
     x.v1 = reinterpret_cast<uint32_t*>(work + 3 * a);
     x.hist = reinterpret_cast<uint32_t*>(work + 4 * a);
-    x.hist2 = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)x.np));
-    x.tot = reinterpret_cast<uint32_t*>(work + 4 * a + 2 * align256(4 * 256 * (size_t)x.np));
+    x.tot = reinterpret_cast<uint32_t*>(work + 4 * a + align256(4 * 256 * (size_t)x.np));
     return x;
   };
   const Side A = side(wmu, nmu), B = side(wms, nms);
@@ -444,15 +428,12 @@ bool group_messages2(const void* bank_dev, const sdx_pulse_batch& bmu, int32_t* 
     const int d = 4 - RS_PASSES + pi;
     const bool even = (pi & 1) == 0;
     const bool last = pi == RS_PASSES - 1;
-    // folded: pass pi reads histogram pi & 1 (hist / hist2) and counts pass pi + 1 into the other
     auto pass = [&](const Side& x, int32_t* order) {
-      uint32_t* hc = (SDX_GROUP_FOLD && (pi & 1)) ? x.hist2 : x.hist;
-      uint32_t* hn = (SDX_GROUP_FOLD && !last) ? ((pi & 1) ? x.hist : x.hist2) : nullptr;
       return RsPass{even ? x.k0 : x.k1, even ? x.v0 : x.v1, even ? x.k1 : x.k0,
-                    last ? reinterpret_cast<uint32_t*>(order) : (even ? x.v1 : x.v0), hc, x.tot, x.n, x.np, hn};
+                    last ? reinterpret_cast<uint32_t*>(order) : (even ? x.v1 : x.v0), x.hist, x.tot, x.n, x.np};
     };
     const RsPass pa = pass(A, omu), pb = pass(B, oms);
-    if (!SDX_GROUP_FOLD || pi == 0) hipLaunchKernelGGL(k_rs_hist2, dim3(A.np + B.np), dim3(RS_T), 0, st, pa, pb, d);
+    hipLaunchKernelGGL(k_rs_hist2, dim3(A.np + B.np), dim3(RS_T), 0, st, pa, pb, d);
     hipLaunchKernelGGL(k_rs_scan_rows2, dim3(2 * (256 / 4)), dim3(256), 0, st, pa, pb);
     hipLaunchKernelGGL(k_rs_scatter2, dim3(A.np + B.np), dim3(RS_T), 0, st, pa, pb, d);
   }
