@@ -2675,10 +2675,301 @@ SDX_DEV void mc_block(const void* __restrict__ bank, const sdx_mc_batch& b, cons
 #undef MCPROF_ADD
 }
 
+// ---------------------------------------------------------------------------------------------
+// compacted MC block (frames of <= 64 characters).  mc_block runs every protocol on
+// every wave: per (wave, protocol) the method and the result staging execute for the ~4 of 64 lanes
+// whose frame passed the protocol's gates, i.e. 4 waves x 12 protocols of mostly idle method passes
+// (measured: the methods + staging are 0.15 of k_mc's 0.18 ms; gates alone 0.03 ms).  Here the gates
+// run lane = frame and leave a 12-bit mask per frame; then each wave takes whole protocols (an LDS
+// counter) and runs the method over the frames of the WHOLE block that passed that protocol's gates,
+// compacted 64 to a pass -- the protocol stays wave-uniform (scalar record loads, mc_method as is) --
+// staging into block-wide pools; a block-level flush places the records in (frame, protocol) order.
+// Results, statuses and raise kinds are the per-frame sequential loop's: a frame raises with the kind
+// of the FIRST protocol (bank order) that raises for it, and then publishes nothing.
+// ---------------------------------------------------------------------------------------------
+constexpr int MC_BREC = 512, MC_BHEAP = 11264;  // block-wide staging pools (bench mean ~97 records,
+                                                 // ~2.9 KB of payload per 256 frames)
+constexpr int MC_CMAXP = 16;                      // protocols of the gate mask (the bank has 12)
+constexpr uint32_t MC_NORAISE = 0xFFFFFFFFu;
+template <int MW>
+struct McLdsC {
+  uint64_t bn[MW * 256];   // bits, polarity as given
+  uint64_t bi[MW * 256];   // bits, polarity inverted
+  StageRec rec[MC_BREC];
+  alignas(16) uint8_t heap[MC_BHEAP];
+  uint16_t gm[256];        // bit p: the frame passed protocol p's gates (and is valid hex)
+  uint16_t nbits[2][256];  // len(bits) as given / inverted (leading zero nibbles dropped)
+  uint8_t fl[256];         // the frame's flags (bits 0-1: message type / version)
+  uint8_t list[4][256];    // per wave: the frames of the protocol it runs
+  uint32_t fraise[256];    // p << 4 | kind of the first raising protocol (bank order), MC_NORAISE: none
+  uint32_t rcur, hcur, pnext, ovf;
+};
+
+template <int MW>
+SDX_DEV void mc_block_c(const void* __restrict__ bank, const sdx_mc_batch& b, const sdx_out& out, const int blk,
+                        const int tid, McLdsC<MW>& L) {
+  const BankView bv = bank_view(bank);
+  const int wave = tid >> 6, lane = tid & 63;
+  const int ntot = b.sel_dev ? b.n_sel : b.n;
+  const int gi = blk * 256 + tid;
+  bool valid = gi < ntot;
+  const int msg = valid ? (b.sel_dev ? b.sel_dev[gi] : gi) : 0;
+  const int nmc = (int)bv.hdr->n_mc;
+  if (tid == 0) {
+    L.rcur = 0;
+    L.hcur = 0;
+    L.pnext = 0;
+    L.ovf = 0;
+  }
+  // ---- lane = frame: this launch's share, hex -> bits (both polarities), the gates of every protocol
+  bool toolong = false;
+  if (valid) {
+    const int hl0 = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - b.offsets_dev[msg]);
+    valid = hl0 <= MC_SHORTW * 16;
+    // a frame longer than the batch's promised bound (0 < max_hex <= 64: no long launch follows) is
+    // marked for a re-run instead of being left without a descriptor
+    if (!valid && b.max_hex > 0 && b.max_hex <= MC_SHORTW * 16) toolong = true;
+  }
+  if (toolong) {
+    sdx_desc d;
+    d.rec_begin = 0;
+    d.n_rec = 0;
+    d.status = SDX_ST_OVF_TILE;
+    d.raise_kind = 0;
+    out.desc_dev[msg] = d;
+    atomicOr(&out.cursor_dev[2], 2u);
+  }
+  int nN = 0, nI = 0;
+  bool hex_ok = false;
+  int clock = 0, mcbit = 0, flags = 0, only = -1;
+  if (valid) {
+    const int64_t off = b.offsets_dev[msg];
+    const int hl = b.len_dev ? b.len_dev[msg] : (int)(b.offsets_dev[msg + 1] - off);
+    clock = b.clock_dev[msg];
+    mcbit = b.mcbitnum_dev[msg];
+    flags = b.flags_dev[msg];
+    if (b.only_dev) only = b.only_dev[msg];
+    hex_ok = hl > 0 && hl <= MW * 16;
+    if (hex_ok) mc_stage<MW>(b.hex_dev + off, hl, &L.bn[tid], &L.bi[tid], &nN, &nI, &hex_ok);
+  }
+  // gates of _demodulate_mc_data (manchester.py:70-89; clockrange fixed to [0] / [1])
+  uint32_t gm = 0;
+  for (int p = 0; p < nmc; ++p) {
+    const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
+    bool go = valid && (only < 0 || only == p);
+    if (go && mcbit < (cld(&r->has_lmin) ? cld(&r->lmin) : -1)) go = false;
+    if (go && mcbit > (cld(&r->has_lmax) ? cld(&r->lmax) : 9999)) go = false;
+    if (go && cld(&r->has_cr) && !((double)clock > cld(&r->cr_lo) && (double)clock < cld(&r->cr_hi))) go = false;
+    gm |= (uint32_t)go << p;
+  }
+  // a frame that is not valid hex raises at its first protocol past the gates (len(None) -> TypeError)
+  // and runs no method
+  const uint32_t r0 = (gm && !hex_ok) ? (((uint32_t)(__ffs(gm) - 1) << 4) | SDX_RAISE_TYPE) : MC_NORAISE;
+  L.gm[tid] = hex_ok ? (uint16_t)gm : (uint16_t)0;
+  L.nbits[0][tid] = (uint16_t)nN;
+  L.nbits[1][tid] = (uint16_t)nI;
+  L.fl[tid] = (uint8_t)(flags & 3);
+  L.fraise[tid] = r0;
+  __syncthreads();
+  // ---- per wave: whole protocols, each over the block's frames that passed its gates, 64 per pass
+  for (;;) {
+    int p = 0;
+    if (lane == 0) p = (int)atomicAdd(&L.pnext, 1u);
+    p = __shfl(p, 0);
+    if (p >= nmc) break;
+    const sdx_mc_proto* r = uniform_ptr(bv.mc + p);
+    int cnt = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f = g * 64 + lane;
+      const bool on = (L.gm[f] >> p) & 1u;
+      const uint64_t m = ballot(on);
+      if (on) L.list[wave][cnt + lanes_below(m)] = (uint8_t)f;
+      cnt += popc64(m);
+    }
+    wave_sync();
+    const bool pinv = cld(&r->invert) != 0;
+    const int method = cld(&r->method);
+    const int pl = cld(&r->pre_len), po = cld(&r->pre_off);
+    for (int i0 = 0; i0 < cnt; i0 += WAVE) {
+      const int i = i0 + lane;
+      const bool act = i < cnt;
+      const int f = act ? (int)L.list[wave][i] : 0;
+      const bool inv = pinv ^ (L.fl[f] != 0);  // (:91-96)
+      const LaneBits BN{&L.bn[f], MW, false}, BI{&L.bi[f], MW, false};
+      const LaneBits& B = inv ? BI : BN;
+      const int nb = L.nbits[inv ? 1 : 0][f];
+      McOut o{0, 0, 0, 0, 0, 0, 0, 0};
+      if (act) {
+        const LaneBits DM{B.base, MW, true};  // mc2dmc(lh/hl) view for Funkbus
+        o = mc_method(r, method, B, nb, nb, DM);
+        int rk = 0;
+        if (o.rc == -1) { rk = SDX_RAISE_TYPE; o.rc = 0; }
+        if (o.rc == -2) { rk = SDX_RAISE_VALUE; o.rc = 0; }
+        if (rk) atomicMin(&L.fraise[f], ((uint32_t)p << 4) | (uint32_t)rk);  // the first raising protocol
+      }
+      const bool has = o.rc == 1;
+      const uint64_t hm = ballot(has);
+      if (!hm) continue;
+      const int plen = has ? pl + o.len : 0;
+      int incl = plen;  // inclusive scan over lanes
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+      }
+      const int wtot = __shfl(incl, WAVE - 1);
+      const int nnew = popc64(hm);
+      uint32_t hb = 0, rb = 0;
+      if (lane == 0) {
+        hb = atomicAdd(&L.hcur, (uint32_t)wtot);
+        rb = atomicAdd(&L.rcur, (uint32_t)nnew);
+      }
+      hb = (uint32_t)__shfl((int)hb, 0);
+      rb = (uint32_t)__shfl((int)rb, 0);
+      const bool fits = hb + (uint32_t)wtot <= (uint32_t)MC_BHEAP && rb + (uint32_t)nnew <= (uint32_t)MC_BREC;
+      if (!fits) {
+        if (lane == 0) L.ovf = 1u;
+        continue;
+      }
+      if (has) {
+        uint8_t* dst = &L.heap[hb + incl - plen];
+        for (int k = 0; k < pl; k += 8) {  // 8 independent loads per step
+          uint8_t c[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) c[j] = (k + j < pl) ? bv.str[po + k + j] : (uint8_t)0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (k + j < pl) dst[k + j] = c[j];
+        }
+        mc_write(r, o, B, nb, nb, dst + pl);
+        StageRec sr;
+        sr.off = hb + (uint32_t)(incl - plen);
+        sr.len = (uint16_t)plen;
+        sr.proto = (uint16_t)p;
+        sr.bitlen = 0;
+        sr.msg = (uint8_t)f;
+        sr.wave = 0;
+        sr.rank = 0;
+        L.rec[rb + lanes_below(hm)] = sr;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- block flush: records bucketed by frame, each frame's in protocol order (flush_tile's scheme)
+  const int nr = (int)(L.rcur < (uint32_t)MC_BREC ? L.rcur : (uint32_t)MC_BREC);
+  const int nh = (int)(((L.hcur < (uint32_t)MC_BHEAP ? L.hcur : (uint32_t)MC_BHEAP) + 15u) & ~15u);
+  const bool bad = L.ovf != 0;
+  // scratch in the (dead) bit rows: per frame the record count, bucket fill, base, wire sums; the
+  // bucketed record indices
+  uint32_t* cntm = reinterpret_cast<uint32_t*>(L.bn);
+  uint32_t* fill = cntm + 256;
+  uint32_t* mbase = fill + 256;
+  uint32_t* wtot = mbase + 256;      // [4] per wave totals of the scan, [4..5] rbase / hbase, [6] st
+  unsigned long long* wsum = reinterpret_cast<unsigned long long*>(L.bi);
+  uint16_t* bidx = reinterpret_cast<uint16_t*>(wsum + 256);
+  static_assert(4 * (3 * 256 + 8) <= (int)sizeof(L.bn) && 8 * 256 + 2 * MC_BREC <= (int)sizeof(L.bi), "flush scratch");
+  const bool raised = L.fraise[tid] != MC_NORAISE;
+  cntm[tid] = 0;
+  fill[tid] = 0;
+  wsum[tid] = 0ull;
+  __syncthreads();
+  if (!bad)
+    for (int k = tid; k < nr; k += 256) {
+      const int f = L.rec[k].msg;
+      if (L.fraise[f] == MC_NORAISE) atomicAdd(&cntm[f], 1u);
+    }
+  __syncthreads();
+  // exclusive scan of the 256 counts (lane = frame): wave scans + the waves' totals
+  const uint32_t c = (valid && !raised && !bad) ? cntm[tid] : 0u;
+  uint32_t x = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wtot[wave] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int w = 0; w < wave; ++w) before += wtot[w];
+  mbase[tid] = before + x - c;
+  if (tid == 0) {
+    const uint32_t nrec = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    uint32_t st = bad ? 2u : 0u, rbase = 0, hbase = 0;
+    if (!bad) {
+      rbase = atomicAdd(&out.cursor_dev[0], nrec);
+      hbase = atomicAdd(&out.cursor_dev[1], (uint32_t)nh);
+      if (rbase + nrec > out.rec_cap || hbase + (uint32_t)nh > out.heap_cap) {
+        st = 3u;
+        atomicOr(&out.cursor_dev[2], 1u);
+      }
+    } else {
+      atomicOr(&out.cursor_dev[2], 2u);
+    }
+    wtot[4] = rbase;
+    wtot[5] = hbase;
+    wtot[6] = st;
+    wtot[7] = nrec;
+  }
+  __syncthreads();
+  const uint32_t rbase = wtot[4], hbase = wtot[5], st = wtot[6], nrec = wtot[7];
+  const bool wx = out.wire_dev != nullptr;
+  if (st == 0) {
+    for (int k = tid; k < nr; k += 256) {
+      const int f = L.rec[k].msg;
+      if (L.fraise[f] != MC_NORAISE) continue;
+      const uint32_t q = atomicAdd(&fill[f], 1u);
+      bidx[mbase[f] + q] = (uint16_t)k;
+    }
+    __syncthreads();
+    for (int j = tid; j < (int)nrec; j += 256) {
+      const StageRec sr = L.rec[bidx[j]];
+      const uint32_t b0 = mbase[sr.msg], b1 = b0 + cntm[sr.msg];
+      uint32_t rk = 0;  // one record per (frame, protocol): its rank = the frame's records of lower protocols
+      for (uint32_t q = b0; q < b1; ++q) rk += L.rec[bidx[q]].proto < sr.proto ? 1u : 0u;
+      const int gf = blk * 256 + sr.msg;
+      sdx_result o;
+      o.payload_off = hbase + sr.off;
+      o.payload_len = sr.len;
+      o.proto = sr.proto;
+      o.bit_length = 0;
+      o.msg = (uint32_t)(b.sel_dev ? b.sel_dev[gf] : gf);
+      out.rec_dev[rbase + b0 + rk] = o;
+      if (wx) {
+        const uint32_t xr = wire_class(bv, SDX_KIND_MC, sr.proto, &L.heap[sr.off], sr.len);
+        if (out.xrec_dev) out.xrec_dev[rbase + b0 + rk] = xr;
+        atomicAdd(&wsum[sr.msg], (unsigned long long)(((uint64_t)sr.len << 32) | wire_bytes_x(xr, sr.len)));
+      }
+    }
+    uint4* hd = reinterpret_cast<uint4*>(out.heap_dev + hbase);
+    const uint4* hs = reinterpret_cast<const uint4*>(L.heap);
+    if ((((uintptr_t)hd) & 15u) == 0) {
+      for (int k = tid; k < (nh >> 4); k += 256) hd[k] = hs[k];
+    } else {
+      for (int k = tid; k < nh; k += 256) out.heap_dev[hbase + k] = L.heap[k];
+    }
+  }
+  if (wx) __syncthreads();  // wsum complete
+  if (valid) {
+    sdx_desc d;
+    d.rec_begin = rbase + mbase[tid];
+    const uint32_t rw = L.fraise[tid];
+    if (rw != MC_NORAISE) { d.status = SDX_ST_RAISED; d.raise_kind = (uint8_t)(rw & 15u); d.n_rec = 0; }
+    else if (st) { d.status = st == 2 ? SDX_ST_OVF_TILE : SDX_ST_OVF_OUT; d.raise_kind = 0; d.n_rec = 0; }
+    else { d.status = SDX_ST_OK; d.raise_kind = 0; d.n_rec = (uint16_t)cntm[tid]; }
+    out.desc_dev[msg] = d;
+    if (wx) out.wire_dev[msg] = (rw == MC_NORAISE && st == 0) ? (uint64_t)wsum[tid] : 0ull;
+  }
+}
+
 template <int MW, bool LONG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LONG ? 1 : SDX_MC_WPE))) void k_mc(const void* __restrict__ bank, sdx_mc_batch b, sdx_out out) {
-  __shared__ McLds<MW> L;
-  mc_block<MW, LONG>(bank, b, out, (int)blockIdx.x, (int)threadIdx.x, L);
+  if constexpr (LONG) {
+    __shared__ McLds<MW> L;
+    mc_block<MW, LONG>(bank, b, out, (int)blockIdx.x, (int)threadIdx.x, L);
+  } else {
+    __shared__ McLdsC<MW> L;
+    mc_block_c<MW>(bank, b, out, (int)blockIdx.x, (int)threadIdx.x, L);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2737,7 +3028,7 @@ union StepLds {
   PulsesLds<SDX_KIND_MU, 4, 64> mu;
   PulsesLds<SDX_KIND_MS, 2, 64> ms2;
   PulsesLds<SDX_KIND_MS, 4, 64> ms4;
-  McLds<MC_SHORTW> mc[2];
+  McLdsC<MC_SHORTW> mc[2];
 };
 static_assert(sizeof(StepLds) <= 81920, "two k_step workgroups per CU (160 KB of LDS)");
 
@@ -2766,7 +3057,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     ms_tile_by_class<MRS>(bank, a.ms, a.ms_out, w, U.ms2, U.ms4, msg_of);
   } else {
     const int half = (int)threadIdx.x >> 8;
-    mc_block<MC_SHORTW, false>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
+    mc_block_c<MC_SHORTW>(bank, a.mc, a.mc_out, 2 * w + half, (int)threadIdx.x & 255, U.mc[half]);
   }
 }
 
@@ -3061,6 +3352,7 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
   // after the fused kernel on the same stream
   const bool ms_fused = step->ms && SDX_MS_NARROW;
   const bool mc_fused = step->mc && step->mc->max_hex > 0 && step->mc->max_hex <= SDX_MC_SHORT_HEX;
+  if (step->mc && (int)bank->hdr.n_mc > sdx::MC_CMAXP) return fail(SDX_EINVAL, "the MC kernel's gate mask holds 16 MC protocols");
   if (step->mu) {
     const sdx_pulse_batch& b = *step->mu;
     if ((uintptr_t)b.mrec_dev & 127) return fail(SDX_EINVAL, "mrec_dev must be 128-byte aligned");
@@ -3109,6 +3401,7 @@ int sdx_demod_step(const sdx_bank* bank, const sdx_step* step, void* hip_stream)
 
 int sdx_demod_mc(const sdx_bank* bank, const sdx_mc_batch* batch, const sdx_out* out, void* hip_stream) {
   if (!bank || !batch || !out) return fail(SDX_EINVAL, "null argument");
+  if ((int)bank->hdr.n_mc > sdx::MC_CMAXP) return fail(SDX_EINVAL, "the MC kernel's gate mask holds 16 MC protocols");
   const int ntot = batch->sel_dev ? batch->n_sel : batch->n;
   if (ntot <= 0) return SDX_OK;
   hipStream_t st = (hipStream_t)hip_stream;
