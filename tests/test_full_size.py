@@ -85,13 +85,15 @@ def test_config_size_vs_c_oracle(kind, seed):
     assert _compare_with_c_oracle(kind, bk, batch, desc, rec, heap) > N // 4   # the corpora decode
 
 
-def test_bench_step_vs_c_oracle():
+@pytest.mark.parametrize("batch", [0, 1, 2])
+def test_bench_step_vs_c_oracle(batch):
     """The kernel the bench times, at the bench's exact configuration, against the C oracle (VERDICT r05
     #1): bench.py's corpora (seeds 42/43/44, 333,333 / 333,333 / 333,334 messages, noise 0.15 / 0.1),
     one sdx_group_step for the MU and MS orders, then ONE sdx_demod_step (k_step: MU, MS and MC tiles,
     the MS length classes, MC with its max_hex bound) into the bench's output capacities -- every
     message's status and ordered result list equal to oracle/sd_oracle_c.c's
-    (message_unsynced.py:11-296, message_synced.py:10-243, manchester.py:49-144)."""
+    (message_unsynced.py:11-296, message_synced.py:10-243, manchester.py:49-144).  batch: each of the
+    three corpora bench.py cycles by default (--batches 3: seeds + 100 * batch)."""
     import torch
     from pysignalduino_amd import bank as B, runtime, synth
     bk = B.Bank()
@@ -99,9 +101,10 @@ def test_bench_step_vs_c_oracle():
     P = bk.protocols
     msgs = 1_000_000
     per = {"MU": msgs // 3, "MS": msgs // 3, "MC": msgs - 2 * (msgs // 3)}
-    corp = {"MU": synth.mu_corpus(P, per["MU"], seed=42, noise_frac=0.15),
-            "MS": synth.ms_corpus(P, per["MS"], seed=43, noise_frac=0.1),
-            "MC": synth.mc_corpus(P, per["MC"], seed=44)}
+    sd = 100 * batch
+    corp = {"MU": synth.mu_corpus(P, per["MU"], seed=42 + sd, noise_frac=0.15),
+            "MS": synth.ms_corpus(P, per["MS"], seed=43 + sd, noise_frac=0.1),
+            "MC": synth.mc_corpus(P, per["MC"], seed=44 + sd)}
     bds = {k: (eng.to_device_mc(c) if k == "MC" else eng.to_device_pulses(c)) for k, c in corp.items()}
     assert 0 < bds["MC"]["max_hex"] <= runtime.MC_HEX_MAX
     caps = {"MU": (12, 320), "MS": (4, 64), "MC": (4, 96)}   # bench.py's capacities
