@@ -42,14 +42,25 @@ def source_hash() -> str:
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     deps = DEPS
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+    hsrc = os.path.join(os.path.dirname(OUT), "obj", "sdx_hash.cpp")
+    built_hash = open(hsrc).read() if os.path.exists(hsrc) else ""
+    if (not force and os.path.exists(OUT) and source_hash() in built_hash and
+            all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps)):
         return OUT
-    # one object per translation unit, compiled in parallel, then one link
+    # one object per translation unit, compiled in parallel, then one link.  A unit is recompiled when
+    # its source or any shared header is newer than its object (the headers are few; every unit may
+    # include them); the source hash lives in a generated unit of its own, rebuilt every time
     objdir = os.path.join(os.path.dirname(OUT), "obj")
     os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, os.path.basename(src) + ".o") for src in SRCS]
-    cmds = [[HIPCC, *FLAGS[:-1], f'-DSDX_SRC_HASH="{source_hash()}"', "-c", src, "-o", obj]
-            for src, obj in zip(SRCS, objs)]
+    hdr_t = max(os.path.getmtime(d) for d in DEPS if d not in SRCS)
+    stale = [(src, obj) for src, obj in zip(SRCS, objs)
+             if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t)]
+    cmds = [[HIPCC, *FLAGS[:-1], "-c", src, "-o", obj] for src, obj in stale]
+    with open(hsrc, "w") as fh:
+        fh.write('extern "C" const char* sdx_source_hash(void) { return "%s"; }\n' % source_hash())
+    hobj = hsrc + ".o"
+    cmds.append(["g++", "-O2", "-fPIC", "-c", hsrc, "-o", hobj])
     if verbose:
         for c in cmds:
             print(" ".join(c))
@@ -57,7 +68,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as ex:
         for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
             f.result()
-    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", *objs, "-o", OUT + ".tmp"]
+    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", *objs, hobj, "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

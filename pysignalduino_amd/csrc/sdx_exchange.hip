@@ -19,17 +19,18 @@
 //               against the part's cursor / capacities, classify the payloads (raw / nibble), count
 //               records, wire payload bytes and payload bytes, block-scan them, block totals;
 //   k_xw_scan   one block per launch: exclusive block offsets, the launch's counts;
-//   k_xw_pack   block = the count block's 256 messages: wire words and wire records (lane = message),
-//               then the payloads (lane = 32 output bytes, coalesced 16-byte stores).  The source
-//               records are in tile order (k_pulses places them per tile); the wire is in message
-//               order, so the pack is also the canonicalisation that makes sharded and un-sharded
-//               runs compare byte for byte.
+//   k_xw_words + k_xw_recs (round 6; k_xw_pack before, kept as the SDX_XCHG_PACK_MSG=1 A/B): the wire
+//               words (lane = message), then every shipped record with its payload (lane = source
+//               record, in each part's own order).  The source records are in tile order (k_pulses
+//               places them per tile); the wire is in message order, so the pack is also the
+//               canonicalisation that makes sharded and un-sharded runs compare byte for byte.
 // Receiver:
 //   k_xu_sum / k_xu_scan / k_xu_write / k_xu_heap  rebuild sdx_desc / sdx_result / one contiguous heap
 //               of the whole job from the gathered wire sections of every rank.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <string>
 
 #include "../../include/sdx.h"
@@ -65,6 +66,7 @@ __host__ __device__ inline uint64_t part_work_bytes(uint32_t n) {
 struct Parts {
   sdx_xchg_part p[XMAX];
   uint64_t work_off[XMAX];
+  int owner[XMAX];      // the launch each part's records ship in (itself, or the launch it overlays); -1 none
   const uint8_t* bank;  // nullptr: raw payloads only
   int k;
 };
@@ -470,6 +472,140 @@ __global__ __launch_bounds__(XT) void k_xw_pack(Parts P, const uint32_t* __restr
   }
 }
 
+// ---- the pack in source-record order (round 6) -----------------------------------------------------
+// k_xw_pack reads the launches' records in WIRE order (message order): the grouping puts consecutive
+// messages in different tiles, so every message's records and payloads are a dependent, scattered
+// read (desc -> record -> payload), and under a concurrently running k_step those latencies are what
+// the pack costs.  The same bytes are produced here from the other side:
+//   k_xw_words  lane = message: the wire word (coalesced descriptor reads);
+//   k_xw_recs   lane = source record of a part (primary or overlay), in the part's own order, so the
+//               record, xrec and payload reads stream; the record's message (sdx_result.msg) gives its
+//               wire place: the message's record / wire-byte prefix from the count (loc + blk) plus its
+//               index in the message and the wire bytes of the message's earlier records (a wave scan;
+//               a message that began in an earlier wave adds them by a short loop).  A record is
+//               shipped iff its message resolves to this part, is shippable (not bad, status OK) and its
+//               range holds the record -- exactly the records the count counted, each once.
+// The stores are scattered instead (fire-and-forget, runs of ~4 records per message).
+__global__ __launch_bounds__(XT) void k_xw_words(Parts P, const uint32_t* __restrict__ counts,
+                                                 uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
+  const int k = blockIdx.y;
+  const sdx_xchg_part& x = P.p[k];
+  if (x.aux || blockIdx.x >= nblk_of(x.n_msgs)) return;
+  PartWork w = part_work(work, P, k);
+  const uint32_t* ck = counts + SDX_XCHG_COUNTS * k;
+  uint64_t so[3];
+  section_offsets(counts, P.k, k, so);
+  uint8_t* s_msg = send + so[0];
+  if (blockIdx.x == 0) {  // deterministic section padding
+    zero_tail(s_msg, 4ull * x.n_msgs, threadIdx.x);
+    zero_tail(send + so[1], 8ull * ck[1], threadIdx.x);
+    zero_tail(send + so[2], ck[2], threadIdx.x);
+  }
+  const uint32_t m = blockIdx.x * XB + threadIdx.x;
+  if (m < x.n_msgs) {
+    sdx_desc d;
+    resolve(P, k, m, &d);
+    const bool bad = (w.loc[m] & BADBIT) != 0;
+    const uint32_t nr = (bad || d.status != SDX_ST_OK) ? 0u : d.n_rec;
+    reinterpret_cast<uint32_t*>(s_msg)[m] =
+        nr | ((uint32_t)(bad ? SDX_ST_OVF_OUT : d.status) << 16) | ((uint32_t)d.raise_kind << 24);
+  }
+}
+
+// the wire bytes of record t of part y (its class as the pack below decides it)
+__device__ inline uint32_t rec_wire_bytes(const Parts& P, const sdx_xchg_part& y, uint32_t t) {
+  const sdx_result rr = reinterpret_cast<const sdx_result*>(y.rec_dev)[t];
+  int dg;
+  if (y.xrec_dev) {
+    const uint32_t xr = nibble_on(P, y) ? y.xrec_dev[t] : 0u;
+    dg = (xr & SDX_XREC_NIB) ? (int)(xr & 0xFFFFu) : -1;
+  } else {
+    dg = nib_digits(affix_of(P.bank, y.kind, rr.proto), y.heap_dev + rr.payload_off, rr.payload_len);
+  }
+  return wire_bytes_of(dg, rr.payload_len);
+}
+
+// grid (record blocks, parts): blockIdx.y = the source part y, owner[y] = the launch it ships in
+__global__ __launch_bounds__(XT) void k_xw_recs(Parts P, const uint32_t* __restrict__ counts,
+                                                uint8_t* __restrict__ work, uint8_t* __restrict__ send) {
+  const int y = blockIdx.y;
+  const sdx_xchg_part& yp = P.p[y];
+  const int k = P.owner[y];
+  if (k < 0) return;
+  uint32_t nrec_c, nheap_c;
+  clamp_counts(yp, &nrec_c, &nheap_c);
+  if (blockIdx.x * XB >= nrec_c) return;  // block-uniform
+  const sdx_xchg_part& x = P.p[k];
+  PartWork w = part_work(work, P, k);
+  uint64_t so[3];
+  section_offsets(counts, P.k, k, so);
+  sdx_wire_rec* s_rec = reinterpret_cast<sdx_wire_rec*>(send + so[1]);
+  uint8_t* s_heap = send + so[2];
+  const uint32_t i = blockIdx.x * XB + threadIdx.x;
+  const int lane = lane_id();
+  bool ok = false;
+  uint32_t m = 0, j = 0, rb = 0, wl = 0;
+  int dg = -1;
+  const uint8_t* s0 = nullptr;
+  uint64_t dst_rec = 0, dst_msg = 0;  // the message's first wire record / its wire payload offset
+  if (i < nrec_c) {
+    const sdx_result rr = reinterpret_cast<const sdx_result*>(yp.rec_dev)[i];
+    m = rr.msg;
+    if (m < x.n_msgs) {
+      sdx_desc d;
+      const int kr = resolve(P, k, m, &d);
+      const uint64_t loc = w.loc[m];
+      ok = kr == y && d.status == SDX_ST_OK && !(loc & BADBIT) && i >= d.rec_begin && i - d.rec_begin < d.n_rec;
+      if (ok) {
+        rb = d.rec_begin;
+        j = i - d.rec_begin;
+        const uint64_t b = w.blk[m / XB];
+        dst_rec = (b >> 32) + (loc >> 32);
+        dst_msg = (uint32_t)b + (uint32_t)loc;
+        const uint8_t* src = yp.heap_dev + rr.payload_off;
+        uint32_t npre = 0;
+        if (yp.xrec_dev) {
+          const uint32_t xr = nibble_on(P, yp) ? yp.xrec_dev[i] : 0u;
+          dg = (xr & SDX_XREC_NIB) ? (int)(xr & 0xFFFFu) : -1;
+          npre = (xr >> 16) & 0xFFu;
+        } else {
+          const Affix a = affix_of(P.bank, yp.kind, rr.proto);
+          dg = nib_digits(a, src, rr.payload_len);
+          npre = a.npre;
+        }
+        sdx_wire_rec o;
+        o.proto = (uint16_t)(rr.proto | (dg >= 0 ? SDX_WIRE_NIB : 0u));
+        o.payload_len = rr.payload_len;
+        o.bit_length = rr.bit_length;
+        s_rec[dst_rec + j] = o;
+        s0 = dg >= 0 ? src + npre : src;
+        wl = wire_bytes_of(dg, rr.payload_len);
+      }
+    }
+  }
+  // the wire bytes of the message's records before this one: the wave's exclusive scan from the
+  // message's first lane in this wave; a message that began before the wave (lane 0's, j > 0) also
+  // counts its records there
+  uint32_t inc = wl;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if (lane >= o) inc += v;
+  }
+  const uint32_t exc = inc - wl;
+  const int head = ok ? lane - (int)j : lane;  // the message's first lane (< 0: an earlier wave)
+  const uint32_t at_head = __shfl(exc, head > 0 ? head : 0);
+  uint32_t carry = 0;
+  if (lane == 0 && ok && j > 0) {
+    for (uint32_t t = rb; t < i; ++t) carry += rec_wire_bytes(P, yp, t);
+  }
+  carry = __shfl(carry, 0);
+  if (ok && wl) {
+    const uint32_t pre = head >= 0 ? exc - at_head : exc + carry;
+    wire_copy(s_heap + dst_msg + pre, s0, dg, wl);
+  }
+}
+
 // ---- receiver ------------------------------------------------------------------------------------
 struct Wire {
   sdx_xchg_wire r[XRANKS];
@@ -641,7 +777,18 @@ static Parts make_parts(const sdx_bank* bank, const sdx_xchg_part* parts, int k)
   for (int i = 0; i < XMAX; ++i) {
     P.p[i] = i < k ? parts[i] : sdx_xchg_part{};
     P.work_off[i] = off;
+    P.owner[i] = -1;
     if (i < k) off += part_work_bytes(parts[i].n_msgs);
+  }
+  for (int i = 0; i < k; ++i) {  // each launch and the overlays along its chain (resolve's walk)
+    if (parts[i].aux) continue;
+    P.owner[i] = i;
+    for (int c = i, hop = 0; hop < CHAIN; ++hop) {
+      const int a = (int)parts[c].alt - 1;
+      if (a < 0 || a >= k) break;
+      if (P.owner[a] < 0) P.owner[a] = i;
+      c = a;
+    }
   }
   return P;
 }
@@ -664,6 +811,25 @@ static uint32_t max_blocks(const sdx_xchg_part* parts, int k) {
   return nb;
 }
 
+// the pack: SDX_XCHG_PACK_MSG=1 in the environment selects the message-order k_xw_pack (A/B);
+// otherwise k_xw_words + k_xw_recs (the same bytes, source-record order)
+static int launch_pack(const sdx_bank* bank, const sdx_xchg_part* parts, int k, const uint32_t* counts_dev,
+                       uint8_t* work, uint8_t* dst, hipStream_t st) {
+  const char* e = getenv("SDX_XCHG_PACK_MSG");  // read per call: a test compares both forms in one process
+  const bool msg_order = e && e[0] == '1';
+  const Parts P = make_parts(bank, parts, k);
+  if (msg_order) {
+    hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, st, P, counts_dev, work, dst);
+    return launched("k_xw_pack");
+  }
+  hipLaunchKernelGGL(k_xw_words, dim3(max_blocks(parts, k), k), dim3(XT), 0, st, P, counts_dev, work, dst);
+  if (int rc = launched("k_xw_words")) return rc;
+  uint32_t nbr = 1;  // record blocks: the largest part's record capacity (blocks past its cursor return)
+  for (int i = 0; i < k; ++i) nbr = nblk_of(parts[i].rec_cap) > nbr ? nblk_of(parts[i].rec_cap) : nbr;
+  hipLaunchKernelGGL(k_xw_recs, dim3(nbr, k), dim3(XT), 0, st, P, counts_dev, work, dst);
+  return launched("k_xw_recs");
+}
+
 extern "C" int sdx_exchange_count(const sdx_bank* bank, const sdx_xchg_part* parts, int k, void* work_dev,
                                   uint64_t work_cap, uint32_t* counts_dev, void* hip_stream) {
   if (int rc = check_parts(parts, k, "sdx_exchange_count")) return rc;
@@ -684,9 +850,7 @@ extern "C" int sdx_exchange_pack(const sdx_bank* bank, const sdx_xchg_part* part
   if (!counts_dev || !send_dev || ((uintptr_t)send_dev & 15u) || send_cap < sdx_exchange_send_bytes(parts, k) ||
       !work_ok(parts, k, work_dev, work_cap))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack: workspace or send buffer too small / unaligned");
-  hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream,
-                     make_parts(bank, parts, k), counts_dev, (uint8_t*)work_dev, send_dev);
-  return launched("k_xw_pack");
+  return launch_pack(bank, parts, k, counts_dev, (uint8_t*)work_dev, send_dev, (hipStream_t)hip_stream);
 }
 
 // the pack into a buffer sized from the host's copy of the counts (the exact layout), e.g. the rank's
@@ -705,9 +869,7 @@ extern "C" int sdx_exchange_pack_into(const sdx_bank* bank, const sdx_xchg_part*
     need += r16(4ull * c[0]) + r16(8ull * c[1]) + r16(c[2]);
   }
   if (dst_cap < need) return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: destination smaller than the wire");
-  hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, (hipStream_t)hip_stream,
-                     make_parts(bank, parts, k), counts_dev, (uint8_t*)work_dev, dst_dev);
-  return launched("k_xw_pack");
+  return launch_pack(bank, parts, k, counts_dev, (uint8_t*)work_dev, dst_dev, (hipStream_t)hip_stream);
 }
 
 extern "C" uint64_t sdx_exchange_unpack_work_bytes(uint32_t n_msgs, uint32_t n_rec) {

@@ -3127,10 +3127,8 @@ int sdx_wgtime_read(unsigned long long* out, int n) {
 #endif
 const char* sdx_last_error(void) { return g_err.c_str(); }
 
-#ifndef SDX_SRC_HASH
-#define SDX_SRC_HASH "unknown"
-#endif
-const char* sdx_source_hash(void) { return SDX_SRC_HASH; }
+// sdx_source_hash(): defined in the build's generated translation unit (build.py, _lib/obj/sdx_hash.cpp),
+// so a change of one source recompiles only that source
 
 int sdx_layout_size(int which) {
   switch (which) {

@@ -420,12 +420,15 @@ def _kernel_exchange(eng=None):
 
 
 @pytest.mark.gpu
-def test_exchange_kernels_match_host_wire():
+@pytest.mark.parametrize("pack_form", ["records", "messages"])
+def test_exchange_kernels_match_host_wire(pack_form, monkeypatch):
     """sdx_exchange_count / sdx_exchange_pack (HIP) == the numpy wire form for K = 3 launches laid
     out like k_pulses output (shuffled tiles, padded heap, RAISED / empty / unowned records), raw and
     in the nibble form (the real bank's MU affixes), and sdx_exchange_unpack over 3 ranks' sections ==
-    wire_decode; an out-of-range message is counted bad."""
+    wire_decode; an out-of-range message is counted bad.  Both packs: source-record order (k_xw_words
+    + k_xw_recs, the default) and message order (k_xw_pack, SDX_XCHG_PACK_MSG=1)."""
     from pysignalduino_amd import bank as bankmod
+    monkeypatch.setenv("SDX_XCHG_PACK_MSG", "1" if pack_form == "messages" else "0")
     dev = torch.device("cuda", 0)
     eng = runtime.Engine(bankmod.Bank(), 0)
     affix = eng.bank.affixes(runtime.KIND_MU)

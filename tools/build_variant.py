@@ -31,7 +31,7 @@ def main():
     inc = ["-I", os.path.join(REPO, "pysignalduino_amd", "csrc")]
     subprocess.run([B.HIPCC, *B.FLAGS[:-1], *inc, *args, "-c", src, "-o", obj], check=True)
     others = [os.path.join(REPO, "pysignalduino_amd", "_lib", "obj", os.path.basename(s) + ".o") for s in B.SRCS
-              if os.path.basename(s) != unit]
+              if os.path.basename(s) != unit] + [os.path.join(REPO, "pysignalduino_amd", "_lib", "obj", "sdx_hash.cpp.o")]
     so = os.path.join(out_dir, f"libsdx_{name}.so")
     subprocess.run([B.HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", obj, *others, "-o", so], check=True)
     print(so)
