@@ -552,6 +552,7 @@ __global__ __launch_bounds__(XT) void k_xw_recs(Parts P, const uint32_t* __restr
   int dg = -1;
   const uint8_t* s0 = nullptr;
   uint64_t dst_rec = 0, dst_msg = 0;  // the message's first wire record / its wire payload offset
+  uint32_t nr = 0, tot_m = 0;         // the message's records and wire payload bytes
   if (i < nrec_c) {
     const sdx_result rr = reinterpret_cast<const sdx_result*>(yp.rec_dev)[i];
     m = rr.msg;
@@ -566,6 +567,11 @@ __global__ __launch_bounds__(XT) void k_xw_recs(Parts P, const uint32_t* __restr
         const uint64_t b = w.blk[m / XB];
         dst_rec = (b >> 32) + (loc >> 32);
         dst_msg = (uint32_t)b + (uint32_t)loc;
+        nr = d.n_rec;
+        const uint32_t m1 = m + 1;  // the next message's wire payload offset (the launch's total at the end)
+        const uint32_t wend = m1 < x.n_msgs ? (uint32_t)w.blk[m1 / XB] + (uint32_t)w.loc[m1]
+                                            : counts[SDX_XCHG_COUNTS * k + 2];
+        tot_m = wend - (uint32_t)dst_msg;
         const uint8_t* src = yp.heap_dev + rr.payload_off;
         uint32_t npre = 0;
         if (yp.xrec_dev) {
@@ -587,9 +593,10 @@ __global__ __launch_bounds__(XT) void k_xw_recs(Parts P, const uint32_t* __restr
       }
     }
   }
-  // the wire bytes of the message's records before this one: the wave's exclusive scan from the
-  // message's first lane in this wave; a message that began before the wave (lane 0's, j > 0) also
-  // counts its records there
+  // the wire bytes of the message's records before this one, from the wave's scan: counted forward
+  // from the message's first lane when it starts in this wave; otherwise backward from its total
+  // (the count's prefixes) when it ends in this wave; a message spanning the whole wave (more than 64
+  // records, rare) has lane 0 add up its earlier records
   uint32_t inc = wl;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -597,15 +604,17 @@ __global__ __launch_bounds__(XT) void k_xw_recs(Parts P, const uint32_t* __restr
     if (lane >= o) inc += v;
   }
   const uint32_t exc = inc - wl;
-  const int head = ok ? lane - (int)j : lane;  // the message's first lane (< 0: an earlier wave)
+  const int head = ok ? lane - (int)j : lane;            // the message's first lane (< 0: an earlier wave)
+  const int tail = ok ? lane + (int)(nr - 1 - j) : lane;  // its last lane (> 63: a later wave)
   const uint32_t at_head = __shfl(exc, head > 0 ? head : 0);
+  const uint32_t at_tail = __shfl(inc, tail < 63 ? tail : 63);
   uint32_t carry = 0;
-  if (lane == 0 && ok && j > 0) {
+  if (lane == 0 && ok && j > 0 && tail > 63) {
     for (uint32_t t = rb; t < i; ++t) carry += rec_wire_bytes(P, yp, t);
   }
   carry = __shfl(carry, 0);
   if (ok && wl) {
-    const uint32_t pre = head >= 0 ? exc - at_head : exc + carry;
+    const uint32_t pre = head >= 0 ? exc - at_head : (tail <= 63 ? tot_m - (at_tail - exc) : exc + carry);
     wire_copy(s_heap + dst_msg + pre, s0, dg, wl);
   }
   }
@@ -819,7 +828,7 @@ static uint32_t max_blocks(const sdx_xchg_part* parts, int k) {
 // the pack: SDX_XCHG_PACK_MSG=1 in the environment selects the message-order k_xw_pack (A/B);
 // otherwise k_xw_words + k_xw_recs (the same bytes, source-record order)
 static int launch_pack(const sdx_bank* bank, const sdx_xchg_part* parts, int k, const uint32_t* counts_dev,
-                       uint8_t* work, uint8_t* dst, hipStream_t st) {
+                       const uint32_t* counts_host, uint8_t* work, uint8_t* dst, hipStream_t st) {
   const char* e = getenv("SDX_XCHG_PACK_MSG");  // read per call: a test compares both forms in one process
   const bool msg_order = e && e[0] == '1';
   const Parts P = make_parts(bank, parts, k);
@@ -829,10 +838,17 @@ static int launch_pack(const sdx_bank* bank, const sdx_xchg_part* parts, int k, 
   }
   hipLaunchKernelGGL(k_xw_words, dim3(max_blocks(parts, k), k), dim3(XT), 0, st, P, counts_dev, work, dst);
   if (int rc = launched("k_xw_words")) return rc;
-  uint32_t nbr = 1;  // record blocks: the largest part's record capacity, at most XREC_GRID (grid-stride)
-  for (int i = 0; i < k; ++i) nbr = nblk_of(parts[i].rec_cap) > nbr ? nblk_of(parts[i].rec_cap) : nbr;
-  nbr = nbr < XREC_GRID ? nbr : XREC_GRID;  // (a bounded grid-stride grid of 1024 blocks measured
-                                            //  slower: 87.7 vs 70.3 us for the bench step)
+  // record blocks: one per 256 records of the largest part's capacity, or, with the host's copy of the
+  // counts, of the largest launch's shipped records (plus one block): the blocks past a part's cursor
+  // return at once but still cost their dispatch (47k of them for the bench step's capacities), and
+  // records past the grid (overlays, records not shipped) are taken by the grid-stride loop.  (A
+  // grid of 1024 blocks per part measured slower: 87.7 vs 70.3 us for the bench step.)
+  uint32_t nbr = 1;
+  for (int i = 0; i < k; ++i) {
+    const uint32_t nb = counts_host ? nblk_of(counts_host[SDX_XCHG_COUNTS * i + 1]) + 1 : nblk_of(parts[i].rec_cap);
+    nbr = nb > nbr ? nb : nbr;
+  }
+  nbr = nbr < XREC_GRID ? nbr : XREC_GRID;
   hipLaunchKernelGGL(k_xw_recs, dim3(nbr, k), dim3(XT), 0, st, P, counts_dev, work, dst);
   return launched("k_xw_recs");
 }
@@ -857,7 +873,7 @@ extern "C" int sdx_exchange_pack(const sdx_bank* bank, const sdx_xchg_part* part
   if (!counts_dev || !send_dev || ((uintptr_t)send_dev & 15u) || send_cap < sdx_exchange_send_bytes(parts, k) ||
       !work_ok(parts, k, work_dev, work_cap))
     return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack: workspace or send buffer too small / unaligned");
-  return launch_pack(bank, parts, k, counts_dev, (uint8_t*)work_dev, send_dev, (hipStream_t)hip_stream);
+  return launch_pack(bank, parts, k, counts_dev, nullptr, (uint8_t*)work_dev, send_dev, (hipStream_t)hip_stream);
 }
 
 // the pack into a buffer sized from the host's copy of the counts (the exact layout), e.g. the rank's
@@ -876,7 +892,7 @@ extern "C" int sdx_exchange_pack_into(const sdx_bank* bank, const sdx_xchg_part*
     need += r16(4ull * c[0]) + r16(8ull * c[1]) + r16(c[2]);
   }
   if (dst_cap < need) return sdx::set_error(SDX_EINVAL, "sdx_exchange_pack_into: destination smaller than the wire");
-  return launch_pack(bank, parts, k, counts_dev, (uint8_t*)work_dev, dst_dev, (hipStream_t)hip_stream);
+  return launch_pack(bank, parts, k, counts_dev, counts_host, (uint8_t*)work_dev, dst_dev, (hipStream_t)hip_stream);
 }
 
 extern "C" uint64_t sdx_exchange_unpack_work_bytes(uint32_t n_msgs, uint32_t n_rec) {
