@@ -79,6 +79,8 @@ def parse():
                          "sdx_group_step (13 launches; A/B)")
     ap.add_argument("--mc-apart", action="store_true",
                     help="A/B: MC's frames in their own launch after k_step (MU + MS) instead of k_step's last range")
+    ap.add_argument("--ms-ungrouped", action="store_true",
+                    help="A/B: group only the MU batch; MS tiles in arrival order")
     ap.add_argument("--group-reuse", action="store_true",
                     help="DIAGNOSTIC, not a valid line: group the batch in the first two steps only and reuse "
                          "the orders (what the per-step grouping costs the step)")
@@ -286,7 +288,8 @@ def main():
     per = {k: (args.msgs // 3 if k != "MC" else args.msgs - 2 * (args.msgs // 3)) if args.kind == "mixed" else args.msgs
            for k in kinds}
     seeds = {"MU": 42, "MS": 43, "MC": 44}
-    nb = max(1, args.batches)
+    # --group-reuse keeps step 0's order for every step: meaningful only on one batch
+    nb = 1 if args.group_reuse else max(1, args.batches)
     corps, bdl = [], []
     for b in range(nb):   # batch b: seeds + 100 b (batch 0 is the corpus of every earlier round's line)
         corp, bds = {}, {}
@@ -346,7 +349,9 @@ def main():
         with torch.cuda.stream(side):
             if si is not None and si % args.kev_every == 0:
                 gev[si][0].record(side)
-            if gkinds == ["MU", "MS"] and not args.group_separate:   # both sorts' passes in the same launches
+            if args.ms_ungrouped:
+                eng.group(runtime.KIND_MU, bds["MU"], bufs=gbufs["MU"][par])
+            elif gkinds == ["MU", "MS"] and not args.group_separate:   # both sorts' passes in the same launches
                 eng.group_step(bds["MU"], bds["MS"], gbufs["MU"][par], gbufs["MS"][par])
             else:
                 for k in gkinds:
@@ -438,8 +443,9 @@ def main():
                 e0.record(stream)
             parts = {}
             for k in ("MU", "MS"):
-                parts[k.lower()] = (bds[k], outs[s_][k], gbufs[k][par][0][:corp[k].n],
-                                    gbufs[k][par][2] if k in mrec_kinds else None)
+                ung = args.ms_ungrouped and k == "MS"
+                parts[k.lower()] = (bds[k], outs[s_][k], None if ung else gbufs[k][par][0][:corp[k].n],
+                                    gbufs[k][par][2] if k in mrec_kinds and not ung else None)
             eng.launch_step(mu=parts["mu"], ms=parts["ms"],
                             mc=(dict(bds["MC"], max_hex=0) if args.mc_apart else bds["MC"], outs[s_]["MC"], None))
             e1 = torch.cuda.Event(enable_timing=tm)
@@ -649,7 +655,7 @@ def main():
                 (", noise-free dense corpus)" if args.corpus == "dense" else ")"),
         "config": {"workload": wl, "kind": args.kind, "corpus": args.corpus, "msgs_per_gpu": sum(per.values()),
                    "batches": nb, "input_bytes_resident": input_bytes,
-                   "parallelism": f"dp{world}", "grouped": bool(gkinds),
+                   "parallelism": f"dp{world}", "grouped": ("MU only" if args.ms_ungrouped else bool(gkinds)),
                    "streams": ("one kernel (k_step: MU, then MS, then MC tiles)" if fused else
                                "one per kind" if args.concurrent and len(kinds) > 1 else
                                "MU, then MS beside MC" if mc_beside_ms else "serial")},
