@@ -278,12 +278,15 @@ def synth_payload(rng, affix, proto):
     return bytes(rng.integers(32, 127, size=nd, dtype=np.uint8))
 
 
-def synth_launch(rng, n, spill=True, affix=None, status_absent=0.0):
+def synth_launch(rng, n, spill=True, affix=None, status_absent=0.0, heavy=0.0):
     """Launch outputs shaped like k_pulses writes them: records per tile of 64 messages in a shuffled
     tile order, tile pieces of the heap 16-byte aligned with gaps, RAISED and empty messages, and
     (``spill``) records past the used range that no message owns.  ``status_absent``: the fraction of
-    descriptors left at ST_ABSENT (an overlay's)."""
+    descriptors left at ST_ABSENT (an overlay's); ``heavy``: the fraction of messages with 60-300
+    records (spanning whole 64-record waves of the exchange's record pass)."""
     nrec = rng.integers(0, 7, size=n) * (rng.random(n) < 0.8)
+    if heavy:
+        nrec = np.where(rng.random(n) < heavy, rng.integers(60, 301, size=n), nrec)
     status = np.where(rng.random(n) < 0.1, runtime.ST_RAISED, runtime.ST_OK)
     nrec[status == runtime.ST_RAISED] = 0
     desc = np.zeros(n, runtime.DESC_DT)
@@ -309,6 +312,37 @@ def synth_launch(rng, n, spill=True, affix=None, status_absent=0.0):
         desc["status"][absent] = runtime.ST_ABSENT
     rec = np.array(recs, runtime.RES_DT) if recs else np.zeros(0, runtime.RES_DT)
     return desc, rec, np.frombuffer(bytes(heap), np.uint8).copy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pack_form", ["records", "messages"])
+def test_exchange_pack_heavy_messages(pack_form, monkeypatch):
+    """Messages of 60-300 records (the record pass's wave scan: a message that starts in an earlier
+    wave and ends in this one is placed from its total, one spanning the whole wave by lane 0's loop)
+    pack to the numpy wire form, raw and nibble, on both packs."""
+    from pysignalduino_amd import bank as bankmod
+    monkeypatch.setenv("SDX_XCHG_PACK_MSG", "1" if pack_form == "messages" else "0")
+    dev = torch.device("cuda", 0)
+    eng = runtime.Engine(bankmod.Bank(), 0)
+    affix = eng.bank.affixes(runtime.KIND_MU)
+    s = torch.cuda.current_stream(dev)
+    for nib in (False, True):
+        rng = np.random.default_rng(17)
+        launches = [synth_launch(rng, n, affix=affix, heavy=h) for n, h in ((700, 0.05), (300, 0.3))]
+        kind = runtime.KIND_MU if nib else runtime.KIND_RAW
+        parts = [_dev_launch(d, r, h, dev, kind=kind) for d, r, h in launches]
+        ex = _kernel_exchange(eng if nib else None)
+        cnt = ex._count_pack_device(sdist._flatten(parts), s).cpu().numpy().reshape(2, runtime.XCHG_COUNTS)
+        want = [sdist.wire_encode(d, r, h, affix=affix if nib else None) for d, r, h in launches]
+        assert max(int(d["n_rec"].max()) for d, _, _ in launches) > 128
+        offs, nb, T = sdist._layout(cnt[None])
+        sv = ex._bufs["send"].cpu().numpy()
+        for k, (m, w, p, _) in enumerate(want):
+            o = offs[0, k]
+            assert list(cnt[k][:3]) == [len(m), len(w), len(p)], (nib, k)
+            assert sv[o[0]: o[0] + 4 * len(m)].tobytes() == m.tobytes(), (nib, k)
+            assert sv[o[1]: o[1] + 8 * len(w)].tobytes() == w.tobytes(), (nib, k)
+            assert sv[o[2]: o[2] + len(p)].tobytes() == p.tobytes(), (nib, k)
 
 
 def test_wire_nibble_form_round_trip():
