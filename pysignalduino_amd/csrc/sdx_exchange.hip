@@ -67,6 +67,7 @@ struct Parts {
   sdx_xchg_part p[XMAX];
   uint64_t work_off[XMAX];
   int owner[XMAX];      // the launch each part's records ship in (itself, or the launch it overlays); -1 none
+  int shared;           // an overlay on the chains of two launches (k_xw_recs assumes one owner per part)
   const uint8_t* bank;  // nullptr: raw payloads only
   int k;
 };
@@ -787,6 +788,7 @@ static Parts make_parts(const sdx_bank* bank, const sdx_xchg_part* parts, int k)
   Parts P;
   uint64_t off = 0;
   P.k = k;
+  P.shared = 0;
   P.bank = bank ? reinterpret_cast<const uint8_t*>(sdx::bank_dev_ptr(bank)) : nullptr;
   for (int i = 0; i < XMAX; ++i) {
     P.p[i] = i < k ? parts[i] : sdx_xchg_part{};
@@ -801,6 +803,7 @@ static Parts make_parts(const sdx_bank* bank, const sdx_xchg_part* parts, int k)
       const int a = (int)parts[c].alt - 1;
       if (a < 0 || a >= k) break;
       if (P.owner[a] < 0) P.owner[a] = i;
+      else if (P.owner[a] != i) P.shared = 1;
       c = a;
     }
   }
@@ -832,7 +835,7 @@ static int launch_pack(const sdx_bank* bank, const sdx_xchg_part* parts, int k, 
   const char* e = getenv("SDX_XCHG_PACK_MSG");  // read per call: a test compares both forms in one process
   const bool msg_order = e && e[0] == '1';
   const Parts P = make_parts(bank, parts, k);
-  if (msg_order) {
+  if (msg_order || P.shared) {  // (an overlay shared by two launches: the message-order pack resolves it)
     hipLaunchKernelGGL(k_xw_pack, dim3(max_blocks(parts, k), k), dim3(XT), 0, st, P, counts_dev, work, dst);
     return launched("k_xw_pack");
   }
